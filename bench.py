@@ -1,0 +1,221 @@
+"""Headline benchmark: frames/s of the segmentation seam at 640x480, batch 8 per
+GPU (BASELINE.json metric, config 3: bf16 pointwise convs on MFMA), on 1..8
+MI355X, one process per GPU.
+
+A step = one pass of the hot path over one batch: 8 synthetic 640x480 RGB
+frames already resident in HBM -> fused preprocess + network -> 8 float masks
+(144x256), then (N > 1) an RCCL all-gather of every rank's masks so each rank
+holds the whole 8N-frame batch in order.  Weak scaling:
+per-GPU work is fixed, global batch = 8N.
+
+Also measured in the same run:
+  * roofline: the dominant kernel's algorithmic bytes per launch / its mean
+    duration from HIP events recorded by the kernel launches themselves
+    (hipExtLaunchKernelGGL on the stream the kernels run on) over a second pass
+    of K steps, against 8 TB/s;
+  * mask max-abs error vs the CPU oracle on this run's frames;
+  * cpu_baseline: the oracle (C restatement, f32) on a bounded sample of the
+    same frames on this host's cores (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(ROOT, "video-stream-segmenetation_amd")
+METRIC = "frames/sec (640×480, batch=8) at 1/2/4/8 MI355X + mask max-abs-err vs ref"
+HBM_PEAK = 8.0e12
+
+
+def _load_pkg():
+    if "vss_amd" in sys.modules:
+        return sys.modules["vss_amd"]
+    spec = importlib.util.spec_from_file_location("vss_amd", os.path.join(PKG_DIR, "__init__.py"),
+                                                  submodule_search_locations=[PKG_DIR])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["vss_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def cpu_baseline(blob, frames, hm, wm, budget_s):
+    """Oracle (C, f32, OpenMP) on a bounded sample of the same frames."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py  # the checker / CPU baseline only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    res = {}
+    for label, nt, budget in (("all", threads, budget_s), ("4", 4, budget_s / 2)):
+        oracle_py.forward(blob, frames[:1], hm, wm, mode=0, nthreads=nt)  # warm
+        done, t0 = 0, time.perf_counter()
+        while True:
+            oracle_py.forward(blob, frames, hm, wm, mode=0, nthreads=nt)
+            done += len(frames)
+            el = time.perf_counter() - t0
+            if el >= budget:
+                break
+        res[label] = (done / el, done, el)
+    v, done, el = res["all"]
+    return {"value": round(v, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+            "value_4_threads": round(res["4"][0], 2),
+            "sample": f"{done} frames of the timed batch (640x480 -> 144x256, f32) in {el:.1f} s on "
+                      f"{threads} threads; 4 threads: {res['4'][1]} frames in {res['4'][2]:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=8, help="frames per GPU per step")
+    ap.add_argument("--frame", default="480x640")
+    ap.add_argument("--model", default="144x256")
+    ap.add_argument("--dtype", default="bf16x2", choices=["bf16x2", "f32"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=8.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    pkg = _load_pkg()
+    import vss_amd.synthetic as syn
+    import vss_amd.costmodel as cm
+
+    fh, fw = (int(v) for v in args.frame.split("x"))
+    hm, wm = (int(v) for v in args.model.split("x"))
+    B = args.batch
+    frames = syn.make_batch(B, fh, fw, 3, start=rank * B)
+    sess = pkg.Session(model_h=hm, model_w=wm, dtype=args.dtype, device_id=dev.index, max_batch=B,
+                       max_frame_h=fh, max_frame_w=fw)
+    if args.no_graph:
+        sess.set_option(pkg.VSS_OPT_USE_GRAPH, 0)
+    d_frames = torch.from_numpy(frames).to(dev)
+    d_masks = torch.empty((B, hm * wm), dtype=torch.float32, device=dev)
+    gathered = torch.empty((world * B, hm * wm), dtype=torch.float32, device=dev) if world > 1 else None
+    stream = torch.cuda.Stream(device=dev)
+    rs, fs = fw * 3, fh * fw * 3
+
+    def step():
+        sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_masks.data_ptr(), stream.cuda_stream)
+        if gathered is not None:
+            dist.all_gather_into_tensor(gathered, d_masks)
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el_max = float(t.item())
+    value = world * B * args.steps / el_max
+
+    # ---- kernel timing pass (events recorded by the launches themselves) ----
+    sess.set_option(pkg.VSS_OPT_PROFILE, 1)
+    with torch.cuda.stream(stream):
+        for _ in range(args.steps):
+            sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_masks.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    ms, cnt = sess.profile_read()
+    sess.set_option(pkg.VSS_OPT_PROFILE, 0)
+
+    blob = open(sess.weights_path, "rb").read()
+    sys.path.insert(0, os.path.join(PKG_DIR, "model"))
+    import make_weights as mw
+    recs, _, _ = mw.parse_blob(blob)
+    costs = cm.layer_costs(recs, hm, wm, fh, fw, 3, pw_weight_bytes=2 if args.dtype == "bf16x2" else 4)
+    dom = int(np.argmax(ms))
+    dom_bytes = cm.launch_bytes(costs[dom], B)
+    achieved = dom_bytes / (ms[dom] * 1e-3)
+    per_layer = [{"layer": i, "kind": costs[i]["kind"], "ms": round(m, 5),
+                  "GBps": round(cm.launch_bytes(costs[i], B) / (m * 1e-3) / 1e9, 1)} for i, m in enumerate(ms)]
+
+    out = None
+    if rank == 0:
+        masks = d_masks.cpu().numpy()
+        err = None
+        cpu = None
+        if not args.no_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle_py
+            ref = oracle_py.forward(blob, frames, hm, wm, mode=0).reshape(B, -1)
+            err = float(np.abs(masks - ref).max())
+            if world == 1:
+                cpu = cpu_baseline(blob, frames, hm, wm, args.cpu_budget_s)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el_max * 1e3 / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if args.dtype == "bf16x2" else "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{B} synthetic {fw}x{fh} RGB u8 frames per GPU per step (resident in HBM) -> "
+                            f"{wm}x{hm} f32 masks" + (", RCCL all-gather of masks" if world > 1 else ""),
+                "global_batch": world * B,
+                "frame": f"{fw}x{fh}x3",
+                "model_res": f"{wm}x{hm}",
+                "pw_gemm": "v_mfma_f32_16x16x32_bf16, f32 activations split hi+lo" if args.dtype == "bf16x2"
+                           else "v_mfma_f32_16x16x4_f32",
+                "graph": not args.no_graph,
+                "parallelism": f"dp{world}",
+            },
+            "mask_max_abs_err": err,
+            "roofline": {
+                "bound": "hbm",
+                "kernel": f"layer {dom} ({costs[dom]['kind']})",
+                "achieved": round(achieved / 1e9, 1),
+                "peak": HBM_PEAK / 1e9,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK, 4),
+                "traffic": None,
+                "alg_bytes_per_launch": dom_bytes,
+                "mean_kernel_ms": round(ms[dom], 5),
+                "events_count": cnt,
+            },
+            "kernels": per_layer,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    sess.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,145 @@
+/*
+ * vss.h — C ABI of the MI355X-native per-frame person-segmentation path.
+ *
+ * Drop-in boundary for steps 1-2 of processFrame
+ * (/root/reference/client/src/core/frameProcessorTest.ts:78-97): frame pixels
+ * in, the seam triple (alphaRaw: Float32Array(maskH*maskW), maskW, maskH) out.
+ * Plain pointers and sizes only.  Each entry point names the reference
+ * interface it replaces; the Node-API and ctypes bindings that sit on top of
+ * it are in INTEGRATION.md.
+ *
+ * Errors: every int-returning call returns VSS_OK (0) or a negative VSS_E_*
+ * code; the message is in vss_last_error(handle) (thread-local when handle is
+ * NULL, e.g. after a failed vss_create).  This mirrors ORT-web's
+ * _OrtGetLastError(code*, msg**) (client/public/ort-wasm-simd-threaded.mjs:50)
+ * behind the rejecting `session.run` promise.
+ *
+ * Threading: one call in flight per handle (VSS_E_BUSY otherwise), which is the
+ * reference's own usage (runModnetExclusive, client/src/core/main.ts:18-22).
+ */
+#ifndef VSS_H_
+#define VSS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VSS_VERSION 10000 /* 1.0.0 */
+
+enum {
+  VSS_OK = 0,
+  VSS_E_INVALID_ARG = -1,
+  VSS_E_HIP = -2,
+  VSS_E_RCCL = -3,
+  VSS_E_BUSY = -4,
+  VSS_E_OOM = -5,
+  VSS_E_IO = -6,
+  VSS_E_UNSUPPORTED = -7
+};
+
+/* Pointwise-GEMM arithmetic (activations are f32 in HBM in every mode). */
+enum {
+  VSS_DTYPE_F32 = 0,    /* v_mfma_f32_16x16x4_f32, exact f32 fma chains            */
+  VSS_DTYPE_BF16X2 = 1  /* v_mfma_f32_16x16x32_bf16 on a hi+lo bf16 split (default) */
+};
+
+/* Mask resolution: model (the reference's seam, frameProcessorTest.ts:96-97). */
+enum { VSS_OUT_MODEL = 0 };
+
+/* Options for vss_set_option. */
+enum {
+  VSS_OPT_USE_GRAPH = 1, /* 1: replay a captured hipGraph per (shape, buffers) (default 1) */
+  VSS_OPT_PROFILE = 2    /* 1: time every kernel with HIP events (eager launches)         */
+};
+
+typedef struct vss_handle vss_handle;
+
+typedef struct vss_config {
+  int model_h, model_w;    /* model input resolution; multiples of 16. Reference: 288x512
+                              (MODEL_INPUT_SIZE, frameProcessorTest.ts:10); default 144x256 */
+  int dtype;               /* VSS_DTYPE_* */
+  int device_id;           /* HIP device ordinal (one handle = one GPU) */
+  int max_batch;           /* frames per call */
+  int max_frame_h, max_frame_w; /* host-staging capacity for vss_segment (channels <= 4) */
+  const char* weights_path;     /* vss weights blob (model/make_weights.py) */
+} vss_config;
+
+typedef struct vss_info {
+  int mask_h, mask_w;      /* (maskH, maskW) of the seam */
+  int n_layers;
+  int dtype;
+  size_t device_bytes;     /* HBM held by the handle */
+} vss_info;
+
+/* status callback for vss_segment_async: called on a runtime thread once the
+ * masks are in masks_out (status = VSS_OK) or the call failed. */
+typedef void (*vss_callback)(void* user, int status);
+
+/* Library version (VSS_VERSION). */
+int vss_version(void);
+
+/* Replaces initializeModnet (client/src/core/model.ts:12-29) /
+ * _OrtCreateSession (ort-wasm-simd-threaded.mjs:51). */
+int vss_create(const vss_config* cfg, vss_handle** out);
+
+/* Replaces InferenceSession.release. */
+void vss_destroy(vss_handle* h);
+
+/* Replaces _OrtGetLastError (ort-wasm-simd-threaded.mjs:50). */
+const char* vss_last_error(const vss_handle* h);
+
+int vss_get_info(const vss_handle* h, vss_info* info);
+
+/* Synchronous host-memory call.  Replaces frameProcessorTest.ts:79-97
+ * (fromPixels .. session.run .. squeezeMaskTo2D) for n frames at once:
+ * frames: n frames of h rows, row_stride bytes per row, frames packed
+ *         back to back (frame stride = h*row_stride), channels 3 (RGB) or 4
+ *         (RGBA; alpha dropped as tf.browser.fromPixels does, :79);
+ * masks_out: n * mask_h * mask_w floats, row-major per frame, in [0,1]. */
+int vss_segment(vss_handle* h, const uint8_t* frames, int n, int height, int width, int channels,
+                size_t row_stride, float* masks_out, int out_mode);
+
+/* Same as vss_segment but returns at once; cb fires when masks_out is filled.
+ * The caller keeps frames and masks_out alive until then (replaces the async
+ * `await session.run`, frameProcessorTest.ts:91). */
+int vss_segment_async(vss_handle* h, const uint8_t* frames, int n, int height, int width,
+                      int channels, size_t row_stride, float* masks_out, int out_mode,
+                      vss_callback cb, void* user);
+
+/* Device-resident variant: d_frames and d_masks are HBM pointers; the work is
+ * enqueued on `stream` (a hipStream_t; NULL = the handle's stream) and not
+ * waited for.  frame_stride = bytes between frames. */
+int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width,
+                       int channels, size_t row_stride, size_t frame_stride, float* d_masks,
+                       void* stream);
+
+/* Preprocessing alone (frameProcessorTest.ts:79-85): d_out = [n][3][mask_h][mask_w]
+ * f32, the exact ORT input tensor. Enqueued on `stream`. */
+int vss_preprocess_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width,
+                          int channels, size_t row_stride, size_t frame_stride, float* d_out,
+                          void* stream);
+
+/* Wait for all work enqueued by this handle. */
+int vss_synchronize(vss_handle* h);
+
+int vss_set_option(vss_handle* h, int option, int value);
+
+/* Per-layer output shape (C, H, W) at the handle's model resolution. */
+int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww);
+
+/* Copy layer `layer`'s output of the most recent forward to host as NHWC f32
+ * [n][H][W][C] (debug / per-layer parity; synchronises the handle). */
+int vss_read_layer(vss_handle* h, int layer, int n, float* host_out);
+
+/* Kernel times from VSS_OPT_PROFILE runs: per layer, the mean over `count`
+ * forwards (ms).  Resets the accumulators. */
+int vss_profile_read(vss_handle* h, double* ms_per_layer, int cap, int* count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VSS_H_ */

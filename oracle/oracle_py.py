@@ -1,0 +1,89 @@
+"""ctypes bindings for liboracle.so (the C restatement).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg — never by the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P, I, Lg = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
+        L.vsso_preprocess.argtypes = [P, I, I, I, I, Lg, Lg, I, I, P]
+        L.vsso_preprocess.restype = I
+        L.vsso_forward.argtypes = [P, Lg, I, P, I, I, I, I, Lg, Lg, I, I, P, I, P]
+        L.vsso_forward.restype = I
+        L.vsso_layer_shapes.argtypes = [P, Lg, I, I, P, I]
+        L.vsso_layer_shapes.restype = I
+        L.vsso_bf16_round.argtypes = [ctypes.c_float]
+        L.vsso_bf16_round.restype = ctypes.c_float
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def preprocess(frames: np.ndarray, hm: int, wm: int) -> np.ndarray:
+    """frames [N,H,W,C] uint8 (C = 3 or 4) -> [N,3,hm,wm] f32."""
+    frames = np.ascontiguousarray(frames)
+    n, h, w, c = frames.shape
+    out = np.empty((n, 3, hm, wm), np.float32)
+    rc = lib().vsso_preprocess(_ptr(frames), n, h, w, c, w * c, h * w * c, hm, wm, _ptr(out))
+    if rc:
+        raise ValueError(f"vsso_preprocess rc={rc}")
+    return out
+
+
+def layer_shapes(blob: bytes, hm: int, wm: int):
+    buf = np.frombuffer(blob, np.uint8)
+    chw = np.zeros(3 * 64, np.int32)
+    nl = lib().vsso_layer_shapes(_ptr(buf), len(blob), hm, wm, _ptr(chw), 64)
+    if nl < 0:
+        raise ValueError("bad blob")
+    return [tuple(int(v) for v in chw[3 * i:3 * i + 3]) for i in range(nl)]
+
+
+def forward(blob: bytes, frames: np.ndarray, hm: int, wm: int, mode: int = 0,
+            nthreads: int = 0, want_taps: bool = False):
+    """Masks [N,hm,wm] f32 (and, with want_taps, per-frame per-layer planar outputs)."""
+    frames = np.ascontiguousarray(frames)
+    n, h, w, c = frames.shape
+    buf = np.frombuffer(blob, np.uint8)
+    masks = np.empty((n, hm, wm), np.float32)
+    taps_arr = None
+    taps_np = None
+    if want_taps:
+        shapes = layer_shapes(blob, hm, wm)
+        nl = len(shapes)
+        taps_np = [[np.empty(s, np.float32) for s in shapes] for _ in range(n)]
+        taps_arr = (ctypes.c_void_p * (n * nl))(*[t.ctypes.data for fr in taps_np for t in fr])
+    rc = lib().vsso_forward(_ptr(buf), len(blob), mode, _ptr(frames), n, h, w, c, w * c, h * w * c,
+                            hm, wm, _ptr(masks), nthreads, taps_arr)
+    if rc:
+        raise ValueError(f"vsso_forward rc={rc}")
+    return (masks, taps_np) if want_taps else masks
+
+
+def bf16_round(x: float) -> float:
+    return lib().vsso_bf16_round(x)

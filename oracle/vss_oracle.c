@@ -1,0 +1,364 @@
+/*
+ * vss_oracle.c — CPU restatement of the per-frame segmentation hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libvss / the package /
+ * the Node addon) links, loads or calls this file.  It is imported only by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+ * checker and the timed CPU baseline ("kind": "port").
+ *
+ * What it restates (reference file:line under /root/reference):
+ *   a1 fromPixels   client/src/core/frameProcessorTest.ts:79  RGB, alpha dropped
+ *   a2 resizeBilinear(frame,[288,512])              :80  tfjs 4.22 defaults
+ *      (alignCorners=false, halfPixelCenters=false; WebGL ResizeBilinearProgram
+ *      form: f32 arithmetic, ratio = (float)(inH/outH computed in double);
+ *      tfjs is a third-party dependency absent from the tree, pinned at 4.22.0
+ *      by client/package-lock.json; its published algorithm is restated here)
+ *   a3 .div(255.0)                                   :81
+ *   a4 .transpose([2,0,1]).expandDims(0)             :82-83  -> NCHW f32
+ *   a6 session.run({input})                          :91  the network: the
+ *      reference's model_q4f16.onnx is MISSING (.MISSING_LARGE_BLOBS:7), so the
+ *      network is the build's own layer table (video-stream-segmenetation_amd/
+ *      model/spec.json + the seeded blob).  PARITY OF THE NETWORK IS UNPINNED
+ *      against the reference; it is pinned against an independent PyTorch-CPU
+ *      functional restatement (oracle/torch_ref.py, tests/golden/).
+ *   a8/a9 squeezeMaskTo2D + (alphaRaw, maskW, maskH) :94-97, :190-201
+ *      -> masks [n][Hm][Wm] f32, row-major, model resolution.
+ *
+ * Layout here is planar NCHW f32 (the GPU path is NHWC and fused: the two are
+ * deliberately different implementations).  mode 0 = f32 everywhere; mode 1 =
+ * "bf16 pointwise" — rounds to bf16 (RNE) at exactly the points spec.json's
+ * "bf16_mode" lists, so GPU-vs-oracle parity in that mode is an arithmetic
+ * check, not an accuracy claim.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define VSSO_MAGIC 0x57535356u
+#define NONE 0xFFFFFFFFu
+enum { K_STEM = 1, K_IR = 2, K_DEC = 3, K_HEAD = 4 };
+enum { F_EXPAND = 1, F_RESIDUAL = 2 };
+enum { O_W1, O_B1, O_WDW, O_BDW, O_W2, O_B2, O_GAMMA, O_BETA };
+
+typedef struct {
+  uint32_t kind, cin, chid, cout, stride, flags, src, skip, off[8];
+} rec_t;
+
+static inline float bf16r(float x) {
+  uint32_t u;
+  memcpy(&u, &x, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  u &= 0xFFFF0000u;
+  memcpy(&x, &u, 4);
+  return x;
+}
+static inline float relu6(float v) { return v < 0.f ? 0.f : (v > 6.f ? 6.f : v); }
+
+/* ---- a2/a3: tfjs legacy bilinear + /255, one output sample ------------- */
+static inline float resize_px(const uint8_t* f, long rs, int c, int h, int w,
+                              float ry, float rx, int y, int x, int ch) {
+  float fy = (float)y * ry, fx = (float)x * rx;
+  int y0 = (int)floorf(fy > 0.f ? fy : 0.f), x0 = (int)floorf(fx > 0.f ? fx : 0.f);
+  int y1 = (int)ceilf(fy); if (y1 > h - 1) y1 = h - 1;
+  int x1 = (int)ceilf(fx); if (x1 > w - 1) x1 = w - 1;
+  float dy = fy - (float)y0, dx = fx - (float)x0;
+  float tl = f[y0 * rs + (long)x0 * c + ch], tr = f[y0 * rs + (long)x1 * c + ch];
+  float bl = f[y1 * rs + (long)x0 * c + ch], br = f[y1 * rs + (long)x1 * c + ch];
+  float top = fmaf(tr - tl, dx, tl);
+  float bot = fmaf(br - bl, dx, bl);
+  float v = fmaf(bot - top, dy, top);
+  return v / 255.0f;
+}
+
+/* frames: n frames, each h rows of row_stride bytes, frame_stride bytes apart,
+ * c = 3 (RGB) or 4 (RGBA).  out: [n][3][Hm][Wm] f32 (the ORT input tensor). */
+int vsso_preprocess(const uint8_t* frames, int n, int h, int w, int c,
+                    long row_stride, long frame_stride, int Hm, int Wm, float* out) {
+  if (!frames || !out || n < 0 || h <= 0 || w <= 0 || (c != 3 && c != 4) || Hm <= 0 || Wm <= 0)
+    return -1;
+  float ry = (float)((double)h / (double)Hm), rx = (float)((double)w / (double)Wm);
+  for (int i = 0; i < n; ++i) {
+    const uint8_t* f = frames + (long)i * frame_stride;
+    for (int ch = 0; ch < 3; ++ch)
+      for (int y = 0; y < Hm; ++y)
+        for (int x = 0; x < Wm; ++x)
+          out[(((long)i * 3 + ch) * Hm + y) * Wm + x] = resize_px(f, row_stride, c, h, w, ry, rx, y, x, ch);
+  }
+  return 0;
+}
+
+/* ---- network pieces (one frame, planar) -------------------------------- */
+typedef struct {
+  float* t;   /* [C][H][W] */
+  int C, H, W;
+  int normed; /* 1: a dec layer's pre-norm output; consumer applies norm+relu */
+  const float *gamma, *beta;
+} act_t;
+
+static float* wcopy(const float* src, long n, int mode) {
+  float* d = (float*)malloc(sizeof(float) * n);
+  for (long i = 0; i < n; ++i) d[i] = mode ? bf16r(src[i]) : src[i];
+  return d;
+}
+
+/* relu(instance_norm(x) * gamma + beta), stats in double over the stored tensor */
+static void norm_relu(const act_t* a, float* out, float eps) {
+  long hw = (long)a->H * a->W;
+#pragma omp parallel for schedule(static)
+  for (int c = 0; c < a->C; ++c) {
+    const float* p = a->t + c * hw;
+    double s = 0;
+    for (long i = 0; i < hw; ++i) s += p[i];
+    double mean = s / (double)hw, v = 0;
+    for (long i = 0; i < hw; ++i) { double d = p[i] - mean; v += d * d; }
+    v /= (double)hw;
+    double rstd = 1.0 / sqrt(v + (double)eps);
+    for (long i = 0; i < hw; ++i) {
+      double y = ((double)p[i] - mean) * rstd * a->gamma[c] + a->beta[c];
+      out[c * hw + i] = y > 0 ? (float)y : 0.f;
+    }
+  }
+}
+
+/* PyTorch upsample_bilinear2d(scale 2, align_corners=False) source index */
+static inline void up_idx(int o, int in, int* i0, int* i1, float* l0, float* l1) {
+  float s = ((float)o + 0.5f) * 0.5f - 0.5f;
+  if (s < 0.f) s = 0.f;
+  int a = (int)s;
+  *i0 = a;
+  *i1 = a + (a < in - 1 ? 1 : 0);
+  *l1 = s - (float)a;
+  *l0 = 1.f - *l1;
+}
+
+static void upsample2x(const float* in, int C, int H, int W, float* out) {
+  int Ho = 2 * H, Wo = 2 * W;
+#pragma omp parallel for schedule(static)
+  for (int c = 0; c < C; ++c)
+    for (int y = 0; y < Ho; ++y) {
+      int y0, y1; float hy0, hy1;
+      up_idx(y, H, &y0, &y1, &hy0, &hy1);
+      for (int x = 0; x < Wo; ++x) {
+        int x0, x1; float wx0, wx1;
+        up_idx(x, W, &x0, &x1, &wx0, &wx1);
+        const float* p = in + (long)c * H * W;
+        float v = hy0 * (wx0 * p[y0 * W + x0] + wx1 * p[y0 * W + x1]) +
+                  hy1 * (wx0 * p[y1 * W + x0] + wx1 * p[y1 * W + x1]);
+        out[((long)c * Ho + y) * Wo + x] = v;
+      }
+    }
+}
+
+/* y[co] = b[co] + sum_ci W[co][ci] * x[ci]  (pointwise, planar, p pixels) */
+static void pointwise(const float* x, int cin, long p, const float* W, const float* b, int cout, float* y) {
+#pragma omp parallel for schedule(static)
+  for (int co = 0; co < cout; ++co) {
+    float* yo = y + co * p;
+    for (long i = 0; i < p; ++i) yo[i] = b[co];
+    for (int ci = 0; ci < cin; ++ci) {
+      float wv = W[(long)co * cin + ci];
+      const float* xi = x + ci * p;
+      for (long i = 0; i < p; ++i) yo[i] += wv * xi[i];
+    }
+  }
+}
+
+/* depthwise 3x3, pad 1, stride s, zero outside */
+static void depthwise(const float* x, int C, int H, int W, int s, const float* wdw, const float* b,
+                      float* y, int Ho, int Wo) {
+#pragma omp parallel for schedule(static)
+  for (int c = 0; c < C; ++c)
+    for (int oy = 0; oy < Ho; ++oy)
+      for (int ox = 0; ox < Wo; ++ox) {
+        float acc = b[c];
+        for (int ky = 0; ky < 3; ++ky) {
+          int iy = s * oy - 1 + ky;
+          if (iy < 0 || iy >= H) continue;
+          for (int kx = 0; kx < 3; ++kx) {
+            int ix = s * ox - 1 + kx;
+            if (ix < 0 || ix >= W) continue;
+            acc += wdw[c * 9 + ky * 3 + kx] * x[((long)c * H + iy) * W + ix];
+          }
+        }
+        y[((long)c * Ho + oy) * Wo + ox] = acc;
+      }
+}
+
+static void round_all(float* p, long n, int mode, int relu6_act) {
+  for (long i = 0; i < n; ++i) {
+    float v = relu6_act ? relu6(p[i]) : p[i];
+    p[i] = mode ? bf16r(v) : v;
+  }
+}
+
+static int forward_one(const rec_t* L, int nl, const float* D, float eps, int mode,
+                       const float* x0, int Hm, int Wm, float* mask, float** taps) {
+  act_t* A = (act_t*)calloc(nl, sizeof(act_t));
+  int rc = 0;
+  for (int li = 0; li < nl; ++li) {
+    const rec_t* r = &L[li];
+    act_t* o = &A[li];
+    if (r->kind == K_STEM) {
+      int H = Hm, W = Wm, Ho = (H + 1) / 2, Wo = (W + 1) / 2, co = r->cout;
+      o->C = co; o->H = Ho; o->W = Wo;
+      o->t = (float*)malloc(sizeof(float) * co * Ho * Wo);
+      const float* w = D + r->off[O_W1];
+      const float* b = D + r->off[O_B1];
+#pragma omp parallel for schedule(static)
+      for (int c = 0; c < co; ++c)
+        for (int oy = 0; oy < Ho; ++oy)
+          for (int ox = 0; ox < Wo; ++ox) {
+            float acc = b[c];
+            for (int ci = 0; ci < 3; ++ci)
+              for (int ky = 0; ky < 3; ++ky) {
+                int iy = 2 * oy - 1 + ky;
+                if (iy < 0 || iy >= H) continue;
+                for (int kx = 0; kx < 3; ++kx) {
+                  int ix = 2 * ox - 1 + kx;
+                  if (ix < 0 || ix >= W) continue;
+                  acc += w[((c * 3 + ci) * 3 + ky) * 3 + kx] * x0[((long)ci * H + iy) * W + ix];
+                }
+              }
+            o->t[((long)c * Ho + oy) * Wo + ox] = acc;
+          }
+      round_all(o->t, (long)co * Ho * Wo, mode, 1);
+    } else if (r->kind == K_IR) {
+      const act_t* in = &A[r->src];
+      int H = in->H, W = in->W, s = r->stride;
+      int Ho = s == 2 ? (H + 1) / 2 : H, Wo = s == 2 ? (W + 1) / 2 : W;
+      long p = (long)H * W, po = (long)Ho * Wo;
+      int ch = (r->flags & F_EXPAND) ? r->chid : r->cin;
+      float* h = (float*)malloc(sizeof(float) * ch * p);
+      if (r->flags & F_EXPAND) {
+        float* w1 = wcopy(D + r->off[O_W1], (long)r->chid * r->cin, mode);
+        pointwise(in->t, r->cin, p, w1, D + r->off[O_B1], ch, h);
+        free(w1);
+        round_all(h, ch * p, mode, 1);
+      } else {
+        memcpy(h, in->t, sizeof(float) * ch * p);
+      }
+      float* d = (float*)malloc(sizeof(float) * ch * po);
+      depthwise(h, ch, H, W, s, D + r->off[O_WDW], D + r->off[O_BDW], d, Ho, Wo);
+      round_all(d, ch * po, mode, 1);
+      o->C = r->cout; o->H = Ho; o->W = Wo;
+      o->t = (float*)malloc(sizeof(float) * r->cout * po);
+      float* w2 = wcopy(D + r->off[O_W2], (long)r->cout * ch, mode);
+      pointwise(d, ch, po, w2, D + r->off[O_B2], r->cout, o->t);
+      free(w2);
+      if (r->flags & F_RESIDUAL)
+        for (long i = 0; i < r->cout * po; ++i) o->t[i] += in->t[i];
+      round_all(o->t, r->cout * po, mode, 0);
+      free(h); free(d);
+    } else if (r->kind == K_DEC) {
+      const act_t* in = &A[r->src];
+      const act_t* sk = &A[r->skip];
+      int H = sk->H, W = sk->W, cl = r->cin, cs = r->chid, cc = cl + cs;
+      long p = (long)H * W;
+      if (in->H * 2 != H || in->W * 2 != W || in->C != cl || sk->C != cs) { rc = -2; break; }
+      float* a = (float*)malloc(sizeof(float) * cl * in->H * in->W);
+      if (in->normed) norm_relu(in, a, eps);
+      else memcpy(a, in->t, sizeof(float) * cl * in->H * in->W);
+      float* cat = (float*)malloc(sizeof(float) * cc * p);
+      upsample2x(a, cl, in->H, in->W, cat);
+      round_all(cat, cl * p, mode, 0);
+      memcpy(cat + cl * p, sk->t, sizeof(float) * cs * p);
+      float* d = (float*)malloc(sizeof(float) * cc * p);
+      depthwise(cat, cc, H, W, 1, D + r->off[O_WDW], D + r->off[O_BDW], d, H, W);
+      round_all(d, cc * p, mode, 0);
+      o->C = r->cout; o->H = H; o->W = W;
+      o->t = (float*)malloc(sizeof(float) * r->cout * p);
+      float* w2 = wcopy(D + r->off[O_W2], (long)r->cout * cc, mode);
+      pointwise(d, cc, p, w2, D + r->off[O_B2], r->cout, o->t);
+      free(w2);
+      round_all(o->t, r->cout * p, mode, 0);
+      o->normed = 1;
+      o->gamma = D + r->off[O_GAMMA];
+      o->beta = D + r->off[O_BETA];
+      free(a); free(cat); free(d);
+    } else if (r->kind == K_HEAD) {
+      const act_t* in = &A[r->src];
+      int H = in->H, W = in->W;
+      long p = (long)H * W;
+      float* a = (float*)malloc(sizeof(float) * in->C * p);
+      if (in->normed) norm_relu(in, a, eps);
+      else memcpy(a, in->t, sizeof(float) * in->C * p);
+      float* z = (float*)malloc(sizeof(float) * p);
+      pointwise(a, r->cin, p, D + r->off[O_W2], D + r->off[O_B2], 1, z);
+      if (2 * H != Hm || 2 * W != Wm) { rc = -3; free(a); free(z); break; }
+      upsample2x(z, 1, H, W, mask);
+      for (long i = 0; i < (long)Hm * Wm; ++i) mask[i] = 1.0f / (1.0f + expf(-mask[i]));
+      o->C = 1; o->H = Hm; o->W = Wm;
+      o->t = (float*)malloc(sizeof(float) * Hm * Wm);
+      memcpy(o->t, mask, sizeof(float) * Hm * Wm);
+      free(a); free(z);
+    } else {
+      rc = -4;
+      break;
+    }
+    if (taps && taps[li]) memcpy(taps[li], o->t, sizeof(float) * (long)o->C * o->H * o->W);
+  }
+  for (int li = 0; li < nl; ++li) free(A[li].t);
+  free(A);
+  return rc;
+}
+
+static int parse(const uint8_t* blob, long bytes, const rec_t** L, int* nl, const float** D, float* eps) {
+  if (!blob || bytes < 32) return -1;
+  const uint32_t* h = (const uint32_t*)blob;
+  if (h[0] != VSSO_MAGIC || h[1] != 1) return -1;
+  *nl = (int)h[2];
+  long nf = h[3];
+  memcpy(eps, &h[4], 4);
+  if (32 + 64L * *nl + 4L * nf > bytes) return -1;
+  *L = (const rec_t*)(blob + 32);
+  *D = (const float*)(blob + 32 + 64L * *nl);
+  return 0;
+}
+
+/* Layer output shapes for a model resolution (C,H,W per layer). */
+int vsso_layer_shapes(const uint8_t* blob, long bytes, int Hm, int Wm, int* chw, int cap) {
+  const rec_t* L; const float* D; int nl; float eps;
+  if (parse(blob, bytes, &L, &nl, &D, &eps)) return -1;
+  if (cap < nl) return -1;
+  for (int i = 0; i < nl; ++i) {
+    const rec_t* r = &L[i];
+    int C = r->cout, H, W;
+    if (r->kind == K_STEM) { H = (Hm + 1) / 2; W = (Wm + 1) / 2; }
+    else if (r->kind == K_IR) {
+      H = chw[r->src * 3 + 1]; W = chw[r->src * 3 + 2];
+      if (r->stride == 2) { H = (H + 1) / 2; W = (W + 1) / 2; }
+    } else if (r->kind == K_DEC) { H = chw[r->skip * 3 + 1]; W = chw[r->skip * 3 + 2]; }
+    else { H = Hm; W = Wm; }
+    chw[i * 3] = C; chw[i * 3 + 1] = H; chw[i * 3 + 2] = W;
+  }
+  return nl;
+}
+
+/* Full forward: frames -> masks [n][Hm][Wm].  taps (optional): per-frame,
+ * per-layer output buffers taps[i*nl + li] (planar), NULL entries skipped. */
+int vsso_forward(const uint8_t* blob, long blob_bytes, int mode,
+                 const uint8_t* frames, int n, int h, int w, int c,
+                 long row_stride, long frame_stride, int Hm, int Wm,
+                 float* masks, int nthreads, float** taps) {
+  const rec_t* L; const float* D; int nl; float eps;
+  if (parse(blob, blob_bytes, &L, &nl, &D, &eps)) return -1;
+  if ((Hm % 16) || (Wm % 16) || n < 0 || !masks) return -1;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+  float* x0 = (float*)malloc(sizeof(float) * 3L * Hm * Wm);
+  int rc = 0;
+  for (int i = 0; i < n && !rc; ++i) {
+    rc = vsso_preprocess(frames + (long)i * frame_stride, 1, h, w, c, row_stride, 0, Hm, Wm, x0);
+    if (!rc) rc = forward_one(L, nl, D, eps, mode, x0, Hm, Wm, masks + (long)i * Hm * Wm,
+                              taps ? taps + (long)i * nl : NULL);
+  }
+  free(x0);
+  return rc;
+}
+
+float vsso_bf16_round(float x) { return bf16r(x); }

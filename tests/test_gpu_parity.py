@@ -1,0 +1,202 @@
+"""GPU parity tests (MI355X): the HIP path through the C ABI against the CPU
+oracle (oracle/vss_oracle.c) and the committed golden vectors.
+
+Bars (stated here, per the task's north star):
+  * preprocessing (frameProcessorTest.ts:79-85): BIT-EXACT with the oracle;
+  * mask (the seam's alphaRaw, :95): max |gpu - oracle| <= 1e-3 for both
+    pointwise modes (f32 MFMA and the bf16 hi+lo split MFMA); measured values
+    are printed (expected O(1e-5));
+  * per-layer f32 activations: max |gpu - oracle| <= 1e-4 * max(1, max|ref|);
+  * batching, graph replay and repeated runs: bitwise identical.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MASK_TOL = 1e-3
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def sess_f32(pkg, torch_cuda):
+    s = pkg.Session(dtype="f32", max_batch=8)
+    yield s
+    s.close()
+
+
+@pytest.fixture(scope="module")
+def sess_bf(pkg, torch_cuda):
+    s = pkg.Session(dtype="bf16x2", max_batch=8)
+    yield s
+    s.close()
+
+
+def _frames(syn, n, h=480, w=640, c=3, start=0):
+    return np.stack([syn.make_frame(start + i, h, w, c) for i in range(n)])
+
+
+def test_preprocess_bitexact(pkg, sess_f32, oracle, synthetic, torch_cuda):
+    torch = torch_cuda
+    for (n, h, w, c) in [(3, 480, 640, 3), (1, 100, 150, 4), (2, 1080, 1920, 3), (1, 144, 256, 3)]:
+        f = _frames(synthetic, n, h, w, c, start=7)
+        want = oracle.preprocess(f, 144, 256)
+        df = torch.from_numpy(f).cuda()
+        out = torch.empty((n, 3, 144, 256), dtype=torch.float32, device="cuda")
+        sess_f32.preprocess_device(df.data_ptr(), n, h, w, c, w * c, h * w * c, out.data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert np.array_equal(got, want), f"preprocess mismatch {n}x{h}x{w}x{c}: {np.abs(got - want).max()}"
+
+
+def test_layers_f32(pkg, sess_f32, oracle, blob, synthetic):
+    f = _frames(synthetic, 2)
+    masks, _, _ = sess_f32.segment_frames(f)
+    _, taps = oracle.forward(blob, f, 144, 256, mode=0, want_taps=True)
+    for li in range(sess_f32.n_layers - 1):
+        got = sess_f32.read_layer(li, 2)
+        ref = np.stack([taps[i][li] for i in range(2)])
+        assert got.shape == ref.shape
+        err = np.abs(got - ref).max()
+        scale = max(1.0, float(np.abs(ref).max()))
+        print(f"layer {li} shape {ref.shape[1:]} max abs err {err:.3e} (scale {scale:.2f})")
+        assert err <= 1e-4 * scale, f"layer {li}: {err}"
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16x2"])
+def test_masks_vs_oracle(pkg, sess_f32, sess_bf, oracle, blob, synthetic, mode):
+    s = sess_f32 if mode == "f32" else sess_bf
+    f = _frames(synthetic, 8)
+    masks, mw, mh = s.segment_frames(f)
+    assert (mw, mh) == (256, 144) and masks.shape == (8, 144 * 256)
+    ref = oracle.forward(blob, f, 144, 256, mode=0).reshape(8, -1)
+    err = np.abs(masks - ref).max()
+    print(f"{mode}: mask max abs err vs oracle = {err:.3e}")
+    assert err <= MASK_TOL
+
+
+@pytest.mark.parametrize("name", ["vga_2f_144x256", "odd_rgba_1f_32x48"])
+def test_masks_vs_golden(pkg, synthetic, name, torch_cuda):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    h, w, c, hm, wm = (int(v) for v in g["shape"])
+    f = np.stack([synthetic.make_frame(int(s), h, w, c) for s in g["seeds"]])
+    for dt in ("f32", "bf16x2"):
+        with pkg.Session(model_h=hm, model_w=wm, dtype=dt, max_batch=len(f), max_frame_h=h, max_frame_w=w) as s:
+            m, mw, mh = s.segment_frames(f)
+            assert (mh, mw) == (hm, wm)
+            err = np.abs(m.reshape(g["masks"].shape) - g["masks"]).max()
+            print(f"{name} {dt}: max abs err vs golden {err:.3e}")
+            assert err <= MASK_TOL
+
+
+def test_reference_model_size_288x512(pkg, oracle, blob, synthetic, torch_cuda):
+    # the reference's own MODEL_INPUT_SIZE (frameProcessorTest.ts:10) from a 720p camera frame
+    f = _frames(synthetic, 2, 720, 1280, 4, start=40)
+    with pkg.Session(model_h=288, model_w=512, dtype="bf16x2", max_batch=2, max_frame_h=720, max_frame_w=1280) as s:
+        m, mw, mh = s.segment_frames(f)
+    assert (mw, mh) == (512, 288)
+    ref = oracle.forward(blob, f, 288, 512, mode=0).reshape(2, -1)
+    err = np.abs(m - ref).max()
+    print(f"288x512: {err:.3e}")
+    assert err <= MASK_TOL
+
+
+def test_segment_frame_seam_triple(sess_bf, synthetic):
+    f = synthetic.make_frame(3)
+    alpha, mw, mh = sess_bf.segment_frame(f)
+    assert alpha.dtype == np.float32 and alpha.shape == (mh * mw,)
+    assert 0.0 <= alpha.min() and alpha.max() <= 1.0
+
+
+def test_batch_invariance_and_determinism(sess_bf, synthetic):
+    f = _frames(synthetic, 8, start=100)
+    full, _, _ = sess_bf.segment_frames(f)
+    again, _, _ = sess_bf.segment_frames(f)
+    assert np.array_equal(full, again)
+    for n in (1, 3, 5):
+        part, _, _ = sess_bf.segment_frames(f[:n])
+        assert np.array_equal(part, full[:n])
+    single, _, _ = sess_bf.segment_frames(f[6:7])
+    assert np.array_equal(single, full[6:7])
+
+
+def test_graph_vs_eager_and_profile(pkg, sess_bf, synthetic):
+    f = _frames(synthetic, 4, start=200)
+    a, _, _ = sess_bf.segment_frames(f)
+    sess_bf.set_option(pkg.VSS_OPT_USE_GRAPH, 0)
+    b, _, _ = sess_bf.segment_frames(f)
+    sess_bf.set_option(pkg.VSS_OPT_PROFILE, 1)
+    c, _, _ = sess_bf.segment_frames(f)
+    sess_bf.set_option(pkg.VSS_OPT_PROFILE, 0)
+    sess_bf.set_option(pkg.VSS_OPT_USE_GRAPH, 1)
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+    ms, cnt = sess_bf.profile_read()
+    assert cnt == 1 and all(m > 0 for m in ms)
+
+
+def test_device_path_row_stride(pkg, sess_bf, synthetic, torch_cuda):
+    torch = torch_cuda
+    f = _frames(synthetic, 3, 480, 640, 3, start=300)
+    ref, _, _ = sess_bf.segment_frames(f)
+    pad = 64  # ragged rows: stride > width*channels
+    buf = np.zeros((3, 480, 640 * 3 + pad), np.uint8)
+    buf[:, :, :640 * 3] = f.reshape(3, 480, -1)
+    d = torch.from_numpy(buf).cuda()
+    out = torch.empty((3, 144 * 256), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        sess_bf.segment_device(d.data_ptr(), 3, 480, 640, 3, 640 * 3 + pad, 480 * (640 * 3 + pad),
+                               out.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_async_and_busy(pkg, sess_bf, synthetic):
+    import threading
+    f = _frames(synthetic, 2, start=400)
+    ref, _, _ = sess_bf.segment_frames(f)
+    done = threading.Event()
+    got = {}
+
+    def cb(masks, mw, mh, status):
+        got["m"], got["s"] = masks.copy(), status
+        done.set()
+
+    sess_bf.segment_frames_async(f, cb)
+    assert done.wait(30)
+    sess_bf.synchronize()
+    assert got["s"] == 0 and np.array_equal(got["m"], ref)
+
+
+def test_argument_errors(pkg, sess_bf, synthetic):
+    f = _frames(synthetic, 9)
+    with pytest.raises(pkg.VssError) as e:
+        sess_bf.segment_frames(f)  # > max_batch
+    assert e.value.code == pkg.VSS_E_INVALID_ARG
+    with pytest.raises(pkg.VssError):
+        sess_bf.segment_frames(np.zeros((1, 2000, 2000, 3), np.uint8))  # > staging capacity
+    with pytest.raises(pkg.VssError):
+        sess_bf.segment_frames(np.zeros((1, 10, 10, 2), np.uint8))
+    # still usable after errors
+    m, _, _ = sess_bf.segment_frames(f[:1])
+    assert np.isfinite(m).all()
+
+
+def test_tiny_and_extreme_frames(pkg, sess_bf, oracle, blob):
+    rng = np.random.default_rng(0)
+    for (h, w) in [(1, 1), (2, 3), (1080, 1920), (37, 1000)]:
+        f = rng.integers(0, 256, size=(1, h, w, 3), dtype=np.uint8)
+        m, _, _ = sess_bf.segment_frames(f)
+        ref = oracle.forward(blob, f, 144, 256, mode=0).reshape(1, -1)
+        assert np.abs(m - ref).max() <= MASK_TOL, (h, w)

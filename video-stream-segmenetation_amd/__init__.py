@@ -1,0 +1,238 @@
+"""Python host mirror of the segmentation seam over libvss.so (include/vss.h).
+
+Reference seam (/root/reference/client/src/core/frameProcessorTest.ts:78-97):
+
+    frame -> tf.browser.fromPixels -> resizeBilinear -> /255 -> NCHW  (:79-85)
+          -> session.run({input})                                      (:91)
+          -> squeezeMaskTo2D -> (alphaRaw, maskW, maskH)               (:94-97)
+
+`Session.segment_frame(frame)` returns exactly that triple (mask as a float32
+array of maskH*maskW, plus maskW, maskH); `segment_frames` does a batch.  The
+TypeScript surface (segmentFrame/segmentFrames) is in ts/ over the same C ABI.
+
+Errors mirror ORT-web's rejecting `session.run`: every failing call raises
+VssError carrying the C code and vss_last_error().  There is no CPU fallback:
+if libvss.so is missing or no HIP device is present, creating a Session raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libvss.so")
+DEFAULT_WEIGHTS = os.path.join(HERE, "model", "vss_weights_seed7.bin")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "vss.h")
+
+VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_IO, VSS_E_UNSUPPORTED = (
+    0, -1, -2, -3, -4, -5, -6, -7)
+DTYPES = {"f32": 0, "bf16x2": 1}
+VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE = 1, 2
+VSS_OUT_MODEL = 0
+
+
+class VssError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"vss error {code}: {msg}")
+        self.code = code
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("model_h", ctypes.c_int), ("model_w", ctypes.c_int), ("dtype", ctypes.c_int),
+                ("device_id", ctypes.c_int), ("max_batch", ctypes.c_int), ("max_frame_h", ctypes.c_int),
+                ("max_frame_w", ctypes.c_int), ("weights_path", ctypes.c_char_p)]
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("mask_h", ctypes.c_int), ("mask_w", ctypes.c_int), ("n_layers", ctypes.c_int),
+                ("dtype", ctypes.c_int), ("device_bytes", ctypes.c_size_t)]
+
+
+CALLBACK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)
+_lib = None
+_lock = threading.Lock()
+
+
+def build(force: bool = False) -> str:
+    """Compile libvss.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.join(HERE, "csrc")], check=True)
+    return LIB_PATH
+
+
+def ensure_weights(path: str = DEFAULT_WEIGHTS) -> str:
+    if not os.path.exists(path):
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("vss_make_weights", os.path.join(HERE, "model", "make_weights.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        mod.write_blob(path)
+    return path
+
+
+def lib() -> ctypes.CDLL:
+    """Load libvss.so; raises (never falls back) when the HIP library is absent."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise VssError(VSS_E_IO, f"libvss.so not built at {LIB_PATH} (run build())")
+            L = ctypes.CDLL(LIB_PATH)
+            P, I, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+            sig = {
+                "vss_version": ([], I),
+                "vss_create": ([ctypes.POINTER(_Config), ctypes.POINTER(P)], I),
+                "vss_destroy": ([P], None),
+                "vss_last_error": ([P], ctypes.c_char_p),
+                "vss_get_info": ([P, ctypes.POINTER(_Info)], I),
+                "vss_segment": ([P, P, I, I, I, I, S, P, I], I),
+                "vss_segment_async": ([P, P, I, I, I, I, S, P, I, CALLBACK, P], I),
+                "vss_segment_device": ([P, P, I, I, I, I, S, S, P, P], I),
+                "vss_preprocess_device": ([P, P, I, I, I, I, S, S, P, P], I),
+                "vss_synchronize": ([P], I),
+                "vss_set_option": ([P, I, I], I),
+                "vss_layer_shape": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)], I),
+                "vss_read_layer": ([P, I, I, P], I),
+                "vss_profile_read": ([P, ctypes.POINTER(ctypes.c_double), I, ctypes.POINTER(I)], I),
+            }
+            for name, (args, res) in sig.items():
+                fn = getattr(L, name)
+                fn.argtypes = args
+                fn.restype = res
+            _lib = L
+        return _lib
+
+
+def _check(rc: int, handle=None):
+    if rc != VSS_OK:
+        msg = lib().vss_last_error(handle)
+        raise VssError(rc, msg.decode() if msg else "")
+
+
+def _as_frames(frames: np.ndarray) -> np.ndarray:
+    """[H,W,C] or [N,H,W,C] uint8, C in {3,4} (tf.browser.fromPixels input)."""
+    a = np.asarray(frames)
+    if a.dtype != np.uint8:
+        raise VssError(VSS_E_INVALID_ARG, "frames must be uint8")
+    if a.ndim == 3:
+        a = a[None]
+    if a.ndim != 4 or a.shape[3] not in (3, 4):
+        raise VssError(VSS_E_INVALID_ARG, "frames must be [N,H,W,3|4]")
+    return np.ascontiguousarray(a)
+
+
+class Session:
+    """One GPU, one model resolution: the MI355X stand-in for an ORT
+    InferenceSession of the segmentation model (model.ts:12-29)."""
+
+    def __init__(self, model_h: int = 144, model_w: int = 256, dtype: str = "bf16x2", device_id: int = 0,
+                 max_batch: int = 8, max_frame_h: int = 1080, max_frame_w: int = 1920,
+                 weights_path: str | None = None):
+        if dtype not in DTYPES:
+            raise VssError(VSS_E_INVALID_ARG, f"dtype must be one of {sorted(DTYPES)}")
+        self.weights_path = ensure_weights(weights_path or DEFAULT_WEIGHTS)
+        cfg = _Config(model_h, model_w, DTYPES[dtype], device_id, max_batch, max_frame_h, max_frame_w,
+                      self.weights_path.encode())
+        h = ctypes.c_void_p()
+        _check(lib().vss_create(ctypes.byref(cfg), ctypes.byref(h)), None)
+        self._h = h
+        info = _Info()
+        _check(lib().vss_get_info(self._h, ctypes.byref(info)), self._h)
+        self.mask_h, self.mask_w, self.n_layers = info.mask_h, info.mask_w, info.n_layers
+        self.device_bytes = info.device_bytes
+        self.dtype, self.max_batch = dtype, max_batch
+        self._pending = []
+
+    # -- lifecycle --------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vss_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- the seam -----------------------------------------------------------
+    def segment_frames(self, frames: np.ndarray):
+        """frames [N,H,W,3|4] uint8 -> (masks float32 [N, maskH*maskW], maskW, maskH)."""
+        f = _as_frames(frames)
+        n, hh, ww, c = f.shape
+        out = np.empty((n, self.mask_h * self.mask_w), np.float32)
+        _check(lib().vss_segment(self._h, f.ctypes.data, n, hh, ww, c, ww * c, out.ctypes.data, VSS_OUT_MODEL),
+               self._h)
+        return out, self.mask_w, self.mask_h
+
+    def segment_frame(self, frame: np.ndarray):
+        """One frame -> (alphaRaw float32[maskH*maskW], maskW, maskH)  (frameProcessorTest.ts:95-97)."""
+        masks, mw, mh = self.segment_frames(frame)
+        return masks[0], mw, mh
+
+    def segment_frames_async(self, frames: np.ndarray, callback):
+        """Returns at once; callback(masks, maskW, maskH, status) fires when done."""
+        f = _as_frames(frames)
+        n, hh, ww, c = f.shape
+        out = np.empty((n, self.mask_h * self.mask_w), np.float32)
+
+        def _done(_user, status, _out=out):
+            callback(_out, self.mask_w, self.mask_h, status)
+
+        cb = CALLBACK(_done)
+        self._pending.append((cb, f, out))
+        _check(lib().vss_segment_async(self._h, f.ctypes.data, n, hh, ww, c, ww * c, out.ctypes.data,
+                                       VSS_OUT_MODEL, cb, None), self._h)
+        return out
+
+    # -- device-resident path (bench, multi-GPU host) ----------------------
+    def segment_device(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int, frame_stride: int,
+                       masks_ptr: int, stream: int = 0):
+        _check(lib().vss_segment_device(self._h, frames_ptr, n, h, w, c, row_stride, frame_stride, masks_ptr,
+                                        stream or None), self._h)
+
+    def preprocess_device(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int,
+                          frame_stride: int, out_ptr: int, stream: int = 0):
+        _check(lib().vss_preprocess_device(self._h, frames_ptr, n, h, w, c, row_stride, frame_stride, out_ptr,
+                                           stream or None), self._h)
+
+    def synchronize(self):
+        _check(lib().vss_synchronize(self._h), self._h)
+        self._pending.clear()
+
+    def set_option(self, option: int, value: int):
+        _check(lib().vss_set_option(self._h, option, value), self._h)
+
+    # -- introspection -----------------------------------------------------
+    def layer_shape(self, layer: int):
+        c, h, w = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().vss_layer_shape(self._h, layer, ctypes.byref(c), ctypes.byref(h), ctypes.byref(w)), self._h)
+        return c.value, h.value, w.value
+
+    def read_layer(self, layer: int, n: int) -> np.ndarray:
+        """Layer output of the latest forward as NCHW float32 (oracle layout)."""
+        c, h, w = self.layer_shape(layer)
+        out = np.empty((n, h, w, c), np.float32)
+        _check(lib().vss_read_layer(self._h, layer, n, out.ctypes.data), self._h)
+        return out.transpose(0, 3, 1, 2).copy()
+
+    def profile_read(self):
+        """(mean ms per layer over profiled forwards, count)."""
+        arr = (ctypes.c_double * self.n_layers)()
+        cnt = ctypes.c_int()
+        _check(lib().vss_profile_read(self._h, arr, self.n_layers, ctypes.byref(cnt)), self._h)
+        return list(arr), cnt.value
+
+
+def version() -> int:
+    return lib().vss_version()

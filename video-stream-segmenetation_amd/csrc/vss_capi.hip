@@ -1,0 +1,703 @@
+// vss_capi.hip — the C ABI (include/vss.h) over the gfx950 kernels.
+//
+// One handle = one GPU + one private HIP stream, mirroring one ORT
+// InferenceSession (/root/reference/client/src/core/model.ts:12-29).  The
+// handle parses the weights blob's layer table once, plans per-layer tiles for
+// its model resolution, keeps every activation NHWC f32 in HBM for max_batch
+// frames, and replays one captured hipGraph per (shape, buffers) key.
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/vss.h"
+#include "vss_kernels.h"
+
+namespace vss {
+using BlockFn = void (*)(BlockParams);
+BlockFn block_kernel(int mode, int stride, int prec);
+void (*stem_kernel16())(StemParams);
+void (*head_kernel())(HeadParams);
+void (*prep_kernel())(PrepParams);
+}  // namespace vss
+
+using namespace vss;
+
+namespace {
+
+constexpr uint32_t kMagic = 0x57535356u, kNone = 0xFFFFFFFFu;
+enum { K_STEM = 1, K_IR = 2, K_DEC = 3, K_HEAD = 4 };
+enum { F_EXPAND = 1, F_RESIDUAL = 2 };
+enum { O_W1, O_B1, O_WDW, O_BDW, O_W2, O_B2, O_GAMMA, O_BETA };
+
+struct Rec {
+  uint32_t kind, cin, chid, cout, stride, flags, src, skip, off[8];
+};
+
+struct LayerPlan {
+  Rec rec{};
+  int C = 0, H = 0, W = 0;     // output shape
+  int inH = 0, inW = 0;        // shape of rec.src's output (x)
+  int mode = -1, stride = 1, chid = 0;
+  int TH = 0, TW = 0, tiles_x = 0, tiles_y = 0, grid_x = 0, grid_y = 0;
+  size_t lds = 0;
+  float* act = nullptr;        // [max_batch][H][W][C]
+  float* part = nullptr;       // DEC: [max_batch][tiles][2][C]
+  const float *b1 = nullptr, *b2 = nullptr, *wdwT = nullptr, *bdw = nullptr, *gamma = nullptr, *beta = nullptr;
+  const float *w1f = nullptr, *w2f = nullptr;
+  const void *w1h = nullptr, *w2h = nullptr;  // bf16 copies
+  const float *stem_w = nullptr, *stem_b = nullptr, *head_w = nullptr;
+  float head_b = 0.f;
+};
+
+using GraphKey = std::tuple<const void*, const void*, int, int, int, int, size_t, size_t>;
+
+thread_local std::string g_tls_error;
+
+}  // namespace
+
+struct vss_handle {
+  vss_config cfg{};
+  std::string weights_path;
+  std::string err;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::vector<Rec> recs;
+  std::vector<float> hdata;
+  float eps = 1e-5f;
+  std::vector<LayerPlan> L;
+  std::vector<void*> dev_allocs;
+  size_t dev_bytes = 0;
+  uint8_t* d_frames = nullptr;
+  float* d_masks = nullptr;
+  size_t frame_cap = 0;
+  uint8_t* h_frames = nullptr;  // pinned staging
+  float* h_masks = nullptr;
+  std::atomic<int> busy{0};
+  int use_graph = 1;
+  int profile = 0;
+  std::map<GraphKey, hipGraphExec_t> graphs;
+  // profiling: ring of event pairs per layer
+  static constexpr int kSlots = 32;
+  std::vector<hipEvent_t> ev;  // [slot][layer][2]
+  std::vector<int> slot_pending;
+  int prof_next = 0;
+  std::vector<double> prof_sum;
+  int prof_count = 0;
+  int last_n = 0;
+};
+
+namespace {
+
+int fail(vss_handle* h, int code, const std::string& msg) {
+  if (h) h->err = msg;
+  else g_tls_error = msg;
+  return code;
+}
+
+#define HIP_TRY(h, expr)                                                                  \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail((h), e_ == hipErrorOutOfMemory ? VSS_E_OOM : VSS_E_HIP,                \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                     \
+  } while (0)
+
+template <class T>
+int dalloc(vss_handle* h, T** p, size_t bytes) {
+  void* q = nullptr;
+  bytes = std::max<size_t>(bytes, 16);
+  hipError_t e = hipMalloc(&q, bytes);
+  if (e != hipSuccess) return fail(h, VSS_E_OOM, "hipMalloc(" + std::to_string(bytes) + ") failed");
+  h->dev_allocs.push_back(q);
+  h->dev_bytes += bytes;
+  *p = static_cast<T*>(q);
+  return VSS_OK;
+}
+
+uint16_t bf16_bits(float f) {  // pointwise weights are bf16-exact: truncation is exact
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+size_t block_lds_bytes(int mode, int stride, int TH, int TW, int cx, int cin, int cout) {
+  const int IH = stride == 2 ? 2 * TH + 1 : TH + 2, IW = stride == 2 ? 2 * TW + 1 : TW + 2;
+  const int P_in_pad = (IH * IW + 15) & ~15, P_out = TH * TW;
+  size_t f = (size_t)P_in_pad * (cx + 4);
+  if (mode == MODE_IR_EXPAND) f += (size_t)P_in_pad * 16;
+  f += 2 * (size_t)P_out * 16;
+  if (mode == MODE_DEC) f += 2 * (size_t)cin + 8 * (size_t)cout;
+  return f * 4;
+}
+
+// Tile choice: the largest output tile that still gives >= 2 workgroups per
+// CU (256 CUs) at max_batch within 64 KiB of LDS; else the one with the most
+// workgroups.
+void choose_tile(LayerPlan& l, int N) {
+  static const int cand[][2] = {{8, 16}, {4, 16}, {8, 8}, {4, 8}, {2, 16}, {2, 8}, {1, 16}};
+  const int cx = l.mode == MODE_DEC ? (int)(l.rec.cin + l.rec.chid) : (int)l.rec.cin;
+  int best = -1;
+  long best_blocks = -1;
+  for (int i = 0; i < (int)(sizeof(cand) / sizeof(cand[0])); ++i) {
+    const int TH = cand[i][0], TW = cand[i][1];
+    const int pout = TH * TW;
+    if ((l.C / 16) * (pout / 16) > 4 * kMaxProjTiles) continue;
+    if (TW > ((l.W + 7) / 8) * 8 && TW > 8) continue;
+    const size_t lds = block_lds_bytes(l.mode, l.stride, TH, TW, cx, (int)l.rec.cin, l.C);
+    if (lds > 64 * 1024) continue;
+    const long blocks = (long)((l.H + TH - 1) / TH) * ((l.W + TW - 1) / TW) * N;
+    if (blocks >= 512) { best = i; break; }
+    if (blocks > best_blocks) { best_blocks = blocks; best = i; }
+  }
+  if (best < 0) best = (int)(sizeof(cand) / sizeof(cand[0])) - 1;
+  l.TH = cand[best][0];
+  l.TW = cand[best][1];
+  l.tiles_x = (l.W + l.TW - 1) / l.TW;
+  l.tiles_y = (l.H + l.TH - 1) / l.TH;
+  l.lds = block_lds_bytes(l.mode, l.stride, l.TH, l.TW, cx, (int)l.rec.cin, l.C);
+}
+
+int load_weights(vss_handle* h) {
+  std::ifstream f(h->weights_path, std::ios::binary);
+  if (!f) return fail(h, VSS_E_IO, "cannot open weights blob '" + h->weights_path + "'");
+  std::vector<char> blob((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  if (blob.size() < 32) return fail(h, VSS_E_IO, "weights blob too short");
+  uint32_t hd[8];
+  std::memcpy(hd, blob.data(), 32);
+  if (hd[0] != kMagic || hd[1] != 1) return fail(h, VSS_E_IO, "bad weights blob magic/version");
+  const uint32_t nl = hd[2], nf = hd[3];
+  std::memcpy(&h->eps, &hd[4], 4);
+  if (32 + 64ull * nl + 4ull * nf > blob.size()) return fail(h, VSS_E_IO, "weights blob truncated");
+  h->recs.resize(nl);
+  std::memcpy(h->recs.data(), blob.data() + 32, 64ull * nl);
+  h->hdata.resize(nf);
+  std::memcpy(h->hdata.data(), blob.data() + 32 + 64ull * nl, 4ull * nf);
+  for (const Rec& r : h->recs)
+    for (uint32_t o : r.off)
+      if (o != kNone && o >= nf) return fail(h, VSS_E_IO, "weights offset out of range");
+  return VSS_OK;
+}
+
+int plan(vss_handle* h) {
+  const int Hm = h->cfg.model_h, Wm = h->cfg.model_w, N = h->cfg.max_batch;
+  const int nl = (int)h->recs.size();
+  h->L.assign(nl, LayerPlan{});
+  for (int i = 0; i < nl; ++i) {
+    LayerPlan& l = h->L[i];
+    const Rec& r = h->recs[i];
+    l.rec = r;
+    l.C = (int)r.cout;
+    auto bad = [&](const char* why) {
+      return fail(h, VSS_E_UNSUPPORTED, "layer " + std::to_string(i) + ": " + why);
+    };
+    if (r.kind != K_STEM && (r.src >= (uint32_t)i)) return bad("src must precede layer");
+    if (r.kind == K_STEM) {
+      if (r.cin != 3 || r.cout != 16 || r.stride != 2) return bad("stem must be 3->16 stride 2");
+      l.H = Hm / 2; l.W = Wm / 2;
+    } else if (r.kind == K_IR) {
+      const LayerPlan& s = h->L[r.src];
+      if ((int)r.cin != s.C) return bad("ir cin != src channels");
+      l.inH = s.H; l.inW = s.W;
+      l.stride = (int)r.stride;
+      if (l.stride != 1 && l.stride != 2) return bad("stride must be 1 or 2");
+      l.H = l.stride == 2 ? (s.H + 1) / 2 : s.H;
+      l.W = l.stride == 2 ? (s.W + 1) / 2 : s.W;
+      l.mode = (r.flags & F_EXPAND) ? MODE_IR_EXPAND : MODE_IR_DIRECT;
+      l.chid = (r.flags & F_EXPAND) ? (int)r.chid : (int)r.cin;
+      if (r.cin % 16 || l.chid % 16 || r.cout % 16) return bad("channels must be multiples of 16");
+      if ((r.flags & F_EXPAND) && r.cin > 64) return bad("expand cin > 64");
+      if (l.mode == MODE_IR_DIRECT && l.stride != 1) return bad("direct ir needs stride 1");
+      if ((r.flags & F_RESIDUAL) && (l.stride != 1 || r.cin != r.cout)) return bad("residual shape");
+    } else if (r.kind == K_DEC) {
+      const LayerPlan& s = h->L[r.src];
+      const LayerPlan& k = h->L[r.skip];
+      if (r.skip >= (uint32_t)i) return bad("skip must precede layer");
+      if ((int)r.cin != s.C || (int)r.chid != k.C) return bad("dec channels");
+      if (2 * s.H != k.H || 2 * s.W != k.W) return bad("dec src must be half the skip res");
+      l.inH = s.H; l.inW = s.W;
+      l.H = k.H; l.W = k.W;
+      l.mode = MODE_DEC;
+      l.chid = (int)(r.cin + r.chid);
+      if (r.cin % 16 || r.chid % 16 || r.cout % 16) return bad("channels must be multiples of 16");
+      if (r.off[O_GAMMA] == kNone || r.off[O_BETA] == kNone) return bad("dec needs gamma/beta");
+    } else if (r.kind == K_HEAD) {
+      const LayerPlan& s = h->L[r.src];
+      if (s.rec.kind != K_DEC) return bad("head src must be a dec layer");
+      if (2 * s.H != Hm || 2 * s.W != Wm) return bad("head src must be half model res");
+      if (r.cin > 64 || r.cin % 4 || (int)r.cin != s.C || r.cout != 1) return bad("head shape");
+      l.inH = s.H; l.inW = s.W;
+      l.H = Hm; l.W = Wm; l.C = 1;
+    } else {
+      return bad("unknown kind");
+    }
+    if (l.mode >= 0) choose_tile(l, N);
+  }
+  if (nl == 0 || h->recs.back().kind != K_HEAD) return fail(h, VSS_E_UNSUPPORTED, "last layer must be the head");
+  return VSS_OK;
+}
+
+int upload(vss_handle* h) {
+  const int N = h->cfg.max_batch;
+  float* d_data = nullptr;
+  int rc = dalloc(h, &d_data, h->hdata.size() * 4);
+  if (rc) return rc;
+  HIP_TRY(h, hipMemcpy(d_data, h->hdata.data(), h->hdata.size() * 4, hipMemcpyHostToDevice));
+  auto dp = [&](uint32_t off) -> const float* { return off == kNone ? nullptr : d_data + off; };
+  // bf16 copies of pointwise weights and [9][C] depthwise weights
+  std::vector<uint16_t> hb;
+  std::vector<float> hw;
+  std::vector<std::pair<size_t, size_t>> boffs(h->L.size(), {SIZE_MAX, SIZE_MAX}), woffs(h->L.size(), {SIZE_MAX, 0});
+  for (size_t i = 0; i < h->L.size(); ++i) {
+    const LayerPlan& l = h->L[i];
+    const Rec& r = l.rec;
+    auto add_b = [&](uint32_t off, size_t cnt) {
+      size_t at = hb.size();
+      for (size_t k = 0; k < cnt; ++k) hb.push_back(bf16_bits(h->hdata[off + k]));
+      while (hb.size() % 8) hb.push_back(0);
+      return at;
+    };
+    if (r.kind == K_IR || r.kind == K_DEC) {
+      if (r.kind == K_IR && (r.flags & F_EXPAND)) boffs[i].first = add_b(r.off[O_W1], (size_t)r.chid * r.cin);
+      boffs[i].second = add_b(r.off[O_W2], (size_t)r.cout * l.chid);
+      size_t at = hw.size();
+      for (int t = 0; t < 9; ++t)
+        for (int c = 0; c < l.chid; ++c) hw.push_back(h->hdata[r.off[O_WDW] + (size_t)c * 9 + t]);
+      woffs[i].first = at;
+    }
+  }
+  uint16_t* d_b = nullptr;
+  float* d_w = nullptr;
+  if ((rc = dalloc(h, &d_b, hb.size() * 2))) return rc;
+  if ((rc = dalloc(h, &d_w, hw.size() * 4))) return rc;
+  if (!hb.empty()) HIP_TRY(h, hipMemcpy(d_b, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+  if (!hw.empty()) HIP_TRY(h, hipMemcpy(d_w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+  for (size_t i = 0; i < h->L.size(); ++i) {
+    LayerPlan& l = h->L[i];
+    const Rec& r = l.rec;
+    if ((rc = dalloc(h, &l.act, (size_t)N * l.H * l.W * l.C * 4))) return rc;
+    if (r.kind == K_STEM) {
+      l.stem_w = dp(r.off[O_W1]);
+      l.stem_b = dp(r.off[O_B1]);
+    } else if (r.kind == K_IR || r.kind == K_DEC) {
+      l.w1f = dp(r.off[O_W1]);
+      l.b1 = dp(r.off[O_B1]);
+      l.bdw = dp(r.off[O_BDW]);
+      l.w2f = dp(r.off[O_W2]);
+      l.b2 = dp(r.off[O_B2]);
+      if (boffs[i].first != SIZE_MAX) l.w1h = d_b + boffs[i].first;
+      l.w2h = d_b + boffs[i].second;
+      l.wdwT = d_w + woffs[i].first;
+      if (r.kind == K_DEC) {
+        l.gamma = dp(r.off[O_GAMMA]);
+        l.beta = dp(r.off[O_BETA]);
+        if ((rc = dalloc(h, &l.part, (size_t)N * l.tiles_x * l.tiles_y * 2 * l.C * 4))) return rc;
+      }
+    } else if (r.kind == K_HEAD) {
+      l.head_w = dp(r.off[O_W2]);
+      l.head_b = h->hdata[r.off[O_B2]];
+    }
+  }
+  return VSS_OK;
+}
+
+int check_frames(vss_handle* h, int n, int fh, int fw, int fc, size_t rs, size_t fs) {
+  if (n < 1 || n > h->cfg.max_batch) return fail(h, VSS_E_INVALID_ARG, "n must be in [1, max_batch]");
+  if (fh < 1 || fw < 1) return fail(h, VSS_E_INVALID_ARG, "bad frame size");
+  if (fc != 3 && fc != 4) return fail(h, VSS_E_INVALID_ARG, "channels must be 3 or 4");
+  if (rs < (size_t)fw * fc) return fail(h, VSS_E_INVALID_ARG, "row_stride < width*channels");
+  if (fs < rs * (size_t)fh) return fail(h, VSS_E_INVALID_ARG, "frame_stride < height*row_stride");
+  return VSS_OK;
+}
+
+// Enqueue the whole forward on stream s (no sync, no alloc: graph-capturable).
+int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs,
+                    size_t fs, float* masks, hipStream_t s, int prof_slot) {
+  const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
+  const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
+  const int nl = (int)h->L.size();
+  for (int i = 0; i < nl; ++i) {
+    LayerPlan& l = h->L[i];
+    const Rec& r = l.rec;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (prof_slot >= 0) {
+      e0 = h->ev[((size_t)prof_slot * nl + i) * 2];
+      e1 = h->ev[((size_t)prof_slot * nl + i) * 2 + 1];
+    }
+    auto go = [&](auto fn, dim3 grid, size_t lds, auto prm) {
+      if (prof_slot >= 0)
+        hipExtLaunchKernelGGL(fn, grid, dim3(kThreads), (uint32_t)lds, s, e0, e1, 0, prm);
+      else
+        hipLaunchKernelGGL(fn, grid, dim3(kThreads), lds, s, prm);
+    };
+    if (r.kind == K_STEM) {
+      StemParams p{};
+      p.frames = frames; p.row_stride = (long)rs; p.frame_stride = (long)fs;
+      p.fh = fh; p.fw = fw; p.fc = fc; p.Hm = Hm; p.Wm = Wm;
+      p.ry = (float)((double)fh / (double)Hm);
+      p.rx = (float)((double)fw / (double)Wm);
+      p.w = l.stem_w; p.b = l.stem_b; p.y = l.act;
+      p.Ho = l.H; p.Wo = l.W; p.cout = l.C;
+      go(stem_kernel16(), dim3((l.W + 31) / 32, (l.H + 7) / 8, n), 0, p);
+    } else if (r.kind == K_IR || r.kind == K_DEC) {
+      const LayerPlan& src = h->L[r.src];
+      BlockParams p{};
+      p.x = src.act;
+      p.y = l.act;
+      p.w1 = prec == PREC_F32 ? (const void*)l.w1f : l.w1h;
+      p.b1 = l.b1;
+      p.wdw = l.wdwT;
+      p.bdw = l.bdw;
+      p.w2 = prec == PREC_F32 ? (const void*)l.w2f : l.w2h;
+      p.b2 = l.b2;
+      p.eps = h->eps;
+      p.N = n; p.H = l.inH; p.W = l.inW; p.Ho = l.H; p.Wo = l.W;
+      p.cin = (int)r.cin; p.cout = l.C; p.chid = l.chid; p.stride = l.stride;
+      p.TH = l.TH; p.TW = l.TW; p.tiles_x = l.tiles_x; p.tiles_y = l.tiles_y;
+      if (r.kind == K_IR) {
+        p.relu6_dw = 1;
+        p.residual = (r.flags & F_RESIDUAL) ? 1 : 0;
+      } else {
+        const LayerPlan& sk = h->L[r.skip];
+        p.skip = sk.act;
+        p.cskip = (int)r.chid;
+        p.relu6_dw = 0;
+        p.out_part = l.part;
+        p.norm_in = src.rec.kind == K_DEC ? 1 : 0;
+        if (p.norm_in) {
+          p.in_part = src.part;
+          p.in_gamma = src.gamma;
+          p.in_beta = src.beta;
+          p.in_tiles = src.tiles_x * src.tiles_y;
+          p.in_hw = src.H * src.W;
+        }
+      }
+      go(block_kernel(l.mode, l.stride, prec), dim3(l.tiles_x, l.tiles_y, n), l.lds, p);
+    } else if (r.kind == K_HEAD) {
+      const LayerPlan& src = h->L[r.src];
+      HeadParams p{};
+      p.x = src.act; p.in_part = src.part; p.gamma = src.gamma; p.beta = src.beta;
+      p.in_tiles = src.tiles_x * src.tiles_y; p.eps = h->eps;
+      p.w = l.head_w; p.b = l.head_b; p.mask = masks;
+      p.N = n; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
+      go(head_kernel(), dim3((Wm + 63) / 64, (Hm + 15) / 16, n), 0, p);
+    }
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+  return VSS_OK;
+}
+
+int harvest_slot(vss_handle* h, int slot) {
+  const int nl = (int)h->L.size();
+  for (int i = 0; i < nl; ++i) {
+    float ms = 0.f;
+    HIP_TRY(h, hipEventSynchronize(h->ev[((size_t)slot * nl + i) * 2 + 1]));
+    HIP_TRY(h, hipEventElapsedTime(&ms, h->ev[((size_t)slot * nl + i) * 2], h->ev[((size_t)slot * nl + i) * 2 + 1]));
+    h->prof_sum[i] += ms;
+  }
+  h->prof_count++;
+  h->slot_pending[slot] = 0;
+  return VSS_OK;
+}
+
+int forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, size_t fs,
+            float* masks, hipStream_t s) {
+  h->last_n = n;
+  if (h->profile) {
+    const int slot = h->prof_next;
+    h->prof_next = (h->prof_next + 1) % vss_handle::kSlots;
+    if (h->slot_pending[slot]) {
+      int rc = harvest_slot(h, slot);
+      if (rc) return rc;
+    }
+    int rc = enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, s, slot);
+    if (!rc) h->slot_pending[slot] = 1;
+    return rc;
+  }
+  if (!h->use_graph) return enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, s, -1);
+  GraphKey key{frames, masks, n, fh, fw, fc, rs, fs};
+  auto it = h->graphs.find(key);
+  if (it == h->graphs.end()) {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    HIP_TRY(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+    int rc = enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, h->stream, -1);
+    hipError_t e = hipStreamEndCapture(h->stream, &g);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+    if (h->graphs.size() >= 16) {  // bound the cache
+      (void)hipGraphExecDestroy(h->graphs.begin()->second);
+      h->graphs.erase(h->graphs.begin());
+    }
+    it = h->graphs.emplace(key, ge).first;
+  }
+  HIP_TRY(h, hipGraphLaunch(it->second, s));
+  return VSS_OK;
+}
+
+struct Busy {
+  vss_handle* h;
+  bool ok;
+  explicit Busy(vss_handle* hh) : h(hh) {
+    int z = 0;
+    ok = h->busy.compare_exchange_strong(z, 1);
+  }
+  void release() { if (ok) { h->busy.store(0); ok = false; } }
+  ~Busy() { release(); }
+};
+
+int stage_in(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, float* masks_out,
+             int out_mode) {
+  if (!frames || !masks_out) return fail(h, VSS_E_INVALID_ARG, "null frames/masks_out");
+  if (out_mode != VSS_OUT_MODEL) return fail(h, VSS_E_UNSUPPORTED, "only VSS_OUT_MODEL masks are supported");
+  int rc = check_frames(h, n, fh, fw, fc, rs, rs * (size_t)fh);
+  if (rc) return rc;
+  const size_t bytes = (size_t)n * fh * rs;
+  if (bytes > h->frame_cap)
+    return fail(h, VSS_E_INVALID_ARG, "frames exceed the handle's staging capacity (max_frame_h/w)");
+  std::memcpy(h->h_frames, frames, bytes);
+  HIP_TRY(h, hipMemcpyAsync(h->d_frames, h->h_frames, bytes, hipMemcpyHostToDevice, h->stream));
+  rc = forward(h, h->d_frames, n, fh, fw, fc, rs, rs * (size_t)fh, h->d_masks, h->stream);
+  if (rc) return rc;
+  const size_t mbytes = (size_t)n * h->cfg.model_h * h->cfg.model_w * 4;
+  HIP_TRY(h, hipMemcpyAsync(h->h_masks, h->d_masks, mbytes, hipMemcpyDeviceToHost, h->stream));
+  return VSS_OK;
+}
+
+struct AsyncCtx {
+  vss_handle* h;
+  float* out;
+  size_t bytes;
+  vss_callback cb;
+  void* user;
+};
+
+void async_done(void* p) {
+  AsyncCtx* c = static_cast<AsyncCtx*>(p);
+  std::memcpy(c->out, c->h->h_masks, c->bytes);
+  c->h->busy.store(0);
+  if (c->cb) c->cb(c->user, VSS_OK);
+  delete c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vss_version(void) { return VSS_VERSION; }
+
+const char* vss_last_error(const vss_handle* h) { return h ? h->err.c_str() : g_tls_error.c_str(); }
+
+int vss_create(const vss_config* cfg, vss_handle** out) {
+  if (!cfg || !out) return fail(nullptr, VSS_E_INVALID_ARG, "null cfg/out");
+  *out = nullptr;
+  if (cfg->model_h <= 0 || cfg->model_w <= 0 || cfg->model_h % 16 || cfg->model_w % 16)
+    return fail(nullptr, VSS_E_INVALID_ARG, "model_h/model_w must be positive multiples of 16");
+  if (cfg->dtype != VSS_DTYPE_F32 && cfg->dtype != VSS_DTYPE_BF16X2)
+    return fail(nullptr, VSS_E_INVALID_ARG, "unknown dtype");
+  if (cfg->max_batch < 1 || cfg->max_frame_h < 1 || cfg->max_frame_w < 1)
+    return fail(nullptr, VSS_E_INVALID_ARG, "max_batch/max_frame_h/max_frame_w must be >= 1");
+  if (!cfg->weights_path) return fail(nullptr, VSS_E_INVALID_ARG, "weights_path is required");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(nullptr, VSS_E_HIP, "no HIP device available");
+  if (cfg->device_id < 0 || cfg->device_id >= ndev) return fail(nullptr, VSS_E_INVALID_ARG, "bad device_id");
+  vss_handle* h = new vss_handle();
+  h->cfg = *cfg;
+  h->weights_path = cfg->weights_path;
+  h->cfg.weights_path = nullptr;
+  h->device = cfg->device_id;
+  auto bail = [&](int rc) {
+    g_tls_error = h->err;
+    vss_destroy(h);
+    return rc;
+  };
+  if (hipSetDevice(h->device) != hipSuccess) return bail(fail(h, VSS_E_HIP, "hipSetDevice failed"));
+  int rc = load_weights(h);
+  if (!rc) rc = plan(h);
+  if (!rc) rc = upload(h);
+  if (rc) return bail(rc);
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(h, VSS_E_HIP, "hipStreamCreate failed"));
+  h->frame_cap = (size_t)cfg->max_batch * cfg->max_frame_h * cfg->max_frame_w * 4;
+  if ((rc = dalloc(h, &h->d_frames, h->frame_cap))) return bail(rc);
+  if ((rc = dalloc(h, &h->d_masks, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w * 4))) return bail(rc);
+  if (hipHostMalloc((void**)&h->h_frames, h->frame_cap, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&h->h_masks, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w * 4,
+                    hipHostMallocDefault) != hipSuccess)
+    return bail(fail(h, VSS_E_OOM, "hipHostMalloc staging failed"));
+  for (auto* fn : {block_kernel(MODE_IR_EXPAND, 1, PREC_F32), block_kernel(MODE_IR_EXPAND, 2, PREC_F32),
+                   block_kernel(MODE_IR_DIRECT, 1, PREC_F32), block_kernel(MODE_DEC, 1, PREC_F32),
+                   block_kernel(MODE_IR_EXPAND, 1, PREC_BF16X2), block_kernel(MODE_IR_EXPAND, 2, PREC_BF16X2),
+                   block_kernel(MODE_IR_DIRECT, 1, PREC_BF16X2), block_kernel(MODE_DEC, 1, PREC_BF16X2)})
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return bail(fail(h, VSS_E_HIP, "hipFuncSetAttribute failed"));
+  const int nl = (int)h->L.size();
+  h->ev.resize((size_t)vss_handle::kSlots * nl * 2);
+  for (auto& e : h->ev)
+    if (hipEventCreate(&e) != hipSuccess) return bail(fail(h, VSS_E_HIP, "hipEventCreate failed"));
+  h->slot_pending.assign(vss_handle::kSlots, 0);
+  h->prof_sum.assign(nl, 0.0);
+  *out = h;
+  return VSS_OK;
+}
+
+void vss_destroy(vss_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (void* p : h->dev_allocs) (void)hipFree(p);
+  if (h->h_frames) (void)hipHostFree(h->h_frames);
+  if (h->h_masks) (void)hipHostFree(h->h_masks);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int vss_get_info(const vss_handle* h, vss_info* info) {
+  if (!h || !info) return VSS_E_INVALID_ARG;
+  info->mask_h = h->cfg.model_h;
+  info->mask_w = h->cfg.model_w;
+  info->n_layers = (int)h->L.size();
+  info->dtype = h->cfg.dtype;
+  info->device_bytes = h->dev_bytes;
+  return VSS_OK;
+}
+
+int vss_segment(vss_handle* h, const uint8_t* frames, int n, int height, int width, int channels,
+                size_t row_stride, float* masks_out, int out_mode) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  Busy b(h);
+  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
+  HIP_TRY(h, hipSetDevice(h->device));
+  int rc = stage_in(h, frames, n, height, width, channels, row_stride, masks_out, out_mode);
+  if (rc) return rc;
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  std::memcpy(masks_out, h->h_masks, (size_t)n * h->cfg.model_h * h->cfg.model_w * 4);
+  return VSS_OK;
+}
+
+int vss_segment_async(vss_handle* h, const uint8_t* frames, int n, int height, int width, int channels,
+                      size_t row_stride, float* masks_out, int out_mode, vss_callback cb, void* user) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  Busy b(h);
+  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
+  HIP_TRY(h, hipSetDevice(h->device));
+  int rc = stage_in(h, frames, n, height, width, channels, row_stride, masks_out, out_mode);
+  if (rc) return rc;
+  AsyncCtx* c = new AsyncCtx{h, masks_out, (size_t)n * h->cfg.model_h * h->cfg.model_w * 4, cb, user};
+  hipError_t e = hipLaunchHostFunc(h->stream, async_done, c);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(h, VSS_E_HIP, std::string("hipLaunchHostFunc: ") + hipGetErrorString(e));
+  }
+  b.ok = false;  // released by async_done
+  return VSS_OK;
+}
+
+int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width, int channels,
+                       size_t row_stride, size_t frame_stride, float* d_masks, void* stream) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (!d_frames || !d_masks) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
+  Busy b(h);
+  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride);
+  if (rc) return rc;
+  HIP_TRY(h, hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  return forward(h, d_frames, n, height, width, channels, row_stride, frame_stride, d_masks, s);
+}
+
+int vss_preprocess_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width, int channels,
+                          size_t row_stride, size_t frame_stride, float* d_out, void* stream) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (!d_frames || !d_out) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride);
+  if (rc) return rc;
+  HIP_TRY(h, hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  PrepParams p{};
+  p.frames = d_frames; p.row_stride = (long)row_stride; p.frame_stride = (long)frame_stride;
+  p.fh = height; p.fw = width; p.fc = channels; p.Hm = h->cfg.model_h; p.Wm = h->cfg.model_w;
+  p.ry = (float)((double)height / (double)p.Hm);
+  p.rx = (float)((double)width / (double)p.Wm);
+  p.out = d_out; p.N = n;
+  const long total = (long)n * p.Hm * p.Wm;
+  const int grid = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(prep_kernel(), dim3(grid), dim3(256), 0, s, p);
+  HIP_TRY(h, hipGetLastError());
+  return VSS_OK;
+}
+
+int vss_synchronize(vss_handle* h) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return VSS_OK;
+}
+
+int vss_set_option(vss_handle* h, int option, int value) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (option == VSS_OPT_USE_GRAPH) h->use_graph = value ? 1 : 0;
+  else if (option == VSS_OPT_PROFILE) h->profile = value ? 1 : 0;
+  else return fail(h, VSS_E_INVALID_ARG, "unknown option");
+  return VSS_OK;
+}
+
+int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww) {
+  if (!h || layer < 0 || layer >= (int)h->L.size()) return VSS_E_INVALID_ARG;
+  if (c) *c = h->L[layer].C;
+  if (hh) *hh = h->L[layer].H;
+  if (ww) *ww = h->L[layer].W;
+  return VSS_OK;
+}
+
+int vss_read_layer(vss_handle* h, int layer, int n, float* host_out) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (layer < 0 || layer >= (int)h->L.size() || !host_out || n < 1 || n > h->cfg.max_batch)
+    return fail(h, VSS_E_INVALID_ARG, "bad layer/n/out");
+  const LayerPlan& l = h->L[layer];
+  if (l.rec.kind == K_HEAD) return fail(h, VSS_E_INVALID_ARG, "the head's output is the mask buffer");
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipDeviceSynchronize());
+  HIP_TRY(h, hipMemcpy(host_out, l.act, (size_t)n * l.H * l.W * l.C * 4, hipMemcpyDeviceToHost));
+  return VSS_OK;
+}
+
+int vss_profile_read(vss_handle* h, double* ms_per_layer, int cap, int* count) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  const int nl = (int)h->L.size();
+  if (!ms_per_layer || cap < nl) return fail(h, VSS_E_INVALID_ARG, "cap < n_layers");
+  HIP_TRY(h, hipSetDevice(h->device));
+  for (int s = 0; s < vss_handle::kSlots; ++s)
+    if (h->slot_pending[s]) {
+      int rc = harvest_slot(h, s);
+      if (rc) return rc;
+    }
+  for (int i = 0; i < nl; ++i) ms_per_layer[i] = h->prof_count ? h->prof_sum[i] / h->prof_count : 0.0;
+  if (count) *count = h->prof_count;
+  std::fill(h->prof_sum.begin(), h->prof_sum.end(), 0.0);
+  h->prof_count = 0;
+  return VSS_OK;
+}
+
+}  // extern "C"
