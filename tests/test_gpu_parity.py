@@ -185,7 +185,8 @@ def test_argument_errors(pkg, sess_bf, synthetic):
         sess_bf.segment_frames(f)  # > max_batch
     assert e.value.code == pkg.VSS_E_INVALID_ARG
     with pytest.raises(pkg.VssError):
-        sess_bf.segment_frames(np.zeros((1, 2000, 2000, 3), np.uint8))  # > staging capacity
+        # > staging capacity (max_batch * 1080 * 1920 * 4 bytes)
+        sess_bf.segment_frames(np.zeros((1, 6000, 4000, 3), np.uint8))
     with pytest.raises(pkg.VssError):
         sess_bf.segment_frames(np.zeros((1, 10, 10, 2), np.uint8))
     # still usable after errors

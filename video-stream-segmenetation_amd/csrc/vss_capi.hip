@@ -23,10 +23,8 @@
 #include "vss_kernels.h"
 
 namespace vss {
-using BlockFn = void (*)(BlockParams);
-BlockFn block_kernel(int mode, int stride, int prec);
 void (*stem_kernel16())(StemParams);
-void (*head_kernel())(HeadParams);
+void (*head_kernel16())(HeadParams);
 void (*prep_kernel())(PrepParams);
 }  // namespace vss
 
@@ -49,12 +47,14 @@ struct LayerPlan {
   int inH = 0, inW = 0;        // shape of rec.src's output (x)
   int mode = -1, stride = 1, chid = 0;
   int TH = 0, TW = 0, tiles_x = 0, tiles_y = 0, grid_x = 0, grid_y = 0;
+  int flags = 0;
   size_t lds = 0;
+  const BlockEntry* entry = nullptr;  // compiled shape (registry)
   float* act = nullptr;        // [max_batch][H][W][C]
   float* part = nullptr;       // DEC: [max_batch][tiles][2][C]
-  const float *b1 = nullptr, *b2 = nullptr, *wdwT = nullptr, *bdw = nullptr, *gamma = nullptr, *beta = nullptr;
-  const float *w1f = nullptr, *w2f = nullptr;
-  const void *w1h = nullptr, *w2h = nullptr;  // bf16 copies
+  const float* wimg = nullptr;  // LDS weight image (block_lds regions w1..b2)
+  int wimg_f4 = 0;
+  const float *gamma = nullptr, *beta = nullptr;
   const float *stem_w = nullptr, *stem_b = nullptr, *head_w = nullptr;
   float head_b = 0.f;
 };
@@ -131,41 +131,43 @@ uint16_t bf16_bits(float f) {  // pointwise weights are bf16-exact: truncation i
   return (uint16_t)(u >> 16);
 }
 
-size_t block_lds_bytes(int mode, int stride, int TH, int TW, int cx, int cin, int cout) {
-  const int IH = stride == 2 ? 2 * TH + 1 : TH + 2, IW = stride == 2 ? 2 * TW + 1 : TW + 2;
-  const int P_in_pad = (IH * IW + 15) & ~15, P_out = TH * TW;
-  size_t f = (size_t)P_in_pad * (cx + 4);
-  if (mode == MODE_IR_EXPAND) f += (size_t)P_in_pad * 16;
-  f += 2 * (size_t)P_out * 16;
-  if (mode == MODE_DEC) f += 2 * (size_t)cin + 8 * (size_t)cout;
-  return f * 4;
+size_t block_lds_bytes(const LayerPlan& l, int TH, int TW) {
+  const int cskip = l.mode == MODE_DEC ? (int)l.rec.chid : 0;
+  return (size_t)block_lds(l.mode, l.stride, TH, TW, (int)l.rec.cin, cskip, l.chid, l.C).total * 4;
 }
 
-// Tile choice: the largest output tile that still gives >= 2 workgroups per
-// CU (256 CUs) at max_batch within 64 KiB of LDS; else the one with the most
-// workgroups.
-void choose_tile(LayerPlan& l, int N) {
-  static const int cand[][2] = {{8, 16}, {4, 16}, {8, 8}, {4, 8}, {2, 16}, {2, 8}, {1, 16}};
-  const int cx = l.mode == MODE_DEC ? (int)(l.rec.cin + l.rec.chid) : (int)l.rec.cin;
-  int best = -1;
-  long best_blocks = -1;
-  for (int i = 0; i < (int)(sizeof(cand) / sizeof(cand[0])); ++i) {
-    const int TH = cand[i][0], TW = cand[i][1];
-    const int pout = TH * TW;
-    if ((l.C / 16) * (pout / 16) > 4 * kMaxProjTiles) continue;
-    if (TW > ((l.W + 7) / 8) * 8 && TW > 8) continue;
-    const size_t lds = block_lds_bytes(l.mode, l.stride, TH, TW, cx, (int)l.rec.cin, l.C);
-    if (lds > 64 * 1024) continue;
-    const long blocks = (long)((l.H + TH - 1) / TH) * ((l.W + TW - 1) / TW) * N;
-    if (blocks >= 512) { best = i; break; }
-    if (blocks > best_blocks) { best_blocks = blocks; best = i; }
+// Tile choice among the compiled shapes for this layer (csrc/vss_registry.inc):
+// the largest tile that still gives >= 2 workgroups per CU (256 CUs) at
+// max_batch, preferring <= 64 KiB of LDS; otherwise the most workgroups.
+int choose_tile(vss_handle* h, LayerPlan& l, int N) {
+  int count = 0;
+  const BlockEntry* reg = block_registry(&count);
+  const int cskip = l.mode == MODE_DEC ? (int)l.rec.chid : 0;
+  const BlockEntry* best = nullptr;
+  long best_score = -1;
+  for (int i = 0; i < count; ++i) {
+    const BlockEntry& e = reg[i];
+    if (e.mode != l.mode || e.stride != l.stride || e.cin != (int)l.rec.cin || e.cskip != cskip ||
+        e.chid != l.chid || e.cout != l.C || e.flags != l.flags)
+      continue;
+    const long blocks = (long)((l.H + e.TH - 1) / e.TH) * ((l.W + e.TW - 1) / e.TW) * N;
+    const size_t lds = block_lds_bytes(l, e.TH, e.TW);
+    // score: enough blocks first, then bigger tiles, then less LDS
+    long score = (blocks >= 512 ? 1L << 40 : blocks << 20) + (long)e.TH * e.TW * 1024 - (long)(lds / 1024);
+    if (blocks >= 512 && lds > 64 * 1024) score -= 1L << 39;
+    if (score > best_score) { best_score = score; best = &e; }
   }
-  if (best < 0) best = (int)(sizeof(cand) / sizeof(cand[0])) - 1;
-  l.TH = cand[best][0];
-  l.TW = cand[best][1];
+  if (!best)
+    return fail(h, VSS_E_UNSUPPORTED,
+                "no compiled kernel for this layer shape (regenerate csrc/vss_registry.inc with "
+                "tools/gen_registry.py and rebuild)");
+  l.entry = best;
+  l.TH = best->TH;
+  l.TW = best->TW;
   l.tiles_x = (l.W + l.TW - 1) / l.TW;
   l.tiles_y = (l.H + l.TH - 1) / l.TH;
-  l.lds = block_lds_bytes(l.mode, l.stride, l.TH, l.TW, cx, (int)l.rec.cin, l.C);
+  l.lds = block_lds_bytes(l, l.TH, l.TW);
+  return VSS_OK;
 }
 
 int load_weights(vss_handle* h) {
@@ -235,13 +237,18 @@ int plan(vss_handle* h) {
       const LayerPlan& s = h->L[r.src];
       if (s.rec.kind != K_DEC) return bad("head src must be a dec layer");
       if (2 * s.H != Hm || 2 * s.W != Wm) return bad("head src must be half model res");
-      if (r.cin > 64 || r.cin % 4 || (int)r.cin != s.C || r.cout != 1) return bad("head shape");
+      if (r.cin != 16 || (int)r.cin != s.C || r.cout != 1) return bad("head must be 16 -> 1");
       l.inH = s.H; l.inW = s.W;
       l.H = Hm; l.W = Wm; l.C = 1;
     } else {
       return bad("unknown kind");
     }
-    if (l.mode >= 0) choose_tile(l, N);
+    if (r.kind == K_IR) l.flags = (r.flags & F_RESIDUAL) ? 2 : 0;
+    if (r.kind == K_DEC) l.flags = h->L[r.src].rec.kind == K_DEC ? 1 : 0;
+    if (l.mode >= 0) {
+      int rc = choose_tile(h, l, N);
+      if (rc) return rc;
+    }
   }
   if (nl == 0 || h->recs.back().kind != K_HEAD) return fail(h, VSS_E_UNSUPPORTED, "last layer must be the head");
   return VSS_OK;
@@ -254,34 +261,52 @@ int upload(vss_handle* h) {
   if (rc) return rc;
   HIP_TRY(h, hipMemcpy(d_data, h->hdata.data(), h->hdata.size() * 4, hipMemcpyHostToDevice));
   auto dp = [&](uint32_t off) -> const float* { return off == kNone ? nullptr : d_data + off; };
-  // bf16 copies of pointwise weights and [9][C] depthwise weights
-  std::vector<uint16_t> hb;
-  std::vector<float> hw;
-  std::vector<std::pair<size_t, size_t>> boffs(h->L.size(), {SIZE_MAX, SIZE_MAX}), woffs(h->L.size(), {SIZE_MAX, 0});
+  // Per-layer LDS weight images: the exact bytes of block_lds regions w1..b2
+  // (pointwise weights as bf16 rows padded to LD1/LD2, dw weights [9][C],
+  // biases), so the kernel prologue is one flat 16-B copy.
+  std::vector<float> img;
+  std::vector<size_t> img_off(h->L.size(), 0), img_len(h->L.size(), 0);
   for (size_t i = 0; i < h->L.size(); ++i) {
     const LayerPlan& l = h->L[i];
     const Rec& r = l.rec;
-    auto add_b = [&](uint32_t off, size_t cnt) {
-      size_t at = hb.size();
-      for (size_t k = 0; k < cnt; ++k) hb.push_back(bf16_bits(h->hdata[off + k]));
-      while (hb.size() % 8) hb.push_back(0);
-      return at;
+    if (r.kind != K_IR && r.kind != K_DEC) continue;
+    // the kernels keep pointwise weights as bf16: require bf16-exact values
+    auto exact = [&](uint32_t off, size_t cnt) {
+      for (size_t k = 0; k < cnt; ++k) {
+        uint32_t u;
+        std::memcpy(&u, &h->hdata[off + k], 4);
+        if (u & 0xFFFFu) return false;
+      }
+      return true;
     };
-    if (r.kind == K_IR || r.kind == K_DEC) {
-      if (r.kind == K_IR && (r.flags & F_EXPAND)) boffs[i].first = add_b(r.off[O_W1], (size_t)r.chid * r.cin);
-      boffs[i].second = add_b(r.off[O_W2], (size_t)r.cout * l.chid);
-      size_t at = hw.size();
-      for (int t = 0; t < 9; ++t)
-        for (int c = 0; c < l.chid; ++c) hw.push_back(h->hdata[r.off[O_WDW] + (size_t)c * 9 + t]);
-      woffs[i].first = at;
+    const bool expand = l.mode == MODE_IR_EXPAND;
+    if ((expand && !exact(r.off[O_W1], (size_t)r.chid * r.cin)) || !exact(r.off[O_W2], (size_t)r.cout * l.chid))
+      return fail(h, VSS_E_UNSUPPORTED, "layer " + std::to_string(i) + ": pointwise weights must be bf16-exact");
+    const int cskip = l.mode == MODE_DEC ? (int)r.chid : 0;
+    const BlockLds B = block_lds(l.mode, l.stride, 1, 16, (int)r.cin, cskip, l.chid, l.C);
+    const size_t base = img.size(), span = (size_t)(B.lr - B.w1);
+    img.resize(base + span, 0.f);
+    float* im = img.data() + base;
+    auto put_bf16 = [&](int region, uint32_t off, int rows, int k, int ld) {
+      uint16_t* d = reinterpret_cast<uint16_t*>(im + (region - B.w1));
+      for (int a = 0; a < rows; ++a)
+        for (int b = 0; b < k; ++b) d[(size_t)a * ld + b] = bf16_bits(h->hdata[off + (size_t)a * k + b]);
+    };
+    if (expand) {
+      put_bf16(B.w1, r.off[O_W1], l.chid, (int)r.cin, B.LD1);
+      for (int c = 0; c < l.chid; ++c) im[B.b1 - B.w1 + c] = h->hdata[r.off[O_B1] + c];
     }
+    put_bf16(B.w2, r.off[O_W2], l.C, l.chid, B.LD2);
+    for (int t = 0; t < 9; ++t)
+      for (int c = 0; c < l.chid; ++c) im[B.wdw - B.w1 + t * l.chid + c] = h->hdata[r.off[O_WDW] + (size_t)c * 9 + t];
+    for (int c = 0; c < l.chid; ++c) im[B.bdw - B.w1 + c] = h->hdata[r.off[O_BDW] + c];
+    for (int c = 0; c < l.C; ++c) im[B.b2 - B.w1 + c] = h->hdata[r.off[O_B2] + c];
+    img_off[i] = base;
+    img_len[i] = span;
   }
-  uint16_t* d_b = nullptr;
-  float* d_w = nullptr;
-  if ((rc = dalloc(h, &d_b, hb.size() * 2))) return rc;
-  if ((rc = dalloc(h, &d_w, hw.size() * 4))) return rc;
-  if (!hb.empty()) HIP_TRY(h, hipMemcpy(d_b, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
-  if (!hw.empty()) HIP_TRY(h, hipMemcpy(d_w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+  float* d_img = nullptr;
+  if ((rc = dalloc(h, &d_img, img.size() * 4))) return rc;
+  if (!img.empty()) HIP_TRY(h, hipMemcpy(d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
   for (size_t i = 0; i < h->L.size(); ++i) {
     LayerPlan& l = h->L[i];
     const Rec& r = l.rec;
@@ -290,14 +315,8 @@ int upload(vss_handle* h) {
       l.stem_w = dp(r.off[O_W1]);
       l.stem_b = dp(r.off[O_B1]);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
-      l.w1f = dp(r.off[O_W1]);
-      l.b1 = dp(r.off[O_B1]);
-      l.bdw = dp(r.off[O_BDW]);
-      l.w2f = dp(r.off[O_W2]);
-      l.b2 = dp(r.off[O_B2]);
-      if (boffs[i].first != SIZE_MAX) l.w1h = d_b + boffs[i].first;
-      l.w2h = d_b + boffs[i].second;
-      l.wdwT = d_w + woffs[i].first;
+      l.wimg = d_img + img_off[i];
+      l.wimg_f4 = (int)(img_len[i] / 4);
       if (r.kind == K_DEC) {
         l.gamma = dp(r.off[O_GAMMA]);
         l.beta = dp(r.off[O_BETA]);
@@ -352,14 +371,9 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
     } else if (r.kind == K_IR || r.kind == K_DEC) {
       const LayerPlan& src = h->L[r.src];
       BlockParams p{};
+      p.wimg = l.wimg;
       p.x = src.act;
       p.y = l.act;
-      p.w1 = prec == PREC_F32 ? (const void*)l.w1f : l.w1h;
-      p.b1 = l.b1;
-      p.wdw = l.wdwT;
-      p.bdw = l.bdw;
-      p.w2 = prec == PREC_F32 ? (const void*)l.w2f : l.w2h;
-      p.b2 = l.b2;
       p.eps = h->eps;
       p.N = n; p.H = l.inH; p.W = l.inW; p.Ho = l.H; p.Wo = l.W;
       p.cin = (int)r.cin; p.cout = l.C; p.chid = l.chid; p.stride = l.stride;
@@ -382,7 +396,7 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
           p.in_hw = src.H * src.W;
         }
       }
-      go(block_kernel(l.mode, l.stride, prec), dim3(l.tiles_x, l.tiles_y, n), l.lds, p);
+      go(l.entry->fn[prec == PREC_F32 ? 0 : 1], dim3(l.tiles_x, l.tiles_y, n), l.lds, p);
     } else if (r.kind == K_HEAD) {
       const LayerPlan& src = h->L[r.src];
       HeadParams p{};
@@ -390,7 +404,7 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       p.in_tiles = src.tiles_x * src.tiles_y; p.eps = h->eps;
       p.w = l.head_w; p.b = l.head_b; p.mask = masks;
       p.N = n; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
-      go(head_kernel(), dim3((Wm + 63) / 64, (Hm + 15) / 16, n), 0, p);
+      go(head_kernel16(), dim3((Wm + 63) / 64, (Hm + 15) / 16, n), 0, p);
     }
   }
   hipError_t e = hipGetLastError();
@@ -543,12 +557,11 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
       hipHostMalloc((void**)&h->h_masks, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w * 4,
                     hipHostMallocDefault) != hipSuccess)
     return bail(fail(h, VSS_E_OOM, "hipHostMalloc staging failed"));
-  for (auto* fn : {block_kernel(MODE_IR_EXPAND, 1, PREC_F32), block_kernel(MODE_IR_EXPAND, 2, PREC_F32),
-                   block_kernel(MODE_IR_DIRECT, 1, PREC_F32), block_kernel(MODE_DEC, 1, PREC_F32),
-                   block_kernel(MODE_IR_EXPAND, 1, PREC_BF16X2), block_kernel(MODE_IR_EXPAND, 2, PREC_BF16X2),
-                   block_kernel(MODE_IR_DIRECT, 1, PREC_BF16X2), block_kernel(MODE_DEC, 1, PREC_BF16X2)})
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-      return bail(fail(h, VSS_E_HIP, "hipFuncSetAttribute failed"));
+  for (const LayerPlan& l : h->L)
+    if (l.entry)
+      for (BlockFn fn : l.entry->fn)
+        if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l.lds) != hipSuccess)
+          return bail(fail(h, VSS_E_HIP, "hipFuncSetAttribute(max dynamic LDS) failed"));
   const int nl = (int)h->L.size();
   h->ev.resize((size_t)vss_handle::kSlots * nl * 2);
   for (auto& e : h->ev)

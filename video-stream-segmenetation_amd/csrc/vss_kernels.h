@@ -18,13 +18,70 @@ enum Prec : int { PREC_F32 = 0, PREC_BF16X2 = 1, PREC_BF16 = 2 };
 enum BlockMode : int { MODE_IR_EXPAND = 0, MODE_IR_DIRECT = 1, MODE_DEC = 2 };
 
 constexpr int kThreads = 256;       // 4 wave64 per workgroup
-constexpr int kMaxProjTiles = 8;    // 16x16 project tiles per wave (cout/16 * pout/16 / 4)
+constexpr int kMaxAcc = 16;         // 16x16 project accumulators per wave
+
+__host__ __device__ constexpr int r4(int v) { return (v + 3) & ~3; }
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+// Geometry + LDS carve (floats) of one k_block instantiation.  Evaluated at
+// compile time in the kernel and at run time by the host planner, so the two
+// can never disagree.  Every region is a multiple of 4 floats (16-B aligned).
+struct BlockLds {
+  int IH, IW, P_in, P_in_pad, P_out, CX, XS, LD1, LD2, SR, SC;
+  int NCB, NPB, NCHUNK, PW, CS, NPBW, NACC;
+  int xt, w1, w2, wdw, bdw, b1, b2, lr, nrm, work, stt, total;
+  int slab_stride;  // floats per wave slab = P_out * (cout + 4)
+};
+
+__host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, int TW, int cin, int cskip, int chid,
+                                                 int cout) {
+  BlockLds L{};
+  L.IH = stride == 2 ? 2 * TH + 1 : TH + 2;
+  L.IW = stride == 2 ? 2 * TW + 1 : TW + 2;
+  L.P_in = L.IH * L.IW;
+  L.P_in_pad = (L.P_in + 15) & ~15;
+  L.P_out = TH * TW;
+  L.CX = mode == 2 /*MODE_DEC*/ ? cin + cskip : cin;
+  L.XS = L.CX + 4;
+  L.LD1 = cin + 8;   // bf16 elements per W1 row in LDS (16-B aligned rows)
+  L.LD2 = chid + 8;  // bf16 elements per W2 row
+  L.SR = (TH + 1) / 2 + 3;
+  L.SC = (TW + 1) / 2 + 3;
+  L.NCB = cout / 16;
+  L.NPB = L.P_out / 16;
+  L.NCHUNK = chid / 16;
+  // work split: EXPAND -> the 4 waves split the hidden chunks (each wave covers
+  // every pixel block); DIRECT/DEC -> waves split pixel blocks first (PW ways),
+  // then chunks (CS ways).
+  L.PW = mode == 0 /*EXPAND*/ ? 1 : (L.NPB >= 4 ? 4 : L.NPB);
+  L.CS = 4 / (L.PW > 0 ? L.PW : 1);
+  L.NPBW = mode == 0 ? L.NPB : L.NPB / (L.PW > 0 ? L.PW : 1);
+  L.NACC = L.NPBW * L.NCB;
+  L.slab_stride = L.P_out * (cout + 4);
+  int o = 0;
+  L.xt = o;  o += r4(L.P_in_pad * L.XS);
+  L.w1 = o;  o += mode == 0 ? r4(chid * L.LD1 / 2) : 0;
+  L.w2 = o;  o += r4(cout * L.LD2 / 2);
+  L.wdw = o; o += r4(9 * chid);
+  L.bdw = o; o += r4(chid);
+  L.b1 = o;  o += mode == 0 ? r4(chid) : 0;
+  L.b2 = o;  o += r4(cout);
+  L.lr = o;  o += mode == 2 ? r4(L.SR * L.SC * cin) : 0;
+  L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;
+  // per-wave scratch during the main loop, reused as the accumulator slabs after it
+  L.work = o;
+  o += cmax(4 * (mode == 0 ? (L.P_in_pad + L.P_out) * 16 : 256), L.CS * L.slab_stride);
+  L.stt = o; o += 512;
+  L.total = o;
+  return L;
+}
 
 // Fused block: [prologue: stage X tile (or upsample+concat)] ->
 //   for each 16-channel chunk c0 of the hidden/concat dim:
 //     (expand pw on MFMA) -> dw3x3 (VALU) -> project pw accumulate (MFMA)
 //   -> epilogue (bias, residual, store, instance-norm partial stats)
 struct BlockParams {
+  const float* wimg;     // the layer's LDS weight image (block_lds regions w1..b2), built by the host
   const float* x;        // IR input [N][H][W][cin]   | DEC low-res src [N][h][w][cin]
   const float* skip;     // DEC skip [N][Ho][Wo][cskip]
   float* y;              // output [N][Ho][Wo][cout]
@@ -54,6 +111,16 @@ struct BlockParams {
   int tiles_x, tiles_y;
   int norm_in;           // DEC: src needs norm+relu
 };
+
+using BlockFn = void (*)(BlockParams);
+
+// One compiled k_block shape (tools/gen_registry.py -> vss_registry.inc).
+// flags: 1 = the decoder's src needs instance norm + ReLU, 2 = residual add.
+struct BlockEntry {
+  int mode, stride, TH, TW, cin, cskip, chid, cout, flags;
+  BlockFn fn[2];  // [PREC_F32, PREC_BF16X2]
+};
+const BlockEntry* block_registry(int* count);
 
 struct StemParams {
   const uint8_t* frames; // [N] frames, row_stride / frame_stride bytes

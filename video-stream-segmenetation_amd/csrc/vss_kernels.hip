@@ -14,13 +14,14 @@
 //   k_stem   : tfjs-legacy bilinear resize + /255 computed on the fly into an
 //              LDS tile, fused with the 3x3 s2 stem conv + ReLU6 (VALU).
 //   k_block  : one inverted-residual or decoder block.  The hidden (expanded)
-//              tensor never touches HBM: the workgroup stages its input tile
-//              (+halo) in LDS once, then walks the hidden channels in chunks
-//              of 16: expand 1x1 (MFMA) -> dw 3x3 (VALU, LDS) -> project 1x1
-//              (MFMA) accumulated in registers across chunks.  Decoder blocks
-//              build the (instance-norm+ReLU'd, 2x bilinear upsampled src ++
-//              skip) concat tile in the prologue and emit per-tile instance-
-//              norm partial sums (deterministic, no atomics).
+//              tensor never touches HBM: the workgroup stages the layer's
+//              weights and its input tile (+halo) in LDS once; its 4 waves then
+//              run independent units of 16 hidden channels: expand 1x1 (MFMA)
+//              -> dw 3x3 (VALU, LDS) -> project 1x1 (MFMA) accumulated in
+//              registers; the waves' partial sums meet in LDS in a fixed order.
+//              Decoder blocks build the (instance-norm+ReLU'd, 2x bilinear
+//              upsampled src ++ skip) concat tile in the prologue and emit
+//              per-tile instance-norm partial sums (deterministic, no atomics).
 //   k_head   : norm+ReLU of d3, 1x1 -> logits in LDS, bilinear 2x, sigmoid.
 //   k_prep   : standalone preprocess to the NCHW f32 ORT input tensor
 //              (frameProcessorTest.ts:85) — bit-exact with the oracle.
@@ -46,25 +47,61 @@ __device__ __forceinline__ f4 reluv(f4 v) {
 // a2/a3: tfjs 4.22 ResizeBilinear (alignCorners=false, halfPixelCenters=false,
 // WebGL program form: f32, ratio = float(inH/outH)) followed by /255.
 // Same operation order as oracle/vss_oracle.c:resize_px -> bit-identical.
-__device__ __forceinline__ void prep_sample(const uint8_t* __restrict__ f, long rs, int fc, int fh,
-                                            int fw, float ry, float rx, int y, int x,
-                                            float& r, float& g, float& b) {
+struct PrepTap {
+  const uint8_t* t0;  // row y0
+  const uint8_t* t1;  // row y1
+  int o0, o1;         // byte offsets of columns x0, x1
+  float dy, dx;
+};
+
+__device__ __forceinline__ PrepTap prep_tap(const uint8_t* __restrict__ f, long rs, int fc, int fh, int fw,
+                                            float ry, float rx, int y, int x) {
+  // hipcc contracts by default: keep `fy = y*ry` rounded before `fy - y0`
+  // (an FMA there changes dy); the lerps below are explicit FMAs on both sides.
+#pragma clang fp contract(off)
   const float fy = (float)y * ry, fx = (float)x * rx;
   const int y0 = (int)floorf(fmaxf(fy, 0.f)), x0 = (int)floorf(fmaxf(fx, 0.f));
   const int y1 = min(fh - 1, (int)ceilf(fy)), x1 = min(fw - 1, (int)ceilf(fx));
-  const float dy = fy - (float)y0, dx = fx - (float)x0;
-  const uint8_t* t0 = f + (long)y0 * rs;
-  const uint8_t* t1 = f + (long)y1 * rs;
-  float out[3];
+  PrepTap t;
+  t.dy = fy - (float)y0;
+  t.dx = fx - (float)x0;
+  t.t0 = f + (long)y0 * rs;
+  t.t1 = f + (long)y1 * rs;
+  t.o0 = x0 * fc;
+  t.o1 = x1 * fc;
+  return t;
+}
+
+// v[0..2] = row y0 col x0 RGB, v[3..5] = (y0, x1), v[6..8] = (y1, x0), v[9..11] = (y1, x1)
+__device__ __forceinline__ void prep_load(const PrepTap& t, uint32_t v[12]) {
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    const float tl = t0[x0 * fc + c], tr = t0[x1 * fc + c];
-    const float bl = t1[x0 * fc + c], br = t1[x1 * fc + c];
+    v[c] = t.t0[t.o0 + c];
+    v[3 + c] = t.t0[t.o1 + c];
+    v[6 + c] = t.t1[t.o0 + c];
+    v[9 + c] = t.t1[t.o1 + c];
+  }
+}
+
+__device__ __forceinline__ void prep_finish(const uint32_t v[12], float dy, float dx, float out[3]) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float tl = (float)v[c], tr = (float)v[3 + c], bl = (float)v[6 + c], br = (float)v[9 + c];
     const float top = __builtin_fmaf(tr - tl, dx, tl);
     const float bot = __builtin_fmaf(br - bl, dx, bl);
-    const float v = __builtin_fmaf(bot - top, dy, top);
-    out[c] = v / 255.0f;
+    const float val = __builtin_fmaf(bot - top, dy, top);
+    out[c] = val / 255.0f;
   }
+}
+
+__device__ __forceinline__ void prep_sample(const uint8_t* __restrict__ f, long rs, int fc, int fh, int fw,
+                                            float ry, float rx, int y, int x, float& r, float& g, float& b) {
+  const PrepTap t = prep_tap(f, rs, fc, fh, fw, ry, rx, y, x);
+  uint32_t v[12];
+  prep_load(t, v);
+  float out[3];
+  prep_finish(v, t.dy, t.dx, out);
   r = out[0]; g = out[1]; b = out[2];
 }
 
@@ -97,15 +134,33 @@ __global__ __launch_bounds__(256) void k_stem(StemParams p) {
   const int n = blockIdx.z, oy0 = blockIdx.y * TH, ox0 = blockIdx.x * TW;
   const uint8_t* f = p.frames + (long)n * p.frame_stride;
   const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
-  for (int i = tid; i < IH * IW; i += 256) {
+  // all frame gathers of this thread issued before any is consumed
+  constexpr int NS = (IH * IW + 255) / 256;
+  uint32_t raw[NS][12];
+  float dys[NS], dxs[NS];
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    const int i = min(tid + 256 * u, IH * IW - 1);
     const int ly = i / IW, lx = i - ly * IW;
-    const int yy = iy0 + ly, xx = ix0 + lx;
-    float r = 0.f, g = 0.f, b = 0.f;
-    if (yy >= 0 && yy < p.Hm && xx >= 0 && xx < p.Wm)
-      prep_sample(f, p.row_stride, p.fc, p.fh, p.fw, p.ry, p.rx, yy, xx, r, g, b);
-    xs[0][ly][lx] = r;
-    xs[1][ly][lx] = g;
-    xs[2][ly][lx] = b;
+    const int yy = min(max(iy0 + ly, 0), p.Hm - 1), xx = min(max(ix0 + lx, 0), p.Wm - 1);
+    const PrepTap t = prep_tap(f, p.row_stride, p.fc, p.fh, p.fw, p.ry, p.rx, yy, xx);
+    prep_load(t, raw[u]);
+    dys[u] = t.dy;
+    dxs[u] = t.dx;
+  }
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    const int i = tid + 256 * u;
+    if (i < IH * IW) {
+      const int ly = i / IW, lx = i - ly * IW;
+      const int yy = iy0 + ly, xx = ix0 + lx;
+      float o[3];
+      prep_finish(raw[u], dys[u], dxs[u], o);
+      const bool valid = yy >= 0 && yy < p.Hm && xx >= 0 && xx < p.Wm;
+      xs[0][ly][lx] = valid ? o[0] : 0.f;
+      xs[1][ly][lx] = valid ? o[1] : 0.f;
+      xs[2][ly][lx] = valid ? o[2] : 0.f;
+    }
   }
   for (int i = tid; i < COUT * 27; i += 256) ws[i] = p.w[i];
   if (tid < COUT) bs[tid] = p.b[tid];
@@ -143,19 +198,22 @@ template <int PREC> struct AFrag;
 template <> struct AFrag<PREC_F32> { using T = f4; };
 template <> struct AFrag<PREC_BF16X2> { using T = bf8; };
 
+// A fragment from the LDS weight image (bf16-exact pointwise weights, rows of
+// `ld` bf16 elements): 4 consecutive weights of row `row` starting at k.
 template <int PREC>
-__device__ __forceinline__ typename AFrag<PREC>::T load_a(const void* w, int ldk, int row, int k);
+__device__ __forceinline__ typename AFrag<PREC>::T lds_a(const uint16_t* w, int ld, int row, int k);
 
 template <>
-__device__ __forceinline__ f4 load_a<PREC_F32>(const void* w, int ldk, int row, int k) {
-  return *reinterpret_cast<const f4*>(static_cast<const float*>(w) + (long)row * ldk + k);
+__device__ __forceinline__ f4 lds_a<PREC_F32>(const uint16_t* w, int ld, int row, int k) {
+  const uint2 v = *reinterpret_cast<const uint2*>(w + row * ld + k);
+  return f4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u), __uint_as_float(v.y << 16),
+            __uint_as_float(v.y & 0xFFFF0000u)};
 }
 template <>
-__device__ __forceinline__ bf8 load_a<PREC_BF16X2>(const void* w, int ldk, int row, int k) {
-  // bf16-exact weights: elements 0-3 pair with the activation hi parts,
-  // 4-7 (the same 4 weights) with the lo parts.
-  const bf4 v = *reinterpret_cast<const bf4*>(static_cast<const __bf16*>(w) + (long)row * ldk + k);
-  return bf8{v.x, v.y, v.z, v.w, v.x, v.y, v.z, v.w};
+__device__ __forceinline__ bf8 lds_a<PREC_BF16X2>(const uint16_t* w, int ld, int row, int k) {
+  // elements 0-3 pair with the activation hi parts, 4-7 (the same weights) with the lo parts
+  const bf4 b = __builtin_bit_cast(bf4, *reinterpret_cast<const uint2*>(w + row * ld + k));
+  return bf8{b.x, b.y, b.z, b.w, b.x, b.y, b.z, b.w};
 }
 
 template <int PREC>
@@ -182,277 +240,409 @@ __device__ __forceinline__ f4 mma16<PREC_BF16X2>(f4 acc, bf8 a, f4 b) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc, 0, 0, 0);
 }
 
-// Fused inverted-residual / decoder block (see header comment).
-// LDS (floats): xt [P_in_pad][XS] | hid [P_in_pad][16] (EXPAND) | dwo [2][P_out][16]
-//               | nrm [2][cin] (DEC) | st [4][2][cout] (DEC)
-template <int MODE, int STRIDE, int PREC>
+// Orders one wave's LDS writes before its other lanes' reads (and keeps the
+// compiler from moving LDS accesses across it); no workgroup barrier.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Instance-norm scale/shift of one frame from the producer's per-tile partial
+// sums part_n[T][2][C], reduced in a fixed order (bitwise reproducible).
+// tmp: 512 floats of LDS.  Ends with a workgroup barrier.
+__device__ __forceinline__ void norm_from_partials(const float* __restrict__ part_n, int T, int C, int hw, float eps,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   float* tmp, float* scale, float* shift) {
+  const int tid = threadIdx.x;
+  const int G = 256 / C, c = tid % C, gg = tid / C;
+  if (gg < G) {
+    float s = 0.f, q = 0.f;
+    for (int t0 = gg; t0 < T; t0 += 8 * G) {
+      float vs[8], vq[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int t = min(t0 + u * G, T - 1);
+        vs[u] = part_n[(2 * t) * C + c];
+        vq[u] = part_n[(2 * t + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (t0 + u * G < T) {
+          s += vs[u];
+          q += vq[u];
+        }
+    }
+    tmp[gg * C + c] = s;
+    tmp[256 + gg * C + c] = q;
+  }
+  __syncthreads();
+  if (tid < C) {
+    float s = 0.f, q = 0.f;
+    for (int k = 0; k < G; ++k) {
+      s += tmp[k * C + tid];
+      q += tmp[256 + k * C + tid];
+    }
+    const float inv = 1.0f / (float)hw;
+    const float mean = s * inv;
+    const float var = fmaxf(q * inv - mean * mean, 0.f);
+    const float rstd = 1.0f / sqrtf(var + eps);
+    const float sc = rstd * gamma[tid];
+    scale[tid] = sc;
+    shift[tid] = beta[tid] - mean * sc;
+  }
+  __syncthreads();
+}
+
+// Copy TOTAL 16-B items (a compile-time count) with up to UMAX loads in flight
+// per thread before any store.  Loads are unconditional at clamped indices (a
+// conditional load makes hipcc branch and wait per element), stores guarded.
+template <int TOTAL, int UMAX = 8, class Load, class Store>
+__device__ __forceinline__ void copy_n(Load ld, Store st) {
+  constexpr int PER = (TOTAL + 255) / 256;
+  constexpr int U = PER < UMAX ? PER : UMAX;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < PER; b += U) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + 256 * (b + u);
+      v[u] = ld(i < TOTAL ? i : TOTAL - 1);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + 256 * (b + u);
+      if (b + u < PER && i < TOTAL) st(i, v[u]);
+    }
+  }
+}
+
+// Fused inverted-residual / decoder block, specialised on its whole shape
+// (every tile and channel extent a compile-time constant: index math folds
+// to shifts/multiplies, loops unroll, accumulators stay in registers).
+//  prologue : the layer's weight image -> LDS (pointwise weights as bf16,
+//             exact), input tile (+halo, zeros outside the image) -> LDS;
+//             decoder: the normalised low-res src region -> LDS, then the 2x
+//             bilinear upsample ++ skip concat tile built from it.
+//  main     : independent per-wave work units, wave-level syncs only.
+//             EXPAND: unit = 16 hidden channels: expand (MFMA) over the whole
+//             input tile -> dw 3x3 (VALU) -> project (MFMA) into acc.
+//             DIRECT/DEC: unit = (16 output pixels, 16 channels): dw -> project.
+//  epilogue : per-wave accumulator slabs in LDS summed in a fixed order
+//             (deterministic), + bias (+ residual), coalesced NHWC stores,
+//             decoder instance-norm partial sums per tile.
+template <int MODE, int STRIDE, int TH, int TW, int CIN, int CSKIP, int CH, int COUT, int FLAGS, int PREC>
 __global__ __launch_bounds__(256) void k_block(BlockParams p) {
+  constexpr BlockLds L = block_lds(MODE, STRIDE, TH, TW, CIN, CSKIP, CH, COUT);
+  constexpr bool NORM_IN = (FLAGS & 1) != 0, RES = (FLAGS & 2) != 0;
+  constexpr int IW = L.IW, P_IN = L.P_in, P_IN_PAD = L.P_in_pad, P_OUT = L.P_out, XS = L.XS;
+  constexpr int NCB = L.NCB, NPB = L.NPB, NCHUNK = L.NCHUNK, PW = L.PW, CS = L.CS, NPBW = L.NPBW;
+  constexpr int RS = COUT + 4, SS = L.slab_stride;
+  static_assert(L.NACC <= kMaxAcc, "too many accumulators per wave");
+  static_assert(CIN % 16 == 0 && CH % 16 == 0 && COUT % 16 == 0 && P_OUT % 16 == 0, "shape");
+  static_assert(MODE != MODE_IR_EXPAND || CIN <= 64, "expand cin <= 64");
+  static_assert(!RES || (STRIDE == 1 && CIN == COUT && MODE != MODE_DEC), "residual shape");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n = blockIdx.z;
-  const int TH = p.TH, TW = p.TW;
   const int oy0 = blockIdx.y * TH, ox0 = blockIdx.x * TW;
-  const int IH = STRIDE == 2 ? 2 * TH + 1 : TH + 2;
-  const int IW = STRIDE == 2 ? 2 * TW + 1 : TW + 2;
   const int iy0 = STRIDE * oy0 - 1, ix0 = STRIDE * ox0 - 1;
-  const int P_in = IH * IW, P_in_pad = (P_in + 15) & ~15;
-  const int P_out = TH * TW;
-  const int CX = MODE == MODE_DEC ? p.cin + p.cskip : p.cin;
-  const int XS = CX + 4;
   const int Ho = p.Ho, Wo = p.Wo;
+  float* xt = smem + L.xt;
+  const uint16_t* w1s = reinterpret_cast<const uint16_t*>(smem + L.w1);
+  const uint16_t* w2s = reinterpret_cast<const uint16_t*>(smem + L.w2);
+  const float* wdws = smem + L.wdw;
+  const float* bdws = smem + L.bdw;
+  const float* b1s = smem + L.b1;
+  const float* b2s = smem + L.b2;
+  float* work = smem + L.work;
+  float* stt = smem + L.stt;
 
-  float* xt = smem;
-  float* hid = xt + P_in_pad * XS;
-  float* dwo = hid + (MODE == MODE_IR_EXPAND ? P_in_pad * 16 : 0);
-  float* nrm = dwo + 2 * P_out * 16;
-  float* st = nrm + (MODE == MODE_DEC ? 2 * p.cin : 0);
+  // ---- prologue 1: the layer's weight image -> LDS ----
+  {
+    constexpr int WIMG_F4 = (L.lr - L.w1) / 4;
+    const f4* src = reinterpret_cast<const f4*>(p.wimg);
+    f4* dst = reinterpret_cast<f4*>(smem + L.w1);
+    copy_n<WIMG_F4>([&](int i) { return src[i]; }, [&](int i, f4 v) { dst[i] = v; });
+  }
 
-  // ---- prologue: stage the input tile (+halo), zero outside the image ----
-  const int C4 = CX >> 2;
+  // ---- prologue 2: the input tile ----
   if constexpr (MODE == MODE_DEC) {
-    const int cl = p.cin;
-    if (p.norm_in) {
-      // instance-norm statistics of the producer, reduced in a fixed order
-      for (int c = tid; c < cl; c += 256) {
-        const float* pp = p.in_part + (long)n * p.in_tiles * 2 * cl;
-        float s = 0.f, q = 0.f;
-        for (int t = 0; t < p.in_tiles; ++t) {
-          s += pp[(2 * t) * cl + c];
-          q += pp[(2 * t + 1) * cl + c];
-        }
-        const float inv = 1.0f / (float)p.in_hw;
-        const float mean = s * inv;
-        const float var = fmaxf(q * inv - mean * mean, 0.f);
-        const float rstd = 1.0f / sqrtf(var + p.eps);
-        const float sc = rstd * p.in_gamma[c];
-        nrm[c] = sc;
-        nrm[cl + c] = p.in_beta[c] - mean * sc;
-      }
-      for (int c = tid; c < 4 * 2 * p.cout; c += 256) st[c] = 0.f;
-      __syncthreads();
-    } else {
-      for (int c = tid; c < 4 * 2 * p.cout; c += 256) st[c] = 0.f;
-    }
-    const int h = p.H, w = p.W;  // low-res src dims (Ho = 2h, Wo = 2w)
-    for (int i = tid; i < P_in_pad * C4; i += 256) {
-      const int pix = i / C4, c4 = i - pix * C4;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      const int ly = pix / IW, lx = pix - ly * IW;
-      const int yy = iy0 + ly, xx = ix0 + lx;
-      if (pix < P_in && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo) {
-        const int c = 4 * c4;
-        if (c < cl) {
-          // PyTorch upsample_bilinear2d(scale 2, align_corners=False)
-          float sy = ((float)yy + 0.5f) * 0.5f - 0.5f;
-          sy = fmaxf(sy, 0.f);
+    constexpr int CL = CIN, C4L = CL / 4, C4S = CSKIP / 4, SR = L.SR, SC = L.SC;
+    const int h = p.H, w = p.W;
+    float* lr = smem + L.lr;
+    float* nrm = smem + L.nrm;
+    if constexpr (NORM_IN)
+      norm_from_partials(p.in_part + (long)n * p.in_tiles * 2 * CL, p.in_tiles, CL, p.in_hw, p.eps, p.in_gamma,
+                         p.in_beta, stt, nrm, nrm + CL);
+    // low-res src region, normalised + ReLU'd once per src pixel
+    const int sy0 = max(0, (oy0 - 1) / 2 - 1), sx0 = max(0, (ox0 - 1) / 2 - 1);
+    const float* xn = p.x + (long)n * h * w * CL;
+    copy_n<SR * SC * C4L>(
+        [&](int i) {
+          const int pr = i / C4L, c4 = i % C4L;
+          const int yy = min(h - 1, sy0 + pr / SC), xx = min(w - 1, sx0 + pr % SC);
+          return *reinterpret_cast<const f4*>(xn + ((long)yy * w + xx) * CL + 4 * c4);
+        },
+        [&](int i, f4 v) {
+          const int c4 = i % C4L;
+          if constexpr (NORM_IN)
+            v = reluv(v * *reinterpret_cast<const f4*>(nrm + 4 * c4) + *reinterpret_cast<const f4*>(nrm + CL + 4 * c4));
+          *reinterpret_cast<f4*>(lr + 4 * i) = v;
+        });
+    // skip channels of the concat tile (zeros outside the image)
+    const float* sn = p.skip + (long)n * Ho * Wo * CSKIP;
+    copy_n<P_IN_PAD * C4S>(
+        [&](int i) {
+          const int pix = i / C4S, c4 = i % C4S;
+          const int yy = min(max(iy0 + pix / IW, 0), Ho - 1), xx = min(max(ix0 + pix % IW, 0), Wo - 1);
+          return *reinterpret_cast<const f4*>(sn + ((long)yy * Wo + xx) * CSKIP + 4 * c4);
+        },
+        [&](int i, f4 v) {
+          const int pix = i / C4S, c4 = i % C4S;
+          const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
+          const bool valid = pix < P_IN && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo;
+          *reinterpret_cast<f4*>(xt + pix * XS + CL + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+        });
+    __syncthreads();
+    // upsampled channels: PyTorch upsample_bilinear2d(scale 2, align_corners=False)
+#pragma unroll
+    for (int k = 0; k < (P_IN_PAD * C4L + 255) / 256; ++k) {
+      const int i = tid + 256 * k;
+      if (i < P_IN_PAD * C4L) {
+        const int pix = i / C4L, c4 = i % C4L;
+        const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (pix < P_IN && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo) {
+          const float sy = fmaxf(((float)yy + 0.5f) * 0.5f - 0.5f, 0.f);
           const int y0 = (int)sy, y1 = y0 + (y0 < h - 1 ? 1 : 0);
           const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
-          float sx = ((float)xx + 0.5f) * 0.5f - 0.5f;
-          sx = fmaxf(sx, 0.f);
+          const float sx = fmaxf(((float)xx + 0.5f) * 0.5f - 0.5f, 0.f);
           const int x0 = (int)sx, x1 = x0 + (x0 < w - 1 ? 1 : 0);
           const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
-          const float* base = p.x + (long)n * h * w * cl + c;
-          f4 v00 = *reinterpret_cast<const f4*>(base + ((long)y0 * w + x0) * cl);
-          f4 v01 = *reinterpret_cast<const f4*>(base + ((long)y0 * w + x1) * cl);
-          f4 v10 = *reinterpret_cast<const f4*>(base + ((long)y1 * w + x0) * cl);
-          f4 v11 = *reinterpret_cast<const f4*>(base + ((long)y1 * w + x1) * cl);
-          if (p.norm_in) {
-            const f4 sc = *reinterpret_cast<const f4*>(nrm + c);
-            const f4 sh = *reinterpret_cast<const f4*>(nrm + cl + c);
-            v00 = reluv(v00 * sc + sh);
-            v01 = reluv(v01 * sc + sh);
-            v10 = reluv(v10 * sc + sh);
-            v11 = reluv(v11 * sc + sh);
-          }
+          const int r0 = min(max(y0 - sy0, 0), SR - 1), r1 = min(max(y1 - sy0, 0), SR - 1);
+          const int q0 = min(max(x0 - sx0, 0), SC - 1), q1 = min(max(x1 - sx0, 0), SC - 1);
+          const f4 v00 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q0) * CL + 4 * c4);
+          const f4 v01 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q1) * CL + 4 * c4);
+          const f4 v10 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q0) * CL + 4 * c4);
+          const f4 v11 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q1) * CL + 4 * c4);
           v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
-        } else {
-          v = *reinterpret_cast<const f4*>(p.skip + (((long)n * Ho + yy) * Wo + xx) * p.cskip + (c - cl));
         }
+        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
       }
-      *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
     }
   } else {
+    constexpr int C4 = CIN / 4;
     const int H = p.H, W = p.W;
-    for (int i = tid; i < P_in_pad * C4; i += 256) {
-      const int pix = i / C4, c4 = i - pix * C4;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      const int ly = pix / IW, lx = pix - ly * IW;
-      const int yy = iy0 + ly, xx = ix0 + lx;
-      if (pix < P_in && yy >= 0 && yy < H && xx >= 0 && xx < W)
-        v = *reinterpret_cast<const f4*>(p.x + (((long)n * H + yy) * W + xx) * p.cin + 4 * c4);
-      *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
-    }
+    const float* xn = p.x + (long)n * H * W * CIN;
+    copy_n<P_IN_PAD * C4>(
+        [&](int i) {
+          const int pix = i / C4, c4 = i % C4;
+          const int yy = min(max(iy0 + pix / IW, 0), H - 1), xx = min(max(ix0 + pix % IW, 0), W - 1);
+          return *reinterpret_cast<const f4*>(xn + ((long)yy * W + xx) * CIN + 4 * c4);
+        },
+        [&](int i, f4 v) {
+          const int pix = i / C4, c4 = i % C4;
+          const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
+          const bool valid = pix < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+          *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+        });
   }
   __syncthreads();
 
-  // ---- main loop over 16-channel chunks of the hidden / concat dim ----
-  const int nchunks = p.chid >> 4;
-  const int NPB = P_out >> 4, NT = (p.cout >> 4) * NPB;
-  const int ldk2 = p.chid;  // project weight row length
-  f4 acc[kMaxProjTiles];
+  // ---- main: per-wave work units ----
+  f4 acc[L.NACC];
 #pragma unroll
-  for (int j = 0; j < kMaxProjTiles; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < L.NACC; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  const int cg = lane & 3;
+  const int pw = wave % PW, cw = wave / PW;
 
-  const int cg = tid & 3;  // dw: this thread's 4-channel group within the chunk
-
-  for (int ck = 0; ck < nchunks; ++ck) {
-    const int c0 = ck << 4;
-    const float* src;
-    int srcS;
-    if constexpr (MODE == MODE_IR_EXPAND) {
-      // expand: hid[pix][0..15] = relu6(W1[c0..c0+15][:] . x[pix][:] + b1), 0 outside image
-      typename AFrag<PREC>::T aw[4];
-      const int nk = p.cin >> 4;
+  if constexpr (MODE == MODE_IR_EXPAND) {
+    float* hid = work + wave * (P_IN_PAD + P_OUT) * 16;
+    float* dwo = hid + P_IN_PAD * 16;
+    constexpr int NK = CIN / 16;
+    for (int ck = wave; ck < NCHUNK; ck += 4) {
+      const int c0 = ck << 4;
+      typename AFrag<PREC>::T aw[NK];
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (s < nk) aw[s] = load_a<PREC>(p.w1, p.cin, c0 + r, 16 * s + 4 * g);
-      const f4 bias = *reinterpret_cast<const f4*>(p.b1 + c0 + 4 * g);
-      for (int cb = wave; cb < (P_in_pad >> 4); cb += 4) {
+      for (int s = 0; s < NK; ++s) aw[s] = lds_a<PREC>(w1s, L.LD1, c0 + r, 16 * s + 4 * g);
+      const f4 bias = *reinterpret_cast<const f4*>(b1s + c0 + 4 * g);
+#pragma unroll 2
+      for (int cb = 0; cb < P_IN_PAD / 16; ++cb) {
         const int pix = cb * 16 + r;
         f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-          if (s < nk) d = mma16<PREC>(d, aw[s], *reinterpret_cast<const f4*>(xt + pix * XS + 16 * s + 4 * g));
-        const int ly = pix / IW, lx = pix - ly * IW;
-        const int yy = iy0 + ly, xx = ix0 + lx;
-        const bool valid = pix < P_in && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
-        const f4 hv = valid ? relu6v(d + bias) : f4{0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<f4*>(hid + pix * 16 + 4 * g) = hv;
+        for (int s = 0; s < NK; ++s) d = mma16<PREC>(d, aw[s], *reinterpret_cast<const f4*>(xt + pix * XS + 16 * s + 4 * g));
+        const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
+        const bool valid = pix < P_IN && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
+        *reinterpret_cast<f4*>(hid + pix * 16 + 4 * g) = valid ? relu6v(d + bias) : f4{0.f, 0.f, 0.f, 0.f};
       }
-      __syncthreads();
-      src = hid;
-      srcS = 16;
-    } else {
-      src = xt + c0;
-      srcS = XS;
-    }
-
-    // depthwise 3x3 (VALU): dwo[ck&1][pix][0..15]
-    {
-      float* dout = dwo + (ck & 1) * P_out * 16;
-      const int C = p.chid;
-      f4 wk[9];
+      wave_sync();
+      {
+        f4 wk[9];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) wk[t] = *reinterpret_cast<const f4*>(p.wdw + t * C + c0 + 4 * cg);
-      const f4 bb = *reinterpret_cast<const f4*>(p.bdw + c0 + 4 * cg);
-      for (int idx = tid; idx < P_out * 4; idx += 256) {
-        const int pix = idx >> 2;
-        const int ly = pix / TW, lx = pix - ly * TW;
-        f4 a = bb;
+        for (int t = 0; t < 9; ++t) wk[t] = *reinterpret_cast<const f4*>(wdws + t * CH + c0 + 4 * cg);
+        const f4 bb = *reinterpret_cast<const f4*>(bdws + c0 + 4 * cg);
+#pragma unroll
+        for (int k = 0; k < P_OUT / 16; ++k) {
+          const int pix = (lane >> 2) + 16 * k;
+          const int ly = pix / TW, lx = pix % TW;
+          f4 a = bb;
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              const int sp = (STRIDE * ly + ky) * IW + (STRIDE * lx + kx);
+              a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(hid + sp * 16 + 4 * cg) + a;
+            }
+          *reinterpret_cast<f4*>(dwo + pix * 16 + 4 * cg) = relu6v(a);
+        }
+      }
+      wave_sync();
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const auto a = lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb)
+          acc[pb * NCB + cb] =
+              mma16<PREC>(acc[pb * NCB + cb], a, *reinterpret_cast<const f4*>(dwo + (pb * 16 + r) * 16 + 4 * g));
+      }
+      wave_sync();
+    }
+  } else {
+    float* dwo = work + wave * 256;
+    const int pl = lane >> 2;
+#pragma unroll
+    for (int i = 0; i < NPBW; ++i) {
+      const int pix = (pw + i * PW) * 16 + pl;
+      const int ly = pix / TW, lx = pix % TW;
+      for (int ck = cw; ck < NCHUNK; ck += CS) {
+        const int c0 = ck << 4;
+        f4 a = *reinterpret_cast<const f4*>(bdws + c0 + 4 * cg);
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int sp = (STRIDE * ly + ky) * IW + (STRIDE * lx + kx);
-            const f4 v = *reinterpret_cast<const f4*>(src + sp * srcS + 4 * cg);
-            a = wk[ky * 3 + kx] * v + a;
-          }
-        if (p.relu6_dw) a = relu6v(a);
-        *reinterpret_cast<f4*>(dout + pix * 16 + 4 * cg) = a;
-      }
-    }
-    __syncthreads();
-
-    // project: acc[tile] += W2[co][c0..c0+15] . dwo[pix][0..15]
-    {
-      const float* dout = dwo + (ck & 1) * P_out * 16;
+          for (int kx = 0; kx < 3; ++kx)
+            a = *reinterpret_cast<const f4*>(wdws + (ky * 3 + kx) * CH + c0 + 4 * cg) *
+                    *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx + kx) * XS + c0 + 4 * cg) + a;
+        if constexpr (MODE == MODE_IR_DIRECT) a = relu6v(a);
+        *reinterpret_cast<f4*>(dwo + pl * 16 + 4 * cg) = a;
+        wave_sync();
+        const f4 b = *reinterpret_cast<const f4*>(dwo + r * 16 + 4 * g);
 #pragma unroll
-      for (int j = 0; j < kMaxProjTiles; ++j) {
-        const int t = wave + 4 * j;
-        if (t < NT) {
-          const int cb = t / NPB, pb = t - cb * NPB;
-          const auto a = load_a<PREC>(p.w2, ldk2, cb * 16 + r, c0 + 4 * g);
-          const f4 b = *reinterpret_cast<const f4*>(dout + (pb * 16 + r) * 16 + 4 * g);
-          acc[j] = mma16<PREC>(acc[j], a, b);
-        }
+        for (int cb = 0; cb < NCB; ++cb)
+          acc[i * NCB + cb] = mma16<PREC>(acc[i * NCB + cb], lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g), b);
+        wave_sync();
       }
     }
-    // no barrier: the next chunk writes hid (last read by this chunk's dw,
-    // fenced above) and the other dwo buffer (last read two chunks ago).
   }
 
-  // ---- epilogue ----
+  // ---- epilogue: slabs -> fixed-order sum, bias, residual, store ----
+  __syncthreads();  // every wave is done with its scratch (reused as slabs)
+  {
+    float* slab = work + cw * SS;
 #pragma unroll
-  for (int j = 0; j < kMaxProjTiles; ++j) {
-    const int t = wave + 4 * j;
-    if (t < NT) {
-      const int cb = t / NPB, pb = t - cb * NPB;
-      const int pix = pb * 16 + r;
-      const int ly = pix / TW, lx = pix - ly * TW;
+    for (int i = 0; i < NPBW; ++i)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int pb = pw + i * PW;
+        *reinterpret_cast<f4*>(slab + (pb * 16 + r) * RS + cb * 16 + 4 * g) = acc[i * NCB + cb];
+      }
+  }
+  __syncthreads();
+  constexpr int C4O = COUT / 4;
+#pragma unroll
+  for (int k = 0; k < (P_OUT * C4O + 255) / 256; ++k) {
+    const int i = tid + 256 * k;
+    if (i < P_OUT * C4O) {
+      const int pix = i / C4O, c4 = i % C4O;
+      const int ly = pix / TW, lx = pix % TW;
       const int oy = oy0 + ly, ox = ox0 + lx;
       const bool valid = oy < Ho && ox < Wo;
-      const int co = cb * 16 + 4 * g;
-      f4 v = acc[j] + *reinterpret_cast<const f4*>(p.b2 + co);
-      if (MODE != MODE_DEC && p.residual)
-        v += *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + co);
-      if (valid) *reinterpret_cast<f4*>(p.y + (((long)n * Ho + oy) * Wo + ox) * p.cout + co) = v;
-      if constexpr (MODE == MODE_DEC) {
-        f4 s = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
-        f4 q = s * s;
+      // slabs of the CS waves that own this pixel block, summed in wave order
+      f4 v = *reinterpret_cast<const f4*>(work + pix * RS + 4 * c4);
 #pragma unroll
-        for (int m = 1; m < 16; m <<= 1) {
-          s.x += __shfl_xor(s.x, m); s.y += __shfl_xor(s.y, m);
-          s.z += __shfl_xor(s.z, m); s.w += __shfl_xor(s.w, m);
-          q.x += __shfl_xor(q.x, m); q.y += __shfl_xor(q.y, m);
-          q.z += __shfl_xor(q.z, m); q.w += __shfl_xor(q.w, m);
-        }
-        if (r == 0) {
-          float* sw = st + wave * 2 * p.cout;
-          *reinterpret_cast<f4*>(sw + co) += s;
-          *reinterpret_cast<f4*>(sw + p.cout + co) += q;
-        }
-      }
+      for (int s = 1; s < CS; ++s) v = v + *reinterpret_cast<const f4*>(work + s * SS + pix * RS + 4 * c4);
+      v = v + *reinterpret_cast<const f4*>(b2s + 4 * c4);
+      if constexpr (RES) v = v + *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + 4 * c4);
+      if (valid) *reinterpret_cast<f4*>(p.y + (((long)n * Ho + oy) * Wo + ox) * COUT + 4 * c4) = v;
+      if constexpr (MODE == MODE_DEC)
+        *reinterpret_cast<f4*>(work + pix * RS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
     }
   }
   if constexpr (MODE == MODE_DEC) {
     __syncthreads();
-    const int tile = blockIdx.y * p.tiles_x + blockIdx.x;
-    float* op = p.out_part + ((long)n * p.tiles_x * p.tiles_y + tile) * 2 * p.cout;
-    for (int c = tid; c < 2 * p.cout; c += 256)
-      op[c] = ((st[c] + st[2 * p.cout + c]) + st[4 * p.cout + c]) + st[6 * p.cout + c];
+    constexpr int G = 256 / COUT;
+    const int c = tid % COUT, gg = tid / COUT;
+    if (gg < G) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int pix = 0; pix < P_OUT; pix += G) {
+        if (pix + gg < P_OUT) {
+          const float v = work[(pix + gg) * RS + c];
+          s += v;
+          q += v * v;
+        }
+      }
+      stt[gg * COUT + c] = s;
+      stt[256 + gg * COUT + c] = q;
+    }
+    __syncthreads();
+    if (tid < COUT) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        s += stt[k * COUT + tid];
+        q += stt[256 + k * COUT + tid];
+      }
+      const int tile = blockIdx.y * p.tiles_x + blockIdx.x;
+      float* op = p.out_part + ((long)n * p.tiles_x * p.tiles_y + tile) * 2 * COUT;
+      op[tid] = s;
+      op[COUT + tid] = q;
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
 // Head: mask tile 16 x 64; logits over the (10 x 34) low-res region in LDS.
+template <int C>
 __global__ __launch_bounds__(256) void k_head(HeadParams p) {
-  constexpr int OTH = 16, OTW = 64, ZR = 10, ZC = 34, ZCP = 35;
-  constexpr int CMAX = 64;
+  constexpr int OTH = 16, OTW = 64, ZR = 10, ZC = 34, ZCP = 35, NZ = (ZR * ZC + 255) / 256;
   __shared__ float z[ZR][ZCP];
-  __shared__ float sc[CMAX], sh[CMAX], wv[CMAX];
+  __shared__ float sc[C], sh[C], wv[C];
+  __shared__ float tmp[512];
   const int tid = threadIdx.x, n = blockIdx.z;
   const int oy0 = blockIdx.y * OTH, ox0 = blockIdx.x * OTW;
-  const int h = p.h, w = p.w_, C = p.cin;
-  for (int c = tid; c < C; c += 256) {
-    const float* pp = p.in_part + (long)n * p.in_tiles * 2 * C;
-    float s = 0.f, q = 0.f;
-    for (int t = 0; t < p.in_tiles; ++t) {
-      s += pp[(2 * t) * C + c];
-      q += pp[(2 * t + 1) * C + c];
-    }
-    const float inv = 1.0f / (float)(h * w);
-    const float mean = s * inv;
-    const float var = fmaxf(q * inv - mean * mean, 0.f);
-    const float rstd = 1.0f / sqrtf(var + p.eps);
-    const float scale = rstd * p.gamma[c];
-    sc[c] = scale;
-    sh[c] = p.beta[c] - mean * scale;
-    wv[c] = p.w[c];
-  }
-  __syncthreads();
+  const int h = p.h, w = p.w_;
   const int zr0 = oy0 / 2 - 1, zc0 = ox0 / 2 - 1;
-  for (int i = tid; i < ZR * ZC; i += 256) {
+  // issue this thread's d3 loads before the statistics reduction
+  f4 xv[NZ][C / 4];
+#pragma unroll
+  for (int u = 0; u < NZ; ++u) {
+    const int i = min(tid + 256 * u, ZR * ZC - 1);
     const int zr = i / ZC, zc = i - zr * ZC;
     const int yy = min(max(zr0 + zr, 0), h - 1), xx = min(max(zc0 + zc, 0), w - 1);
-    const float* px = p.x + (((long)n * h + yy) * w + xx) * C;
-    float acc = 0.f;
-    for (int c = 0; c < C; c += 4) {
-      const f4 v = *reinterpret_cast<const f4*>(px + c);
-      const f4 a = reluv(v * *reinterpret_cast<const f4*>(sc + c) + *reinterpret_cast<const f4*>(sh + c));
-      acc += a.x * wv[c] + a.y * wv[c + 1] + a.z * wv[c + 2] + a.w * wv[c + 3];
+    const f4* px = reinterpret_cast<const f4*>(p.x + (((long)n * h + yy) * w + xx) * C);
+#pragma unroll
+    for (int q = 0; q < C / 4; ++q) xv[u][q] = px[q];
+  }
+  for (int c = tid; c < C; c += 256) wv[c] = p.w[c];
+  norm_from_partials(p.in_part + (long)n * p.in_tiles * 2 * C, p.in_tiles, C, h * w, p.eps, p.gamma, p.beta, tmp,
+                     sc, sh);
+#pragma unroll
+  for (int u = 0; u < NZ; ++u) {
+    const int i = tid + 256 * u;
+    if (i < ZR * ZC) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < C / 4; ++q) {
+        const f4 a = reluv(xv[u][q] * *reinterpret_cast<const f4*>(sc + 4 * q) + *reinterpret_cast<const f4*>(sh + 4 * q));
+        acc += a.x * wv[4 * q] + a.y * wv[4 * q + 1] + a.z * wv[4 * q + 2] + a.w * wv[4 * q + 3];
+      }
+      z[i / ZC][i % ZC] = acc + p.b;
     }
-    z[zr][zc] = acc + p.b;
   }
   __syncthreads();
 #pragma unroll
@@ -477,26 +667,24 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// Host-visible launch table (used by vss_capi.hip).
-using BlockFn = void (*)(BlockParams);
+// Host-visible launch table (used by vss_capi.hip): one entry per compiled
+// block shape, generated from the layer table by tools/gen_registry.py.
+#define VSS_BLOCK(M, S, TH, TW, CI, CK, CH, CO, FL)                                    \
+  {M, S, TH, TW, CI, CK, CH, CO, FL,                                                  \
+   {k_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC_F32>,                              \
+    k_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC_BF16X2>}},
+static const BlockEntry kBlocks[] = {
+#include "vss_registry.inc"
+};
+#undef VSS_BLOCK
 
-BlockFn block_kernel(int mode, int stride, int prec) {
-#define VSS_SEL(M, S, P) \
-  if (mode == M && stride == S && prec == P) return k_block<M, S, P>;
-  VSS_SEL(MODE_IR_EXPAND, 1, PREC_F32)
-  VSS_SEL(MODE_IR_EXPAND, 2, PREC_F32)
-  VSS_SEL(MODE_IR_DIRECT, 1, PREC_F32)
-  VSS_SEL(MODE_DEC, 1, PREC_F32)
-  VSS_SEL(MODE_IR_EXPAND, 1, PREC_BF16X2)
-  VSS_SEL(MODE_IR_EXPAND, 2, PREC_BF16X2)
-  VSS_SEL(MODE_IR_DIRECT, 1, PREC_BF16X2)
-  VSS_SEL(MODE_DEC, 1, PREC_BF16X2)
-#undef VSS_SEL
-  return nullptr;
+const BlockEntry* block_registry(int* count) {
+  *count = (int)(sizeof(kBlocks) / sizeof(kBlocks[0]));
+  return kBlocks;
 }
 
 void (*stem_kernel16())(StemParams) { return k_stem<16>; }
-void (*head_kernel())(HeadParams) { return k_head; }
+void (*head_kernel16())(HeadParams) { return k_head<16>; }
 void (*prep_kernel())(PrepParams) { return k_prep; }
 
 }  // namespace vss
