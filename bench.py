@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_traffic.json"),
+                    help="per-kernel HBM traffic from tools/prof_summary.py (PMC passes)")
     args = ap.parse_args()
 
     import torch
@@ -155,8 +157,14 @@ def main():
     dom = int(np.argmax(ms))
     dom_bytes = cm.launch_bytes(costs[dom], B)
     achieved = dom_bytes / (ms[dom] * 1e-3)
-    per_layer = [{"layer": i, "kind": costs[i]["kind"], "ms": round(m, 5),
+    names = [sess.layer_kernel(i) for i in range(len(ms))]
+    per_layer = [{"layer": i, "kind": costs[i]["kind"], "kernel": names[i], "ms": round(m, 5),
                   "GBps": round(cm.launch_bytes(costs[i], B) / (m * 1e-3) / 1e9, 1)} for i, m in enumerate(ms)]
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        t = json.load(open(args.traffic_json)).get(names[dom])
+        if t and t.get("traffic_bytes"):
+            traffic = round(t["traffic_bytes"] / 1e6, 3)
 
     out = None
     if rank == 0:
@@ -197,12 +205,13 @@ def main():
             "mask_max_abs_err": err,
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"layer {dom} ({costs[dom]['kind']})",
+                "kernel": f"layer {dom} ({costs[dom]['kind']}): {names[dom]}",
                 "achieved": round(achieved / 1e9, 1),
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "MB/launch (rocprofv3 PMC: 2*FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
                 "alg_bytes_per_launch": dom_bytes,
                 "mean_kernel_ms": round(ms[dom], 5),
                 "events_count": cnt,

@@ -65,7 +65,14 @@ typedef struct vss_config {
   int max_batch;           /* frames per call */
   int max_frame_h, max_frame_w; /* host-staging capacity for vss_segment (channels <= 4) */
   const char* weights_path;     /* vss weights blob (model/make_weights.py) */
+  int flags;                    /* VSS_CREATE_* */
 } vss_config;
+
+/* vss_config.flags */
+enum {
+  VSS_CREATE_NO_AUTOTUNE = 1 /* keep the planner's tile per layer instead of timing every compiled
+                                tile at max_batch during vss_create (results are identical either way) */
+};
 
 typedef struct vss_info {
   int mask_h, mask_w;      /* (maskH, maskW) of the seam */
@@ -133,6 +140,12 @@ int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww);
 /* Copy layer `layer`'s output of the most recent forward to host as NHWC f32
  * [n][H][W][C] (debug / per-layer parity; synchronises the handle). */
 int vss_read_layer(vss_handle* h, int layer, int n, float* host_out);
+
+/* The kernel that runs layer `layer` as rocprofv3 names it, e.g.
+ * "void vss::k_block<2, 1, 8, 8, 32, 16, 48, 16, 1, 1>(vss::BlockParams)"
+ * (template arguments: mode, stride, tile h, tile w, cin, cskip, chid, cout,
+ * flags, precision).  Returns the string length, or a negative code. */
+int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap);
 
 /* Kernel times from VSS_OPT_PROFILE runs: per layer, the mean over `count`
  * forwards (ms).  Resets the accumulators. */

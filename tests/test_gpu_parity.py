@@ -201,3 +201,14 @@ def test_tiny_and_extreme_frames(pkg, sess_bf, oracle, blob):
         m, _, _ = sess_bf.segment_frames(f)
         ref = oracle.forward(blob, f, 144, 256, mode=0).reshape(1, -1)
         assert np.abs(m - ref).max() <= MASK_TOL, (h, w)
+
+
+def test_results_independent_of_tiling(pkg, sess_bf, synthetic):
+    # the planner / autotuner may pick different tiles per batch size; the
+    # arithmetic is tile-invariant, so the masks must be bitwise identical
+    f = _frames(synthetic, 3, start=500)
+    ref, _, _ = sess_bf.segment_frames(f)
+    for mb, at in ((3, False), (32, True), (1, True)):
+        with pkg.Session(dtype="bf16x2", max_batch=mb, autotune=at) as s:
+            got = np.concatenate([s.segment_frames(f[i:i + mb])[0] for i in range(0, 3, mb)])
+        assert np.array_equal(got, ref), (mb, at)

@@ -1,0 +1,76 @@
+"""Summarise a tools/prof_run.sh output directory into profiles/.
+
+Reads the rocprofv3 kernel-trace stats (mean duration per kernel) and the two
+PMC passes (FETCH_SIZE, WRITE_SIZE per dispatch) and writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats table as collected
+  profiles/<tag>_summary.md         per-kernel duration, HBM bytes, GB/s
+  profiles/<tag>_traffic.json       {kernel name: {...}} read by bench.py
+
+HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md §HBM and
+cdna_hip_programming.md §7: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so it is
+doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  Infinity-Cache hits are
+counted by these memory-side counters (they are L2-miss traffic, not strictly
+DRAM traffic) — stated in the summary.
+
+    python tools/prof_summary.py gpurun_out/prof_r01 r01
+"""
+from __future__ import annotations
+
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
+    pmc = defaultdict(lambda: defaultdict(list))
+    for kind in ("fetch", "write"):
+        p = os.path.join(src, kind, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            pmc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    rows = []
+    traffic = {}
+    for s in stats:
+        name = s["Name"]
+        avg_ns = float(s["AverageNs"])
+        f = pmc.get(name, {}).get("FETCH_SIZE", [])
+        w = pmc.get(name, {}).get("WRITE_SIZE", [])
+        fetch_b = 2.0 * 1024.0 * (sum(f) / len(f)) if f else None
+        write_b = 1024.0 * (sum(w) / len(w)) if w else None
+        tb = (fetch_b or 0.0) + (write_b or 0.0) if (f or w) else None
+        rows.append((name, int(s["Calls"]), avg_ns, fetch_b, write_b, tb))
+        traffic[name] = {"avg_ns": avg_ns, "calls": int(s["Calls"]), "fetch_bytes": fetch_b,
+                         "write_bytes": write_b, "traffic_bytes": tb,
+                         "traffic_GBps": (tb / avg_ns) if tb else None}
+    json.dump(traffic, open(os.path.join(out, f"{tag}_traffic.json"), "w"), indent=1)
+    log = open(os.path.join(src, "trace.log")).read().strip().splitlines()
+    bench_line = next((l for l in reversed(log) if l.startswith("{")), "")
+    with open(os.path.join(out, f"{tag}_summary.md"), "w") as fh:
+        fh.write(f"# rocprofv3 summary `{tag}`\n\n")
+        fh.write("Command: `bash tools/prof_run.sh " + tag + " ...` (kernel trace + stats pass; separate FETCH_SIZE "
+                 "and WRITE_SIZE PMC passes).  HBM bytes = 2 x FETCH_SIZE KiB + WRITE_SIZE KiB (gfx950 "
+                 "correction); memory-side counters include Infinity-Cache hits.\n\n")
+        fh.write("| kernel | calls | mean us | HBM read MB/launch | HBM write MB/launch | GB/s (PMC) |\n")
+        fh.write("|---|---|---|---|---|---|\n")
+        for name, calls, ns, fb, wb, tb in rows:
+            fh.write(f"| `{name}` | {calls} | {ns / 1e3:.2f} | {fb / 1e6 if fb else 0:.3f} | "
+                     f"{wb / 1e6 if wb else 0:.3f} | {tb / ns if tb else 0:.0f} |\n")
+        if bench_line:
+            fh.write("\nbench line of the traced run:\n\n```\n" + bench_line + "\n```\n")
+    print(open(os.path.join(out, f"{tag}_summary.md")).read())
+
+
+if __name__ == "__main__":
+    main()

@@ -32,6 +32,7 @@ VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_I
     0, -1, -2, -3, -4, -5, -6, -7)
 DTYPES = {"f32": 0, "bf16x2": 1}
 VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE = 1, 2
+VSS_CREATE_NO_AUTOTUNE = 1
 VSS_OUT_MODEL = 0
 
 
@@ -44,7 +45,7 @@ class VssError(RuntimeError):
 class _Config(ctypes.Structure):
     _fields_ = [("model_h", ctypes.c_int), ("model_w", ctypes.c_int), ("dtype", ctypes.c_int),
                 ("device_id", ctypes.c_int), ("max_batch", ctypes.c_int), ("max_frame_h", ctypes.c_int),
-                ("max_frame_w", ctypes.c_int), ("weights_path", ctypes.c_char_p)]
+                ("max_frame_w", ctypes.c_int), ("weights_path", ctypes.c_char_p), ("flags", ctypes.c_int)]
 
 
 class _Info(ctypes.Structure):
@@ -98,6 +99,7 @@ def lib() -> ctypes.CDLL:
                 "vss_layer_shape": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)], I),
                 "vss_read_layer": ([P, I, I, P], I),
                 "vss_profile_read": ([P, ctypes.POINTER(ctypes.c_double), I, ctypes.POINTER(I)], I),
+                "vss_layer_kernel": ([P, I, ctypes.c_char_p, I], I),
             }
             for name, (args, res) in sig.items():
                 fn = getattr(L, name)
@@ -131,12 +133,12 @@ class Session:
 
     def __init__(self, model_h: int = 144, model_w: int = 256, dtype: str = "bf16x2", device_id: int = 0,
                  max_batch: int = 8, max_frame_h: int = 1080, max_frame_w: int = 1920,
-                 weights_path: str | None = None):
+                 weights_path: str | None = None, autotune: bool = True):
         if dtype not in DTYPES:
             raise VssError(VSS_E_INVALID_ARG, f"dtype must be one of {sorted(DTYPES)}")
         self.weights_path = ensure_weights(weights_path or DEFAULT_WEIGHTS)
         cfg = _Config(model_h, model_w, DTYPES[dtype], device_id, max_batch, max_frame_h, max_frame_w,
-                      self.weights_path.encode())
+                      self.weights_path.encode(), 0 if autotune else 1)
         h = ctypes.c_void_p()
         _check(lib().vss_create(ctypes.byref(cfg), ctypes.byref(h)), None)
         self._h = h
@@ -218,6 +220,14 @@ class Session:
         c, h, w = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _check(lib().vss_layer_shape(self._h, layer, ctypes.byref(c), ctypes.byref(h), ctypes.byref(w)), self._h)
         return c.value, h.value, w.value
+
+    def layer_kernel(self, layer: int) -> str:
+        """The kernel running `layer`, named as rocprofv3 reports it."""
+        buf = ctypes.create_string_buffer(256)
+        rc = lib().vss_layer_kernel(self._h, layer, buf, 256)
+        if rc < 0:
+            _check(rc, self._h)
+        return buf.value.decode()
 
     def read_layer(self, layer: int, n: int) -> np.ndarray:
         """Layer output of the latest forward as NCHW float32 (oracle layout)."""

@@ -51,7 +51,7 @@ struct LayerPlan {
   size_t lds = 0;
   const BlockEntry* entry = nullptr;  // compiled shape (registry)
   float* act = nullptr;        // [max_batch][H][W][C]
-  float* part = nullptr;       // DEC: [max_batch][tiles][2][C]
+  int acc_off = -1;            // DEC: offset of its [2][C] norm accumulator in a frame's row of d_acc
   const float* wimg = nullptr;  // LDS weight image (block_lds regions w1..b2)
   int wimg_f4 = 0;
   const float *gamma = nullptr, *beta = nullptr;
@@ -75,6 +75,8 @@ struct vss_handle {
   std::vector<float> hdata;
   float eps = 1e-5f;
   std::vector<LayerPlan> L;
+  unsigned long long* d_acc = nullptr;  // decoder instance-norm accumulators [max_batch][acc_stride]
+  int acc_stride = 0;
   std::vector<void*> dev_allocs;
   size_t dev_bytes = 0;
   uint8_t* d_frames = nullptr;
@@ -136,6 +138,15 @@ size_t block_lds_bytes(const LayerPlan& l, int TH, int TW) {
   return (size_t)block_lds(l.mode, l.stride, TH, TW, (int)l.rec.cin, cskip, l.chid, l.C).total * 4;
 }
 
+void set_tile(LayerPlan& l, const BlockEntry* e) {
+  l.entry = e;
+  l.TH = e->TH;
+  l.TW = e->TW;
+  l.tiles_x = (l.W + l.TW - 1) / l.TW;
+  l.tiles_y = (l.H + l.TH - 1) / l.TH;
+  l.lds = block_lds_bytes(l, l.TH, l.TW);
+}
+
 // Tile choice among the compiled shapes for this layer (csrc/vss_registry.inc):
 // the largest tile that still gives >= 2 workgroups per CU (256 CUs) at
 // max_batch, preferring <= 64 KiB of LDS; otherwise the most workgroups.
@@ -161,13 +172,22 @@ int choose_tile(vss_handle* h, LayerPlan& l, int N) {
     return fail(h, VSS_E_UNSUPPORTED,
                 "no compiled kernel for this layer shape (regenerate csrc/vss_registry.inc with "
                 "tools/gen_registry.py and rebuild)");
-  l.entry = best;
-  l.TH = best->TH;
-  l.TW = best->TW;
-  l.tiles_x = (l.W + l.TW - 1) / l.TW;
-  l.tiles_y = (l.H + l.TH - 1) / l.TH;
-  l.lds = block_lds_bytes(l, l.TH, l.TW);
+  set_tile(l, best);
   return VSS_OK;
+}
+
+std::vector<const BlockEntry*> tile_candidates(const LayerPlan& l) {
+  int count = 0;
+  const BlockEntry* reg = block_registry(&count);
+  const int cskip = l.mode == MODE_DEC ? (int)l.rec.chid : 0;
+  std::vector<const BlockEntry*> out;
+  for (int i = 0; i < count; ++i) {
+    const BlockEntry& e = reg[i];
+    if (e.mode == l.mode && e.stride == l.stride && e.cin == (int)l.rec.cin && e.cskip == cskip && e.chid == l.chid &&
+        e.cout == l.C && e.flags == l.flags)
+      out.push_back(&e);
+  }
+  return out;
 }
 
 int load_weights(vss_handle* h) {
@@ -306,11 +326,17 @@ int upload(vss_handle* h) {
   }
   float* d_img = nullptr;
   if ((rc = dalloc(h, &d_img, img.size() * 4))) return rc;
+  int acc_total = 0;
+  for (const LayerPlan& l : h->L)
+    if (l.rec.kind == K_DEC) acc_total += 2 * l.C;
+  if ((rc = dalloc(h, &h->d_acc, (size_t)N * std::max(acc_total, 2) * 8))) return rc;
+  HIP_TRY(h, hipMemset(h->d_acc, 0, (size_t)N * std::max(acc_total, 2) * 8));
   if (!img.empty()) HIP_TRY(h, hipMemcpy(d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
   for (size_t i = 0; i < h->L.size(); ++i) {
     LayerPlan& l = h->L[i];
     const Rec& r = l.rec;
     if ((rc = dalloc(h, &l.act, (size_t)N * l.H * l.W * l.C * 4))) return rc;
+    HIP_TRY(h, hipMemset(l.act, 0, (size_t)N * l.H * l.W * l.C * 4));
     if (r.kind == K_STEM) {
       l.stem_w = dp(r.off[O_W1]);
       l.stem_b = dp(r.off[O_B1]);
@@ -320,7 +346,8 @@ int upload(vss_handle* h) {
       if (r.kind == K_DEC) {
         l.gamma = dp(r.off[O_GAMMA]);
         l.beta = dp(r.off[O_BETA]);
-        if ((rc = dalloc(h, &l.part, (size_t)N * l.tiles_x * l.tiles_y * 2 * l.C * 4))) return rc;
+        l.acc_off = h->acc_stride;
+        h->acc_stride += 2 * l.C;
       }
     } else if (r.kind == K_HEAD) {
       l.head_w = dp(r.off[O_W2]);
@@ -337,6 +364,38 @@ int check_frames(vss_handle* h, int n, int fh, int fw, int fc, size_t rs, size_t
   if (rs < (size_t)fw * fc) return fail(h, VSS_E_INVALID_ARG, "row_stride < width*channels");
   if (fs < rs * (size_t)fh) return fail(h, VSS_E_INVALID_ARG, "frame_stride < height*row_stride");
   return VSS_OK;
+}
+
+BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n) {
+  const Rec& r = l.rec;
+  const LayerPlan& src = h->L[r.src];
+  BlockParams p{};
+  p.wimg = l.wimg;
+  p.x = src.act;
+  p.y = l.act;
+  p.eps = h->eps;
+  p.N = n; p.H = l.inH; p.W = l.inW; p.Ho = l.H; p.Wo = l.W;
+  p.cin = (int)r.cin; p.cout = l.C; p.chid = l.chid; p.stride = l.stride;
+  p.TH = l.TH; p.TW = l.TW; p.tiles_x = l.tiles_x; p.tiles_y = l.tiles_y;
+  p.acc_stride = h->acc_stride;
+  if (r.kind == K_IR) {
+    p.relu6_dw = 1;
+    p.residual = (r.flags & F_RESIDUAL) ? 1 : 0;
+  } else {
+    const LayerPlan& sk = h->L[r.skip];
+    p.skip = sk.act;
+    p.cskip = (int)r.chid;
+    p.relu6_dw = 0;
+    p.out_acc = h->d_acc + l.acc_off;
+    p.norm_in = src.rec.kind == K_DEC ? 1 : 0;
+    if (p.norm_in) {
+      p.in_acc = h->d_acc + src.acc_off;
+      p.in_gamma = src.gamma;
+      p.in_beta = src.beta;
+      p.in_hw = src.H * src.W;
+    }
+  }
+  return p;
 }
 
 // Enqueue the whole forward on stream s (no sync, no alloc: graph-capturable).
@@ -367,41 +426,17 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       p.rx = (float)((double)fw / (double)Wm);
       p.w = l.stem_w; p.b = l.stem_b; p.y = l.act;
       p.Ho = l.H; p.Wo = l.W; p.cout = l.C;
+      p.acc_zero = h->d_acc;
+      p.acc_stride = h->acc_stride;
       go(stem_kernel16(), dim3((l.W + 31) / 32, (l.H + 7) / 8, n), 0, p);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
-      const LayerPlan& src = h->L[r.src];
-      BlockParams p{};
-      p.wimg = l.wimg;
-      p.x = src.act;
-      p.y = l.act;
-      p.eps = h->eps;
-      p.N = n; p.H = l.inH; p.W = l.inW; p.Ho = l.H; p.Wo = l.W;
-      p.cin = (int)r.cin; p.cout = l.C; p.chid = l.chid; p.stride = l.stride;
-      p.TH = l.TH; p.TW = l.TW; p.tiles_x = l.tiles_x; p.tiles_y = l.tiles_y;
-      if (r.kind == K_IR) {
-        p.relu6_dw = 1;
-        p.residual = (r.flags & F_RESIDUAL) ? 1 : 0;
-      } else {
-        const LayerPlan& sk = h->L[r.skip];
-        p.skip = sk.act;
-        p.cskip = (int)r.chid;
-        p.relu6_dw = 0;
-        p.out_part = l.part;
-        p.norm_in = src.rec.kind == K_DEC ? 1 : 0;
-        if (p.norm_in) {
-          p.in_part = src.part;
-          p.in_gamma = src.gamma;
-          p.in_beta = src.beta;
-          p.in_tiles = src.tiles_x * src.tiles_y;
-          p.in_hw = src.H * src.W;
-        }
-      }
+      const BlockParams p = block_params(h, l, n);
       go(l.entry->fn[prec == PREC_F32 ? 0 : 1], dim3(l.tiles_x, l.tiles_y, n), l.lds, p);
     } else if (r.kind == K_HEAD) {
       const LayerPlan& src = h->L[r.src];
       HeadParams p{};
-      p.x = src.act; p.in_part = src.part; p.gamma = src.gamma; p.beta = src.beta;
-      p.in_tiles = src.tiles_x * src.tiles_y; p.eps = h->eps;
+      p.x = src.act; p.in_acc = h->d_acc + src.acc_off; p.acc_stride = h->acc_stride;
+      p.gamma = src.gamma; p.beta = src.beta; p.eps = h->eps;
       p.w = l.head_w; p.b = l.head_b; p.mask = masks;
       p.N = n; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
       go(head_kernel16(), dim3((Wm + 63) / 64, (Hm + 15) / 16, n), 0, p);
@@ -511,6 +546,52 @@ void async_done(void* p) {
   delete c;
 }
 
+// Autotune: time every compiled tile of every block layer at max_batch on
+// this device and keep the fastest.  The kernels' arithmetic does not depend
+// on the tile (see block_lds), so this changes speed only, never results.
+int autotune(vss_handle* h) {
+  const int N = h->cfg.max_batch;
+  const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIP_TRY(h, hipEventCreate(&e0));
+  HIP_TRY(h, hipEventCreate(&e1));
+  int rc = VSS_OK;
+  for (LayerPlan& l : h->L) {
+    if (l.mode < 0) continue;
+    const std::vector<const BlockEntry*> cands = tile_candidates(l);
+    if (cands.size() < 2) continue;
+    const BlockEntry* best = l.entry;
+    float best_ms = 1e30f;
+    for (const BlockEntry* e : cands) {
+      set_tile(l, e);
+      if (hipFuncSetAttribute((const void*)e->fn[pi], hipFuncAttributeMaxDynamicSharedMemorySize, (int)l.lds) !=
+          hipSuccess)
+        continue;
+      const BlockParams p = block_params(h, l, N);
+      const dim3 grid(l.tiles_x, l.tiles_y, N);
+      for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(kThreads), l.lds, h->stream, p);
+      (void)hipEventRecord(e0, h->stream);
+      for (int k = 0; k < 8; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(kThreads), l.lds, h->stream, p);
+      (void)hipEventRecord(e1, h->stream);
+      float ms = 0.f;
+      if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess ||
+          hipGetLastError() != hipSuccess) {
+        rc = fail(h, VSS_E_HIP, "autotune launch failed");
+        break;
+      }
+      if (ms < best_ms * 0.98f) {  // ties keep the earlier (planner-preferred) shape
+        best_ms = ms;
+        best = e;
+      }
+    }
+    set_tile(l, best);
+    if (rc) break;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -568,6 +649,7 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
     if (hipEventCreate(&e) != hipSuccess) return bail(fail(h, VSS_E_HIP, "hipEventCreate failed"));
   h->slot_pending.assign(vss_handle::kSlots, 0);
   h->prof_sum.assign(nl, 0.0);
+  if (!(cfg->flags & VSS_CREATE_NO_AUTOTUNE) && (rc = autotune(h))) return bail(rc);
   *out = h;
   return VSS_OK;
 }
@@ -682,6 +764,23 @@ int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww) {
   if (hh) *hh = h->L[layer].H;
   if (ww) *ww = h->L[layer].W;
   return VSS_OK;
+}
+
+int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap) {
+  if (!h || layer < 0 || layer >= (int)h->L.size() || !buf || cap < 1) return VSS_E_INVALID_ARG;
+  const LayerPlan& l = h->L[layer];
+  const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
+  char tmp[160];
+  if (l.rec.kind == K_STEM) std::snprintf(tmp, sizeof(tmp), "void vss::k_stem<16>(vss::StemParams)");
+  else if (l.rec.kind == K_HEAD) std::snprintf(tmp, sizeof(tmp), "void vss::k_head<16>(vss::HeadParams)");
+  else {
+    const BlockEntry* e = l.entry;
+    std::snprintf(tmp, sizeof(tmp), "void vss::k_block<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>(vss::BlockParams)",
+                  e->mode, e->stride, e->TH, e->TW, e->cin, e->cskip, e->chid, e->cout, e->flags, prec);
+  }
+  const int len = (int)std::strlen(tmp);
+  std::snprintf(buf, (size_t)cap, "%s", tmp);
+  return len;
 }
 
 int vss_read_layer(vss_handle* h, int layer, int n, float* host_out) {

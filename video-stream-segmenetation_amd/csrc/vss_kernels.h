@@ -28,7 +28,7 @@ __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 // can never disagree.  Every region is a multiple of 4 floats (16-B aligned).
 struct BlockLds {
   int IH, IW, P_in, P_in_pad, P_out, CX, XS, LD1, LD2, SR, SC;
-  int NCB, NPB, NCHUNK, PW, CS, NPBW, NACC;
+  int NCB, NPB, NCHUNK, PW, CS, NPBW, NACC;  // CS = chunk groups, PW = pixel-block groups
   int xt, w1, w2, wdw, bdw, b1, b2, lr, nrm, work, stt, total;
   int slab_stride;  // floats per wave slab = P_out * (cout + 4)
 };
@@ -50,12 +50,14 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   L.NCB = cout / 16;
   L.NPB = L.P_out / 16;
   L.NCHUNK = chid / 16;
-  // work split: EXPAND -> the 4 waves split the hidden chunks (each wave covers
-  // every pixel block); DIRECT/DEC -> waves split pixel blocks first (PW ways),
-  // then chunks (CS ways).
-  L.PW = mode == 0 /*EXPAND*/ ? 1 : (L.NPB >= 4 ? 4 : L.NPB);
-  L.CS = 4 / (L.PW > 0 ? L.PW : 1);
-  L.NPBW = mode == 0 ? L.NPB : L.NPB / (L.PW > 0 ? L.PW : 1);
+  // work split: the 16-channel chunks are dealt to CS = GC groups of waves,
+  // GC in {1, 2, 4} fixed by the channel count alone (so the order in which a
+  // pixel's partial sums are added never depends on the tile: results are
+  // bitwise identical for every tile the planner may pick); the remaining
+  // PW = 4 / GC waves of a group split the pixel blocks.  EXPAND has GC = 4.
+  L.CS = L.NCHUNK >= 4 ? 4 : (L.NCHUNK >= 2 ? 2 : 1);
+  L.PW = 4 / L.CS;
+  L.NPBW = L.NPB / L.PW;
   L.NACC = L.NPBW * L.NCB;
   L.slab_stride = L.P_out * (cout + 4);
   int o = 0;
@@ -71,7 +73,7 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   // per-wave scratch during the main loop, reused as the accumulator slabs after it
   L.work = o;
   o += cmax(4 * (mode == 0 ? (L.P_in_pad + L.P_out) * 16 : 256), L.CS * L.slab_stride);
-  L.stt = o; o += 512;
+  L.stt = o; o += 1024;  // 4 KiB: stats scratch (int64 pairs)
   L.total = o;
   return L;
 }
@@ -92,15 +94,18 @@ struct BlockParams {
   const float* bdw;
   const void* w2;        // project [cout][chid or ccat]
   const float* b2;       // [cout]
-  // instance norm on the input (DEC whose src is DEC): src partial stats
-  const float* in_part;  // [N][in_tiles][2][cin]
-  const float* in_gamma;
+  // Instance norm, exact and order-free: every decoder workgroup adds the
+  // fixed-point sums of its tile's outputs (sum v*2^32, sum v^2*2^24, int64)
+  // to its frame's accumulator with device-scope atomics; the consumer (the
+  // next kernel) turns the totals into scale/shift.  The stem kernel zeroes
+  // the accumulators of every frame at the start of each forward.
+  const unsigned long long* in_acc;  // DEC with norm_in: src accumulator [N][acc_stride] + src offset
+  const float* in_gamma;             // src layer's norm affine [cin]
   const float* in_beta;
-  int in_tiles;          // tiles per frame of the producer
-  int in_hw;             // pixels per frame of the producer
+  int in_hw;                         // pixels per frame of the src
+  unsigned long long* out_acc;       // DEC: this layer's accumulator [N][acc_stride] + offset ([2][cout])
+  int acc_stride;                    // int64 elements per frame over all decoder layers
   float eps;
-  // instance norm stats of this layer's output (DEC)
-  float* out_part;       // [N][tiles_y*tiles_x][2][cout]
   int N, H, W;           // input spatial (IR: x dims; DEC: skip/output dims)
   int Ho, Wo;            // output spatial
   int cin, cskip, chid, cout;   // chid = hidden (IR expand) or channels fed to dw
@@ -132,14 +137,16 @@ struct StemParams {
   const float* b;
   float* y;              // [N][Ho][Wo][cout]
   int Ho, Wo, cout;
+  unsigned long long* acc_zero;  // all decoder norm accumulators [N][acc_stride]: zeroed here
+  int acc_stride;
 };
 
 struct HeadParams {
   const float* x;        // pre-norm dec output [N][h][w][cin]
-  const float* in_part;  // [N][in_tiles][2][cin]
-  const float* gamma;
+  const unsigned long long* in_acc;  // its norm accumulator (see BlockParams), frame stride acc_stride
+  int acc_stride;
+  const float* gamma;    // its norm affine [cin]
   const float* beta;
-  int in_tiles;
   float eps;
   const float* w;        // [cin]
   float b;
@@ -147,6 +154,18 @@ struct HeadParams {
   int N, h, w_, cin;
   int Hm, Wm;
 };
+
+// Instance-norm scale/shift of one channel from the exact fixed-point totals.
+__host__ __device__ inline void norm_affine(unsigned long long s_fx, unsigned long long q_fx, int hw, float eps,
+                                            float gamma, float beta, float* scale, float* shift) {
+  const double mean = (double)(long long)s_fx * 0x1p-32 / (double)hw;
+  const double ex2 = (double)(long long)q_fx * 0x1p-24 / (double)hw;
+  const double var = ex2 - mean * mean > 0.0 ? ex2 - mean * mean : 0.0;
+  const float rstd = (float)(1.0 / __builtin_sqrt(var + (double)eps));
+  const float sc = rstd * gamma;
+  *scale = sc;
+  *shift = beta - (float)mean * sc;
+}
 
 struct PrepParams {      // standalone preprocess: frames -> [N][3][Hm][Wm] f32
   const uint8_t* frames;

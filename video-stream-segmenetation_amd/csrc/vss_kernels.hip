@@ -162,6 +162,9 @@ __global__ __launch_bounds__(256) void k_stem(StemParams p) {
       xs[2][ly][lx] = valid ? o[2] : 0.f;
     }
   }
+  // start of the forward: zero this frame's decoder norm accumulators
+  if (blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = tid; i < p.acc_stride; i += 256) p.acc_zero[(long)n * p.acc_stride + i] = 0ull;
   for (int i = tid; i < COUT * 27; i += 256) ws[i] = p.w[i];
   if (tid < COUT) bs[tid] = p.b[tid];
   __syncthreads();
@@ -248,90 +251,50 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// Instance-norm scale/shift of one frame from the producer's per-tile partial
-// sums part_n[T][2][C], reduced in a fixed order (bitwise reproducible).
-// tmp: 512 floats of LDS.  Ends with a workgroup barrier.
-__device__ __forceinline__ void norm_from_partials(const float* __restrict__ part_n, int T, int C, int hw, float eps,
-                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                   float* tmp, float* scale, float* shift) {
-  const int tid = threadIdx.x;
-  const int G = 256 / C, c = tid % C, gg = tid / C;
-  if (gg < G) {
-    float s = 0.f, q = 0.f;
-    for (int t0 = gg; t0 < T; t0 += 8 * G) {
-      float vs[8], vq[8];
+// Registers holding one thread's share of a TOTAL-item (16-B items) copy.
+// issue(): every load of the copy in flight (unconditional at clamped indices:
+// a conditional load makes hipcc branch and wait per element); commit():
+// consume them (waits land at the first use).  Issuing several copies before
+// committing any costs one memory round trip instead of one per copy.
+template <int TOTAL>
+struct Staged {
+  static constexpr int PER = (TOTAL + 255) / 256;
+  f4 v[PER > 0 ? PER : 1];
+  template <class Load>
+  __device__ __forceinline__ void issue(Load ld) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int t = min(t0 + u * G, T - 1);
-        vs[u] = part_n[(2 * t) * C + c];
-        vq[u] = part_n[(2 * t + 1) * C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (t0 + u * G < T) {
-          s += vs[u];
-          q += vq[u];
-        }
-    }
-    tmp[gg * C + c] = s;
-    tmp[256 + gg * C + c] = q;
-  }
-  __syncthreads();
-  if (tid < C) {
-    float s = 0.f, q = 0.f;
-    for (int k = 0; k < G; ++k) {
-      s += tmp[k * C + tid];
-      q += tmp[256 + k * C + tid];
-    }
-    const float inv = 1.0f / (float)hw;
-    const float mean = s * inv;
-    const float var = fmaxf(q * inv - mean * mean, 0.f);
-    const float rstd = 1.0f / sqrtf(var + eps);
-    const float sc = rstd * gamma[tid];
-    scale[tid] = sc;
-    shift[tid] = beta[tid] - mean * sc;
-  }
-  __syncthreads();
-}
-
-// Copy TOTAL 16-B items (a compile-time count) with up to UMAX loads in flight
-// per thread before any store.  Loads are unconditional at clamped indices (a
-// conditional load makes hipcc branch and wait per element), stores guarded.
-template <int TOTAL, int UMAX = 8, class Load, class Store>
-__device__ __forceinline__ void copy_n(Load ld, Store st) {
-  constexpr int PER = (TOTAL + 255) / 256;
-  constexpr int U = PER < UMAX ? PER : UMAX;
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int b = 0; b < PER; b += U) {
-    f4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = tid + 256 * (b + u);
+    for (int u = 0; u < PER; ++u) {
+      const int i = (int)threadIdx.x + 256 * u;
       v[u] = ld(i < TOTAL ? i : TOTAL - 1);
     }
+  }
+  template <class Store>
+  __device__ __forceinline__ void commit(Store st) const {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = tid + 256 * (b + u);
-      if (b + u < PER && i < TOTAL) st(i, v[u]);
+    for (int u = 0; u < PER; ++u) {
+      const int i = (int)threadIdx.x + 256 * u;
+      if (i < TOTAL) st(i, v[u]);
     }
   }
-}
+};
 
 // Fused inverted-residual / decoder block, specialised on its whole shape
 // (every tile and channel extent a compile-time constant: index math folds
 // to shifts/multiplies, loops unroll, accumulators stay in registers).
-//  prologue : the layer's weight image -> LDS (pointwise weights as bf16,
-//             exact), input tile (+halo, zeros outside the image) -> LDS;
-//             decoder: the normalised low-res src region -> LDS, then the 2x
-//             bilinear upsample ++ skip concat tile built from it.
+//  prologue : every global load of the block issued first (the layer's weight
+//             image, the input tile + halo, or for the decoder the low-res src
+//             region, the skip tile and the src's norm scale/shift), then
+//             committed to LDS; the decoder builds the 2x bilinear upsample
+//             (norm + ReLU on the fly) ++ skip concat tile.
 //  main     : independent per-wave work units, wave-level syncs only.
 //             EXPAND: unit = 16 hidden channels: expand (MFMA) over the whole
 //             input tile -> dw 3x3 (VALU) -> project (MFMA) into acc.
 //             DIRECT/DEC: unit = (16 output pixels, 16 channels): dw -> project.
 //  epilogue : per-wave accumulator slabs in LDS summed in a fixed order
-//             (deterministic), + bias (+ residual), coalesced NHWC stores,
-//             decoder instance-norm partial sums per tile.
+//             (deterministic), + bias (+ residual), coalesced NHWC stores;
+//             decoder: per-tile instance-norm partial sums, and the last
+//             workgroup of each frame to arrive reduces them (fixed order) into
+//             the frame's scale/shift for the consumer.
 template <int MODE, int STRIDE, int TH, int TW, int CIN, int CSKIP, int CH, int COUT, int FLAGS, int PREC>
 __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   constexpr BlockLds L = block_lds(MODE, STRIDE, TH, TW, CIN, CSKIP, CH, COUT);
@@ -343,6 +306,8 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   static_assert(CIN % 16 == 0 && CH % 16 == 0 && COUT % 16 == 0 && P_OUT % 16 == 0, "shape");
   static_assert(MODE != MODE_IR_EXPAND || CIN <= 64, "expand cin <= 64");
   static_assert(!RES || (STRIDE == 1 && CIN == COUT && MODE != MODE_DEC), "residual shape");
+  static_assert(MODE != MODE_IR_EXPAND || CS == 4, "expand deals its chunks to the 4 waves");
+  static_assert(NPB % PW == 0, "pixel blocks must split evenly over the wave groups");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -360,54 +325,58 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   float* work = smem + L.work;
   float* stt = smem + L.stt;
 
-  // ---- prologue 1: the layer's weight image -> LDS ----
-  {
-    constexpr int WIMG_F4 = (L.lr - L.w1) / 4;
-    const f4* src = reinterpret_cast<const f4*>(p.wimg);
-    f4* dst = reinterpret_cast<f4*>(smem + L.w1);
-    copy_n<WIMG_F4>([&](int i) { return src[i]; }, [&](int i, f4 v) { dst[i] = v; });
-  }
-
-  // ---- prologue 2: the input tile ----
+  // ---- prologue: issue every load, then commit to LDS ----
+  constexpr int WIMG_F4 = (L.lr - L.w1) / 4;
+  const f4* wsrc = reinterpret_cast<const f4*>(p.wimg);
+  f4* wdst = reinterpret_cast<f4*>(smem + L.w1);
   if constexpr (MODE == MODE_DEC) {
     constexpr int CL = CIN, C4L = CL / 4, C4S = CSKIP / 4, SR = L.SR, SC = L.SC;
     const int h = p.H, w = p.W;
     float* lr = smem + L.lr;
     float* nrm = smem + L.nrm;
-    if constexpr (NORM_IN)
-      norm_from_partials(p.in_part + (long)n * p.in_tiles * 2 * CL, p.in_tiles, CL, p.in_hw, p.eps, p.in_gamma,
-                         p.in_beta, stt, nrm, nrm + CL);
-    // low-res src region, normalised + ReLU'd once per src pixel
     const int sy0 = max(0, (oy0 - 1) / 2 - 1), sx0 = max(0, (ox0 - 1) / 2 - 1);
     const float* xn = p.x + (long)n * h * w * CL;
-    copy_n<SR * SC * C4L>(
-        [&](int i) {
-          const int pr = i / C4L, c4 = i % C4L;
-          const int yy = min(h - 1, sy0 + pr / SC), xx = min(w - 1, sx0 + pr % SC);
-          return *reinterpret_cast<const f4*>(xn + ((long)yy * w + xx) * CL + 4 * c4);
-        },
-        [&](int i, f4 v) {
-          const int c4 = i % C4L;
-          if constexpr (NORM_IN)
-            v = reluv(v * *reinterpret_cast<const f4*>(nrm + 4 * c4) + *reinterpret_cast<const f4*>(nrm + CL + 4 * c4));
-          *reinterpret_cast<f4*>(lr + 4 * i) = v;
-        });
-    // skip channels of the concat tile (zeros outside the image)
     const float* sn = p.skip + (long)n * Ho * Wo * CSKIP;
-    copy_n<P_IN_PAD * C4S>(
-        [&](int i) {
-          const int pix = i / C4S, c4 = i % C4S;
-          const int yy = min(max(iy0 + pix / IW, 0), Ho - 1), xx = min(max(ix0 + pix % IW, 0), Wo - 1);
-          return *reinterpret_cast<const f4*>(sn + ((long)yy * Wo + xx) * CSKIP + 4 * c4);
-        },
-        [&](int i, f4 v) {
-          const int pix = i / C4S, c4 = i % C4S;
-          const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
-          const bool valid = pix < P_IN && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo;
-          *reinterpret_cast<f4*>(xt + pix * XS + CL + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
-        });
+    // src instance norm: this thread's 2 channels of exact totals (issued first)
+    ulonglong2 acc_s = {0ull, 0ull}, acc_q = {0ull, 0ull};
+    if constexpr (NORM_IN) {
+      const ulonglong2* ia = reinterpret_cast<const ulonglong2*>(p.in_acc + (long)n * p.acc_stride);
+      const int k = tid < CL / 2 ? tid : 0;
+      acc_s = ia[k];
+      acc_q = ia[CL / 2 + k];
+    }
+    Staged<SR * SC * C4L> st_lr;
+    Staged<P_IN_PAD * C4S> st_sk;
+    Staged<WIMG_F4> st_w;
+    st_lr.issue([&](int i) {
+      const int pr = i / C4L, c4 = i % C4L;
+      const int yy = min(h - 1, sy0 + pr / SC), xx = min(w - 1, sx0 + pr % SC);
+      return *reinterpret_cast<const f4*>(xn + ((long)yy * w + xx) * CL + 4 * c4);
+    });
+    st_sk.issue([&](int i) {
+      const int pix = i / C4S, c4 = i % C4S;
+      const int yy = min(max(iy0 + pix / IW, 0), Ho - 1), xx = min(max(ix0 + pix % IW, 0), Wo - 1);
+      return *reinterpret_cast<const f4*>(sn + ((long)yy * Wo + xx) * CSKIP + 4 * c4);
+    });
+    st_w.issue([&](int i) { return wsrc[i]; });
+    if constexpr (NORM_IN)
+      if (tid < CL / 2) {
+        norm_affine(acc_s.x, acc_q.x, p.in_hw, p.eps, p.in_gamma[2 * tid], p.in_beta[2 * tid], nrm + 2 * tid,
+                    nrm + CL + 2 * tid);
+        norm_affine(acc_s.y, acc_q.y, p.in_hw, p.eps, p.in_gamma[2 * tid + 1], p.in_beta[2 * tid + 1],
+                    nrm + 2 * tid + 1, nrm + CL + 2 * tid + 1);
+      }
+    st_lr.commit([&](int i, f4 v) { reinterpret_cast<f4*>(lr)[i] = v; });
+    st_sk.commit([&](int i, f4 v) {
+      const int pix = i / C4S, c4 = i % C4S;
+      const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
+      const bool valid = pix < P_IN && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo;
+      *reinterpret_cast<f4*>(xt + pix * XS + CL + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+    });
+    st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     __syncthreads();
     // upsampled channels: PyTorch upsample_bilinear2d(scale 2, align_corners=False)
+    // of relu(src * scale + shift) (the src's instance norm, applied per tap)
 #pragma unroll
     for (int k = 0; k < (P_IN_PAD * C4L + 255) / 256; ++k) {
       const int i = tid + 256 * k;
@@ -424,10 +393,18 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
           const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
           const int r0 = min(max(y0 - sy0, 0), SR - 1), r1 = min(max(y1 - sy0, 0), SR - 1);
           const int q0 = min(max(x0 - sx0, 0), SC - 1), q1 = min(max(x1 - sx0, 0), SC - 1);
-          const f4 v00 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q0) * CL + 4 * c4);
-          const f4 v01 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q1) * CL + 4 * c4);
-          const f4 v10 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q0) * CL + 4 * c4);
-          const f4 v11 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q1) * CL + 4 * c4);
+          f4 v00 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q0) * CL + 4 * c4);
+          f4 v01 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q1) * CL + 4 * c4);
+          f4 v10 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q0) * CL + 4 * c4);
+          f4 v11 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q1) * CL + 4 * c4);
+          if constexpr (NORM_IN) {
+            const f4 sc = *reinterpret_cast<const f4*>(nrm + 4 * c4);
+            const f4 sh = *reinterpret_cast<const f4*>(nrm + CL + 4 * c4);
+            v00 = reluv(v00 * sc + sh);
+            v01 = reluv(v01 * sc + sh);
+            v10 = reluv(v10 * sc + sh);
+            v11 = reluv(v11 * sc + sh);
+          }
           v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
         }
         *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
@@ -437,18 +414,21 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
     constexpr int C4 = CIN / 4;
     const int H = p.H, W = p.W;
     const float* xn = p.x + (long)n * H * W * CIN;
-    copy_n<P_IN_PAD * C4>(
-        [&](int i) {
-          const int pix = i / C4, c4 = i % C4;
-          const int yy = min(max(iy0 + pix / IW, 0), H - 1), xx = min(max(ix0 + pix % IW, 0), W - 1);
-          return *reinterpret_cast<const f4*>(xn + ((long)yy * W + xx) * CIN + 4 * c4);
-        },
-        [&](int i, f4 v) {
-          const int pix = i / C4, c4 = i % C4;
-          const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
-          const bool valid = pix < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
-          *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
-        });
+    Staged<P_IN_PAD * C4> st_x;
+    Staged<WIMG_F4> st_w;
+    st_x.issue([&](int i) {
+      const int pix = i / C4, c4 = i % C4;
+      const int yy = min(max(iy0 + pix / IW, 0), H - 1), xx = min(max(ix0 + pix % IW, 0), W - 1);
+      return *reinterpret_cast<const f4*>(xn + ((long)yy * W + xx) * CIN + 4 * c4);
+    });
+    st_w.issue([&](int i) { return wsrc[i]; });
+    st_x.commit([&](int i, f4 v) {
+      const int pix = i / C4, c4 = i % C4;
+      const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
+      const bool valid = pix < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+    });
+    st_w.commit([&](int i, f4 v) { wdst[i] = v; });
   }
   __syncthreads();
 
@@ -573,34 +553,34 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
     }
   }
   if constexpr (MODE == MODE_DEC) {
+    // this tile's exact fixed-point sums, added to the frame's accumulator
+    // (integer adds are associative: the totals do not depend on the tiling
+    // or on the order the workgroups arrive in)
     __syncthreads();
     constexpr int G = 256 / COUT;
+    long long* st64 = reinterpret_cast<long long*>(stt);
     const int c = tid % COUT, gg = tid / COUT;
     if (gg < G) {
-      float s = 0.f, q = 0.f;
+      long long s = 0, q = 0;
 #pragma unroll
       for (int pix = 0; pix < P_OUT; pix += G) {
         if (pix + gg < P_OUT) {
           const float v = work[(pix + gg) * RS + c];
-          s += v;
-          q += v * v;
+          s += (long long)__builtin_rintf(v * 0x1p32f);
+          q += (long long)__builtin_rintf(v * v * 0x1p24f);
         }
       }
-      stt[gg * COUT + c] = s;
-      stt[256 + gg * COUT + c] = q;
+      st64[gg * COUT + c] = s;
+      st64[256 + gg * COUT + c] = q;
     }
     __syncthreads();
-    if (tid < COUT) {
-      float s = 0.f, q = 0.f;
+    if (tid < 2 * COUT) {
+      const int base = tid < COUT ? tid : 256 + (tid - COUT);
+      long long t = 0;
 #pragma unroll
-      for (int k = 0; k < G; ++k) {
-        s += stt[k * COUT + tid];
-        q += stt[256 + k * COUT + tid];
-      }
-      const int tile = blockIdx.y * p.tiles_x + blockIdx.x;
-      float* op = p.out_part + ((long)n * p.tiles_x * p.tiles_y + tile) * 2 * COUT;
-      op[tid] = s;
-      op[COUT + tid] = q;
+      for (int k = 0; k < G; ++k) t += st64[base + k * COUT];
+      __hip_atomic_fetch_add(p.out_acc + (long)n * p.acc_stride + tid, (unsigned long long)t, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -612,7 +592,6 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
   constexpr int OTH = 16, OTW = 64, ZR = 10, ZC = 34, ZCP = 35, NZ = (ZR * ZC + 255) / 256;
   __shared__ float z[ZR][ZCP];
   __shared__ float sc[C], sh[C], wv[C];
-  __shared__ float tmp[512];
   const int tid = threadIdx.x, n = blockIdx.z;
   const int oy0 = blockIdx.y * OTH, ox0 = blockIdx.x * OTW;
   const int h = p.h, w = p.w_;
@@ -628,9 +607,12 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
 #pragma unroll
     for (int q = 0; q < C / 4; ++q) xv[u][q] = px[q];
   }
-  for (int c = tid; c < C; c += 256) wv[c] = p.w[c];
-  norm_from_partials(p.in_part + (long)n * p.in_tiles * 2 * C, p.in_tiles, C, h * w, p.eps, p.gamma, p.beta, tmp,
-                     sc, sh);
+  if (tid < C) {
+    wv[tid] = p.w[tid];
+    const unsigned long long* ia = p.in_acc + (long)n * p.acc_stride;
+    norm_affine(ia[tid], ia[C + tid], h * w, p.eps, p.gamma[tid], p.beta[tid], sc + tid, sh + tid);
+  }
+  __syncthreads();
 #pragma unroll
   for (int u = 0; u < NZ; ++u) {
     const int i = tid + 256 * u;

@@ -1,0 +1,284 @@
+// vss_napi.cc — thin Node-API addon over the C ABI (include/vss.h).
+//
+// Replaces, for the TypeScript host, ORT-web's JS<->WASM glue
+// (/root/reference/client/public/ort-wasm-simd-threaded.mjs:50-53, the
+// _OrtCreateSession/_OrtRun/_OrtGetLastError exports behind
+// InferenceSession.run).  Exports:
+//   version() -> number
+//   create(opts) -> handle            (opts: modelH, modelW, dtype, deviceId, maxBatch,
+//                                       maxFrameH, maxFrameW, weightsPath, autotune)
+//   info(handle) -> {maskW, maskH, nLayers, deviceBytes}
+//   segment(handle, frames: Uint8Array|Uint8ClampedArray, n, height, width, channels, rowStride)
+//       -> Promise<Float32Array>      (n * maskH * maskW masks; rejects with Error(vss_last_error))
+//   destroy(handle)
+// segment runs vss_segment on a libuv worker thread (napi_create_async_work),
+// so the event loop is not blocked — as `await session.run` does not block.
+#include <node_api.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "../../../include/vss.h"
+
+namespace {
+
+#define NAPI_OK(env, call)                                                   \
+  do {                                                                       \
+    if ((call) != napi_ok) {                                                 \
+      napi_throw_error((env), nullptr, "node-api call failed: " #call);      \
+      return nullptr;                                                        \
+    }                                                                        \
+  } while (0)
+
+struct Handle {
+  vss_handle* h = nullptr;
+  int mask_h = 0, mask_w = 0;
+};
+
+void finalize_handle(napi_env, void* data, void*) {
+  Handle* hd = static_cast<Handle*>(data);
+  if (hd->h) vss_destroy(hd->h);
+  delete hd;
+}
+
+Handle* get_handle(napi_env env, napi_value v) {
+  void* p = nullptr;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, nullptr, "expected a vss handle");
+    return nullptr;
+  }
+  Handle* hd = static_cast<Handle*>(p);
+  if (!hd->h) {
+    napi_throw_error(env, nullptr, "vss handle already destroyed");
+    return nullptr;
+  }
+  return hd;
+}
+
+bool get_int_prop(napi_env env, napi_value obj, const char* key, int* out) {
+  bool has = false;
+  if (napi_has_named_property(env, obj, key, &has) != napi_ok || !has) return false;
+  napi_value v;
+  napi_get_named_property(env, obj, key, &v);
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  if (t == napi_boolean) {
+    bool b = false;
+    napi_get_value_bool(env, v, &b);
+    *out = b ? 1 : 0;
+    return true;
+  }
+  return napi_get_value_int32(env, v, out) == napi_ok;
+}
+
+bool get_str_prop(napi_env env, napi_value obj, const char* key, std::string* out) {
+  bool has = false;
+  if (napi_has_named_property(env, obj, key, &has) != napi_ok || !has) return false;
+  napi_value v;
+  napi_get_named_property(env, obj, key, &v);
+  size_t len = 0;
+  if (napi_get_value_string_utf8(env, v, nullptr, 0, &len) != napi_ok) return false;
+  out->resize(len);
+  napi_get_value_string_utf8(env, v, &(*out)[0], len + 1, &len);
+  return true;
+}
+
+napi_value Version(napi_env env, napi_callback_info) {
+  napi_value r;
+  NAPI_OK(env, napi_create_int32(env, vss_version(), &r));
+  return r;
+}
+
+napi_value Create(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  vss_config cfg{};
+  cfg.model_h = 144; cfg.model_w = 256; cfg.dtype = VSS_DTYPE_BF16X2; cfg.device_id = 0;
+  cfg.max_batch = 8; cfg.max_frame_h = 1080; cfg.max_frame_w = 1920;
+  std::string weights, dtype;
+  int autotune = 1;
+  if (argc >= 1) {
+    get_int_prop(env, argv[0], "modelH", &cfg.model_h);
+    get_int_prop(env, argv[0], "modelW", &cfg.model_w);
+    get_int_prop(env, argv[0], "deviceId", &cfg.device_id);
+    get_int_prop(env, argv[0], "maxBatch", &cfg.max_batch);
+    get_int_prop(env, argv[0], "maxFrameH", &cfg.max_frame_h);
+    get_int_prop(env, argv[0], "maxFrameW", &cfg.max_frame_w);
+    get_int_prop(env, argv[0], "autotune", &autotune);
+    get_str_prop(env, argv[0], "weightsPath", &weights);
+    if (get_str_prop(env, argv[0], "dtype", &dtype)) {
+      if (dtype == "f32") cfg.dtype = VSS_DTYPE_F32;
+      else if (dtype == "bf16x2") cfg.dtype = VSS_DTYPE_BF16X2;
+      else {
+        napi_throw_range_error(env, nullptr, "dtype must be 'f32' or 'bf16x2'");
+        return nullptr;
+      }
+    }
+  }
+  cfg.weights_path = weights.c_str();
+  cfg.flags = autotune ? 0 : VSS_CREATE_NO_AUTOTUNE;
+  vss_handle* h = nullptr;
+  const int rc = vss_create(&cfg, &h);
+  if (rc != VSS_OK) {
+    const std::string msg = "vss_create failed (" + std::to_string(rc) + "): " + vss_last_error(nullptr);
+    napi_throw_error(env, std::to_string(rc).c_str(), msg.c_str());
+    return nullptr;
+  }
+  Handle* hd = new Handle();
+  hd->h = h;
+  vss_info inf{};
+  vss_get_info(h, &inf);
+  hd->mask_h = inf.mask_h;
+  hd->mask_w = inf.mask_w;
+  napi_value ext;
+  NAPI_OK(env, napi_create_external(env, hd, finalize_handle, nullptr, &ext));
+  return ext;
+}
+
+napi_value Info(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Handle* hd = get_handle(env, argv[0]);
+  if (!hd) return nullptr;
+  vss_info inf{};
+  vss_get_info(hd->h, &inf);
+  napi_value o, v;
+  NAPI_OK(env, napi_create_object(env, &o));
+  napi_create_int32(env, inf.mask_w, &v);
+  napi_set_named_property(env, o, "maskW", v);
+  napi_create_int32(env, inf.mask_h, &v);
+  napi_set_named_property(env, o, "maskH", v);
+  napi_create_int32(env, inf.n_layers, &v);
+  napi_set_named_property(env, o, "nLayers", v);
+  napi_create_double(env, (double)inf.device_bytes, &v);
+  napi_set_named_property(env, o, "deviceBytes", v);
+  return o;
+}
+
+napi_value Destroy(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  void* p = nullptr;
+  if (napi_get_value_external(env, argv[0], &p) == napi_ok && p) {
+    Handle* hd = static_cast<Handle*>(p);
+    if (hd->h) vss_destroy(hd->h);
+    hd->h = nullptr;
+  }
+  return nullptr;
+}
+
+struct SegmentWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  napi_ref frames_ref = nullptr, out_ref = nullptr;
+  vss_handle* h = nullptr;
+  const uint8_t* frames = nullptr;
+  float* out = nullptr;
+  int n = 0, height = 0, width = 0, channels = 0;
+  size_t row_stride = 0, out_count = 0;
+  int rc = 0;
+  std::string err;
+};
+
+void SegmentExecute(napi_env, void* data) {  // libuv worker thread: no JS calls here
+  SegmentWork* w = static_cast<SegmentWork*>(data);
+  w->rc = vss_segment(w->h, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out, VSS_OUT_MODEL);
+  if (w->rc != VSS_OK) w->err = vss_last_error(w->h);
+}
+
+void SegmentComplete(napi_env env, napi_status, void* data) {
+  SegmentWork* w = static_cast<SegmentWork*>(data);
+  napi_value ab = nullptr;
+  napi_get_reference_value(env, w->out_ref, &ab);
+  if (w->rc == VSS_OK) {
+    napi_value arr;
+    napi_create_typedarray(env, napi_float32_array, w->out_count, ab, 0, &arr);
+    napi_resolve_deferred(env, w->deferred, arr);
+  } else {
+    napi_value msg, code, e;
+    const std::string m = "vss_segment failed (" + std::to_string(w->rc) + "): " + w->err;
+    napi_create_string_utf8(env, m.c_str(), m.size(), &msg);
+    napi_create_string_utf8(env, std::to_string(w->rc).c_str(), NAPI_AUTO_LENGTH, &code);
+    napi_create_error(env, code, msg, &e);
+    napi_reject_deferred(env, w->deferred, e);
+  }
+  napi_delete_reference(env, w->frames_ref);
+  napi_delete_reference(env, w->out_ref);
+  napi_delete_async_work(env, w->work);
+  delete w;
+}
+
+napi_value Segment(napi_env env, napi_callback_info info) {
+  size_t argc = 7;
+  napi_value argv[7];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  if (argc < 7) {
+    napi_throw_type_error(env, nullptr, "segment(handle, frames, n, height, width, channels, rowStride)");
+    return nullptr;
+  }
+  Handle* hd = get_handle(env, argv[0]);
+  if (!hd) return nullptr;
+  bool is_ta = false;
+  napi_is_typedarray(env, argv[1], &is_ta);
+  if (!is_ta) {
+    napi_throw_type_error(env, nullptr, "frames must be a Uint8Array or Uint8ClampedArray");
+    return nullptr;
+  }
+  napi_typedarray_type tt;
+  size_t len = 0, off = 0;
+  void* data = nullptr;
+  napi_value buf;
+  NAPI_OK(env, napi_get_typedarray_info(env, argv[1], &tt, &len, &data, &buf, &off));
+  if (tt != napi_uint8_array && tt != napi_uint8_clamped_array) {
+    napi_throw_type_error(env, nullptr, "frames must be a Uint8Array or Uint8ClampedArray");
+    return nullptr;
+  }
+  SegmentWork* w = new SegmentWork();
+  int rs = 0;
+  napi_get_value_int32(env, argv[2], &w->n);
+  napi_get_value_int32(env, argv[3], &w->height);
+  napi_get_value_int32(env, argv[4], &w->width);
+  napi_get_value_int32(env, argv[5], &w->channels);
+  napi_get_value_int32(env, argv[6], &rs);
+  w->row_stride = (size_t)rs;
+  if (w->n < 1 || w->height < 1 || rs < 1 || len < (size_t)w->n * w->height * w->row_stride) {
+    delete w;
+    napi_throw_range_error(env, nullptr, "frames buffer smaller than n * height * rowStride");
+    return nullptr;
+  }
+  w->h = hd->h;
+  w->frames = static_cast<const uint8_t*>(data);
+  w->out_count = (size_t)w->n * hd->mask_h * hd->mask_w;
+  napi_value ab;
+  void* out = nullptr;
+  NAPI_OK(env, napi_create_arraybuffer(env, w->out_count * 4, &out, &ab));
+  w->out = static_cast<float*>(out);
+  napi_create_reference(env, argv[1], 1, &w->frames_ref);  // keep the frames alive until done
+  napi_create_reference(env, ab, 1, &w->out_ref);
+  napi_value promise, name;
+  NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
+  napi_create_string_utf8(env, "vss_segment", NAPI_AUTO_LENGTH, &name);
+  NAPI_OK(env, napi_create_async_work(env, nullptr, name, SegmentExecute, SegmentComplete, w, &w->work));
+  NAPI_OK(env, napi_queue_async_work(env, w->work));
+  return promise;
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+  const napi_property_descriptor props[] = {
+      {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"create", nullptr, Create, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"info", nullptr, Info, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"segment", nullptr, Segment, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"destroy", nullptr, Destroy, nullptr, nullptr, nullptr, napi_default, nullptr},
+  };
+  napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
+  return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)
