@@ -1,0 +1,30 @@
+// Driver for tests/test_ts.py: segment raw frames with the TypeScript host
+// (segment.js, generated from segment.ts) and write the masks back.
+//   node run_segment.js <frames.bin> <n> <height> <width> <channels> <out.bin> <dtype>
+'use strict';
+const fs = require('fs');
+const path = require('path');
+const seg = require(path.join(__dirname, '..', '..', 'video-stream-segmenetation_amd', 'ts', 'segment.js'));
+
+async function main() {
+  const [framesPath, n, h, w, c, outPath, dtype] = process.argv.slice(2);
+  const N = +n, H = +h, W = +w, C = +c;
+  const raw = fs.readFileSync(framesPath);
+  const bytes = H * W * C;
+  const frames = [];
+  for (let i = 0; i < N; i++) {
+    frames.push({ data: new Uint8Array(raw.buffer, raw.byteOffset + i * bytes, bytes), width: W, height: H, channels: C });
+  }
+  const s = new seg.Segmenter({ dtype: dtype, maxBatch: N, maxFrameWidth: W, maxFrameHeight: H });
+  // concurrent calls are serialised (runModnetExclusive semantics)
+  const [batch, single] = await Promise.all([s.segmentFrames(frames), s.segmentFrame(frames[0])]);
+  let rejected = false;
+  try { await s.segmentFrames(frames.concat(frames)); } catch (e) { rejected = e instanceof RangeError; }
+  const out = Buffer.from(batch.masks.buffer, batch.masks.byteOffset, batch.masks.byteLength);
+  fs.writeFileSync(outPath, out);
+  const same = single.mask.every((v, i) => v === batch.masks[i]);
+  console.log(JSON.stringify({ width: batch.width, height: batch.height, count: batch.count,
+                               singleMatchesBatch: same, oversizeRejected: rejected, version: seg.version() }));
+  s.close();
+}
+main().catch((e) => { console.error(e); process.exit(1); });

@@ -328,7 +328,7 @@ int upload(vss_handle* h) {
   if ((rc = dalloc(h, &d_img, img.size() * 4))) return rc;
   int acc_total = 0;
   for (const LayerPlan& l : h->L)
-    if (l.rec.kind == K_DEC) acc_total += 2 * l.C;
+    if (l.rec.kind == K_DEC) acc_total += kAccSlots * 2 * l.C;
   if ((rc = dalloc(h, &h->d_acc, (size_t)N * std::max(acc_total, 2) * 8))) return rc;
   HIP_TRY(h, hipMemset(h->d_acc, 0, (size_t)N * std::max(acc_total, 2) * 8));
   if (!img.empty()) HIP_TRY(h, hipMemcpy(d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
@@ -347,7 +347,7 @@ int upload(vss_handle* h) {
         l.gamma = dp(r.off[O_GAMMA]);
         l.beta = dp(r.off[O_BETA]);
         l.acc_off = h->acc_stride;
-        h->acc_stride += 2 * l.C;
+        h->acc_stride += kAccSlots * 2 * l.C;
       }
     } else if (r.kind == K_HEAD) {
       l.head_w = dp(r.off[O_W2]);

@@ -19,6 +19,8 @@ enum BlockMode : int { MODE_IR_EXPAND = 0, MODE_IR_DIRECT = 1, MODE_DEC = 2 };
 
 constexpr int kThreads = 256;       // 4 wave64 per workgroup
 constexpr int kMaxAcc = 16;         // 16x16 project accumulators per wave
+constexpr int kAccSlots = 16;       // instance-norm accumulator slots per frame and layer
+                                    // (spreads the producers' atomics over 16x the cache lines)
 
 __host__ __device__ constexpr int r4(int v) { return (v + 3) & ~3; }
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -70,9 +72,11 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   L.b2 = o;  o += r4(cout);
   L.lr = o;  o += mode == 2 ? r4(L.SR * L.SC * cin) : 0;
   L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;
-  // per-wave scratch during the main loop, reused as the accumulator slabs after it
+  // per-wave scratch during the main loop, reused as the accumulator slabs
+  // after it; for the decoder also the staging of the src's norm slots
   L.work = o;
-  o += cmax(4 * (mode == 0 ? (L.P_in_pad + L.P_out) * 16 : 256), L.CS * L.slab_stride);
+  o += cmax(cmax(4 * (mode == 0 ? (L.P_in_pad + L.P_out) * 16 : 256), L.CS * L.slab_stride),
+            mode == 2 ? kAccSlots * 2 * cin * 2 : 0);
   L.stt = o; o += 1024;  // 4 KiB: stats scratch (int64 pairs)
   L.total = o;
   return L;
@@ -99,11 +103,13 @@ struct BlockParams {
   // to its frame's accumulator with device-scope atomics; the consumer (the
   // next kernel) turns the totals into scale/shift.  The stem kernel zeroes
   // the accumulators of every frame at the start of each forward.
-  const unsigned long long* in_acc;  // DEC with norm_in: src accumulator [N][acc_stride] + src offset
+  const unsigned long long* in_acc;  // DEC with norm_in: src accumulator [N][acc_stride] + src offset,
+                                     // kAccSlots slots of [2][cin] (sum, sum of squares)
   const float* in_gamma;             // src layer's norm affine [cin]
   const float* in_beta;
   int in_hw;                         // pixels per frame of the src
-  unsigned long long* out_acc;       // DEC: this layer's accumulator [N][acc_stride] + offset ([2][cout])
+  unsigned long long* out_acc;       // DEC: this layer's accumulator [N][acc_stride] + offset
+                                     // (kAccSlots slots of [2][cout]; workgroup -> slot tile % kAccSlots)
   int acc_stride;                    // int64 elements per frame over all decoder layers
   float eps;
   int N, H, W;           // input spatial (IR: x dims; DEC: skip/output dims)

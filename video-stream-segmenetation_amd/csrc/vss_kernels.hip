@@ -337,14 +337,13 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
     const int sy0 = max(0, (oy0 - 1) / 2 - 1), sx0 = max(0, (ox0 - 1) / 2 - 1);
     const float* xn = p.x + (long)n * h * w * CL;
     const float* sn = p.skip + (long)n * Ho * Wo * CSKIP;
-    // src instance norm: this thread's 2 channels of exact totals (issued first)
-    ulonglong2 acc_s = {0ull, 0ull}, acc_q = {0ull, 0ull};
-    if constexpr (NORM_IN) {
-      const ulonglong2* ia = reinterpret_cast<const ulonglong2*>(p.in_acc + (long)n * p.acc_stride);
-      const int k = tid < CL / 2 ? tid : 0;
-      acc_s = ia[k];
-      acc_q = ia[CL / 2 + k];
-    }
+    // src instance norm: every slot of the frame's exact totals (issued first)
+    constexpr int NSLOT16 = NORM_IN ? kAccSlots * 2 * CL / 2 : 0;  // 16-B items
+    Staged<NSLOT16> st_slots;
+    if constexpr (NORM_IN)
+      st_slots.issue([&](int i) {
+        return reinterpret_cast<const f4*>(p.in_acc + (long)n * p.acc_stride)[i];
+      });
     Staged<SR * SC * C4L> st_lr;
     Staged<P_IN_PAD * C4S> st_sk;
     Staged<WIMG_F4> st_w;
@@ -359,13 +358,7 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
       return *reinterpret_cast<const f4*>(sn + ((long)yy * Wo + xx) * CSKIP + 4 * c4);
     });
     st_w.issue([&](int i) { return wsrc[i]; });
-    if constexpr (NORM_IN)
-      if (tid < CL / 2) {
-        norm_affine(acc_s.x, acc_q.x, p.in_hw, p.eps, p.in_gamma[2 * tid], p.in_beta[2 * tid], nrm + 2 * tid,
-                    nrm + CL + 2 * tid);
-        norm_affine(acc_s.y, acc_q.y, p.in_hw, p.eps, p.in_gamma[2 * tid + 1], p.in_beta[2 * tid + 1],
-                    nrm + 2 * tid + 1, nrm + CL + 2 * tid + 1);
-      }
+    if constexpr (NORM_IN) st_slots.commit([&](int i, f4 v) { reinterpret_cast<f4*>(work)[i] = v; });
     st_lr.commit([&](int i, f4 v) { reinterpret_cast<f4*>(lr)[i] = v; });
     st_sk.commit([&](int i, f4 v) {
       const int pix = i / C4S, c4 = i % C4S;
@@ -375,6 +368,20 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
     });
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     __syncthreads();
+    if constexpr (NORM_IN) {
+      // sum the slots (exact, any order) -> the src's scale/shift
+      const unsigned long long* sl = reinterpret_cast<const unsigned long long*>(work);
+      if (tid < CL) {
+        unsigned long long s_fx = 0, q_fx = 0;
+#pragma unroll
+        for (int k = 0; k < kAccSlots; ++k) {
+          s_fx += sl[k * 2 * CL + tid];
+          q_fx += sl[k * 2 * CL + CL + tid];
+        }
+        norm_affine(s_fx, q_fx, p.in_hw, p.eps, p.in_gamma[tid], p.in_beta[tid], nrm + tid, nrm + CL + tid);
+      }
+      __syncthreads();
+    }
     // upsampled channels: PyTorch upsample_bilinear2d(scale 2, align_corners=False)
     // of relu(src * scale + shift) (the src's instance norm, applied per tap)
 #pragma unroll
@@ -579,8 +586,9 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
       long long t = 0;
 #pragma unroll
       for (int k = 0; k < G; ++k) t += st64[base + k * COUT];
-      __hip_atomic_fetch_add(p.out_acc + (long)n * p.acc_stride + tid, (unsigned long long)t, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+      const int slot = (blockIdx.y * p.tiles_x + blockIdx.x) % kAccSlots;
+      __hip_atomic_fetch_add(p.out_acc + (long)n * p.acc_stride + slot * 2 * COUT + tid, (unsigned long long)t,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -607,10 +615,22 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
 #pragma unroll
     for (int q = 0; q < C / 4; ++q) xv[u][q] = px[q];
   }
-  if (tid < C) {
-    wv[tid] = p.w[tid];
+  // the d3 norm: all slots of the frame's exact totals (2 x C int64 per slot)
+  __shared__ unsigned long long slots[kAccSlots * 2 * C];
+  {
     const unsigned long long* ia = p.in_acc + (long)n * p.acc_stride;
-    norm_affine(ia[tid], ia[C + tid], h * w, p.eps, p.gamma[tid], p.beta[tid], sc + tid, sh + tid);
+    for (int i = tid; i < kAccSlots * 2 * C; i += 256) slots[i] = ia[i];
+  }
+  if (tid < C) wv[tid] = p.w[tid];
+  __syncthreads();
+  if (tid < C) {
+    unsigned long long s_fx = 0, q_fx = 0;
+#pragma unroll
+    for (int k = 0; k < kAccSlots; ++k) {
+      s_fx += slots[k * 2 * C + tid];
+      q_fx += slots[k * 2 * C + C + tid];
+    }
+    norm_affine(s_fx, q_fx, h * w, p.eps, p.gamma[tid], p.beta[tid], sc + tid, sh + tid);
   }
   __syncthreads();
 #pragma unroll
