@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--model", default="144x256")
     ap.add_argument("--dtype", default="bf16x2", choices=["bf16x2", "f32"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--branches", type=int, default=1, help="concurrent sub-batch chains inside the graph")
     ap.add_argument("--cpu-budget-s", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_traffic.json"),
@@ -109,6 +110,7 @@ def main():
                        max_frame_h=fh, max_frame_w=fw)
     if args.no_graph:
         sess.set_option(pkg.VSS_OPT_USE_GRAPH, 0)
+    sess.set_option(pkg.VSS_OPT_BRANCHES, args.branches)
     d_frames = torch.from_numpy(frames).to(dev)
     d_masks = torch.empty((B, hm * wm), dtype=torch.float32, device=dev)
     gathered = torch.empty((world * B, hm * wm), dtype=torch.float32, device=dev) if world > 1 else None
@@ -200,6 +202,7 @@ def main():
                 "pw_gemm": "v_mfma_f32_16x16x32_bf16, f32 activations split hi+lo" if args.dtype == "bf16x2"
                            else "v_mfma_f32_16x16x4_f32",
                 "graph": not args.no_graph,
+                "branches": args.branches,
                 "parallelism": f"dp{world}",
             },
             "mask_max_abs_err": err,

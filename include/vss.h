@@ -52,7 +52,9 @@ enum { VSS_OUT_MODEL = 0 };
 /* Options for vss_set_option. */
 enum {
   VSS_OPT_USE_GRAPH = 1, /* 1: replay a captured hipGraph per (shape, buffers) (default 1) */
-  VSS_OPT_PROFILE = 2    /* 1: time every kernel with HIP events (eager launches)         */
+  VSS_OPT_PROFILE = 2,   /* 1: time every kernel with HIP events (eager launches)         */
+  VSS_OPT_BRANCHES = 3   /* 1..8: split a batch into that many sub-batches whose chains run
+                            concurrently on forked streams inside the graph (default 1) */
 };
 
 typedef struct vss_handle vss_handle;
@@ -150,6 +152,49 @@ int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap);
 /* Kernel times from VSS_OPT_PROFILE runs: per layer, the mean over `count`
  * forwards (ms).  Resets the accumulators. */
 int vss_profile_read(vss_handle* h, double* ms_per_layer, int cap, int* count);
+
+/* ---- §8(f) row 1: the reference's mask post-processing, on the GPU ----------
+ * processFrame's steps after the seam (frameProcessorTest.ts:115-169):
+ * temporalEMA (:218) -> morphologicalOpening (:644) -> jointBilateral3x3 with the
+ * guide image (:230, :315) -> refineAlphaOnce (:270) -> alphaToImageData (:204),
+ * computed in doubles with f32 stores as the reference's JS does.  The guide
+ * (a browser-canvas resample in the reference) is the frame's tfjs-legacy
+ * bilinear resample at mask resolution, rounded half up to u8. */
+typedef struct vss_post_config {
+  double ema;            /* config.EMA                      (0.55, frameProcessorTest.ts:12) */
+  double noise_cutoff;   /* config.NOISE_CUTOFF             (0.06, :13) */
+  double high_threshold; /* config.HIGH_THRESHOLD           (0.95, :14) */
+  double gamma;          /* config.GAMMA                    (0.4,  :15) */
+  double sigma_spatial;  /* config.BILATERAL_SIGMA_SPATIAL  (1.0,  :17) */
+  double sigma_range;    /* config.BILATERAL_SIGMA_RANGE    (12.0, :18) */
+  int use_bilateral;     /* config.USE_BILATERAL            (1,    :16) */
+} vss_post_config;
+
+/* The reference's defaultConfig (frameProcessorTest.ts:20-28). */
+void vss_post_config_default(vss_post_config* cfg);
+
+/* Post-processing state of ONE video stream: prevAlpha (frameProcessorTest.ts:47),
+ * reset = the stream's next frame is its first.  One call in flight per state. */
+typedef struct vss_post_state vss_post_state;
+int vss_post_create(vss_handle* h, const vss_post_config* cfg, vss_post_state** out);
+void vss_post_destroy(vss_post_state* st);
+int vss_post_reset(vss_post_state* st);
+/* Live knob changes, like the settings sliders (client/script.ts:16-25). */
+int vss_post_set_config(vss_post_state* st, const vss_post_config* cfg);
+
+/* n CONSECUTIVE frames of the state's stream (HBM pointers, enqueued on `stream`):
+ * d_masks = the seam's masks [n][mask_h][mask_w] (e.g. from vss_segment_device),
+ * d_frames = the same frames (for the guide); outputs (either may be NULL):
+ * d_alpha [n][mask_h][mask_w] f32 = refinedAlpha (:166), d_alpha_u8 = the
+ * ImageData alpha bytes (:169, :213). */
+int vss_postprocess_device(vss_post_state* st, const uint8_t* d_frames, int n, int height, int width,
+                           int channels, size_t row_stride, size_t frame_stride, const float* d_masks,
+                           float* d_alpha, uint8_t* d_alpha_u8, void* stream);
+
+/* Host-memory convenience: seam + post chain for n consecutive frames of the
+ * state's stream (replaces frameProcessorTest.ts:78-169 up to putImageData). */
+int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, int n, int height, int width,
+                     int channels, size_t row_stride, float* alpha_out, uint8_t* alpha_u8_out);
 
 #ifdef __cplusplus
 }

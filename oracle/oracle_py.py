@@ -34,6 +34,10 @@ def lib():
         L.vsso_forward.restype = I
         L.vsso_layer_shapes.argtypes = [P, Lg, I, I, P, I]
         L.vsso_layer_shapes.restype = I
+        L.vsso_post.argtypes = [P, I, I, I, P, I, I, I, Lg, Lg, P, P, P, P, P]
+        L.vsso_post.restype = I
+        L.vsso_post_guide.argtypes = [P, I, I, I, I, Lg, Lg, I, I, P]
+        L.vsso_post_guide.restype = I
         L.vsso_bf16_round.argtypes = [ctypes.c_float]
         L.vsso_bf16_round.restype = ctypes.c_float
         _lib = L
@@ -87,3 +91,47 @@ def forward(blob: bytes, frames: np.ndarray, hm: int, wm: int, mode: int = 0,
 
 def bf16_round(x: float) -> float:
     return lib().vsso_bf16_round(x)
+
+
+class PostConfig(ctypes.Structure):
+    """Mirror of vsso_post_cfg; defaults = frameProcessorTest.ts:12-18."""
+    _fields_ = [("ema", ctypes.c_double), ("noise_cutoff", ctypes.c_double), ("high_threshold", ctypes.c_double),
+                ("gamma", ctypes.c_double), ("sigma_spatial", ctypes.c_double), ("sigma_range", ctypes.c_double),
+                ("use_bilateral", ctypes.c_int)]
+
+    @classmethod
+    def default(cls):
+        return cls(0.55, 0.06, 0.95, 0.4, 1.0, 12.0, 1)
+
+
+def post_guide(frames: np.ndarray, h: int, w: int) -> np.ndarray:
+    frames = np.ascontiguousarray(frames)
+    n, fh, fw, c = frames.shape
+    out = np.empty((n, h, w, 3), np.uint8)
+    if lib().vsso_post_guide(_ptr(frames), n, fh, fw, c, fw * c, fh * fw * c, h, w, _ptr(out)):
+        raise ValueError("vsso_post_guide")
+    return out
+
+
+class PostState:
+    """prevAlpha of one video stream (frameProcessorTest.ts:47)."""
+
+    def __init__(self, h: int, w: int):
+        self.alpha = np.zeros((h, w), np.float32)
+        self.valid = ctypes.c_int(0)
+
+
+def post(masks: np.ndarray, frames: np.ndarray, state: PostState, cfg: PostConfig | None = None):
+    """(refined alpha [n][H][W] f32, alpha bytes [n][H][W] u8) for consecutive frames of one stream."""
+    masks = np.ascontiguousarray(masks, np.float32)
+    frames = np.ascontiguousarray(frames)
+    n, H, W = masks.shape
+    _, fh, fw, c = frames.shape
+    cfg = cfg or PostConfig.default()
+    a = np.empty((n, H, W), np.float32)
+    u = np.empty((n, H, W), np.uint8)
+    rc = lib().vsso_post(_ptr(masks), n, H, W, _ptr(frames), fh, fw, c, fw * c, fh * fw * c, ctypes.byref(cfg),
+                         _ptr(state.alpha), ctypes.byref(state.valid), _ptr(a), _ptr(u))
+    if rc:
+        raise ValueError(f"vsso_post rc={rc}")
+    return a, u

@@ -362,3 +362,151 @@ int vsso_forward(const uint8_t* blob, long blob_bytes, int mode,
 }
 
 float vsso_bf16_round(float x) { return bf16r(x); }
+
+/* ======================================================================
+ * §8(f) row 1 — the post-processing chain that consumes the seam's mask,
+ * restated from the reference's JavaScript (numbers are JS doubles; every
+ * array is a Float32Array, so each stored value is rounded to f32):
+ *   temporalEMA            frameProcessorTest.ts:218-227 (state = prevAlpha, :47)
+ *   morphologicalOpening   :644-685  (3x3 min then 3x3 max, 1-px border left 0)
+ *   sampleGuidePixels      :315-321  browser canvas resampling, not reproducible:
+ *                          defined here as the same tfjs-legacy
+ *                          bilinear as the model input, rounded half up to u8
+ *   jointBilateral3x3      :230-266  (sigma_s 1, sigma_r 12: exp() in doubles)
+ *   refineAlphaOnce        :270-313  (no face prior: the prior is always null)
+ *   alphaToImageData       :204-216  (Math.round(clamp(a)*255) -> u8 alpha)
+ * The warp (:102-112) and the prior closing (:157) never act in the reference
+ * (lastAffine / facePrior stay null) and are not restated.
+ * ====================================================================== */
+typedef struct {
+  double ema, noise_cutoff, high_threshold, gamma, sigma_spatial, sigma_range;
+  int use_bilateral;
+} vsso_post_cfg;
+
+static uint8_t guide_px(const uint8_t* f, long rs, int c, int h, int w, float ry, float rx, int y, int x, int ch) {
+  float fy = (float)y * ry, fx = (float)x * rx;
+  int y0 = (int)floorf(fy > 0.f ? fy : 0.f), x0 = (int)floorf(fx > 0.f ? fx : 0.f);
+  int y1 = (int)ceilf(fy); if (y1 > h - 1) y1 = h - 1;
+  int x1 = (int)ceilf(fx); if (x1 > w - 1) x1 = w - 1;
+  float dy = fy - (float)y0, dx = fx - (float)x0;
+  float tl = f[y0 * rs + (long)x0 * c + ch], tr = f[y0 * rs + (long)x1 * c + ch];
+  float bl = f[y1 * rs + (long)x0 * c + ch], br = f[y1 * rs + (long)x1 * c + ch];
+  float top = fmaf(tr - tl, dx, tl);
+  float bot = fmaf(br - bl, dx, bl);
+  float val = fmaf(bot - top, dy, top);
+  return (uint8_t)floorf(val + 0.5f);
+}
+
+/* Post-process n consecutive frames of ONE video stream.
+ * masks: [n][H][W] raw seam masks; frames: the n source frames (for the guide);
+ * state: [H][W] prevAlpha, *state_valid 0 before the stream's first frame;
+ * out_alpha: [n][H][W] refined f32 (may be NULL); out_u8: [n][H][W] alpha bytes (may be NULL). */
+int vsso_post(const float* masks, int n, int H, int W, const uint8_t* frames, int fh, int fw, int fc,
+              long row_stride, long frame_stride, const vsso_post_cfg* cfg, float* state, int* state_valid,
+              float* out_alpha, uint8_t* out_u8) {
+  if (!masks || !frames || !cfg || !state || !state_valid || n < 0 || H < 3 || W < 3) return -1;
+  long P = (long)H * W;
+  float* ema = (float*)malloc(sizeof(float) * P);
+  float* er = (float*)malloc(sizeof(float) * P);
+  float* op = (float*)malloc(sizeof(float) * P);
+  float* gd = (float*)malloc(sizeof(float) * P);
+  uint8_t* guide = (uint8_t*)malloc(4 * P);
+  float ry = (float)((double)fh / (double)H), rx = (float)((double)fw / (double)W);
+  for (int t = 0; t < n; ++t) {
+    const float* cur = masks + (long)t * P;
+    /* temporalEMA :218-227 */
+    if (!*state_valid) {
+      memcpy(state, cur, sizeof(float) * P);
+      memcpy(ema, cur, sizeof(float) * P);
+      *state_valid = 1;
+    } else {
+      for (long i = 0; i < P; ++i) state[i] = (float)(cfg->ema * (double)state[i] + (1.0 - cfg->ema) * (double)cur[i]);
+      memcpy(ema, state, sizeof(float) * P);
+    }
+    /* morphologicalOpening :644-685 */
+    memset(er, 0, sizeof(float) * P);
+    memset(op, 0, sizeof(float) * P);
+    for (int y = 1; y < H - 1; ++y)
+      for (int x = 1; x < W - 1; ++x) {
+        float m = 1.0f;
+        for (int dy = -1; dy <= 1; ++dy)
+          for (int dx = -1; dx <= 1; ++dx) {
+            float v = ema[(y + dy) * W + x + dx];
+            if (v < m) m = v;
+          }
+        er[y * W + x] = m;
+      }
+    for (int y = 1; y < H - 1; ++y)
+      for (int x = 1; x < W - 1; ++x) {
+        float m = 0.0f;
+        for (int dy = -1; dy <= 1; ++dy)
+          for (int dx = -1; dx <= 1; ++dx) {
+            float v = er[(y + dy) * W + x + dx];
+            if (v > m) m = v;
+          }
+        op[y * W + x] = m;
+      }
+    /* jointBilateral3x3 :230-266 with the guide of :315-321 */
+    const float* a = op;
+    if (cfg->use_bilateral) {
+      const uint8_t* f = frames + (long)t * frame_stride;
+      for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x)
+          for (int ch = 0; ch < 3; ++ch) guide[(y * W + x) * 4 + ch] = guide_px(f, row_stride, fc, fh, fw, ry, rx, y, x, ch);
+      double ts2 = 2.0 * cfg->sigma_spatial * cfg->sigma_spatial, tr2 = 2.0 * cfg->sigma_range * cfg->sigma_range;
+      for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+          long idx = (long)y * W + x;
+          int r0 = guide[idx * 4], g0 = guide[idx * 4 + 1], b0 = guide[idx * 4 + 2];
+          double sw = 0, sa = 0;
+          for (int dy = -1; dy <= 1; ++dy) {
+            int yy = y + dy;
+            if (yy < 0 || yy >= H) continue;
+            for (int dx = -1; dx <= 1; ++dx) {
+              int xx = x + dx;
+              if (xx < 0 || xx >= W) continue;
+              long j = (long)yy * W + xx;
+              int dr = guide[j * 4] - r0, dg = guide[j * 4 + 1] - g0, db = guide[j * 4 + 2] - b0;
+              double range2 = dr * dr + dg * dg + db * db, spatial2 = dx * dx + dy * dy;
+              double wgt = exp(-spatial2 / ts2) * exp(-range2 / tr2);
+              sw += wgt;
+              sa += wgt * (double)op[j];
+            }
+          }
+          gd[idx] = sw > 0 ? (float)(sa / sw) : op[idx];
+        }
+      a = gd;
+    }
+    /* refineAlphaOnce :270-313 (prior undefined) and alphaToImageData :204-216 */
+    double lo = cfg->noise_cutoff, hi = cfg->high_threshold;
+    double denom = hi - lo > 1e-6 ? hi - lo : 1e-6;
+    for (long i = 0; i < P; ++i) {
+      double v = a[i];
+      if (v <= lo) v = 0;
+      else if (v >= hi) v = 1;
+      else v = pow((v - lo) / denom, cfg->gamma);
+      float vf = (float)v;
+      if (out_alpha) out_alpha[(long)t * P + i] = vf;
+      if (out_u8) {
+        double c = vf < 0.f ? 0.0 : (vf > 1.f ? 1.0 : (double)vf);
+        out_u8[(long)t * P + i] = (uint8_t)floor(c * 255.0 + 0.5);
+      }
+    }
+  }
+  free(ema); free(er); free(op); free(gd); free(guide);
+  return 0;
+}
+
+/* The guide image of the post chain as defined above: [n][H][W][3] u8. */
+int vsso_post_guide(const uint8_t* frames, int n, int fh, int fw, int fc, long row_stride, long frame_stride,
+                    int H, int W, uint8_t* out) {
+  if (!frames || !out || n < 0 || H < 1 || W < 1) return -1;
+  float ry = (float)((double)fh / (double)H), rx = (float)((double)fw / (double)W);
+  for (int t = 0; t < n; ++t)
+    for (int y = 0; y < H; ++y)
+      for (int x = 0; x < W; ++x)
+        for (int ch = 0; ch < 3; ++ch)
+          out[(((long)t * H + y) * W + x) * 3 + ch] =
+              guide_px(frames + (long)t * frame_stride, row_stride, fc, fh, fw, ry, rx, y, x, ch);
+  return 0;
+}

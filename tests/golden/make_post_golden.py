@@ -1,0 +1,133 @@
+"""Golden vectors for the post-processing chain, produced by THE REFERENCE'S
+OWN CODE run under Node in this container.
+
+Run from the repo root (needs /root/reference and node):
+    python tests/golden/make_post_golden.py
+
+The five pure functions the reference applies to the seam's mask
+(/root/reference/client/src/core/frameProcessorTest.ts):
+    temporalEMA :218-227, morphologicalOpening :644-685, jointBilateral3x3
+    :230-266, refineAlphaOnce :270-313, alphaToImageData :204-216
+plus the config block :12-30 and `let prevAlpha` :47 are cut out of the
+reference file as text at generation time, type-stripped with
+video-stream-segmenetation_amd/ts/strip_types.py, and executed by Node in the
+order processFrame calls them (:115-169; the warp and the face-prior closing
+never act).  No reference source is stored in this repository:
+only the input and output vectors (tests/golden/post_chain.npz).
+
+Inputs: 4 consecutive masks of one stream (the CPU oracle's masks of
+synthetic frames at model res 48x64, made to move between frames) and the
+guide image.  The reference's guide is a browser-canvas resample
+(sampleGuidePixels :315-321) that cannot be reproduced; SURVEY.md §8(f)
+defines it as the model input's tfjs-legacy bilinear, rounded half up to u8 —
+computed here by the oracle and stored in the fixture.
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference/client/src/core/frameProcessorTest.ts"
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+FUNCS = ["alphaToImageData", "temporalEMA", "jointBilateral3x3", "refineAlphaOnce", "morphologicalOpening"]
+
+
+def extract(src: str, name: str) -> str:
+    """The text of `function name(...) ... { ... }` (parens and braces matched)."""
+    i = src.index(f"function {name}(")
+    k = src.index("(", i)
+    depth = 0
+    while True:
+        depth += {"(": 1, ")": -1}.get(src[k], 0)
+        if depth == 0:
+            break
+        k += 1
+    j = src.index("{", k)
+    depth = 0
+    for k in range(j, len(src)):
+        if src[k] == "{":
+            depth += 1
+        elif src[k] == "}":
+            depth -= 1
+            if depth == 0:
+                return src[i:k + 1]
+    raise ValueError(name)
+
+
+def main():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("strip_types", os.path.join(
+        ROOT, "video-stream-segmenetation_amd", "ts", "strip_types.py"))
+    st = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(st)
+    from conftest import load_pkg
+    pkg = load_pkg()
+    import oracle_py
+    import vss_amd.synthetic as syn
+
+    src = open(REF).read()
+    lines = src.split("\n")
+    cfg_block = "\n".join(lines[11:30]).replace("export const", "const").replace("export let", "let")
+    prev = "let prevAlpha = null;"
+    funcs = "\n\n".join(extract(src, f) for f in FUNCS)
+    body = st.strip(cfg_block + "\n" + prev + "\n" + funcs)
+    body = body.replace("'use strict';\n", "")
+
+    n, H, W, fh, fw = 4, 48, 64, 120, 160
+    frames = np.stack([syn.make_frame(900 + (t % 2), fh, fw, 3) for t in range(n)])
+    blob = open(pkg.ensure_weights(), "rb").read()
+    masks = oracle_py.forward(blob, frames, H, W, mode=0)
+    masks = np.ascontiguousarray(masks.astype(np.float32))
+    guide = oracle_py.post_guide(frames, H, W)  # [n][H][W][3] u8
+
+    harness = body + r"""
+class ImageData { constructor(w, h) { this.width = w; this.height = h; this.data = new Uint8ClampedArray(w * h * 4); } }
+const fs = require('fs');
+const [mp, gp, n, H, W, op] = process.argv.slice(2);
+const N = +n, h = +H, w = +W, P = h * w;
+const mb = fs.readFileSync(mp), gb = fs.readFileSync(gp);
+const outA = new Float32Array(N * P), outU = new Uint8Array(N * P);
+for (let t = 0; t < N; t++) {
+  const alphaRaw = new Float32Array(mb.buffer.slice(mb.byteOffset + t * P * 4, mb.byteOffset + (t + 1) * P * 4));
+  const guide = new Uint8ClampedArray(P * 4);
+  for (let i = 0; i < P; i++) { for (let c = 0; c < 3; c++) guide[i * 4 + c] = gb[(t * P + i) * 3 + c]; guide[i * 4 + 3] = 255; }
+  // processFrame :115-169 (no warp, no face prior)
+  const emaAlpha = temporalEMA(alphaRaw);
+  const openedAlpha = morphologicalOpening(emaAlpha, w, h);
+  const guidedAlpha = config.USE_BILATERAL ? jointBilateral3x3(openedAlpha, guide, w, h) : openedAlpha;
+  const refinedAlpha = refineAlphaOnce(guidedAlpha, config.NOISE_CUTOFF, config.HIGH_THRESHOLD, config.GAMMA, undefined);
+  const img = alphaToImageData(refinedAlpha, w, h);
+  outA.set(refinedAlpha, t * P);
+  for (let i = 0; i < P; i++) outU[t * P + i] = img.data[i * 4 + 3];
+}
+fs.writeFileSync(op + '.f32', Buffer.from(outA.buffer));
+fs.writeFileSync(op + '.u8', Buffer.from(outU.buffer));
+console.log(JSON.stringify(config));
+"""
+    with tempfile.TemporaryDirectory() as td:
+        js = os.path.join(td, "post.js")
+        open(js, "w").write(harness)
+        masks.tofile(os.path.join(td, "m.bin"))
+        guide.tofile(os.path.join(td, "g.bin"))
+        out = subprocess.run(["node", js, os.path.join(td, "m.bin"), os.path.join(td, "g.bin"), str(n), str(H),
+                              str(W), os.path.join(td, "o")], capture_output=True, text=True, check=True)
+        cfg = json.loads(out.stdout.strip().splitlines()[-1])
+        ref_a = np.fromfile(os.path.join(td, "o.f32"), np.float32).reshape(n, H, W)
+        ref_u = np.fromfile(os.path.join(td, "o.u8"), np.uint8).reshape(n, H, W)
+    path = os.path.join(HERE, "post_chain.npz")
+    np.savez_compressed(path, seeds=np.array([900 + (t % 2) for t in range(n)]), frame_hw=np.array([fh, fw]),
+                        masks=masks, guide=guide, config=np.array(json.dumps(cfg)), alpha=ref_a, alpha_u8=ref_u)
+    print(path, os.path.getsize(path), "bytes; config", cfg, "alpha mean", float(ref_a.mean()))
+
+
+if __name__ == "__main__":
+    main()

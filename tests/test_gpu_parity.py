@@ -212,3 +212,18 @@ def test_results_independent_of_tiling(pkg, sess_bf, synthetic):
         with pkg.Session(dtype="bf16x2", max_batch=mb, autotune=at) as s:
             got = np.concatenate([s.segment_frames(f[i:i + mb])[0] for i in range(0, 3, mb)])
         assert np.array_equal(got, ref), (mb, at)
+
+
+def test_branches_bitwise(pkg, sess_bf, synthetic, torch_cuda):
+    torch = torch_cuda
+    f = _frames(synthetic, 8, start=700)
+    ref, _, _ = sess_bf.segment_frames(f)
+    d = torch.from_numpy(f).cuda()
+    out = torch.empty((8, 144 * 256), dtype=torch.float32, device="cuda")
+    for br in (2, 3, 8):
+        sess_bf.set_option(pkg.VSS_OPT_BRANCHES, br)
+        out.zero_()
+        sess_bf.segment_device(d.data_ptr(), 8, 480, 640, 3, 640 * 3, 480 * 640 * 3, out.data_ptr(), 0)
+        sess_bf.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref), br
+    sess_bf.set_option(pkg.VSS_OPT_BRANCHES, 1)

@@ -31,7 +31,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "vss.h")
 VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_IO, VSS_E_UNSUPPORTED = (
     0, -1, -2, -3, -4, -5, -6, -7)
 DTYPES = {"f32": 0, "bf16x2": 1}
-VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE = 1, 2
+VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_BRANCHES = 1, 2, 3
 VSS_CREATE_NO_AUTOTUNE = 1
 VSS_OUT_MODEL = 0
 
@@ -51,6 +51,26 @@ class _Config(ctypes.Structure):
 class _Info(ctypes.Structure):
     _fields_ = [("mask_h", ctypes.c_int), ("mask_w", ctypes.c_int), ("n_layers", ctypes.c_int),
                 ("dtype", ctypes.c_int), ("device_bytes", ctypes.c_size_t)]
+
+
+class PostConfig(ctypes.Structure):
+    """vss_post_config: the reference's post-processing knobs
+    (frameProcessorTest.ts:12-18; defaults = defaultConfig :20-28)."""
+    _fields_ = [("ema", ctypes.c_double), ("noise_cutoff", ctypes.c_double), ("high_threshold", ctypes.c_double),
+                ("gamma", ctypes.c_double), ("sigma_spatial", ctypes.c_double), ("sigma_range", ctypes.c_double),
+                ("use_bilateral", ctypes.c_int)]
+    # the reference's config keys -> fields
+    KEYS = {"EMA": "ema", "NOISE_CUTOFF": "noise_cutoff", "HIGH_THRESHOLD": "high_threshold", "GAMMA": "gamma",
+            "BILATERAL_SIGMA_SPATIAL": "sigma_spatial", "BILATERAL_SIGMA_RANGE": "sigma_range",
+            "USE_BILATERAL": "use_bilateral"}
+
+    @classmethod
+    def default(cls, **overrides):
+        c = cls()
+        lib().vss_post_config_default(ctypes.byref(c))
+        for k, v in overrides.items():
+            setattr(c, cls.KEYS.get(k, k), int(v) if cls.KEYS.get(k, k) == "use_bilateral" else float(v))
+        return c
 
 
 CALLBACK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)
@@ -100,6 +120,13 @@ def lib() -> ctypes.CDLL:
                 "vss_read_layer": ([P, I, I, P], I),
                 "vss_profile_read": ([P, ctypes.POINTER(ctypes.c_double), I, ctypes.POINTER(I)], I),
                 "vss_layer_kernel": ([P, I, ctypes.c_char_p, I], I),
+                "vss_post_config_default": ([ctypes.POINTER(PostConfig)], None),
+                "vss_post_create": ([P, ctypes.POINTER(PostConfig), ctypes.POINTER(P)], I),
+                "vss_post_destroy": ([P], None),
+                "vss_post_reset": ([P], I),
+                "vss_post_set_config": ([P, ctypes.POINTER(PostConfig)], I),
+                "vss_postprocess_device": ([P, P, I, I, I, I, S, S, P, P, P, P], I),
+                "vss_segment_post": ([P, P, P, I, I, I, I, S, P, P], I),
             }
             for name, (args, res) in sig.items():
                 fn = getattr(L, name)
@@ -148,9 +175,12 @@ class Session:
         self.device_bytes = info.device_bytes
         self.dtype, self.max_batch = dtype, max_batch
         self._pending = []
+        self._posts = []
 
     # -- lifecycle --------------------------------------------------------
     def close(self):
+        for p in getattr(self, "_posts", []):
+            p.close()
         if getattr(self, "_h", None):
             lib().vss_destroy(self._h)
             self._h = None
@@ -242,6 +272,61 @@ class Session:
         cnt = ctypes.c_int()
         _check(lib().vss_profile_read(self._h, arr, self.n_layers, ctypes.byref(cnt)), self._h)
         return list(arr), cnt.value
+
+
+class PostChain:
+    """The reference's per-stream mask post-processing (processFrame
+    frameProcessorTest.ts:115-169: temporalEMA -> morphologicalOpening ->
+    jointBilateral3x3 -> refineAlphaOnce -> alphaToImageData) on the GPU.
+
+    One PostChain per video stream: it holds that stream's prevAlpha (:47);
+    feed it the stream's frames in order.  reset() = the next frame is first."""
+
+    def __init__(self, session: Session, config: PostConfig | None = None, **overrides):
+        self.session = session
+        self.config = config if config is not None else PostConfig.default(**overrides)
+        st = ctypes.c_void_p()
+        _check(lib().vss_post_create(session._h, ctypes.byref(self.config), ctypes.byref(st)), session._h)
+        self._st = st
+        session._posts.append(self)
+
+    def close(self):
+        if getattr(self, "_st", None):
+            lib().vss_post_destroy(self._st)
+            self._st = None
+
+    def reset(self):
+        _check(lib().vss_post_reset(self._st), self.session._h)
+
+    def set_config(self, config: PostConfig | None = None, **overrides):
+        """Live knob change (the settings sliders, client/script.ts:16-25)."""
+        c = config if config is not None else PostConfig.default()
+        if config is None:
+            for f, _ in PostConfig._fields_:
+                setattr(c, f, getattr(self.config, f))
+            for k, v in overrides.items():
+                f = PostConfig.KEYS.get(k, k)
+                setattr(c, f, int(v) if f == "use_bilateral" else float(v))
+        _check(lib().vss_post_set_config(self._st, ctypes.byref(c)), self.session._h)
+        self.config = c
+
+    def segment(self, frames: np.ndarray):
+        """Consecutive frames [N,H,W,3|4] u8 -> (refinedAlpha f32 [N, maskH*maskW],
+        alpha bytes u8 [N, maskH*maskW], maskW, maskH)."""
+        s = self.session
+        f = _as_frames(frames)
+        n, hh, ww, c = f.shape
+        a = np.empty((n, s.mask_h * s.mask_w), np.float32)
+        u = np.empty((n, s.mask_h * s.mask_w), np.uint8)
+        _check(lib().vss_segment_post(s._h, self._st, f.ctypes.data, n, hh, ww, c, ww * c, a.ctypes.data,
+                                      u.ctypes.data), s._h)
+        return a, u, s.mask_w, s.mask_h
+
+    def process_device(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int, frame_stride: int,
+                       masks_ptr: int, alpha_ptr: int = 0, alpha_u8_ptr: int = 0, stream: int = 0):
+        _check(lib().vss_postprocess_device(self._st, frames_ptr or None, n, h, w, c, row_stride, frame_stride,
+                                            masks_ptr, alpha_ptr or None, alpha_u8_ptr or None, stream or None),
+               self.session._h)
 
 
 def version() -> int:

@@ -84,9 +84,15 @@ struct vss_handle {
   size_t frame_cap = 0;
   uint8_t* h_frames = nullptr;  // pinned staging
   float* h_masks = nullptr;
+  float* d_post_alpha = nullptr;  // vss_segment_post outputs [max_batch][P]
+  uint8_t* d_post_u8 = nullptr;
   std::atomic<int> busy{0};
   int use_graph = 1;
   int profile = 0;
+  static constexpr int kMaxBranches = 8;
+  int branches = 1;  // parallel sub-batch chains inside the captured graph
+  hipStream_t branch_streams[kMaxBranches] = {};
+  hipEvent_t fork_ev = nullptr, join_ev[kMaxBranches] = {};
   std::map<GraphKey, hipGraphExec_t> graphs;
   // profiling: ring of event pairs per layer
   static constexpr int kSlots = 32;
@@ -366,13 +372,17 @@ int check_frames(vss_handle* h, int n, int fh, int fw, int fc, size_t rs, size_t
   return VSS_OK;
 }
 
-BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n) {
+size_t frame_elems(const LayerPlan& l) { return (size_t)l.H * l.W * l.C; }
+
+// Kernel parameters of block layer l for frames [f0, f0 + n) of the batch.
+BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n, int f0 = 0) {
   const Rec& r = l.rec;
   const LayerPlan& src = h->L[r.src];
+  const size_t fa = (size_t)f0 * h->acc_stride;
   BlockParams p{};
   p.wimg = l.wimg;
-  p.x = src.act;
-  p.y = l.act;
+  p.x = src.act + f0 * frame_elems(src);
+  p.y = l.act + f0 * frame_elems(l);
   p.eps = h->eps;
   p.N = n; p.H = l.inH; p.W = l.inW; p.Ho = l.H; p.Wo = l.W;
   p.cin = (int)r.cin; p.cout = l.C; p.chid = l.chid; p.stride = l.stride;
@@ -383,13 +393,13 @@ BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n) {
     p.residual = (r.flags & F_RESIDUAL) ? 1 : 0;
   } else {
     const LayerPlan& sk = h->L[r.skip];
-    p.skip = sk.act;
+    p.skip = sk.act + f0 * frame_elems(sk);
     p.cskip = (int)r.chid;
     p.relu6_dw = 0;
-    p.out_acc = h->d_acc + l.acc_off;
+    p.out_acc = h->d_acc + fa + l.acc_off;
     p.norm_in = src.rec.kind == K_DEC ? 1 : 0;
     if (p.norm_in) {
-      p.in_acc = h->d_acc + src.acc_off;
+      p.in_acc = h->d_acc + fa + src.acc_off;
       p.in_gamma = src.gamma;
       p.in_beta = src.beta;
       p.in_hw = src.H * src.W;
@@ -398,9 +408,10 @@ BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n) {
   return p;
 }
 
-// Enqueue the whole forward on stream s (no sync, no alloc: graph-capturable).
+// Enqueue the whole forward for frames [f0, f0 + n) on stream s (frames and
+// masks point at frame f0; no sync, no alloc: graph-capturable).
 int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs,
-                    size_t fs, float* masks, hipStream_t s, int prof_slot) {
+                    size_t fs, float* masks, hipStream_t s, int prof_slot, int f0 = 0) {
   const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
   const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
   const int nl = (int)h->L.size();
@@ -424,18 +435,20 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       p.fh = fh; p.fw = fw; p.fc = fc; p.Hm = Hm; p.Wm = Wm;
       p.ry = (float)((double)fh / (double)Hm);
       p.rx = (float)((double)fw / (double)Wm);
-      p.w = l.stem_w; p.b = l.stem_b; p.y = l.act;
+      p.w = l.stem_w; p.b = l.stem_b; p.y = l.act + f0 * frame_elems(l);
       p.Ho = l.H; p.Wo = l.W; p.cout = l.C;
-      p.acc_zero = h->d_acc;
+      p.acc_zero = h->d_acc + (size_t)f0 * h->acc_stride;
       p.acc_stride = h->acc_stride;
       go(stem_kernel16(), dim3((l.W + 31) / 32, (l.H + 7) / 8, n), 0, p);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
-      const BlockParams p = block_params(h, l, n);
+      const BlockParams p = block_params(h, l, n, f0);
       go(l.entry->fn[prec == PREC_F32 ? 0 : 1], dim3(l.tiles_x, l.tiles_y, n), l.lds, p);
     } else if (r.kind == K_HEAD) {
       const LayerPlan& src = h->L[r.src];
       HeadParams p{};
-      p.x = src.act; p.in_acc = h->d_acc + src.acc_off; p.acc_stride = h->acc_stride;
+      p.x = src.act + f0 * frame_elems(src);
+      p.in_acc = h->d_acc + (size_t)f0 * h->acc_stride + src.acc_off;
+      p.acc_stride = h->acc_stride;
       p.gamma = src.gamma; p.beta = src.beta; p.eps = h->eps;
       p.w = l.head_w; p.b = l.head_b; p.mask = masks;
       p.N = n; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
@@ -481,7 +494,25 @@ int forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc,
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     HIP_TRY(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
-    int rc = enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, h->stream, -1);
+    // Independent sub-batches on forked streams: their kernels overlap, which
+    // fills the GPU while each chain waits on memory latency.
+    const int nb = std::max(1, std::min(h->branches, n));
+    int rc = VSS_OK;
+    if (nb == 1) {
+      rc = enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, h->stream, -1);
+    } else {
+      (void)hipEventRecord(h->fork_ev, h->stream);
+      const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
+      for (int b = 0; b < nb && !rc; ++b) {
+        const int f0 = (int)((long)n * b / nb), f1 = (int)((long)n * (b + 1) / nb);
+        hipStream_t bs = h->branch_streams[b];
+        (void)hipStreamWaitEvent(bs, h->fork_ev, 0);
+        rc = enqueue_forward(h, frames + (size_t)f0 * fs, f1 - f0, fh, fw, fc, rs, fs,
+                             masks + (size_t)f0 * Hm * Wm, bs, -1, f0);
+        (void)hipEventRecord(h->join_ev[b], bs);
+        (void)hipStreamWaitEvent(h->stream, h->join_ev[b], 0);
+      }
+    }
     hipError_t e = hipStreamEndCapture(h->stream, &g);
     if (rc) {
       if (g) (void)hipGraphDestroy(g);
@@ -631,9 +662,17 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
   if (rc) return bail(rc);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(h, VSS_E_HIP, "hipStreamCreate failed"));
+  for (int b = 0; b < vss_handle::kMaxBranches; ++b)
+    if (hipStreamCreateWithFlags(&h->branch_streams[b], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->join_ev[b], hipEventDisableTiming) != hipSuccess)
+      return bail(fail(h, VSS_E_HIP, "branch stream/event create failed"));
+  if (hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(h, VSS_E_HIP, "hipEventCreate failed"));
   h->frame_cap = (size_t)cfg->max_batch * cfg->max_frame_h * cfg->max_frame_w * 4;
   if ((rc = dalloc(h, &h->d_frames, h->frame_cap))) return bail(rc);
   if ((rc = dalloc(h, &h->d_masks, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w * 4))) return bail(rc);
+  if ((rc = dalloc(h, &h->d_post_alpha, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w * 4))) return bail(rc);
+  if ((rc = dalloc(h, &h->d_post_u8, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w))) return bail(rc);
   if (hipHostMalloc((void**)&h->h_frames, h->frame_cap, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&h->h_masks, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w * 4,
                     hipHostMallocDefault) != hipSuccess)
@@ -661,6 +700,11 @@ void vss_destroy(vss_handle* h) {
   for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto e : h->ev)
     if (e) (void)hipEventDestroy(e);
+  for (int b = 0; b < vss_handle::kMaxBranches; ++b) {
+    if (h->branch_streams[b]) (void)hipStreamDestroy(h->branch_streams[b]);
+    if (h->join_ev[b]) (void)hipEventDestroy(h->join_ev[b]);
+  }
+  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
   for (void* p : h->dev_allocs) (void)hipFree(p);
   if (h->h_frames) (void)hipHostFree(h->h_frames);
   if (h->h_masks) (void)hipHostFree(h->h_masks);
@@ -754,6 +798,14 @@ int vss_set_option(vss_handle* h, int option, int value) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (option == VSS_OPT_USE_GRAPH) h->use_graph = value ? 1 : 0;
   else if (option == VSS_OPT_PROFILE) h->profile = value ? 1 : 0;
+  else if (option == VSS_OPT_BRANCHES) {
+    if (value < 1 || value > vss_handle::kMaxBranches) return fail(h, VSS_E_INVALID_ARG, "branches must be 1..8");
+    if (value != h->branches) {
+      for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+      h->graphs.clear();
+    }
+    h->branches = value;
+  }
   else return fail(h, VSS_E_INVALID_ARG, "unknown option");
   return VSS_OK;
 }
@@ -809,6 +861,194 @@ int vss_profile_read(vss_handle* h, double* ms_per_layer, int cap, int* count) {
   if (count) *count = h->prof_count;
   std::fill(h->prof_sum.begin(), h->prof_sum.end(), 0.0);
   h->prof_count = 0;
+  return VSS_OK;
+}
+
+}  // extern "C"
+
+// ---- post-processing chain (vss_post.hip) ----------------------------------
+struct vss_post_state {
+  vss_handle* h = nullptr;
+  vss_post_config cfg{};
+  float* state = nullptr;   // [P] prevAlpha
+  int* valid = nullptr;     // device flag: 0 before the stream's first frame
+  float* ema = nullptr;     // [max_batch][P]
+  double* rtab = nullptr;   // exp(-r / (2 sigma_r^2)), r in [0, 3*255^2]
+  double sw[3] = {0, 0, 0};
+  double tab_sigma = -1.0;
+  std::string err;
+};
+
+namespace {
+
+constexpr int kRangeTab = 3 * 255 * 255 + 1;
+
+int post_fail(vss_post_state* st, int code, const std::string& msg) {
+  st->err = msg;
+  if (st->h) st->h->err = msg;
+  return code;
+}
+
+// Bilateral weights as the reference computes them (Math.exp of the same
+// double quotients); built on the host so they are the exact doubles the
+// oracle's libm produces.
+int post_tables(vss_post_state* st) {
+  const vss_post_config& c = st->cfg;
+  const double ts2 = 2.0 * c.sigma_spatial * c.sigma_spatial, tr2 = 2.0 * c.sigma_range * c.sigma_range;
+  for (int k = 0; k < 3; ++k) st->sw[k] = std::exp(-(double)k / ts2);
+  if (st->tab_sigma != c.sigma_range) {
+    std::vector<double> t(kRangeTab);
+    for (int r = 0; r < kRangeTab; ++r) t[r] = std::exp(-(double)r / tr2);
+    if (hipMemcpy(st->rtab, t.data(), t.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+      return post_fail(st, VSS_E_HIP, "post: table upload failed");
+    st->tab_sigma = c.sigma_range;
+  }
+  return VSS_OK;
+}
+
+int post_enqueue(vss_post_state* st, const uint8_t* d_frames, int n, int fh, int fw, int fc, size_t rs, size_t fs,
+                 const float* d_masks, float* d_alpha, uint8_t* d_u8, hipStream_t s) {
+  vss_handle* h = st->h;
+  const int H = h->cfg.model_h, W = h->cfg.model_w;
+  PostEmaParams pe{};
+  pe.masks = d_masks;
+  pe.ema = st->ema;
+  pe.state = st->state;
+  pe.valid = st->valid;
+  pe.n = n;
+  pe.P = (long)H * W;
+  pe.a = st->cfg.ema;
+  launch_post_ema(pe, s);
+  HIP_TRY(h, hipMemsetAsync(st->valid, 1, sizeof(int), s));  // the stream has seen its first frame
+  PostFilterParams pf{};
+  pf.ema = st->ema;
+  pf.frames = d_frames;
+  pf.row_stride = (long)rs;
+  pf.frame_stride = (long)fs;
+  pf.fh = fh; pf.fw = fw; pf.fc = fc;
+  pf.ry = (float)((double)fh / (double)H);
+  pf.rx = (float)((double)fw / (double)W);
+  pf.H = H; pf.W = W;
+  pf.rtab = st->rtab;
+  for (int k = 0; k < 3; ++k) pf.sw[k] = st->sw[k];
+  pf.lo = st->cfg.noise_cutoff;
+  pf.hi = st->cfg.high_threshold;
+  pf.denom = std::max(1e-6, st->cfg.high_threshold - st->cfg.noise_cutoff);
+  pf.gamma = st->cfg.gamma;
+  pf.use_bilateral = st->cfg.use_bilateral;
+  pf.alpha = d_alpha;
+  pf.alpha_u8 = d_u8;
+  launch_post_filter(pf, n, s);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return post_fail(st, VSS_E_HIP, std::string("post launch: ") + hipGetErrorString(e));
+  return VSS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void vss_post_config_default(vss_post_config* c) {
+  if (!c) return;
+  c->ema = 0.55;
+  c->noise_cutoff = 0.06;
+  c->high_threshold = 0.95;
+  c->gamma = 0.4;
+  c->sigma_spatial = 1.0;
+  c->sigma_range = 12.0;
+  c->use_bilateral = 1;
+}
+
+int vss_post_create(vss_handle* h, const vss_post_config* cfg, vss_post_state** out) {
+  if (!h || !out) return fail(h, VSS_E_INVALID_ARG, "null handle/out");
+  *out = nullptr;
+  if (h->cfg.model_h < 3 || h->cfg.model_w < 3) return fail(h, VSS_E_UNSUPPORTED, "mask too small for post");
+  vss_post_state* st = new vss_post_state();
+  st->h = h;
+  if (cfg) st->cfg = *cfg;
+  else vss_post_config_default(&st->cfg);
+  const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
+  auto bail = [&](int rc) {
+    vss_post_destroy(st);
+    return rc;
+  };
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (hipMalloc(&st->state, P * 4) != hipSuccess || hipMalloc(&st->valid, 16) != hipSuccess ||
+      hipMalloc(&st->ema, P * 4 * h->cfg.max_batch) != hipSuccess ||
+      hipMalloc(&st->rtab, (size_t)kRangeTab * 8) != hipSuccess)
+    return bail(fail(h, VSS_E_OOM, "post: hipMalloc failed"));
+  if (hipMemset(st->valid, 0, 16) != hipSuccess || hipMemset(st->state, 0, P * 4) != hipSuccess)
+    return bail(fail(h, VSS_E_HIP, "post: hipMemset failed"));
+  int rc = post_tables(st);
+  if (rc) return bail(rc);
+  *out = st;
+  return VSS_OK;
+}
+
+void vss_post_destroy(vss_post_state* st) {
+  if (!st) return;
+  if (st->h) {
+    (void)hipSetDevice(st->h->device);
+    (void)hipStreamSynchronize(st->h->stream);
+  }
+  if (st->state) (void)hipFree(st->state);
+  if (st->valid) (void)hipFree(st->valid);
+  if (st->ema) (void)hipFree(st->ema);
+  if (st->rtab) (void)hipFree(st->rtab);
+  delete st;
+}
+
+int vss_post_reset(vss_post_state* st) {
+  if (!st) return VSS_E_INVALID_ARG;
+  HIP_TRY(st->h, hipSetDevice(st->h->device));
+  HIP_TRY(st->h, hipStreamSynchronize(st->h->stream));
+  HIP_TRY(st->h, hipMemset(st->valid, 0, sizeof(int)));
+  return VSS_OK;
+}
+
+int vss_post_set_config(vss_post_state* st, const vss_post_config* cfg) {
+  if (!st || !cfg) return VSS_E_INVALID_ARG;
+  if (cfg->sigma_spatial <= 0 || cfg->sigma_range <= 0) return post_fail(st, VSS_E_INVALID_ARG, "sigmas must be > 0");
+  HIP_TRY(st->h, hipSetDevice(st->h->device));
+  HIP_TRY(st->h, hipStreamSynchronize(st->h->stream));
+  st->cfg = *cfg;
+  return post_tables(st);
+}
+
+int vss_postprocess_device(vss_post_state* st, const uint8_t* d_frames, int n, int height, int width, int channels,
+                           size_t row_stride, size_t frame_stride, const float* d_masks, float* d_alpha,
+                           uint8_t* d_alpha_u8, void* stream) {
+  if (!st) return fail(nullptr, VSS_E_INVALID_ARG, "null post state");
+  vss_handle* h = st->h;
+  if (!d_masks || (!d_frames && st->cfg.use_bilateral)) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride);
+  if (rc) return rc;
+  HIP_TRY(h, hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  return post_enqueue(st, d_frames, n, height, width, channels, row_stride, frame_stride, d_masks, d_alpha,
+                      d_alpha_u8, s);
+}
+
+int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, int n, int height, int width,
+                     int channels, size_t row_stride, float* alpha_out, uint8_t* alpha_u8_out) {
+  if (!h || !st || st->h != h) return fail(h, VSS_E_INVALID_ARG, "handle / post state mismatch");
+  if (!alpha_out && !alpha_u8_out) return fail(h, VSS_E_INVALID_ARG, "no output requested");
+  Busy b(h);
+  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
+  HIP_TRY(h, hipSetDevice(h->device));
+  const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
+  int rc = stage_in(h, frames, n, height, width, channels, row_stride, h->h_masks, VSS_OUT_MODEL);
+  if (rc) return rc;
+  // outputs: alpha into d_masks' tail is not allowed (masks are the input): use the post scratch
+  float* d_alpha = alpha_out ? h->d_post_alpha : nullptr;
+  uint8_t* d_u8 = alpha_u8_out ? h->d_post_u8 : nullptr;
+  rc = post_enqueue(st, h->d_frames, n, height, width, channels, row_stride, row_stride * (size_t)height,
+                    h->d_masks, d_alpha, d_u8, h->stream);
+  if (rc) return rc;
+  if (alpha_out) HIP_TRY(h, hipMemcpyAsync(alpha_out, d_alpha, (size_t)n * P * 4, hipMemcpyDeviceToHost, h->stream));
+  if (alpha_u8_out)
+    HIP_TRY(h, hipMemcpyAsync(alpha_u8_out, d_u8, (size_t)n * P, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
   return VSS_OK;
 }
 

@@ -5,6 +5,8 @@
 #include <cstddef>
 #include <cstdint>
 
+#include <hip/hip_runtime.h>
+
 namespace vss {
 
 // Arithmetic used for the pointwise (1x1) GEMMs.
@@ -182,5 +184,34 @@ struct PrepParams {      // standalone preprocess: frames -> [N][3][Hm][Wm] f32
   float* out;
   int N;
 };
+
+// Post-processing chain (vss_post.hip)
+struct PostEmaParams {
+  const float* masks;  // [n][P] raw seam masks
+  float* ema;          // [n][P] EMA outputs
+  float* state;        // [P] prevAlpha
+  const int* valid;    // 0 before the stream's first frame
+  int n;
+  long P;
+  double a;            // config.EMA
+};
+
+struct PostFilterParams {
+  const float* ema;      // [n][H][W]
+  const uint8_t* frames; // the n source frames (guide)
+  long row_stride, frame_stride;
+  int fh, fw, fc;
+  float ry, rx;
+  int H, W;
+  const double* rtab;    // exp(-r / (2 sigma_r^2)), r = 0 .. 3*255^2
+  double sw[3];          // exp(-s / (2 sigma_s^2)), s = 0, 1, 2
+  double lo, hi, denom, gamma;
+  int use_bilateral;
+  float* alpha;          // [n][H][W] refined (may be null)
+  uint8_t* alpha_u8;     // [n][H][W] (may be null)
+};
+
+void launch_post_ema(const PostEmaParams& p, hipStream_t s);
+void launch_post_filter(const PostFilterParams& p, int n, hipStream_t s);
 
 }  // namespace vss

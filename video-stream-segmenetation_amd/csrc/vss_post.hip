@@ -1,0 +1,183 @@
+// vss_post.hip — §8(f) row 1: the reference's mask post-processing on the GPU.
+//
+// The chain processFrame applies to the seam's mask
+// (/root/reference/client/src/core/frameProcessorTest.ts:115-169):
+//   temporalEMA :218-227 -> morphologicalOpening :644-685 -> jointBilateral3x3
+//   :230-266 (guide :315-321) -> refineAlphaOnce :270-313 -> alphaToImageData
+//   :204-216.
+// The reference computes in JS doubles and stores every intermediate in a
+// Float32Array; these kernels do exactly that (double arithmetic, f32 stores,
+// no FMA contraction), so they agree with the reference's own code run under
+// Node (tests/golden/post_chain.npz) bit for bit up to the last-ulp
+// differences of pow() between math libraries.  The guide image (a browser
+// canvas resample in the reference) is defined as the model input's
+// tfjs-legacy bilinear rounded half up to u8.
+//
+//   k_post_ema    : per pixel, the EMA recurrence over the batch's consecutive
+//                   frames (all loads in flight), state = prevAlpha (:47).
+//   k_post_filter : per frame and 8x32 output tile: 3x3 erosion then dilation
+//                   (halo 3, the 1-px image border left 0), the guide, the
+//                   joint bilateral (weights from a host-built exp table),
+//                   refine, u8 alpha.
+#include <hip/hip_runtime.h>
+
+#include "vss_kernels.h"
+
+namespace vss {
+
+__global__ __launch_bounds__(256) void k_post_ema(PostEmaParams p) {
+#pragma clang fp contract(off)
+  const bool valid = *p.valid != 0;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < p.P; i += (long)gridDim.x * 256) {
+    float prev = p.state[i];
+    for (int t0 = 0; t0 < p.n; t0 += 8) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = p.masks[(long)min(t0 + u, p.n - 1) * p.P + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int t = t0 + u;
+        if (t < p.n) {
+          // temporalEMA: the first frame of a stream passes through and seeds prevAlpha
+          const float e = (!valid && t == 0) ? x[u] : (float)(p.a * (double)prev + (1.0 - p.a) * (double)x[u]);
+          p.ema[(long)t * p.P + i] = e;
+          prev = e;
+        }
+      }
+    }
+    p.state[i] = prev;
+  }
+}
+
+// guide pixel: tfjs-legacy bilinear of the frame at (y, x), rounded half up to u8
+__device__ __forceinline__ unsigned guide_rgb(const uint8_t* f, long rs, int fc, int fh, int fw, float ry, float rx,
+                                              int y, int x) {
+#pragma clang fp contract(off)
+  const float fy = (float)y * ry, fx = (float)x * rx;
+  const int y0 = (int)floorf(fmaxf(fy, 0.f)), x0 = (int)floorf(fmaxf(fx, 0.f));
+  const int y1 = min(fh - 1, (int)ceilf(fy)), x1 = min(fw - 1, (int)ceilf(fx));
+  const float dy = fy - (float)y0, dx = fx - (float)x0;
+  const uint8_t* t0 = f + (long)y0 * rs;
+  const uint8_t* t1 = f + (long)y1 * rs;
+  unsigned rgb = 0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float tl = t0[x0 * fc + c], tr = t0[x1 * fc + c], bl = t1[x0 * fc + c], br = t1[x1 * fc + c];
+    const float top = __builtin_fmaf(tr - tl, dx, tl);
+    const float bot = __builtin_fmaf(br - bl, dx, bl);
+    const float v = __builtin_fmaf(bot - top, dy, top);
+    rgb |= (unsigned)floorf(v + 0.5f) << (8 * c);
+  }
+  return rgb;
+}
+
+template <int TH, int TW>
+__global__ __launch_bounds__(256) void k_post_filter(PostFilterParams p) {
+#pragma clang fp contract(off)
+  constexpr int EH = TH + 6, EW = TW + 6, RH = TH + 4, RW = TW + 4, OH = TH + 2, OW = TW + 2;
+  __shared__ float E[EH][EW];
+  __shared__ float R[RH][RW];
+  __shared__ float O[OH][OW];
+  __shared__ unsigned G[OH][OW];
+  const int tid = threadIdx.x, t = blockIdx.z;
+  const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
+  const int H = p.H, W = p.W;
+  const float* e = p.ema + (long)t * H * W;
+  // EMA values on the halo-3 region (outside the image: never read as data)
+  for (int i = tid; i < EH * EW; i += 256) {
+    const int ly = i / EW, lx = i % EW;
+    const int yy = min(max(y0 - 3 + ly, 0), H - 1), xx = min(max(x0 - 3 + lx, 0), W - 1);
+    E[ly][lx] = e[(long)yy * W + xx];
+  }
+  // guide on the halo-1 region
+  if (p.use_bilateral) {
+    const uint8_t* f = p.frames + (long)t * p.frame_stride;
+    for (int i = tid; i < OH * OW; i += 256) {
+      const int ly = i / OW, lx = i % OW;
+      const int yy = y0 - 1 + ly, xx = x0 - 1 + lx;
+      G[ly][lx] = (yy >= 0 && yy < H && xx >= 0 && xx < W)
+                      ? guide_rgb(f, p.row_stride, p.fc, p.fh, p.fw, p.ry, p.rx, yy, xx) : 0u;
+    }
+  }
+  __syncthreads();
+  // erosion (3x3 min, start 1.0) on the interior, 0 on the image border
+  for (int i = tid; i < RH * RW; i += 256) {
+    const int ly = i / RW, lx = i % RW;
+    const int yy = y0 - 2 + ly, xx = x0 - 2 + lx;
+    float m = 0.f;
+    if (yy >= 1 && yy < H - 1 && xx >= 1 && xx < W - 1) {
+      m = 1.0f;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) m = E[ly + dy][lx + dx] < m ? E[ly + dy][lx + dx] : m;
+    }
+    R[ly][lx] = m;
+  }
+  __syncthreads();
+  // dilation (3x3 max, start 0.0) of the erosion
+  for (int i = tid; i < OH * OW; i += 256) {
+    const int ly = i / OW, lx = i % OW;
+    const int yy = y0 - 1 + ly, xx = x0 - 1 + lx;
+    float m = 0.f;
+    if (yy >= 1 && yy < H - 1 && xx >= 1 && xx < W - 1) {
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) m = R[ly + dy][lx + dx] > m ? R[ly + dy][lx + dx] : m;
+    }
+    O[ly][lx] = m;
+  }
+  __syncthreads();
+  for (int i = tid; i < TH * TW; i += 256) {
+    const int ly = i / TW, lx = i % TW;
+    const int y = y0 + ly, x = x0 + lx;
+    if (y >= H || x >= W) continue;
+    float v = O[ly + 1][lx + 1];
+    if (p.use_bilateral) {
+      const unsigned c0 = G[ly + 1][lx + 1];
+      const int r0 = c0 & 255, g0 = (c0 >> 8) & 255, b0 = (c0 >> 16) & 255;
+      double sw = 0.0, sa = 0.0;
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy) {
+        if (y + dy < 0 || y + dy >= H) continue;
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (x + dx < 0 || x + dx >= W) continue;
+          const unsigned c = G[ly + 1 + dy][lx + 1 + dx];
+          const int dr = (int)(c & 255) - r0, dg = (int)((c >> 8) & 255) - g0, db = (int)((c >> 16) & 255) - b0;
+          const double wgt = p.sw[dx * dx + dy * dy] * p.rtab[dr * dr + dg * dg + db * db];
+          sw += wgt;
+          sa += wgt * (double)O[ly + 1 + dy][lx + 1 + dx];
+        }
+      }
+      if (sw > 0.0) v = (float)(sa / sw);
+    }
+    // refineAlphaOnce (no face prior)
+    double r = v;
+    if (r <= p.lo) r = 0.0;
+    else if (r >= p.hi) r = 1.0;
+    else r = pow((r - p.lo) / p.denom, p.gamma);
+    const float rf = (float)r;
+    const long o = ((long)t * H + y) * W + x;
+    if (p.alpha) p.alpha[o] = rf;
+    if (p.alpha_u8) {
+      const double a = rf < 0.f ? 0.0 : (rf > 1.f ? 1.0 : (double)rf);
+      p.alpha_u8[o] = (uint8_t)floor(a * 255.0 + 0.5);  // Math.round(a * 255)
+    }
+  }
+}
+
+constexpr int kPostTH = 8, kPostTW = 32;
+
+void launch_post_ema(const PostEmaParams& p, hipStream_t s) {
+  const int grid = (int)std::min<long>((p.P + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_post_ema, dim3(grid), dim3(256), 0, s, p);
+}
+
+void launch_post_filter(const PostFilterParams& p, int n, hipStream_t s) {
+  hipLaunchKernelGGL((k_post_filter<kPostTH, kPostTW>), dim3((p.W + kPostTW - 1) / kPostTW, (p.H + kPostTH - 1) / kPostTH, n),
+                     dim3(256), 0, s, p);
+}
+
+}  // namespace vss
