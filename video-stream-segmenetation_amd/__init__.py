@@ -24,7 +24,9 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libvss.so")
+# VSS_LIBRARY selects another build of the same ABI (e.g. lib/libvss_trace.so
+# for tools/trace_phases.py); the default is the in-tree product library.
+LIB_PATH = os.environ.get("VSS_LIBRARY") or os.path.join(HERE, "lib", "libvss.so")
 DEFAULT_WEIGHTS = os.path.join(HERE, "model", "vss_weights_seed7.bin")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "vss.h")
 

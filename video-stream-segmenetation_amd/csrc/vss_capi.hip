@@ -12,6 +12,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -48,6 +49,9 @@ struct LayerPlan {
   int mode = -1, stride = 1, chid = 0;
   int TH = 0, TW = 0, tiles_x = 0, tiles_y = 0, grid_x = 0, grid_y = 0;
   int flags = 0;
+  int ks = 1, xp = 1, sp = 1;  // hidden split of this layer, parts of its x / skip (block_flags)
+  size_t part_stride = 0;      // floats between the parts of act
+  long wimg_stride = 0;        // floats between the slices' weight images
   size_t lds = 0;
   const BlockEntry* entry = nullptr;  // compiled shape (registry)
   float* act = nullptr;        // [max_batch][H][W][C]
@@ -64,6 +68,8 @@ using GraphKey = std::tuple<const void*, const void*, int, int, int, int, size_t
 thread_local std::string g_tls_error;
 
 }  // namespace
+
+constexpr long kDefaultKsplitPixels = 256;
 
 struct vss_handle {
   vss_config cfg{};
@@ -84,6 +90,10 @@ struct vss_handle {
   size_t frame_cap = 0;
   uint8_t* h_frames = nullptr;  // pinned staging
   float* h_masks = nullptr;
+#ifdef VSS_TRACE
+  std::vector<unsigned long long*> trace;  // per layer, [grid][4] stamps
+  std::vector<int> trace_wgs;              // workgroups of the layer's last launch
+#endif
   float* d_post_alpha = nullptr;  // vss_segment_post outputs [max_batch][P]
   uint8_t* d_post_u8 = nullptr;
   std::atomic<int> busy{0};
@@ -91,6 +101,9 @@ struct vss_handle {
   int profile = 0;
   static constexpr int kMaxBranches = 8;
   int branches = 1;  // parallel sub-batch chains inside the captured graph
+  // expand layers with at most this many output pixels per frame split their
+  // hidden channels over ks_max() workgroups (env VSS_KSPLIT_PIXELS overrides)
+  long ksplit_pixels = kDefaultKsplitPixels;
   hipStream_t branch_streams[kMaxBranches] = {};
   hipEvent_t fork_ev = nullptr, join_ev[kMaxBranches] = {};
   std::map<GraphKey, hipGraphExec_t> graphs;
@@ -141,7 +154,18 @@ uint16_t bf16_bits(float f) {  // pointwise weights are bf16-exact: truncation i
 
 size_t block_lds_bytes(const LayerPlan& l, int TH, int TW) {
   const int cskip = l.mode == MODE_DEC ? (int)l.rec.chid : 0;
-  return (size_t)block_lds(l.mode, l.stride, TH, TW, (int)l.rec.cin, cskip, l.chid, l.C).total * 4;
+  return (size_t)block_lds(l.mode, l.stride, TH, TW, (int)l.rec.cin, cskip, l.chid / l.ks, l.C).total * 4;
+}
+
+// Largest hidden split of an expand layer that leaves every wave >= 1 chunk of
+// 16 channels (mirrors ks_max() in tools/gen_registry.py, which compiles the
+// split variants).
+int ks_max(const LayerPlan& l) {
+  if (l.mode != MODE_IR_EXPAND) return 1;
+  const int nchunk = l.chid / 16;
+  for (int k : {4, 3, 2})
+    if (nchunk % k == 0 && nchunk / k >= 4) return k;
+  return 1;
 }
 
 void set_tile(LayerPlan& l, const BlockEntry* e) {
@@ -165,7 +189,7 @@ int choose_tile(vss_handle* h, LayerPlan& l, int N) {
   for (int i = 0; i < count; ++i) {
     const BlockEntry& e = reg[i];
     if (e.mode != l.mode || e.stride != l.stride || e.cin != (int)l.rec.cin || e.cskip != cskip ||
-        e.chid != l.chid || e.cout != l.C || e.flags != l.flags)
+        e.chid != l.chid / l.ks || e.cout != l.C || e.flags != l.flags)
       continue;
     const long blocks = (long)((l.H + e.TH - 1) / e.TH) * ((l.W + e.TW - 1) / e.TW) * N;
     const size_t lds = block_lds_bytes(l, e.TH, e.TW);
@@ -189,7 +213,7 @@ std::vector<const BlockEntry*> tile_candidates(const LayerPlan& l) {
   std::vector<const BlockEntry*> out;
   for (int i = 0; i < count; ++i) {
     const BlockEntry& e = reg[i];
-    if (e.mode == l.mode && e.stride == l.stride && e.cin == (int)l.rec.cin && e.cskip == cskip && e.chid == l.chid &&
+    if (e.mode == l.mode && e.stride == l.stride && e.cin == (int)l.rec.cin && e.cskip == cskip && e.chid == l.chid / l.ks &&
         e.cout == l.C && e.flags == l.flags)
       out.push_back(&e);
   }
@@ -269,8 +293,14 @@ int plan(vss_handle* h) {
     } else {
       return bad("unknown kind");
     }
-    if (r.kind == K_IR) l.flags = (r.flags & F_RESIDUAL) ? 2 : 0;
-    if (r.kind == K_DEC) l.flags = h->L[r.src].rec.kind == K_DEC ? 1 : 0;
+    // hidden split: expand layers whose output has at most ksplit_pixels
+    // pixels per frame (a function of the model resolution only, so results
+    // never depend on the batch or the autotuner)
+    if (l.mode == MODE_IR_EXPAND && (long)l.H * l.W <= h->ksplit_pixels) l.ks = ks_max(l);
+    if (r.kind == K_IR || r.kind == K_DEC) l.xp = h->L[r.src].ks;
+    if (r.kind == K_DEC) l.sp = h->L[r.skip].ks;
+    if (r.kind == K_IR) l.flags = block_flags(0, (r.flags & F_RESIDUAL) != 0, l.xp, 1, l.ks);
+    if (r.kind == K_DEC) l.flags = block_flags(h->L[r.src].rec.kind == K_DEC, 0, l.xp, l.sp, 1);
     if (l.mode >= 0) {
       int rc = choose_tile(h, l, N);
       if (rc) return rc;
@@ -309,26 +339,31 @@ int upload(vss_handle* h) {
     if ((expand && !exact(r.off[O_W1], (size_t)r.chid * r.cin)) || !exact(r.off[O_W2], (size_t)r.cout * l.chid))
       return fail(h, VSS_E_UNSUPPORTED, "layer " + std::to_string(i) + ": pointwise weights must be bf16-exact");
     const int cskip = l.mode == MODE_DEC ? (int)r.chid : 0;
-    const BlockLds B = block_lds(l.mode, l.stride, 1, 16, (int)r.cin, cskip, l.chid, l.C);
-    const size_t base = img.size(), span = (size_t)(B.lr - B.w1);
-    img.resize(base + span, 0.f);
-    float* im = img.data() + base;
-    auto put_bf16 = [&](int region, uint32_t off, int rows, int k, int ld) {
-      uint16_t* d = reinterpret_cast<uint16_t*>(im + (region - B.w1));
-      for (int a = 0; a < rows; ++a)
-        for (int b = 0; b < k; ++b) d[(size_t)a * ld + b] = bf16_bits(h->hdata[off + (size_t)a * k + b]);
-    };
-    if (expand) {
-      put_bf16(B.w1, r.off[O_W1], l.chid, (int)r.cin, B.LD1);
-      for (int c = 0; c < l.chid; ++c) im[B.b1 - B.w1 + c] = h->hdata[r.off[O_B1] + c];
-    }
-    put_bf16(B.w2, r.off[O_W2], l.C, l.chid, B.LD2);
-    for (int t = 0; t < 9; ++t)
-      for (int c = 0; c < l.chid; ++c) im[B.wdw - B.w1 + t * l.chid + c] = h->hdata[r.off[O_WDW] + (size_t)c * 9 + t];
-    for (int c = 0; c < l.chid; ++c) im[B.bdw - B.w1 + c] = h->hdata[r.off[O_BDW] + c];
-    for (int c = 0; c < l.C; ++c) im[B.b2 - B.w1 + c] = h->hdata[r.off[O_B2] + c];
-    img_off[i] = base;
+    const int cs = l.chid / l.ks;  // hidden channels per slice
+    const BlockLds B = block_lds(l.mode, l.stride, 1, 16, (int)r.cin, cskip, cs, l.C);
+    const size_t span = (size_t)(B.lr - B.w1);  // one slice's image (floats, multiple of 4)
+    img_off[i] = img.size();
     img_len[i] = span;
+    for (int sl = 0; sl < l.ks; ++sl) {
+      const int h0 = sl * cs;  // first hidden channel of the slice
+      const size_t base = img.size();
+      img.resize(base + span, 0.f);
+      float* im = img.data() + base;
+      auto bf = [&](uint32_t off, size_t k) { return bf16_bits(h->hdata[off + k]); };
+      if (expand) {
+        uint16_t* d = reinterpret_cast<uint16_t*>(im + (B.w1 - B.w1));
+        for (int a = 0; a < cs; ++a)
+          for (int b = 0; b < (int)r.cin; ++b) d[(size_t)a * B.LD1 + b] = bf(r.off[O_W1], (size_t)(h0 + a) * r.cin + b);
+        for (int c = 0; c < cs; ++c) im[B.b1 - B.w1 + c] = h->hdata[r.off[O_B1] + h0 + c];
+      }
+      uint16_t* d2 = reinterpret_cast<uint16_t*>(im + (B.w2 - B.w1));
+      for (int a = 0; a < l.C; ++a)
+        for (int b = 0; b < cs; ++b) d2[(size_t)a * B.LD2 + b] = bf(r.off[O_W2], (size_t)a * l.chid + h0 + b);
+      for (int t = 0; t < 9; ++t)
+        for (int c = 0; c < cs; ++c) im[B.wdw - B.w1 + t * cs + c] = h->hdata[r.off[O_WDW] + (size_t)(h0 + c) * 9 + t];
+      for (int c = 0; c < cs; ++c) im[B.bdw - B.w1 + c] = h->hdata[r.off[O_BDW] + h0 + c];
+      for (int c = 0; c < l.C; ++c) im[B.b2 - B.w1 + c] = h->hdata[r.off[O_B2] + c];
+    }
   }
   float* d_img = nullptr;
   if ((rc = dalloc(h, &d_img, img.size() * 4))) return rc;
@@ -341,14 +376,24 @@ int upload(vss_handle* h) {
   for (size_t i = 0; i < h->L.size(); ++i) {
     LayerPlan& l = h->L[i];
     const Rec& r = l.rec;
-    if ((rc = dalloc(h, &l.act, (size_t)N * l.H * l.W * l.C * 4))) return rc;
-    HIP_TRY(h, hipMemset(l.act, 0, (size_t)N * l.H * l.W * l.C * 4));
+    l.part_stride = (size_t)N * l.H * l.W * l.C;
+    if ((rc = dalloc(h, &l.act, l.part_stride * l.ks * 4))) return rc;
+    HIP_TRY(h, hipMemset(l.act, 0, l.part_stride * l.ks * 4));
+#ifdef VSS_TRACE
+    if (h->trace.size() != h->L.size()) {
+      h->trace.assign(h->L.size(), nullptr);
+      h->trace_wgs.assign(h->L.size(), 0);
+    }
+    if ((rc = dalloc(h, &h->trace[i], (size_t)N * l.H * l.W * 16 * 8))) return rc;
+    HIP_TRY(h, hipMemset(h->trace[i], 0, (size_t)N * l.H * l.W * 16 * 8));
+#endif
     if (r.kind == K_STEM) {
       l.stem_w = dp(r.off[O_W1]);
       l.stem_b = dp(r.off[O_B1]);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
       l.wimg = d_img + img_off[i];
       l.wimg_f4 = (int)(img_len[i] / 4);
+      l.wimg_stride = (long)img_len[i];
       if (r.kind == K_DEC) {
         l.gamma = dp(r.off[O_GAMMA]);
         l.beta = dp(r.off[O_BETA]);
@@ -381,6 +426,9 @@ BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n, int f0 
   const size_t fa = (size_t)f0 * h->acc_stride;
   BlockParams p{};
   p.wimg = l.wimg;
+  p.wimg_stride = l.wimg_stride;
+  p.x_part_stride = (long)src.part_stride;
+  p.y_part_stride = (long)l.part_stride;
   p.x = src.act + f0 * frame_elems(src);
   p.y = l.act + f0 * frame_elems(l);
   p.eps = h->eps;
@@ -394,6 +442,7 @@ BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n, int f0 
   } else {
     const LayerPlan& sk = h->L[r.skip];
     p.skip = sk.act + f0 * frame_elems(sk);
+    p.skip_part_stride = (long)sk.part_stride;
     p.cskip = (int)r.chid;
     p.relu6_dw = 0;
     p.out_acc = h->d_acc + fa + l.acc_off;
@@ -439,10 +488,20 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       p.Ho = l.H; p.Wo = l.W; p.cout = l.C;
       p.acc_zero = h->d_acc + (size_t)f0 * h->acc_stride;
       p.acc_stride = h->acc_stride;
+#ifdef VSS_TRACE
+      p.trace = h->trace[i];
+      h->trace_wgs[i] = ((l.W + 31) / 32) * ((l.H + 7) / 8) * n;
+#endif
       go(stem_kernel16(), dim3((l.W + 31) / 32, (l.H + 7) / 8, n), 0, p);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
+#ifdef VSS_TRACE
+      BlockParams p = block_params(h, l, n, f0);
+      p.trace = h->trace[i];
+      h->trace_wgs[i] = l.tiles_x * l.tiles_y * n * l.ks;
+#else
       const BlockParams p = block_params(h, l, n, f0);
-      go(l.entry->fn[prec == PREC_F32 ? 0 : 1], dim3(l.tiles_x, l.tiles_y, n), l.lds, p);
+#endif
+      go(l.entry->fn[prec == PREC_F32 ? 0 : 1], dim3(l.tiles_x, l.tiles_y, n * l.ks), l.lds, p);
     } else if (r.kind == K_HEAD) {
       const LayerPlan& src = h->L[r.src];
       HeadParams p{};
@@ -452,6 +511,10 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       p.gamma = src.gamma; p.beta = src.beta; p.eps = h->eps;
       p.w = l.head_w; p.b = l.head_b; p.mask = masks;
       p.N = n; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
+#ifdef VSS_TRACE
+      p.trace = h->trace[i];
+      h->trace_wgs[i] = ((Wm + 63) / 64) * ((Hm + 15) / 16) * n;
+#endif
       go(head_kernel16(), dim3((Wm + 63) / 64, (Hm + 15) / 16, n), 0, p);
     }
   }
@@ -599,7 +662,7 @@ int autotune(vss_handle* h) {
           hipSuccess)
         continue;
       const BlockParams p = block_params(h, l, N);
-      const dim3 grid(l.tiles_x, l.tiles_y, N);
+      const dim3 grid(l.tiles_x, l.tiles_y, N * l.ks);
       for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(kThreads), l.lds, h->stream, p);
       (void)hipEventRecord(e0, h->stream);
       for (int k = 0; k < 8; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(kThreads), l.lds, h->stream, p);
@@ -656,6 +719,7 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
     return rc;
   };
   if (hipSetDevice(h->device) != hipSuccess) return bail(fail(h, VSS_E_HIP, "hipSetDevice failed"));
+  if (const char* ev = std::getenv("VSS_KSPLIT_PIXELS")) h->ksplit_pixels = std::atol(ev);
   int rc = load_weights(h);
   if (!rc) rc = plan(h);
   if (!rc) rc = upload(h);
@@ -843,7 +907,15 @@ int vss_read_layer(vss_handle* h, int layer, int n, float* host_out) {
   if (l.rec.kind == K_HEAD) return fail(h, VSS_E_INVALID_ARG, "the head's output is the mask buffer");
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipDeviceSynchronize());
-  HIP_TRY(h, hipMemcpy(host_out, l.act, (size_t)n * l.H * l.W * l.C * 4, hipMemcpyDeviceToHost));
+  const size_t cnt = (size_t)n * l.H * l.W * l.C;
+  HIP_TRY(h, hipMemcpy(host_out, l.act, cnt * 4, hipMemcpyDeviceToHost));
+  if (l.ks > 1) {  // a split layer's value = its parts summed in part order, as its consumers do
+    std::vector<float> part(cnt);
+    for (int q = 1; q < l.ks; ++q) {
+      HIP_TRY(h, hipMemcpy(part.data(), l.act + q * l.part_stride, cnt * 4, hipMemcpyDeviceToHost));
+      for (size_t k = 0; k < cnt; ++k) host_out[k] += part[k];
+    }
+  }
   return VSS_OK;
 }
 
@@ -1053,3 +1125,15 @@ int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, i
 }
 
 }  // extern "C"
+
+#ifdef VSS_TRACE
+// Trace build only: the stamps of `layer`'s last launch, [wgs][16] u64
+// (s_memrealtime ticks, 100 MHz).  Returns the workgroup count.
+extern "C" int vss_trace_read(vss_handle* h, int layer, unsigned long long* out, int cap) {
+  if (!h || layer < 0 || layer >= (int)h->L.size() || !out) return VSS_E_INVALID_ARG;
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  const int wgs = std::min(h->trace_wgs[layer], cap);
+  HIP_TRY(h, hipMemcpy(out, h->trace[layer], (size_t)wgs * 16 * 8, hipMemcpyDeviceToHost));
+  return wgs;
+}
+#endif

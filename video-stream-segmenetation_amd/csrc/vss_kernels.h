@@ -19,6 +19,22 @@ enum Prec : int { PREC_F32 = 0, PREC_BF16X2 = 1, PREC_BF16 = 2 };
 
 enum BlockMode : int { MODE_IR_EXPAND = 0, MODE_IR_DIRECT = 1, MODE_DEC = 2 };
 
+// k_block FLAGS: bit 0 the decoder's src needs instance norm + ReLU, bit 1
+// residual add, bits 2-3 XP-1, bits 4-5 SP-1, bits 6-7 KS-1 where
+//   KS = hidden-channel split of this (expand) layer: KS workgroups per tile,
+//        slice s owns hidden channels [s*chid/KS, (s+1)*chid/KS) and writes
+//        its partial project sum to part s of the output (bias and residual
+//        in part 0): deep low-res layers get KS x the workgroups and 1/KS of
+//        the weights per workgroup;
+//   XP / SP = parts of the x / skip input, summed in part order (fixed, so
+//        results never depend on the tiling) as the prologue loads them.
+__host__ __device__ constexpr int block_flags(int norm_in, int residual, int xp, int sp, int ks) {
+  return (norm_in ? 1 : 0) | (residual ? 2 : 0) | ((xp - 1) << 2) | ((sp - 1) << 4) | ((ks - 1) << 6);
+}
+__host__ __device__ constexpr int flags_xp(int f) { return ((f >> 2) & 3) + 1; }
+__host__ __device__ constexpr int flags_sp(int f) { return ((f >> 4) & 3) + 1; }
+__host__ __device__ constexpr int flags_ks(int f) { return ((f >> 6) & 3) + 1; }
+
 constexpr int kThreads = 256;       // 4 wave64 per workgroup
 constexpr int kMaxAcc = 16;         // 16x16 project accumulators per wave
 constexpr int kAccSlots = 16;       // instance-norm accumulator slots per frame and layer
@@ -33,7 +49,7 @@ __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 struct BlockLds {
   int IH, IW, P_in, P_in_pad, P_out, CX, XS, LD1, LD2, SR, SC;
   int NCB, NPB, NCHUNK, PW, CS, NPBW, NACC;  // CS = chunk groups, PW = pixel-block groups
-  int xt, w1, w2, wdw, bdw, b1, b2, lr, nrm, work, stt, total;
+  int xt, xr, w1, w2, wdw, bdw, b1, b2, lr, nrm, work, stt, total;
   int slab_stride;  // floats per wave slab = P_out * (cout + 4)
 };
 
@@ -66,6 +82,9 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   L.slab_stride = L.P_out * (cout + 4);
   int o = 0;
   L.xt = o;  o += r4(L.P_in_pad * L.XS);
+  // expand blocks keep xt as MFMA operands (bf16 hi/lo pairs in the split
+  // mode); the residual-capable shape keeps the exact f32 centre here
+  L.xr = o;  o += (mode == 0 && stride == 1 && cin == cout) ? r4(L.P_out * cin) : 0;
   L.w1 = o;  o += mode == 0 ? r4(chid * L.LD1 / 2) : 0;
   L.w2 = o;  o += r4(cout * L.LD2 / 2);
   L.wdw = o; o += r4(9 * chid);
@@ -88,8 +107,36 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
 //   for each 16-channel chunk c0 of the hidden/concat dim:
 //     (expand pw on MFMA) -> dw3x3 (VALU) -> project pw accumulate (MFMA)
 //   -> epilogue (bias, residual, store, instance-norm partial stats)
+// Opt-in phase trace (make trace -> libvss_trace.so; never in the product
+// build): thread 0 of every workgroup stamps s_memrealtime (100 MHz, one
+// clock for the whole device) at: 0 start, 1 prologue committed, 2 main
+// done, 3 end, 4 every prologue load landed, 5 decoder src norm ready, 6
+// every prologue load issued; slots 8-15 the same points in shader clocks
+// (s_memtime), so the trace also gives the core clock.
+#ifdef VSS_TRACE
+#define VSS_TRACE_FIELD unsigned long long* trace;
+#define VSS_STAMP(k)                                                                                  \
+  do {                                                                                                \
+    if (threadIdx.x == 0 && p.trace) {                                                                \
+      unsigned long long* t_ = p.trace + (((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 16; \
+      t_[(k)] = __builtin_amdgcn_s_memrealtime();                                                     \
+      t_[8 + (k)] = __builtin_amdgcn_s_memtime();                                                     \
+    }                                                                                                 \
+  } while (0)
+#else
+#define VSS_TRACE_FIELD
+#define VSS_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 struct BlockParams {
-  const float* wimg;     // the layer's LDS weight image (block_lds regions w1..b2), built by the host
+  const float* wimg;     // the layer's LDS weight image (block_lds regions w1..b2), built by the host;
+                         // with KS > 1 one image per hidden slice, wimg_stride floats apart
+  long wimg_stride;
+  long x_part_stride;    // floats between the parts of x / skip / y (see block_flags)
+  long skip_part_stride;
+  long y_part_stride;
   const float* x;        // IR input [N][H][W][cin]   | DEC low-res src [N][h][w][cin]
   const float* skip;     // DEC skip [N][Ho][Wo][cskip]
   float* y;              // output [N][Ho][Wo][cout]
@@ -123,6 +170,7 @@ struct BlockParams {
   int TH, TW;            // output tile
   int tiles_x, tiles_y;
   int norm_in;           // DEC: src needs norm+relu
+  VSS_TRACE_FIELD
 };
 
 using BlockFn = void (*)(BlockParams);
@@ -147,6 +195,7 @@ struct StemParams {
   int Ho, Wo, cout;
   unsigned long long* acc_zero;  // all decoder norm accumulators [N][acc_stride]: zeroed here
   int acc_stride;
+  VSS_TRACE_FIELD
 };
 
 struct HeadParams {
@@ -161,6 +210,7 @@ struct HeadParams {
   float* mask;           // [N][Hm][Wm] f32
   int N, h, w_, cin;
   int Hm, Wm;
+  VSS_TRACE_FIELD
 };
 
 // Instance-norm scale/shift of one channel from the exact fixed-point totals.

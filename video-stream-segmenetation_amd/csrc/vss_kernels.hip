@@ -128,14 +128,20 @@ template <int COUT>
 __global__ __launch_bounds__(256) void k_stem(StemParams p) {
   constexpr int TH = 8, TW = 32, IH = 2 * TH + 1, IW = 2 * TW + 1, IWP = IW + 1;
   __shared__ float xs[3][IH][IWP];
-  __shared__ float ws[COUT * 27];
+  __shared__ __attribute__((aligned(16))) float ws[27 * COUT];  // [tap][c]: 4 channels per LDS read
   __shared__ float bs[COUT];
   const int tid = threadIdx.x;
   const int n = blockIdx.z, oy0 = blockIdx.y * TH, ox0 = blockIdx.x * TW;
   const uint8_t* f = p.frames + (long)n * p.frame_stride;
   const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
+  VSS_STAMP(0);
   // all frame gathers of this thread issued before any is consumed
-  constexpr int NS = (IH * IW + 255) / 256;
+  constexpr int NS = (IH * IW + 255) / 256, NW = (27 * COUT + 255) / 256;
+  // the weights' loads go out first (they are consumed after the gathers)
+  float wr[NW];
+#pragma unroll
+  for (int u = 0; u < NW; ++u) wr[u] = p.w[min(tid + 256 * u, 27 * COUT - 1)];
+  const float br = p.b[min(tid, COUT - 1)];
   uint32_t raw[NS][12];
   float dys[NS], dxs[NS];
 #pragma unroll
@@ -165,9 +171,15 @@ __global__ __launch_bounds__(256) void k_stem(StemParams p) {
   // start of the forward: zero this frame's decoder norm accumulators
   if (blockIdx.x == 0 && blockIdx.y == 0)
     for (int i = tid; i < p.acc_stride; i += 256) p.acc_zero[(long)n * p.acc_stride + i] = 0ull;
-  for (int i = tid; i < COUT * 27; i += 256) ws[i] = p.w[i];
-  if (tid < COUT) bs[tid] = p.b[tid];
+#pragma unroll
+  for (int u = 0; u < NW; ++u) {
+    const int i = tid + 256 * u;  // p.w is [c][27]
+    if (i < 27 * COUT) ws[(i % 27) * COUT + i / 27] = wr[u];
+  }
+  if (tid < COUT) bs[tid] = br;
   __syncthreads();
+  VSS_STAMP(1);
+  VSS_STAMP(2);
   const int ly = tid / TW, lx = tid - ly * TW;
   float acc[COUT];
 #pragma unroll
@@ -179,8 +191,15 @@ __global__ __launch_bounds__(256) void k_stem(StemParams p) {
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const float xv = xs[ci][2 * ly + ky][2 * lx + kx];
+        const f4* wt = reinterpret_cast<const f4*>(ws + (ci * 9 + ky * 3 + kx) * COUT);
 #pragma unroll
-        for (int c = 0; c < COUT; ++c) acc[c] = __builtin_fmaf(ws[c * 27 + ci * 9 + ky * 3 + kx], xv, acc[c]);
+        for (int q = 0; q < COUT / 4; ++q) {
+          const f4 w4 = wt[q];
+          acc[4 * q] = __builtin_fmaf(w4.x, xv, acc[4 * q]);
+          acc[4 * q + 1] = __builtin_fmaf(w4.y, xv, acc[4 * q + 1]);
+          acc[4 * q + 2] = __builtin_fmaf(w4.z, xv, acc[4 * q + 2]);
+          acc[4 * q + 3] = __builtin_fmaf(w4.w, xv, acc[4 * q + 3]);
+        }
       }
   const int oy = oy0 + ly, ox = ox0 + lx;
   if (oy < p.Ho && ox < p.Wo) {
@@ -189,6 +208,7 @@ __global__ __launch_bounds__(256) void k_stem(StemParams p) {
     for (int q = 0; q < COUT / 4; ++q)
       o[q] = f4{relu6f(acc[4 * q]), relu6f(acc[4 * q + 1]), relu6f(acc[4 * q + 2]), relu6f(acc[4 * q + 3])};
   }
+  VSS_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------
@@ -243,6 +263,29 @@ __device__ __forceinline__ f4 mma16<PREC_BF16X2>(f4 acc, bf8 a, f4 b) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc, 0, 0, 0);
 }
 
+// B operands stored ready for the MFMA: f32 as is, or for the split mode the
+// (hi, lo) bf16 pairs of mma16<PREC_BF16X2> packed in the same 16 bytes, so the
+// conversion happens once when the tile is written, not once per use.
+template <int PREC>
+__device__ __forceinline__ f4 to_operand(f4 v) {
+  if constexpr (PREC == PREC_F32) {
+    return v;
+  } else {
+    const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
+    const __bf16 l0 = (__bf16)(v.x - (float)h0), l1 = (__bf16)(v.y - (float)h1);
+    const __bf16 l2 = (__bf16)(v.z - (float)h2), l3 = (__bf16)(v.w - (float)h3);
+    return __builtin_bit_cast(f4, bf8{h0, h1, h2, h3, l0, l1, l2, l3});
+  }
+}
+
+template <int PREC>
+__device__ __forceinline__ f4 mma16_op(f4 acc, typename AFrag<PREC>::T a, f4 op) {
+  if constexpr (PREC == PREC_F32)
+    return mma16<PREC_F32>(acc, a, op);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf8, op), acc, 0, 0, 0);
+}
+
 // Orders one wave's LDS writes before its other lanes' reads (and keeps the
 // compiler from moving LDS accesses across it); no workgroup barrier.
 __device__ __forceinline__ void wave_sync() {
@@ -278,6 +321,21 @@ struct Staged {
   }
 };
 
+// Commit XP staged copies of the same items as their sum, in part order.
+template <int TOTAL, int XP, class Store>
+__device__ __forceinline__ void commit_sum(const Staged<TOTAL> (&st)[XP], Store store) {
+#pragma unroll
+  for (int u = 0; u < Staged<TOTAL>::PER; ++u) {
+    const int i = (int)threadIdx.x + 256 * u;
+    if (i < TOTAL) {
+      f4 v = st[0].v[u];
+#pragma unroll
+      for (int q = 1; q < XP; ++q) v = v + st[q].v[u];
+      store(i, v);
+    }
+  }
+}
+
 // Fused inverted-residual / decoder block, specialised on its whole shape
 // (every tile and channel extent a compile-time constant: index math folds
 // to shifts/multiplies, loops unroll, accumulators stay in registers).
@@ -299,6 +357,9 @@ template <int MODE, int STRIDE, int TH, int TW, int CIN, int CSKIP, int CH, int 
 __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   constexpr BlockLds L = block_lds(MODE, STRIDE, TH, TW, CIN, CSKIP, CH, COUT);
   constexpr bool NORM_IN = (FLAGS & 1) != 0, RES = (FLAGS & 2) != 0;
+  constexpr int XP = flags_xp(FLAGS), SP = flags_sp(FLAGS), KS = flags_ks(FLAGS);
+  static_assert(KS == 1 || MODE == MODE_IR_EXPAND, "only expand layers split their hidden channels");
+  static_assert(SP == 1 || MODE == MODE_DEC, "skip parts: decoder only");
   constexpr int IW = L.IW, P_IN = L.P_in, P_IN_PAD = L.P_in_pad, P_OUT = L.P_out, XS = L.XS;
   constexpr int NCB = L.NCB, NPB = L.NPB, NCHUNK = L.NCHUNK, PW = L.PW, CS = L.CS, NPBW = L.NPBW;
   constexpr int RS = COUT + 4, SS = L.slab_stride;
@@ -311,7 +372,8 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int n = blockIdx.z;
+  const int n = KS == 1 ? (int)blockIdx.z : (int)blockIdx.z / KS;  // grid z = frame * KS + slice
+  const int ks = KS == 1 ? 0 : (int)blockIdx.z % KS;
   const int oy0 = blockIdx.y * TH, ox0 = blockIdx.x * TW;
   const int iy0 = STRIDE * oy0 - 1, ix0 = STRIDE * ox0 - 1;
   const int Ho = p.Ho, Wo = p.Wo;
@@ -324,10 +386,11 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   const float* b2s = smem + L.b2;
   float* work = smem + L.work;
   float* stt = smem + L.stt;
+  VSS_STAMP(0);
 
   // ---- prologue: issue every load, then commit to LDS ----
   constexpr int WIMG_F4 = (L.lr - L.w1) / 4;
-  const f4* wsrc = reinterpret_cast<const f4*>(p.wimg);
+  const f4* wsrc = reinterpret_cast<const f4*>(p.wimg + ks * p.wimg_stride);
   f4* wdst = reinterpret_cast<f4*>(smem + L.w1);
   if constexpr (MODE == MODE_DEC) {
     constexpr int CL = CIN, C4L = CL / 4, C4S = CSKIP / 4, SR = L.SR, SC = L.SC;
@@ -344,29 +407,35 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
       st_slots.issue([&](int i) {
         return reinterpret_cast<const f4*>(p.in_acc + (long)n * p.acc_stride)[i];
       });
-    Staged<SR * SC * C4L> st_lr;
-    Staged<P_IN_PAD * C4S> st_sk;
+    Staged<SR * SC * C4L> st_lr[XP];
+    Staged<P_IN_PAD * C4S> st_sk[SP];
     Staged<WIMG_F4> st_w;
-    st_lr.issue([&](int i) {
-      const int pr = i / C4L, c4 = i % C4L;
-      const int yy = min(h - 1, sy0 + pr / SC), xx = min(w - 1, sx0 + pr % SC);
-      return *reinterpret_cast<const f4*>(xn + ((long)yy * w + xx) * CL + 4 * c4);
-    });
-    st_sk.issue([&](int i) {
-      const int pix = i / C4S, c4 = i % C4S;
-      const int yy = min(max(iy0 + pix / IW, 0), Ho - 1), xx = min(max(ix0 + pix % IW, 0), Wo - 1);
-      return *reinterpret_cast<const f4*>(sn + ((long)yy * Wo + xx) * CSKIP + 4 * c4);
-    });
+#pragma unroll
+    for (int q = 0; q < XP; ++q)
+      st_lr[q].issue([&](int i) {
+        const int pr = i / C4L, c4 = i % C4L;
+        const int yy = min(h - 1, sy0 + pr / SC), xx = min(w - 1, sx0 + pr % SC);
+        return *reinterpret_cast<const f4*>(xn + q * p.x_part_stride + ((long)yy * w + xx) * CL + 4 * c4);
+      });
+#pragma unroll
+    for (int q = 0; q < SP; ++q)
+      st_sk[q].issue([&](int i) {
+        const int pix = i / C4S, c4 = i % C4S;
+        const int yy = min(max(iy0 + pix / IW, 0), Ho - 1), xx = min(max(ix0 + pix % IW, 0), Wo - 1);
+        return *reinterpret_cast<const f4*>(sn + q * p.skip_part_stride + ((long)yy * Wo + xx) * CSKIP + 4 * c4);
+      });
     st_w.issue([&](int i) { return wsrc[i]; });
+    VSS_STAMP(6);  // every load issued
     if constexpr (NORM_IN) st_slots.commit([&](int i, f4 v) { reinterpret_cast<f4*>(work)[i] = v; });
-    st_lr.commit([&](int i, f4 v) { reinterpret_cast<f4*>(lr)[i] = v; });
-    st_sk.commit([&](int i, f4 v) {
+    commit_sum(st_lr, [&](int i, f4 v) { reinterpret_cast<f4*>(lr)[i] = v; });
+    commit_sum(st_sk, [&](int i, f4 v) {
       const int pix = i / C4S, c4 = i % C4S;
       const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
       const bool valid = pix < P_IN && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo;
       *reinterpret_cast<f4*>(xt + pix * XS + CL + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
     });
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
+    VSS_STAMP(4);
     __syncthreads();
     if constexpr (NORM_IN) {
       // sum the slots (exact, any order) -> the src's scale/shift
@@ -379,6 +448,14 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
           q_fx += sl[k * 2 * CL + CL + tid];
         }
         norm_affine(s_fx, q_fx, p.in_hw, p.eps, p.in_gamma[tid], p.in_beta[tid], nrm + tid, nrm + CL + tid);
+      }
+      __syncthreads();
+      VSS_STAMP(5);
+      // relu(src * scale + shift) once per low-res element, in place
+      for (int i = tid; i < SR * SC * C4L; i += 256) {
+        const int c4 = i % C4L;
+        f4* v = reinterpret_cast<f4*>(lr) + i;
+        *v = reluv(*v * *reinterpret_cast<const f4*>(nrm + 4 * c4) + *reinterpret_cast<const f4*>(nrm + CL + 4 * c4));
       }
       __syncthreads();
     }
@@ -400,18 +477,10 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
           const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
           const int r0 = min(max(y0 - sy0, 0), SR - 1), r1 = min(max(y1 - sy0, 0), SR - 1);
           const int q0 = min(max(x0 - sx0, 0), SC - 1), q1 = min(max(x1 - sx0, 0), SC - 1);
-          f4 v00 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q0) * CL + 4 * c4);
-          f4 v01 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q1) * CL + 4 * c4);
-          f4 v10 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q0) * CL + 4 * c4);
-          f4 v11 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q1) * CL + 4 * c4);
-          if constexpr (NORM_IN) {
-            const f4 sc = *reinterpret_cast<const f4*>(nrm + 4 * c4);
-            const f4 sh = *reinterpret_cast<const f4*>(nrm + CL + 4 * c4);
-            v00 = reluv(v00 * sc + sh);
-            v01 = reluv(v01 * sc + sh);
-            v10 = reluv(v10 * sc + sh);
-            v11 = reluv(v11 * sc + sh);
-          }
+          const f4 v00 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q0) * CL + 4 * c4);
+          const f4 v01 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q1) * CL + 4 * c4);
+          const f4 v10 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q0) * CL + 4 * c4);
+          const f4 v11 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q1) * CL + 4 * c4);
           v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
         }
         *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
@@ -421,34 +490,46 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
     constexpr int C4 = CIN / 4;
     const int H = p.H, W = p.W;
     const float* xn = p.x + (long)n * H * W * CIN;
-    Staged<P_IN_PAD * C4> st_x;
+    Staged<P_IN_PAD * C4> st_x[XP];
     Staged<WIMG_F4> st_w;
-    st_x.issue([&](int i) {
-      const int pix = i / C4, c4 = i % C4;
-      const int yy = min(max(iy0 + pix / IW, 0), H - 1), xx = min(max(ix0 + pix % IW, 0), W - 1);
-      return *reinterpret_cast<const f4*>(xn + ((long)yy * W + xx) * CIN + 4 * c4);
-    });
+#pragma unroll
+    for (int q = 0; q < XP; ++q)
+      st_x[q].issue([&](int i) {
+        const int pix = i / C4, c4 = i % C4;
+        const int yy = min(max(iy0 + pix / IW, 0), H - 1), xx = min(max(ix0 + pix % IW, 0), W - 1);
+        return *reinterpret_cast<const f4*>(xn + q * p.x_part_stride + ((long)yy * W + xx) * CIN + 4 * c4);
+      });
     st_w.issue([&](int i) { return wsrc[i]; });
-    st_x.commit([&](int i, f4 v) {
+    VSS_STAMP(6);  // every load issued
+    commit_sum(st_x, [&](int i, f4 v) {
       const int pix = i / C4, c4 = i % C4;
-      const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
+      const int py = pix / IW, px = pix % IW;
+      const int yy = iy0 + py, xx = ix0 + px;
       const bool valid = pix < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
-      *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+      const f4 x = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (MODE == MODE_IR_EXPAND) {
+        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = to_operand<PREC>(x);
+        if constexpr (RES)
+          if (py >= 1 && py <= TH && px >= 1 && px <= TW)
+            *reinterpret_cast<f4*>(smem + L.xr + ((py - 1) * TW + px - 1) * CIN + 4 * c4) = x;
+      } else {
+        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = x;
+      }
     });
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
+    VSS_STAMP(4);
   }
   __syncthreads();
+  VSS_STAMP(1);
 
   // ---- main: per-wave work units ----
   f4 acc[L.NACC];
 #pragma unroll
   for (int t = 0; t < L.NACC; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-  const int cg = lane & 3;
   const int pw = wave % PW, cw = wave / PW;
 
   if constexpr (MODE == MODE_IR_EXPAND) {
     float* hid = work + wave * (P_IN_PAD + P_OUT) * 16;
-    float* dwo = hid + P_IN_PAD * 16;
     constexpr int NK = CIN / 16;
     for (int ck = wave; ck < NCHUNK; ck += 4) {
       const int c0 = ck << 4;
@@ -456,25 +537,31 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
 #pragma unroll
       for (int s = 0; s < NK; ++s) aw[s] = lds_a<PREC>(w1s, L.LD1, c0 + r, 16 * s + 4 * g);
       const f4 bias = *reinterpret_cast<const f4*>(b1s + c0 + 4 * g);
-#pragma unroll 2
-      for (int cb = 0; cb < P_IN_PAD / 16; ++cb) {
+      constexpr int NCBI = P_IN_PAD / 16, UNR = NCBI <= 6 ? NCBI : 2;
+#pragma unroll UNR
+      for (int cb = 0; cb < NCBI; ++cb) {
         const int pix = cb * 16 + r;
         f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < NK; ++s) d = mma16<PREC>(d, aw[s], *reinterpret_cast<const f4*>(xt + pix * XS + 16 * s + 4 * g));
+        for (int s = 0; s < NK; ++s) d = mma16_op<PREC>(d, aw[s], *reinterpret_cast<const f4*>(xt + pix * XS + 16 * s + 4 * g));
         const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
         const bool valid = pix < P_IN && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
         *reinterpret_cast<f4*>(hid + pix * 16 + 4 * g) = valid ? relu6v(d + bias) : f4{0.f, 0.f, 0.f, 0.f};
       }
       wave_sync();
+      // dw 3x3 computed straight into the project MFMA's B layout: lane (r, g)
+      // evaluates pixel r of the block for hidden channels c0+4g..c0+4g+3
       {
         f4 wk[9];
 #pragma unroll
-        for (int t = 0; t < 9; ++t) wk[t] = *reinterpret_cast<const f4*>(wdws + t * CH + c0 + 4 * cg);
-        const f4 bb = *reinterpret_cast<const f4*>(bdws + c0 + 4 * cg);
+        for (int t = 0; t < 9; ++t) wk[t] = *reinterpret_cast<const f4*>(wdws + t * CH + c0 + 4 * g);
+        const f4 bb = *reinterpret_cast<const f4*>(bdws + c0 + 4 * g);
+        typename AFrag<PREC>::T a2[NCB];
 #pragma unroll
-        for (int k = 0; k < P_OUT / 16; ++k) {
-          const int pix = (lane >> 2) + 16 * k;
+        for (int cb = 0; cb < NCB; ++cb) a2[cb] = lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) {
+          const int pix = pb * 16 + r;
           const int ly = pix / TW, lx = pix % TW;
           f4 a = bb;
 #pragma unroll
@@ -482,52 +569,43 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
               const int sp = (STRIDE * ly + ky) * IW + (STRIDE * lx + kx);
-              a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(hid + sp * 16 + 4 * cg) + a;
+              a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(hid + sp * 16 + 4 * g) + a;
             }
-          *reinterpret_cast<f4*>(dwo + pix * 16 + 4 * cg) = relu6v(a);
+          const f4 b = to_operand<PREC>(relu6v(a));
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) acc[pb * NCB + cb] = mma16_op<PREC>(acc[pb * NCB + cb], a2[cb], b);
         }
       }
-      wave_sync();
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        const auto a = lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g);
-#pragma unroll
-        for (int pb = 0; pb < NPB; ++pb)
-          acc[pb * NCB + cb] =
-              mma16<PREC>(acc[pb * NCB + cb], a, *reinterpret_cast<const f4*>(dwo + (pb * 16 + r) * 16 + 4 * g));
-      }
-      wave_sync();
+      wave_sync();  // this chunk's hid reads before the next chunk's expand writes
     }
   } else {
-    float* dwo = work + wave * 256;
-    const int pl = lane >> 2;
+    // dw 3x3 straight into the project MFMA's B layout (lane (r, g): pixel r
+    // of the block, channels c0+4g..c0+4g+3); no LDS round trip, no syncs
 #pragma unroll
     for (int i = 0; i < NPBW; ++i) {
-      const int pix = (pw + i * PW) * 16 + pl;
+      const int pix = (pw + i * PW) * 16 + r;
       const int ly = pix / TW, lx = pix % TW;
       for (int ck = cw; ck < NCHUNK; ck += CS) {
         const int c0 = ck << 4;
-        f4 a = *reinterpret_cast<const f4*>(bdws + c0 + 4 * cg);
+        f4 a = *reinterpret_cast<const f4*>(bdws + c0 + 4 * g);
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx)
-            a = *reinterpret_cast<const f4*>(wdws + (ky * 3 + kx) * CH + c0 + 4 * cg) *
-                    *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx + kx) * XS + c0 + 4 * cg) + a;
+            a = *reinterpret_cast<const f4*>(wdws + (ky * 3 + kx) * CH + c0 + 4 * g) *
+                    *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx + kx) * XS + c0 + 4 * g) + a;
         if constexpr (MODE == MODE_IR_DIRECT) a = relu6v(a);
-        *reinterpret_cast<f4*>(dwo + pl * 16 + 4 * cg) = a;
-        wave_sync();
-        const f4 b = *reinterpret_cast<const f4*>(dwo + r * 16 + 4 * g);
+        const f4 b = to_operand<PREC>(a);
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb)
-          acc[i * NCB + cb] = mma16<PREC>(acc[i * NCB + cb], lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g), b);
-        wave_sync();
+          acc[i * NCB + cb] = mma16_op<PREC>(acc[i * NCB + cb], lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g), b);
       }
     }
   }
 
   // ---- epilogue: slabs -> fixed-order sum, bias, residual, store ----
   __syncthreads();  // every wave is done with its scratch (reused as slabs)
+  VSS_STAMP(2);
   {
     float* slab = work + cw * SS;
 #pragma unroll
@@ -552,9 +630,17 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
       f4 v = *reinterpret_cast<const f4*>(work + pix * RS + 4 * c4);
 #pragma unroll
       for (int s = 1; s < CS; ++s) v = v + *reinterpret_cast<const f4*>(work + s * SS + pix * RS + 4 * c4);
-      v = v + *reinterpret_cast<const f4*>(b2s + 4 * c4);
-      if constexpr (RES) v = v + *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + 4 * c4);
-      if (valid) *reinterpret_cast<f4*>(p.y + (((long)n * Ho + oy) * Wo + ox) * COUT + 4 * c4) = v;
+      if (KS == 1 || ks == 0) {  // bias and residual belong to part 0
+        v = v + *reinterpret_cast<const f4*>(b2s + 4 * c4);
+        if constexpr (RES) {
+          if constexpr (MODE == MODE_IR_EXPAND)
+            v = v + *reinterpret_cast<const f4*>(smem + L.xr + pix * CIN + 4 * c4);
+          else
+            v = v + *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + 4 * c4);
+        }
+      }
+      if (valid)
+        *reinterpret_cast<f4*>(p.y + ks * p.y_part_stride + (((long)n * Ho + oy) * Wo + ox) * COUT + 4 * c4) = v;
       if constexpr (MODE == MODE_DEC)
         *reinterpret_cast<f4*>(work + pix * RS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
     }
@@ -591,6 +677,7 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  VSS_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------
@@ -604,6 +691,7 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
   const int oy0 = blockIdx.y * OTH, ox0 = blockIdx.x * OTW;
   const int h = p.h, w = p.w_;
   const int zr0 = oy0 / 2 - 1, zc0 = ox0 / 2 - 1;
+  VSS_STAMP(0);
   // issue this thread's d3 loads before the statistics reduction
   f4 xv[NZ][C / 4];
 #pragma unroll
@@ -633,6 +721,7 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
     norm_affine(s_fx, q_fx, h * w, p.eps, p.gamma[tid], p.beta[tid], sc + tid, sh + tid);
   }
   __syncthreads();
+  VSS_STAMP(1);
 #pragma unroll
   for (int u = 0; u < NZ; ++u) {
     const int i = tid + 256 * u;
@@ -647,6 +736,7 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
     }
   }
   __syncthreads();
+  VSS_STAMP(2);
 #pragma unroll
   for (int k = 0; k < (OTH * OTW) / 256; ++k) {
     const int idx = tid + 256 * k;
@@ -666,6 +756,7 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
       p.mask[((long)n * p.Hm + oy) * p.Wm + ox] = 1.0f / (1.0f + expf(-v));
     }
   }
+  VSS_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------
