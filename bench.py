@@ -15,7 +15,11 @@ Also measured in the same run:
     of K steps, against 8 TB/s;
   * mask max-abs error vs the CPU oracle on this run's frames;
   * cpu_baseline: the oracle (C restatement, f32) on a bounded sample of the
-    same frames on this host's cores (rank 0, N=1 only).
+    same frames on this host's cores (rank 0, N=1 only);
+  * post: the GPU post-processing chain (EMA ->
+    opening -> joint bilateral -> refine -> u8 alpha) over the same batch as
+    consecutive frames of one stream: frames/s, its HBM roofline and parity
+    with the oracle (rank 0, outside the headline's timed region).
 """
 from __future__ import annotations
 
@@ -68,6 +72,59 @@ def cpu_baseline(blob, frames, hm, wm, budget_s):
                       f"{threads} threads; 4 threads: {res['4'][1]} frames in {res['4'][2]:.1f} s"}
 
 
+def post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, steps, warmup, cpu_s):
+    """Time the post chain on the seam's masks; check it against the oracle."""
+    import torch
+    import vss_amd.costmodel as cm
+    P = hm * wm
+    chain = pkg.PostChain(sess)
+    d_alpha = torch.empty((B, P), dtype=torch.float32, device=d_masks.device)
+    d_u8 = torch.empty((B, P), dtype=torch.uint8, device=d_masks.device)
+    rs, fs = fw * 3, fh * fw * 3
+
+    def run():
+        chain.process_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_masks.data_ptr(), d_alpha.data_ptr(),
+                             d_u8.data_ptr(), stream.cuda_stream)
+
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            run()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    # parity: a fresh stream state over this batch vs the oracle on the same masks
+    chain.reset()
+    with torch.cuda.stream(stream):
+        run()
+    torch.cuda.synchronize()
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+    masks = d_masks.cpu().numpy().reshape(B, hm, wm)
+    want_a, want_u = oracle_py.post(masks, frames, oracle_py.PostState(hm, wm))
+    got_a = d_alpha.cpu().numpy().reshape(B, hm, wm)
+    got_u = d_u8.cpu().numpy().reshape(B, hm, wm)
+    cpu = None
+    if cpu_s > 0:
+        done, t0 = 0, time.perf_counter()
+        st = oracle_py.PostState(hm, wm)
+        while time.perf_counter() - t0 < cpu_s:
+            oracle_py.post(masks, frames, st)
+            done += B
+        cpu = round(done / (time.perf_counter() - t0), 1)
+    chain.close()
+    b = cm.post_bytes(hm, wm, fh, fw, 3, B)
+    achieved = b["total"] * B / (ms * 1e-3)
+    return {"value": round(B / (ms * 1e-3), 1), "unit": "frames/s", "ms_per_batch": round(ms, 5),
+            "alg_bytes_per_frame": round(b["total"]), "GBps": round(achieved / 1e9, 1),
+            "frac": round(achieved / HBM_PEAK, 4), "alpha_max_abs_err": float(np.abs(got_a - want_a).max()),
+            "u8_mismatches": int((got_u != want_u).sum()), "cpu_baseline_fps_1thread": cpu,
+            "kernels": "k_post_ema + k_post_filter (timed together with torch events on the launch stream)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -81,6 +138,7 @@ def main():
     ap.add_argument("--branches", type=int, default=1, help="concurrent sub-batch chains inside the graph")
     ap.add_argument("--cpu-budget-s", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-post", action="store_true", help="skip the post-processing leg")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_traffic.json"),
                     help="per-kernel HBM traffic from tools/prof_summary.py (PMC passes)")
     args = ap.parse_args()
@@ -168,6 +226,11 @@ def main():
         if t and t.get("traffic_bytes"):
             traffic = round(t["traffic_bytes"] / 1e6, 3)
 
+    post = None
+    if rank == 0 and not args.no_post:
+        post = post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, args.steps,
+                        args.warmup, 0.0 if args.no_cpu else 2.0)
+
     out = None
     if rank == 0:
         masks = d_masks.cpu().numpy()
@@ -221,6 +284,7 @@ def main():
             },
             "kernels": per_layer,
             "cpu_baseline": cpu,
+            "post": post,
         }
         print(json.dumps(out), flush=True)
     sess.close()

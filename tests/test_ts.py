@@ -68,3 +68,36 @@ def test_node_segment_matches_oracle_and_python_host(addon_built, pkg, oracle, b
     with pkg.Session(dtype=dtype, max_batch=3, max_frame_h=480, max_frame_w=640) as s:
         py, _, _ = s.segment_frames(frames)
     assert np.array_equal(masks, py)
+
+
+@pytest.mark.gpu
+def test_node_post_chain_matches_oracle_and_python_host(addon_built, pkg, oracle, synthetic, tmp_path):
+    """PostChain (TS) over two calls of one stream == the oracle chain on the
+    GPU's masks == the Python host's PostChain, bit for bit; a live knob change
+    (USE_BILATERAL off, GAMMA 1) after reset matches the oracle too."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n, h, w = 4, 240, 320
+    frames = np.stack([synthetic.make_frame(700 + i, h, w, 3) for i in range(n)])
+    fp, op = tmp_path / "frames.bin", tmp_path / "post"
+    frames.tofile(fp)
+    out = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "run_post.js"), str(fp), str(n), str(h), str(w),
+                          "3", str(op), "bf16x2"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    assert info == {"width": 256, "height": 144, "count": n, "badConfigRejected": True}
+    alpha = np.fromfile(str(op) + ".f32", np.float32).reshape(n, 144, 256)
+    u8 = np.fromfile(str(op) + ".u8", np.uint8).reshape(n, 144, 256)
+    nobil = np.fromfile(str(op) + "_nobil.f32", np.float32).reshape(n, 144, 256)
+    with pkg.Session(dtype="bf16x2", max_batch=n, max_frame_h=h, max_frame_w=w) as s:
+        masks = s.segment_frames(frames)[0].reshape(n, 144, 256)
+        chain = pkg.PostChain(s)
+        pa, pu, _, _ = chain.segment(frames)
+    want_a, want_u = oracle.post(masks, frames, oracle.PostState(144, 256))
+    assert np.array_equal(alpha, want_a) and np.array_equal(u8, want_u)
+    assert np.array_equal(alpha, pa.reshape(alpha.shape)) and np.array_equal(u8, pu.reshape(u8.shape))
+    cfg = oracle.PostConfig.default()
+    cfg.use_bilateral, cfg.gamma = 0, 1.0
+    want_nb, _ = oracle.post(masks, frames, oracle.PostState(144, 256), cfg)
+    assert np.array_equal(nobil, want_nb)

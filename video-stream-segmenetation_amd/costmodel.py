@@ -106,3 +106,18 @@ if __name__ == "__main__":
         print(x)
     print(summary(recs, 144, 256, 480, 640))
     _ = math
+
+
+def post_bytes(hm: int, wm: int, fh: int, fw: int, fc: int = 3, n: int = 8) -> dict:
+    """Compulsory HBM bytes per frame of the post-processing chain (csrc/vss_post.hip)
+    for n consecutive frames per call:
+      k_post_ema    : seam mask read + EMA write (4+4 B/px) + the stream state
+                      read and written once per call (8 B/px / n);
+      k_post_filter : EMA read (4 B/px), the guide's frame rows (rows touched x
+                      row bytes, as the stem), refinedAlpha f32 write + alpha u8
+                      write (5 B/px)."""
+    p = hm * wm
+    frame = rows_touched(fh, hm) * fw * fc
+    ema = 8 * p + 8 * p / n
+    filt = 4 * p + frame + 5 * p
+    return {"ema": ema, "filter": filt, "total": ema + filt, "frame": frame}

@@ -11,13 +11,22 @@
 //   segment(handle, frames: Uint8Array|Uint8ClampedArray, n, height, width, channels, rowStride)
 //       -> Promise<Float32Array>      (n * maskH * maskW masks; rejects with Error(vss_last_error))
 //   destroy(handle)
+//   postCreate(handle, config?) -> post     (config keys as the reference's `config`:
+//                                             EMA, NOISE_CUTOFF, HIGH_THRESHOLD, GAMMA,
+//                                             USE_BILATERAL, BILATERAL_SIGMA_SPATIAL,
+//                                             BILATERAL_SIGMA_RANGE; frameProcessorTest.ts:12-30)
+//   postSetConfig(post, config), postReset(post), postDestroy(post)
+//   segmentPost(handle, post, frames, n, height, width, channels, rowStride)
+//       -> Promise<{alpha: Float32Array, alphaU8: Uint8Array}>   (processFrame :78-169)
 // segment runs vss_segment on a libuv worker thread (napi_create_async_work),
 // so the event loop is not blocked — as `await session.run` does not block.
 #include <node_api.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../../include/vss.h"
 
@@ -31,15 +40,47 @@ namespace {
     }                                                                        \
   } while (0)
 
+struct Post;
+
 struct Handle {
   vss_handle* h = nullptr;
   int mask_h = 0, mask_w = 0;
+  std::vector<Post*> posts;  // destroyed before the handle, whatever order the GC finalizes in
 };
+
+struct Post {
+  Handle* hd = nullptr;
+  vss_post_state* st = nullptr;
+};
+
+void release_handle(Handle* hd) {
+  for (Post* p : hd->posts) {
+    if (p->st) vss_post_destroy(p->st);
+    p->st = nullptr;
+    p->hd = nullptr;
+  }
+  hd->posts.clear();
+  if (hd->h) vss_destroy(hd->h);
+  hd->h = nullptr;
+}
 
 void finalize_handle(napi_env, void* data, void*) {
   Handle* hd = static_cast<Handle*>(data);
-  if (hd->h) vss_destroy(hd->h);
+  release_handle(hd);
   delete hd;
+}
+
+void release_post(Post* p) {
+  if (p->st) vss_post_destroy(p->st);
+  p->st = nullptr;
+  if (p->hd) p->hd->posts.erase(std::remove(p->hd->posts.begin(), p->hd->posts.end(), p), p->hd->posts.end());
+  p->hd = nullptr;
+}
+
+void finalize_post(napi_env, void* data, void*) {
+  Post* p = static_cast<Post*>(data);
+  release_post(p);
+  delete p;
 }
 
 Handle* get_handle(napi_env env, napi_value v) {
@@ -163,11 +204,112 @@ napi_value Destroy(napi_env env, napi_callback_info info) {
   napi_value argv[1];
   NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
   void* p = nullptr;
-  if (napi_get_value_external(env, argv[0], &p) == napi_ok && p) {
-    Handle* hd = static_cast<Handle*>(p);
-    if (hd->h) vss_destroy(hd->h);
-    hd->h = nullptr;
+  if (napi_get_value_external(env, argv[0], &p) == napi_ok && p) release_handle(static_cast<Handle*>(p));
+  return nullptr;
+}
+
+bool get_double_prop(napi_env env, napi_value obj, const char* key, double* out) {
+  bool has = false;
+  if (napi_has_named_property(env, obj, key, &has) != napi_ok || !has) return false;
+  napi_value v;
+  napi_get_named_property(env, obj, key, &v);
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  if (t == napi_boolean) {
+    bool b = false;
+    napi_get_value_bool(env, v, &b);
+    *out = b ? 1.0 : 0.0;
+    return true;
   }
+  return napi_get_value_double(env, v, out) == napi_ok;
+}
+
+// The reference's config object (frameProcessorTest.ts:12-18) -> vss_post_config.
+void read_post_config(napi_env env, napi_value obj, vss_post_config* c) {
+  double ub = c->use_bilateral;
+  get_double_prop(env, obj, "EMA", &c->ema);
+  get_double_prop(env, obj, "NOISE_CUTOFF", &c->noise_cutoff);
+  get_double_prop(env, obj, "HIGH_THRESHOLD", &c->high_threshold);
+  get_double_prop(env, obj, "GAMMA", &c->gamma);
+  get_double_prop(env, obj, "BILATERAL_SIGMA_SPATIAL", &c->sigma_spatial);
+  get_double_prop(env, obj, "BILATERAL_SIGMA_RANGE", &c->sigma_range);
+  if (get_double_prop(env, obj, "USE_BILATERAL", &ub)) c->use_bilateral = ub != 0.0 ? 1 : 0;
+}
+
+void throw_vss(napi_env env, const char* what, int rc, const char* msg) {
+  const std::string m = std::string(what) + " failed (" + std::to_string(rc) + "): " + (msg ? msg : "");
+  napi_throw_error(env, std::to_string(rc).c_str(), m.c_str());
+}
+
+Post* get_post(napi_env env, napi_value v) {
+  void* p = nullptr;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, nullptr, "expected a vss post state");
+    return nullptr;
+  }
+  Post* ps = static_cast<Post*>(p);
+  if (!ps->st) {
+    napi_throw_error(env, nullptr, "vss post state already destroyed");
+    return nullptr;
+  }
+  return ps;
+}
+
+napi_value PostCreate(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Handle* hd = argc >= 1 ? get_handle(env, argv[0]) : nullptr;
+  if (!hd) return nullptr;
+  vss_post_config cfg;
+  vss_post_config_default(&cfg);
+  if (argc >= 2) read_post_config(env, argv[1], &cfg);
+  vss_post_state* st = nullptr;
+  const int rc = vss_post_create(hd->h, &cfg, &st);
+  if (rc != VSS_OK) {
+    throw_vss(env, "vss_post_create", rc, vss_last_error(hd->h));
+    return nullptr;
+  }
+  Post* p = new Post();
+  p->hd = hd;
+  p->st = st;
+  hd->posts.push_back(p);
+  napi_value ext;
+  NAPI_OK(env, napi_create_external(env, p, finalize_post, nullptr, &ext));
+  return ext;
+}
+
+napi_value PostSetConfig(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Post* p = argc >= 2 ? get_post(env, argv[0]) : nullptr;
+  if (!p) return nullptr;
+  vss_post_config cfg;
+  vss_post_config_default(&cfg);
+  read_post_config(env, argv[1], &cfg);
+  const int rc = vss_post_set_config(p->st, &cfg);
+  if (rc != VSS_OK) throw_vss(env, "vss_post_set_config", rc, vss_last_error(p->hd->h));
+  return nullptr;
+}
+
+napi_value PostReset(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Post* p = argc >= 1 ? get_post(env, argv[0]) : nullptr;
+  if (!p) return nullptr;
+  const int rc = vss_post_reset(p->st);
+  if (rc != VSS_OK) throw_vss(env, "vss_post_reset", rc, vss_last_error(p->hd->h));
+  return nullptr;
+}
+
+napi_value PostDestroy(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  void* p = nullptr;
+  if (argc >= 1 && napi_get_value_external(env, argv[0], &p) == napi_ok && p) release_post(static_cast<Post*>(p));
   return nullptr;
 }
 
@@ -175,9 +317,12 @@ struct SegmentWork {
   napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
   napi_ref frames_ref = nullptr, out_ref = nullptr;
+  napi_ref u8_ref = nullptr;             // segmentPost: the alpha bytes
   vss_handle* h = nullptr;
+  vss_post_state* post = nullptr;        // segmentPost only
   const uint8_t* frames = nullptr;
   float* out = nullptr;
+  uint8_t* out_u8 = nullptr;
   int n = 0, height = 0, width = 0, channels = 0;
   size_t row_stride = 0, out_count = 0;
   int rc = 0;
@@ -186,7 +331,12 @@ struct SegmentWork {
 
 void SegmentExecute(napi_env, void* data) {  // libuv worker thread: no JS calls here
   SegmentWork* w = static_cast<SegmentWork*>(data);
-  w->rc = vss_segment(w->h, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out, VSS_OUT_MODEL);
+  if (w->post)
+    w->rc = vss_segment_post(w->h, w->post, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out,
+                             w->out_u8);
+  else
+    w->rc =
+        vss_segment(w->h, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out, VSS_OUT_MODEL);
   if (w->rc != VSS_OK) w->err = vss_last_error(w->h);
 }
 
@@ -197,10 +347,21 @@ void SegmentComplete(napi_env env, napi_status, void* data) {
   if (w->rc == VSS_OK) {
     napi_value arr;
     napi_create_typedarray(env, napi_float32_array, w->out_count, ab, 0, &arr);
-    napi_resolve_deferred(env, w->deferred, arr);
+    if (w->post) {
+      napi_value ab8 = nullptr, arr8, o;
+      napi_get_reference_value(env, w->u8_ref, &ab8);
+      napi_create_typedarray(env, napi_uint8_array, w->out_count, ab8, 0, &arr8);
+      napi_create_object(env, &o);
+      napi_set_named_property(env, o, "alpha", arr);
+      napi_set_named_property(env, o, "alphaU8", arr8);
+      napi_resolve_deferred(env, w->deferred, o);
+    } else {
+      napi_resolve_deferred(env, w->deferred, arr);
+    }
   } else {
     napi_value msg, code, e;
-    const std::string m = "vss_segment failed (" + std::to_string(w->rc) + "): " + w->err;
+    const std::string m = std::string(w->post ? "vss_segment_post" : "vss_segment") + " failed (" +
+                          std::to_string(w->rc) + "): " + w->err;
     napi_create_string_utf8(env, m.c_str(), m.size(), &msg);
     napi_create_string_utf8(env, std::to_string(w->rc).c_str(), NAPI_AUTO_LENGTH, &code);
     napi_create_error(env, code, msg, &e);
@@ -208,20 +369,35 @@ void SegmentComplete(napi_env env, napi_status, void* data) {
   }
   napi_delete_reference(env, w->frames_ref);
   napi_delete_reference(env, w->out_ref);
+  if (w->u8_ref) napi_delete_reference(env, w->u8_ref);
   napi_delete_async_work(env, w->work);
   delete w;
 }
 
-napi_value Segment(napi_env env, napi_callback_info info) {
-  size_t argc = 7;
-  napi_value argv[7];
-  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
-  if (argc < 7) {
-    napi_throw_type_error(env, nullptr, "segment(handle, frames, n, height, width, channels, rowStride)");
+// segment(handle, frames, ...) and segmentPost(handle, post, frames, ...)
+napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post) {
+  size_t argc = 8;
+  napi_value all[8];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, all, nullptr, nullptr));
+  const size_t need = with_post ? 8 : 7;
+  if (argc < need) {
+    napi_throw_type_error(env, nullptr,
+                          with_post ? "segmentPost(handle, post, frames, n, height, width, channels, rowStride)"
+                                    : "segment(handle, frames, n, height, width, channels, rowStride)");
     return nullptr;
   }
-  Handle* hd = get_handle(env, argv[0]);
+  Handle* hd = get_handle(env, all[0]);
   if (!hd) return nullptr;
+  Post* ps = nullptr;
+  if (with_post) {
+    ps = get_post(env, all[1]);
+    if (!ps) return nullptr;
+    if (ps->hd != hd) {
+      napi_throw_error(env, nullptr, "post state belongs to another handle");
+      return nullptr;
+    }
+  }
+  napi_value* argv = with_post ? all + 1 : all;
   bool is_ta = false;
   napi_is_typedarray(env, argv[1], &is_ta);
   if (!is_ta) {
@@ -251,21 +427,32 @@ napi_value Segment(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   w->h = hd->h;
+  w->post = ps ? ps->st : nullptr;
   w->frames = static_cast<const uint8_t*>(data);
   w->out_count = (size_t)w->n * hd->mask_h * hd->mask_w;
   napi_value ab;
   void* out = nullptr;
   NAPI_OK(env, napi_create_arraybuffer(env, w->out_count * 4, &out, &ab));
   w->out = static_cast<float*>(out);
+  if (ps) {
+    napi_value ab8;
+    void* out8 = nullptr;
+    NAPI_OK(env, napi_create_arraybuffer(env, w->out_count, &out8, &ab8));
+    w->out_u8 = static_cast<uint8_t*>(out8);
+    napi_create_reference(env, ab8, 1, &w->u8_ref);
+  }
   napi_create_reference(env, argv[1], 1, &w->frames_ref);  // keep the frames alive until done
   napi_create_reference(env, ab, 1, &w->out_ref);
   napi_value promise, name;
   NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
-  napi_create_string_utf8(env, "vss_segment", NAPI_AUTO_LENGTH, &name);
+  napi_create_string_utf8(env, ps ? "vss_segment_post" : "vss_segment", NAPI_AUTO_LENGTH, &name);
   NAPI_OK(env, napi_create_async_work(env, nullptr, name, SegmentExecute, SegmentComplete, w, &w->work));
   NAPI_OK(env, napi_queue_async_work(env, w->work));
   return promise;
 }
+
+napi_value Segment(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, false); }
+napi_value SegmentPost(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, true); }
 
 napi_value Init(napi_env env, napi_value exports) {
   const napi_property_descriptor props[] = {
@@ -274,6 +461,11 @@ napi_value Init(napi_env env, napi_value exports) {
       {"info", nullptr, Info, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"segment", nullptr, Segment, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"destroy", nullptr, Destroy, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"postCreate", nullptr, PostCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"postSetConfig", nullptr, PostSetConfig, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"postReset", nullptr, PostReset, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"postDestroy", nullptr, PostDestroy, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"segmentPost", nullptr, SegmentPost, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;
