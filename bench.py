@@ -115,6 +115,29 @@ def post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, st
             oracle_py.post(masks, frames, st)
             done += B
         cpu = round(done / (time.perf_counter() - t0), 1)
+    # compositing (§8(f) row 3) of the same batch: frames + alpha bytes -> RGBA canvas
+    d_rgba = torch.empty((B, fh, fw, 4), dtype=torch.uint8, device=d_masks.device)
+
+    def comp():
+        pkg.composite_device(sess, d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_u8.data_ptr(), d_rgba.data_ptr(),
+                             stream=stream.cuda_stream)
+
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            comp()
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        for _ in range(steps):
+            comp()
+        c1.record(stream)
+    torch.cuda.synchronize()
+    cms = c0.elapsed_time(c1) / steps
+    comp_ok = bool(np.array_equal(d_rgba.cpu().numpy(), oracle_py.composite(frames, got_u)))
+    cbytes = fh * fw * 3 + hm * wm + fh * fw * 4
+    composite = {"value": round(B / (cms * 1e-3), 1), "unit": "frames/s", "ms_per_batch": round(cms, 5),
+                 "alg_bytes_per_frame": cbytes, "GBps": round(cbytes * B / (cms * 1e-3) / 1e9, 1),
+                 "frac": round(cbytes * B / (cms * 1e-3) / HBM_PEAK, 4), "bitexact_vs_oracle": comp_ok,
+                 "kernel": "k_composite (frame u8 RGB + mask alpha u8 -> RGBA u8 at frame resolution)"}
     chain.close()
     b = cm.post_bytes(hm, wm, fh, fw, 3, B)
     achieved = b["total"] * B / (ms * 1e-3)
@@ -122,7 +145,8 @@ def post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, st
             "alg_bytes_per_frame": round(b["total"]), "GBps": round(achieved / 1e9, 1),
             "frac": round(achieved / HBM_PEAK, 4), "alpha_max_abs_err": float(np.abs(got_a - want_a).max()),
             "u8_mismatches": int((got_u != want_u).sum()), "cpu_baseline_fps_1thread": cpu,
-            "kernels": "k_post_ema + k_post_filter (timed together with torch events on the launch stream)"}
+            "kernels": "k_post_ema + k_post_filter (timed together with torch events on the launch stream)",
+            "composite": composite}
 
 
 def main():

@@ -196,6 +196,24 @@ int vss_postprocess_device(vss_post_state* st, const uint8_t* d_frames, int n, i
 int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, int n, int height, int width,
                      int channels, size_t row_stride, float* alpha_out, uint8_t* alpha_u8_out);
 
+/* ---- §8(f) row 3: compositing (frameProcessorTest.ts:170-178) ----------------
+ * The output canvas (= the video's size, client/src/core/main.ts:43-44) after
+ * drawImage(video) and 'destination-in' drawImage(maskCanvas): RGBA u8
+ * (ImageData layout, not premultiplied), colour = the frame's, alpha = the
+ * mask's alpha bytes upscaled to the frame (half-pixel bilinear in f32, rounded
+ * half up — a definition: browser canvas filtering is not reproducible), colour
+ * 0 where alpha is 0.  d_alpha_u8 = [n][mask_h][mask_w] (vss_postprocess_device).
+ * out_row_stride: multiple of 4 bytes, >= 4 * width. */
+int vss_composite_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width, int channels,
+                         size_t row_stride, size_t frame_stride, const uint8_t* d_alpha_u8, uint8_t* d_out_rgba,
+                         size_t out_row_stride, size_t out_frame_stride, void* stream);
+
+/* Host-memory convenience: seam + post chain + compositing for n consecutive
+ * frames of the state's stream -> out_rgba [n][height][width][4]
+ * (replaces processFrame frameProcessorTest.ts:78-178). */
+int vss_segment_composite(vss_handle* h, vss_post_state* st, const uint8_t* frames, int n, int height, int width,
+                          int channels, size_t row_stride, uint8_t* out_rgba);
+
 #ifdef __cplusplus
 }
 #endif

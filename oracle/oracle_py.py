@@ -38,6 +38,8 @@ def lib():
         L.vsso_post.restype = I
         L.vsso_post_guide.argtypes = [P, I, I, I, I, Lg, Lg, I, I, P]
         L.vsso_post_guide.restype = I
+        L.vsso_composite.argtypes = [P, I, I, I, I, Lg, Lg, P, I, I, P]
+        L.vsso_composite.restype = I
         L.vsso_bf16_round.argtypes = [ctypes.c_float]
         L.vsso_bf16_round.restype = ctypes.c_float
         _lib = L
@@ -135,3 +137,16 @@ def post(masks: np.ndarray, frames: np.ndarray, state: PostState, cfg: PostConfi
     if rc:
         raise ValueError(f"vsso_post rc={rc}")
     return a, u
+
+
+def composite(frames: np.ndarray, alpha_u8: np.ndarray) -> np.ndarray:
+    """frames [n,fh,fw,3|4] u8 + mask alpha bytes [n,H,W] u8 -> RGBA [n,fh,fw,4] u8
+    (frameProcessorTest.ts:170-178 as defined in vss_oracle.c)."""
+    frames = np.ascontiguousarray(frames)
+    alpha_u8 = np.ascontiguousarray(alpha_u8, np.uint8)
+    n, fh, fw, c = frames.shape
+    _, H, W = alpha_u8.shape
+    out = np.empty((n, fh, fw, 4), np.uint8)
+    if lib().vsso_composite(_ptr(frames), n, fh, fw, c, fw * c, fh * fw * c, _ptr(alpha_u8), H, W, _ptr(out)):
+        raise ValueError("vsso_composite")
+    return out

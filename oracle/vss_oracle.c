@@ -510,3 +510,52 @@ int vsso_post_guide(const uint8_t* frames, int n, int fh, int fw, int fc, long r
               guide_px(frames + (long)t * frame_stride, row_stride, fc, fh, fw, ry, rx, y, x, ch);
   return 0;
 }
+
+/* §8(f) row 3 — compositing (frameProcessorTest.ts:170-178):
+ *   maskCtx.putImageData(alphaToImageData(refinedAlpha))         mask canvas, maskW x maskH
+ *   outputCtx.drawImage(video, 0, 0, outW, outH)                  output canvas = video size
+ *                                                                 (client/src/core/main.ts:43-44)
+ *   globalCompositeOperation = 'destination-in'; drawImage(maskCanvas, 0, 0, outW, outH)
+ * i.e. every output pixel keeps the frame's colour with alpha = the mask's
+ * alpha upscaled to the frame.  The browser's canvas filtering is not
+ * reproducible bit for bit, so it is DEFINED here as the half-pixel bilinear
+ * (align_corners=False) of the u8 alpha in f32, rounded half up; a pixel whose
+ * alpha is 0 reads back with colour 0 (canvas stores premultiplied colour).
+ * Output: non-premultiplied RGBA u8 (ImageData layout), [n][fh][fw][4]. */
+static inline void up_coord(int o, float scale, int in, int* i0, int* i1, float* l) {
+  float s = ((float)o + 0.5f) * scale - 0.5f;
+  if (s < 0.f) s = 0.f;
+  int a = (int)s;
+  if (a > in - 1) a = in - 1;
+  *i0 = a;
+  *i1 = a < in - 1 ? a + 1 : a;
+  *l = s - (float)a;
+}
+
+int vsso_composite(const uint8_t* frames, int n, int fh, int fw, int fc, long row_stride, long frame_stride,
+                   const uint8_t* alpha, int H, int W, uint8_t* out) {
+  if (!frames || !alpha || !out || n < 0 || fh < 1 || fw < 1 || (fc != 3 && fc != 4) || H < 1 || W < 1) return -1;
+  const float sy = (float)H / (float)fh, sx = (float)W / (float)fw;
+  for (int t = 0; t < n; ++t) {
+    const uint8_t* a = alpha + (long)t * H * W;
+    for (int y = 0; y < fh; ++y) {
+      int y0, y1;
+      float ly;
+      up_coord(y, sy, H, &y0, &y1, &ly);
+      const uint8_t* f = frames + (long)t * frame_stride + (long)y * row_stride;
+      uint8_t* o = out + (((long)t * fh + y) * fw) * 4;
+      for (int x = 0; x < fw; ++x) {
+        int x0, x1;
+        float lx;
+        up_coord(x, sx, W, &x0, &x1, &lx);
+        const float a00 = a[y0 * W + x0], a01 = a[y0 * W + x1], a10 = a[y1 * W + x0], a11 = a[y1 * W + x1];
+        const float top = fmaf(a01 - a00, lx, a00), bot = fmaf(a11 - a10, lx, a10);
+        const float v = fmaf(bot - top, ly, top);
+        const uint8_t A = (uint8_t)floorf(v + 0.5f);
+        for (int c = 0; c < 3; ++c) o[x * 4 + c] = A ? f[x * fc + c] : 0;
+        o[x * 4 + 3] = A;
+      }
+    }
+  }
+  return 0;
+}

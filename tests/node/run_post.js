@@ -23,6 +23,10 @@ async function main() {
   await post.reset();
   await post.setConfig({ USE_BILATERAL: false, GAMMA: 1.0 });
   const d = await post.processFrames(frames);
+  await post.reset();
+  await post.setConfig({});
+  const comp = await post.compositeFrames(frames);
+  fs.writeFileSync(outPrefix + '_rgba.u8', Buffer.from(comp.rgba.buffer, comp.rgba.byteOffset, comp.rgba.byteLength));
   let rejected = false;
   try { await post.setConfig({ BILATERAL_SIGMA_RANGE: 0 }); } catch (e) { rejected = e.code === '-1'; }
   const cat = (x, y, T) => { const o = new T(x.length + y.length); o.set(x, 0); o.set(y, x.length); return o; };

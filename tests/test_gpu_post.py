@@ -150,3 +150,49 @@ def test_post_errors(pkg, torch_cuda):
             chain.segment(np.zeros((3, 32, 32, 3), np.uint8))
         with pytest.raises(pkg.VssError):
             chain.set_config(BILATERAL_SIGMA_RANGE=0.0)
+
+
+@pytest.mark.parametrize("geom", [(2, 480, 640, 3, 144, 256, 0, 0), (3, 100, 150, 4, 48, 64, 40, 24),
+                                  (1, 1080, 1920, 3, 144, 256, 0, 0), (2, 7, 5, 3, 48, 64, 0, 8)])
+def test_composite_bitexact_vs_oracle(pkg, torch_cuda, synthetic, oracle, geom):
+    """§8(f) row 3: the RGBA output canvas, bit-exact with the oracle, incl. padded
+    input rows, padded output rows, tiny frames (mask larger than the frame)."""
+    torch = torch_cuda
+    n, fh, fw, c, H, W, pad_in, pad_out = geom
+    frames = _frames(synthetic, range(80, 80 + n), fh, fw, c)
+    rng = np.random.default_rng(fh)
+    alpha = rng.integers(0, 256, (n, H, W), dtype=np.uint8)
+    alpha[:, : H // 4] = 0
+    alpha[:, -H // 4:] = 255
+    want = oracle.composite(frames, alpha)
+    rs = fw * c + pad_in
+    padded = np.zeros((n, fh, rs), np.uint8)
+    padded[:, :, :fw * c] = frames.reshape(n, fh, fw * c)
+    ors = fw * 4 + pad_out
+    with pkg.Session(model_h=H, model_w=W, dtype="f32", max_batch=4, autotune=False) as s:
+        df = torch.from_numpy(padded).cuda()
+        da = torch.from_numpy(alpha).cuda()
+        do = torch.full((n, fh, ors), 0xAB, dtype=torch.uint8, device="cuda")
+        pkg.composite_device(s, df.data_ptr(), n, fh, fw, c, rs, fh * rs, da.data_ptr(), do.data_ptr(), ors, fh * ors,
+                             torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = do.cpu().numpy()
+    assert np.array_equal(got[:, :, :fw * 4].reshape(want.shape), want)
+    assert np.all(got[:, :, fw * 4:] == 0xAB)  # row padding untouched
+
+
+def test_segment_composite_end_to_end(pkg, torch_cuda, synthetic, oracle):
+    """processFrame :78-178 in one call == oracle(post(GPU masks)) composited, across
+    two calls of one stream."""
+    with pkg.Session(dtype="bf16x2", max_batch=4, max_frame_h=480, max_frame_w=640) as s:
+        chain = pkg.PostChain(s)
+        st = oracle.PostState(s.mask_h, s.mask_w)
+        for call in range(2):
+            frames = _frames(synthetic, range(90 + 4 * call, 94 + 4 * call), 480, 640, 4)
+            masks = s.segment_frames(frames)[0].reshape(4, s.mask_h, s.mask_w)
+            got = chain.composite(frames)
+            _, want_u = oracle.post(masks, frames, st)
+            want = oracle.composite(frames, want_u)
+            assert np.array_equal(got, want), f"call {call}: {(got != want).sum()} bytes differ"
+        with pytest.raises(pkg.VssError):  # more output than the handle holds
+            chain.composite(np.zeros((4, 1080, 1920, 3), np.uint8))

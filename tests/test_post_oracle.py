@@ -78,3 +78,22 @@ def test_post_refine_edges(oracle, synthetic):
             if not bil:  # without the bilateral the border stays exactly 0
                 assert np.all(a[0, 0, :] == 0) and np.all(a[0, :, 0] == 0)
                 assert np.all(a[0, 1:-1, 1:-1] == want)
+
+
+def test_composite_oracle_identity_and_transparency(oracle):
+    """Compositing (frameProcessorTest.ts:170-178 as defined in vss_oracle.c): at
+    equal resolution the alpha passes through; alpha 0 reads back colour 0."""
+    rng = np.random.default_rng(5)
+    frames = rng.integers(0, 256, (2, 12, 20, 3), dtype=np.uint8)
+    alpha = rng.integers(0, 256, (2, 12, 20), dtype=np.uint8)
+    alpha[0, :3] = 0
+    out = oracle.composite(frames, alpha)
+    assert np.array_equal(out[..., 3], alpha)
+    vis = alpha > 0
+    assert np.array_equal(out[..., :3][vis], frames[vis])
+    assert not out[..., :3][~vis].any()
+    # upscaling a constant alpha keeps it constant; RGBA input drops its own alpha
+    rgba = np.concatenate([frames, np.full((2, 12, 20, 1), 7, np.uint8)], -1)
+    out2 = oracle.composite(np.ascontiguousarray(np.repeat(np.repeat(rgba, 3, 1), 2, 2)),
+                            np.full((2, 12, 20), 200, np.uint8))
+    assert np.all(out2[..., 3] == 200)

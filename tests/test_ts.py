@@ -101,3 +101,6 @@ def test_node_post_chain_matches_oracle_and_python_host(addon_built, pkg, oracle
     cfg.use_bilateral, cfg.gamma = 0, 1.0
     want_nb, _ = oracle.post(masks, frames, oracle.PostState(144, 256), cfg)
     assert np.array_equal(nobil, want_nb)
+    # compositing after reset + default config: the RGBA canvases of the same frames
+    rgba = np.fromfile(str(op) + "_rgba.u8", np.uint8).reshape(n, h, w, 4)
+    assert np.array_equal(rgba, oracle.composite(frames, want_u))

@@ -129,6 +129,8 @@ def lib() -> ctypes.CDLL:
                 "vss_post_set_config": ([P, ctypes.POINTER(PostConfig)], I),
                 "vss_postprocess_device": ([P, P, I, I, I, I, S, S, P, P, P, P], I),
                 "vss_segment_post": ([P, P, P, I, I, I, I, S, P, P], I),
+                "vss_composite_device": ([P, P, I, I, I, I, S, S, P, P, S, S, P], I),
+                "vss_segment_composite": ([P, P, P, I, I, I, I, S, P], I),
             }
             for name, (args, res) in sig.items():
                 fn = getattr(L, name)
@@ -324,11 +326,31 @@ class PostChain:
                                       u.ctypes.data), s._h)
         return a, u, s.mask_w, s.mask_h
 
+    def composite(self, frames: np.ndarray) -> np.ndarray:
+        """Consecutive frames [N,H,W,3|4] u8 -> the output canvas after compositing
+        (frameProcessorTest.ts:170-178): RGBA u8 [N,H,W,4]."""
+        s = self.session
+        f = _as_frames(frames)
+        n, hh, ww, c = f.shape
+        out = np.empty((n, hh, ww, 4), np.uint8)
+        _check(lib().vss_segment_composite(s._h, self._st, f.ctypes.data, n, hh, ww, c, ww * c, out.ctypes.data),
+               s._h)
+        return out
+
     def process_device(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int, frame_stride: int,
                        masks_ptr: int, alpha_ptr: int = 0, alpha_u8_ptr: int = 0, stream: int = 0):
         _check(lib().vss_postprocess_device(self._st, frames_ptr or None, n, h, w, c, row_stride, frame_stride,
                                             masks_ptr, alpha_ptr or None, alpha_u8_ptr or None, stream or None),
                self.session._h)
+
+
+def composite_device(session: Session, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int,
+                     frame_stride: int, alpha_u8_ptr: int, out_ptr: int, out_row_stride: int = 0,
+                     out_frame_stride: int = 0, stream: int = 0):
+    """HBM in/out compositing: frames + mask alpha bytes -> RGBA frames."""
+    ors = out_row_stride or w * 4
+    _check(lib().vss_composite_device(session._h, frames_ptr, n, h, w, c, row_stride, frame_stride, alpha_u8_ptr,
+                                      out_ptr, ors, out_frame_stride or ors * h, stream or None), session._h)
 
 
 def version() -> int:

@@ -94,6 +94,7 @@ struct vss_handle {
   std::vector<unsigned long long*> trace;  // per layer, [grid][4] stamps
   std::vector<int> trace_wgs;              // workgroups of the layer's last launch
 #endif
+  uint8_t* d_comp = nullptr;      // vss_segment_composite output, allocated on first use
   float* d_post_alpha = nullptr;  // vss_segment_post outputs [max_batch][P]
   uint8_t* d_post_u8 = nullptr;
   std::atomic<int> busy{0};
@@ -1137,3 +1138,76 @@ extern "C" int vss_trace_read(vss_handle* h, int layer, unsigned long long* out,
   return wgs;
 }
 #endif
+
+// ---- compositing (vss_post.hip k_composite) ---------------------------------
+namespace {
+
+int composite_enqueue(vss_handle* h, const uint8_t* d_frames, int n, int fh, int fw, int fc, size_t rs, size_t fs,
+                      const uint8_t* d_alpha, uint8_t* d_out, size_t ors, size_t ofs, hipStream_t s) {
+  CompositeParams p{};
+  p.frames = d_frames;
+  p.row_stride = (long)rs;
+  p.frame_stride = (long)fs;
+  p.fh = fh; p.fw = fw; p.fc = fc;
+  p.alpha = d_alpha;
+  p.H = h->cfg.model_h; p.W = h->cfg.model_w;
+  p.sy = (float)p.H / (float)fh;
+  p.sx = (float)p.W / (float)fw;
+  p.out = d_out;
+  p.out_row_stride = (long)ors;
+  p.out_frame_stride = (long)ofs;
+  launch_composite(p, n, s);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("composite launch: ") + hipGetErrorString(e));
+  return VSS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vss_composite_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width, int channels,
+                         size_t row_stride, size_t frame_stride, const uint8_t* d_alpha_u8, uint8_t* d_out_rgba,
+                         size_t out_row_stride, size_t out_frame_stride, void* stream) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (!d_frames || !d_alpha_u8 || !d_out_rgba) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride);
+  if (rc) return rc;
+  if (out_row_stride < (size_t)width * 4 || out_row_stride % 4 || out_frame_stride < out_row_stride * height ||
+      (reinterpret_cast<uintptr_t>(d_out_rgba) & 3))
+    return fail(h, VSS_E_INVALID_ARG, "bad RGBA output geometry (row stride >= 4*width, multiple of 4)");
+  HIP_TRY(h, hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  return composite_enqueue(h, d_frames, n, height, width, channels, row_stride, frame_stride, d_alpha_u8,
+                           d_out_rgba, out_row_stride, out_frame_stride, s);
+}
+
+int vss_segment_composite(vss_handle* h, vss_post_state* st, const uint8_t* frames, int n, int height, int width,
+                          int channels, size_t row_stride, uint8_t* out_rgba) {
+  if (!h || !st || st->h != h) return fail(h, VSS_E_INVALID_ARG, "handle / post state mismatch");
+  if (!out_rgba) return fail(h, VSS_E_INVALID_ARG, "null output");
+  Busy b(h);
+  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (!h->d_comp) {
+    const size_t cap = (size_t)h->cfg.max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w * 4;
+    int rc = dalloc(h, &h->d_comp, cap);
+    if (rc) return rc;
+  }
+  int rc = stage_in(h, frames, n, height, width, channels, row_stride, h->h_masks, VSS_OUT_MODEL);
+  if (rc) return rc;
+  const size_t fs = row_stride * (size_t)height, ors = (size_t)width * 4, ofs = ors * height;
+  if ((size_t)n * ofs > (size_t)h->cfg.max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w * 4)
+    return fail(h, VSS_E_INVALID_ARG, "RGBA output exceeds the handle's capacity (max_batch, max_frame_h/w)");
+  rc = post_enqueue(st, h->d_frames, n, height, width, channels, row_stride, fs, h->d_masks, nullptr, h->d_post_u8,
+                    h->stream);
+  if (rc) return rc;
+  rc = composite_enqueue(h, h->d_frames, n, height, width, channels, row_stride, fs, h->d_post_u8, h->d_comp, ors,
+                         ofs, h->stream);
+  if (rc) return rc;
+  HIP_TRY(h, hipMemcpyAsync(out_rgba, h->d_comp, (size_t)n * ofs, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return VSS_OK;
+}
+
+}  // extern "C"

@@ -261,6 +261,19 @@ struct PostFilterParams {
   uint8_t* alpha_u8;     // [n][H][W] (may be null)
 };
 
+// §8(f) row 3: destination-in compositing of the frame by the upscaled mask alpha
+struct CompositeParams {
+  const uint8_t* frames;  // [n] frames, row_stride / frame_stride bytes, fc = 3 or 4
+  long row_stride, frame_stride;
+  int fh, fw, fc;
+  const uint8_t* alpha;   // [n][H][W] u8 (the post chain's alpha bytes)
+  int H, W;
+  float sy, sx;           // (float)H / fh, (float)W / fw
+  uint8_t* out;           // [n] RGBA frames, out_row_stride / out_frame_stride bytes
+  long out_row_stride, out_frame_stride;
+};
+void launch_composite(const CompositeParams& p, int n, hipStream_t s);
+
 void launch_post_ema(const PostEmaParams& p, hipStream_t s);
 void launch_post_filter(const PostFilterParams& p, int n, hipStream_t s);
 

@@ -168,6 +168,61 @@ __global__ __launch_bounds__(256) void k_post_filter(PostFilterParams p) {
   }
 }
 
+// destination-in compositing (frameProcessorTest.ts:170-178, output canvas =
+// the video's size, main.ts:43-44): the frame's colour, alpha = the half-pixel
+// bilinear of the mask's u8 alpha at frame resolution, rounded half up; colour
+// 0 where alpha is 0 (a canvas stores premultiplied colour).  Thread = 4
+// consecutive pixels of a row: one 16-B RGBA store; the alpha taps come from
+// the L2-resident mask.  A tile of 256 x 4 pixels per workgroup.
+__device__ __forceinline__ void up_coord(int o, float scale, int in, int& i0, int& i1, float& l) {
+#pragma clang fp contract(off)
+  float s = ((float)o + 0.5f) * scale - 0.5f;
+  s = fmaxf(s, 0.f);
+  const int a = min((int)s, in - 1);
+  i0 = a;
+  i1 = a < in - 1 ? a + 1 : a;
+  l = s - (float)a;
+}
+
+__global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
+#pragma clang fp contract(off)
+  const int t = blockIdx.z;
+  const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int x0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
+  if (y >= p.fh || x0 >= p.fw) return;
+  int ya, yb;
+  float ly;
+  up_coord(y, p.sy, p.H, ya, yb, ly);
+  const uint8_t* a = p.alpha + (long)t * p.H * p.W;
+  const uint8_t* ra = a + (long)ya * p.W;
+  const uint8_t* rb = a + (long)yb * p.W;
+  const uint8_t* f = p.frames + (long)t * p.frame_stride + (long)y * p.row_stride;
+  uint32_t px[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int x = min(x0 + k, p.fw - 1);
+    int xa, xb;
+    float lx;
+    up_coord(x, p.sx, p.W, xa, xb, lx);
+    const float a00 = ra[xa], a01 = ra[xb], a10 = rb[xa], a11 = rb[xb];
+    const float top = __builtin_fmaf(a01 - a00, lx, a00), bot = __builtin_fmaf(a11 - a10, lx, a10);
+    const uint32_t A = (uint32_t)floorf(__builtin_fmaf(bot - top, ly, top) + 0.5f);
+    const uint8_t* q = f + (long)x * p.fc;
+    const uint32_t rgb = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
+    px[k] = A ? (rgb | (A << 24)) : 0u;
+  }
+  uint8_t* o = p.out + (long)t * p.out_frame_stride + (long)y * p.out_row_stride + (long)x0 * 4;
+  if (x0 + 4 <= p.fw && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+    *reinterpret_cast<uint4*>(o) = make_uint4(px[0], px[1], px[2], px[3]);
+  } else {
+    for (int k = 0; k < 4 && x0 + k < p.fw; ++k) reinterpret_cast<uint32_t*>(o)[k] = px[k];
+  }
+}
+
+void launch_composite(const CompositeParams& p, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_composite, dim3((p.fw + 255) / 256, (p.fh + 3) / 4, n), dim3(256), 0, s, p);
+}
+
 constexpr int kPostTH = 8, kPostTW = 32;
 
 void launch_post_ema(const PostEmaParams& p, hipStream_t s) {

@@ -18,6 +18,8 @@
 //   postSetConfig(post, config), postReset(post), postDestroy(post)
 //   segmentPost(handle, post, frames, n, height, width, channels, rowStride)
 //       -> Promise<{alpha: Float32Array, alphaU8: Uint8Array}>   (processFrame :78-169)
+//   segmentComposite(handle, post, frames, n, height, width, channels, rowStride)
+//       -> Promise<Uint8Array>   RGBA output canvases, n * height * width * 4 (:78-178)
 // segment runs vss_segment on a libuv worker thread (napi_create_async_work),
 // so the event loop is not blocked — as `await session.run` does not block.
 #include <node_api.h>
@@ -319,7 +321,8 @@ struct SegmentWork {
   napi_ref frames_ref = nullptr, out_ref = nullptr;
   napi_ref u8_ref = nullptr;             // segmentPost: the alpha bytes
   vss_handle* h = nullptr;
-  vss_post_state* post = nullptr;        // segmentPost only
+  vss_post_state* post = nullptr;        // segmentPost / segmentComposite
+  bool composite = false;                // segmentComposite: out_u8 holds the RGBA canvases
   const uint8_t* frames = nullptr;
   float* out = nullptr;
   uint8_t* out_u8 = nullptr;
@@ -331,7 +334,10 @@ struct SegmentWork {
 
 void SegmentExecute(napi_env, void* data) {  // libuv worker thread: no JS calls here
   SegmentWork* w = static_cast<SegmentWork*>(data);
-  if (w->post)
+  if (w->composite)
+    w->rc = vss_segment_composite(w->h, w->post, w->frames, w->n, w->height, w->width, w->channels, w->row_stride,
+                                  w->out_u8);
+  else if (w->post)
     w->rc = vss_segment_post(w->h, w->post, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out,
                              w->out_u8);
   else
@@ -344,7 +350,12 @@ void SegmentComplete(napi_env env, napi_status, void* data) {
   SegmentWork* w = static_cast<SegmentWork*>(data);
   napi_value ab = nullptr;
   napi_get_reference_value(env, w->out_ref, &ab);
-  if (w->rc == VSS_OK) {
+  if (w->rc == VSS_OK && w->composite) {
+    napi_value ab8 = nullptr, arr8;
+    napi_get_reference_value(env, w->u8_ref, &ab8);
+    napi_create_typedarray(env, napi_uint8_array, (size_t)w->n * w->height * w->width * 4, ab8, 0, &arr8);
+    napi_resolve_deferred(env, w->deferred, arr8);
+  } else if (w->rc == VSS_OK) {
     napi_value arr;
     napi_create_typedarray(env, napi_float32_array, w->out_count, ab, 0, &arr);
     if (w->post) {
@@ -360,7 +371,8 @@ void SegmentComplete(napi_env env, napi_status, void* data) {
     }
   } else {
     napi_value msg, code, e;
-    const std::string m = std::string(w->post ? "vss_segment_post" : "vss_segment") + " failed (" +
+    const std::string m = std::string(w->composite ? "vss_segment_composite"
+                                                   : (w->post ? "vss_segment_post" : "vss_segment")) + " failed (" +
                           std::to_string(w->rc) + "): " + w->err;
     napi_create_string_utf8(env, m.c_str(), m.size(), &msg);
     napi_create_string_utf8(env, std::to_string(w->rc).c_str(), NAPI_AUTO_LENGTH, &code);
@@ -375,7 +387,7 @@ void SegmentComplete(napi_env env, napi_status, void* data) {
 }
 
 // segment(handle, frames, ...) and segmentPost(handle, post, frames, ...)
-napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post) {
+napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post, bool composite = false) {
   size_t argc = 8;
   napi_value all[8];
   NAPI_OK(env, napi_get_cb_info(env, info, &argc, all, nullptr, nullptr));
@@ -434,10 +446,12 @@ napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post) {
   void* out = nullptr;
   NAPI_OK(env, napi_create_arraybuffer(env, w->out_count * 4, &out, &ab));
   w->out = static_cast<float*>(out);
+  w->composite = composite;
   if (ps) {
     napi_value ab8;
     void* out8 = nullptr;
-    NAPI_OK(env, napi_create_arraybuffer(env, w->out_count, &out8, &ab8));
+    const size_t bytes8 = composite ? (size_t)w->n * w->height * w->width * 4 : w->out_count;
+    NAPI_OK(env, napi_create_arraybuffer(env, bytes8, &out8, &ab8));
     w->out_u8 = static_cast<uint8_t*>(out8);
     napi_create_reference(env, ab8, 1, &w->u8_ref);
   }
@@ -453,6 +467,7 @@ napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post) {
 
 napi_value Segment(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, false); }
 napi_value SegmentPost(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, true); }
+napi_value SegmentComposite(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, true, true); }
 
 napi_value Init(napi_env env, napi_value exports) {
   const napi_property_descriptor props[] = {
@@ -466,6 +481,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"postReset", nullptr, PostReset, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"postDestroy", nullptr, PostDestroy, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"segmentPost", nullptr, SegmentPost, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"segmentComposite", nullptr, SegmentComposite, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;
