@@ -163,6 +163,9 @@ def main():
     ap.add_argument("--cpu-budget-s", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-post", action="store_true", help="skip the post-processing leg")
+    ap.add_argument("--persistent", action="store_true",
+                    help="run the forward as ONE persistent k_forward launch (VSS_FORWARD=1) instead of "
+                         "one launch per layer")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_traffic.json"),
                     help="per-kernel HBM traffic from tools/prof_summary.py (PMC passes)")
     args = ap.parse_args()
@@ -188,25 +191,45 @@ def main():
     hm, wm = (int(v) for v in args.model.split("x"))
     B = args.batch
     frames = syn.make_batch(B, fh, fw, 3, start=rank * B)
+    if args.persistent:
+        os.environ["VSS_FORWARD"] = "1"  # read by vss_create
     sess = pkg.Session(model_h=hm, model_w=wm, dtype=args.dtype, device_id=dev.index, max_batch=B,
                        max_frame_h=fh, max_frame_w=fw)
     if args.no_graph:
         sess.set_option(pkg.VSS_OPT_USE_GRAPH, 0)
     sess.set_option(pkg.VSS_OPT_BRANCHES, args.branches)
     d_frames = torch.from_numpy(frames).to(dev)
-    d_masks = torch.empty((B, hm * wm), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world * B, hm * wm), dtype=torch.float32, device=dev) if world > 1 else None
+    # two mask buffers: the all-gather of step i (RCCL's own stream) overlaps the
+    # forward of step i+1; step i+2 waits for gather i before it rewrites buffer i%2
+    d_masks2 = [torch.empty((B, hm * wm), dtype=torch.float32, device=dev) for _ in range(2)]
+    d_masks = d_masks2[0]
+    gathered2 = [torch.empty((world * B, hm * wm), dtype=torch.float32, device=dev) for _ in range(2)] \
+        if world > 1 else None
+    pending = [None, None]
     stream = torch.cuda.Stream(device=dev)
     rs, fs = fw * 3, fh * fw * 3
+    it = [0]
 
     def step():
-        sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_masks.data_ptr(), stream.cuda_stream)
-        if gathered is not None:
-            dist.all_gather_into_tensor(gathered, d_masks)
+        k = it[0] & 1
+        it[0] += 1
+        if pending[k] is not None:
+            pending[k].wait()  # the forward's stream waits for gather i-2 (reads this buffer)
+            pending[k] = None
+        sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_masks2[k].data_ptr(), stream.cuda_stream)
+        if gathered2 is not None:
+            pending[k] = dist.all_gather_into_tensor(gathered2[k], d_masks2[k], async_op=True)
+
+    def drain():
+        for k in range(2):
+            if pending[k] is not None:
+                pending[k].wait()
+                pending[k] = None
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
             step()
+        drain()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -214,10 +237,15 @@ def main():
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
+        drain()
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
+    if world > 1:  # the gathered batch holds every rank's masks in frame order
+        last = (it[0] - 1) & 1
+        assert torch.equal(gathered2[last][rank * B:(rank + 1) * B], d_masks2[last])
+    d_masks = d_masks2[(it[0] - 1) & 1]
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -225,28 +253,55 @@ def main():
     value = world * B * args.steps / el_max
 
     # ---- kernel timing pass (events recorded by the launches themselves) ----
-    sess.set_option(pkg.VSS_OPT_PROFILE, 1)
-    with torch.cuda.stream(stream):
-        for _ in range(args.steps):
-            sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_masks.data_ptr(), stream.cuda_stream)
-    torch.cuda.synchronize(dev)
+    persistent = sess.persistent
+
+    def profiled_pass():
+        sess.set_option(pkg.VSS_OPT_PROFILE, 1)
+        with torch.cuda.stream(stream):
+            for _ in range(args.steps):
+                sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_masks.data_ptr(),
+                                    stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        sess.set_option(pkg.VSS_OPT_PROFILE, 0)
+
+    fwd_ms = fwd_cnt = None
+    if persistent:
+        profiled_pass()
+        fwd_ms, fwd_cnt = sess.profile_read_forward()
+        faults = sess.forward_faults()
+        if faults:
+            raise RuntimeError(f"k_forward: {faults} dependency waits gave up")
+        sess.set_option(pkg.VSS_OPT_FORWARD, 0)  # per-layer breakdown from layer launches
+    profiled_pass()
     ms, cnt = sess.profile_read()
-    sess.set_option(pkg.VSS_OPT_PROFILE, 0)
+    if persistent:
+        sess.set_option(pkg.VSS_OPT_FORWARD, 1)
 
     blob = open(sess.weights_path, "rb").read()
     sys.path.insert(0, os.path.join(PKG_DIR, "model"))
     import make_weights as mw
     recs, _, _ = mw.parse_blob(blob)
     costs = cm.layer_costs(recs, hm, wm, fh, fw, 3, pw_weight_bytes=2 if args.dtype == "bf16x2" else 4)
-    dom = int(np.argmax(ms))
-    dom_bytes = cm.launch_bytes(costs[dom], B)
-    achieved = dom_bytes / (ms[dom] * 1e-3)
     names = [sess.layer_kernel(i) for i in range(len(ms))]
     per_layer = [{"layer": i, "kind": costs[i]["kind"], "kernel": names[i], "ms": round(m, 5),
                   "GBps": round(cm.launch_bytes(costs[i], B) / (m * 1e-3) / 1e9, 1)} for i, m in enumerate(ms)]
+    if persistent:
+        # the dominant (only) kernel is the whole forward: every layer's
+        # compulsory HBM bytes (each activation written once, read once)
+        dom_name = sess.forward_kernel()
+        dom_label = f"persistent forward: {dom_name}"
+        dom_bytes = sum(cm.launch_bytes(c, B) for c in costs)
+        dom_ms, dom_cnt = fwd_ms, fwd_cnt
+    else:
+        dom = int(np.argmax(ms))
+        dom_name = names[dom]
+        dom_label = f"layer {dom} ({costs[dom]['kind']}): {dom_name}"
+        dom_bytes = cm.launch_bytes(costs[dom], B)
+        dom_ms, dom_cnt = ms[dom], cnt
+    achieved = dom_bytes / (dom_ms * 1e-3)
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json):
-        t = json.load(open(args.traffic_json)).get(names[dom])
+        t = json.load(open(args.traffic_json)).get(dom_name)
         if t and t.get("traffic_bytes"):
             traffic = round(t["traffic_bytes"] / 1e6, 3)
 
@@ -282,20 +337,21 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"{B} synthetic {fw}x{fh} RGB u8 frames per GPU per step (resident in HBM) -> "
-                            f"{wm}x{hm} f32 masks" + (", RCCL all-gather of masks" if world > 1 else ""),
+                            f"{wm}x{hm} f32 masks" + (", RCCL all-gather of masks (overlapped with the next step's forward)" if world > 1 else ""),
                 "global_batch": world * B,
                 "frame": f"{fw}x{fh}x3",
                 "model_res": f"{wm}x{hm}",
                 "pw_gemm": "v_mfma_f32_16x16x32_bf16, f32 activations split hi+lo" if args.dtype == "bf16x2"
                            else "v_mfma_f32_16x16x4_f32",
                 "graph": not args.no_graph,
+                "persistent_forward": persistent,
                 "branches": args.branches,
                 "parallelism": f"dp{world}",
             },
             "mask_max_abs_err": err,
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"layer {dom} ({costs[dom]['kind']}): {names[dom]}",
+                "kernel": dom_label,
                 "achieved": round(achieved / 1e9, 1),
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",
@@ -303,10 +359,14 @@ def main():
                 "traffic": traffic,
                 "traffic_unit": "MB/launch (rocprofv3 PMC: 2*FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
                 "alg_bytes_per_launch": dom_bytes,
-                "mean_kernel_ms": round(ms[dom], 5),
-                "events_count": cnt,
+                "mean_kernel_ms": round(dom_ms, 5),
+                "events_count": dom_cnt,
             },
             "kernels": per_layer,
+            "kernels_note": ("per-layer breakdown from the same plan run as one launch per layer "
+                             "(VSS_OPT_FORWARD=0); the headline runs the persistent forward")
+                            if persistent else "one launch per layer",
+            "layer_launches_sum_ms": round(float(sum(ms)), 5),
             "cpu_baseline": cpu,
             "post": post,
         }

@@ -53,8 +53,19 @@ enum { VSS_OUT_MODEL = 0 };
 enum {
   VSS_OPT_USE_GRAPH = 1, /* 1: replay a captured hipGraph per (shape, buffers) (default 1) */
   VSS_OPT_PROFILE = 2,   /* 1: time every kernel with HIP events (eager launches)         */
-  VSS_OPT_BRANCHES = 3   /* 1..8: split a batch into that many sub-batches whose chains run
-                            concurrently on forked streams inside the graph (default 1) */
+  VSS_OPT_BRANCHES = 3,  /* 1..8: split a batch into that many sub-batches whose chains run
+                            concurrently on forked streams inside the graph (default 1;
+                            ignored while VSS_OPT_FORWARD is 1) */
+  VSS_OPT_FORWARD = 4,   /* 1: the whole forward as ONE persistent launch (k_forward: tasks =
+                            (layer, frame, tile) taken from ticket counters, per-frame
+                            dependency counters instead of kernel boundaries); 0: one launch
+                            per layer (default: measured faster).  Available when
+                            the handle was created with env VSS_FORWARD=1 (the planner then
+                            restricts tiles to the persistent forward's table and skips the
+                            autotuner).  Results are bitwise identical either way. */
+  VSS_OPT_FORWARD_FAULTS = 5 /* vss_get_option only: dependency waits of k_forward that gave up
+                                (bounded spins; 0 in a correct run).  Synchronises the device
+                                and clears the count. */
 };
 
 typedef struct vss_handle vss_handle;
@@ -135,6 +146,16 @@ int vss_preprocess_device(vss_handle* h, const uint8_t* d_frames, int n, int hei
 int vss_synchronize(vss_handle* h);
 
 int vss_set_option(vss_handle* h, int option, int value);
+int vss_get_option(vss_handle* h, int option, int* value);
+
+/* Name of the persistent forward's kernel as rocprofv3 reports it, e.g.
+ * "void vss::k_forward<1>(vss::FwdParams)"; VSS_E_UNSUPPORTED when the plan
+ * has none.  Returns the string length. */
+int vss_forward_kernel(const vss_handle* h, char* buf, int cap);
+
+/* Mean k_forward duration (ms) over the VSS_OPT_PROFILE forwards that ran it
+ * (HIP events recorded by the launch itself); resets the accumulator. */
+int vss_profile_read_forward(vss_handle* h, double* ms, int* count);
 
 /* Per-layer output shape (C, H, W) at the handle's model resolution. */
 int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww);

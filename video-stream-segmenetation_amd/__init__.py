@@ -33,7 +33,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "vss.h")
 VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_IO, VSS_E_UNSUPPORTED = (
     0, -1, -2, -3, -4, -5, -6, -7)
 DTYPES = {"f32": 0, "bf16x2": 1}
-VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_BRANCHES = 1, 2, 3
+VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_BRANCHES, VSS_OPT_FORWARD, VSS_OPT_FORWARD_FAULTS = 1, 2, 3, 4, 5
 VSS_CREATE_NO_AUTOTUNE = 1
 VSS_OUT_MODEL = 0
 
@@ -118,6 +118,9 @@ def lib() -> ctypes.CDLL:
                 "vss_preprocess_device": ([P, P, I, I, I, I, S, S, P, P], I),
                 "vss_synchronize": ([P], I),
                 "vss_set_option": ([P, I, I], I),
+                "vss_get_option": ([P, I, ctypes.POINTER(I)], I),
+                "vss_forward_kernel": ([P, ctypes.c_char_p, I], I),
+                "vss_profile_read_forward": ([P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I)], I),
                 "vss_layer_shape": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)], I),
                 "vss_read_layer": ([P, I, I, P], I),
                 "vss_profile_read": ([P, ctypes.POINTER(ctypes.c_double), I, ctypes.POINTER(I)], I),
@@ -248,6 +251,32 @@ class Session:
 
     def set_option(self, option: int, value: int):
         _check(lib().vss_set_option(self._h, option, value), self._h)
+
+    def get_option(self, option: int) -> int:
+        v = ctypes.c_int()
+        _check(lib().vss_get_option(self._h, option, ctypes.byref(v)), self._h)
+        return v.value
+
+    @property
+    def persistent(self) -> bool:
+        """True when forwards run as ONE persistent k_forward launch."""
+        return bool(self.get_option(VSS_OPT_FORWARD))
+
+    def forward_faults(self) -> int:
+        """k_forward dependency waits that gave up since the last call (0 = healthy)."""
+        return self.get_option(VSS_OPT_FORWARD_FAULTS)
+
+    def forward_kernel(self) -> str | None:
+        """The persistent forward's kernel name as rocprofv3 reports it (None if unsupported)."""
+        buf = ctypes.create_string_buffer(128)
+        rc = lib().vss_forward_kernel(self._h, buf, 128)
+        return buf.value.decode() if rc > 0 else None
+
+    def profile_read_forward(self):
+        """(mean k_forward ms over profiled forwards, count)."""
+        ms, cnt = ctypes.c_double(), ctypes.c_int()
+        _check(lib().vss_profile_read_forward(self._h, ctypes.byref(ms), ctypes.byref(cnt)), self._h)
+        return ms.value, cnt.value
 
     # -- introspection -----------------------------------------------------
     def layer_shape(self, layer: int):

@@ -70,6 +70,11 @@ thread_local std::string g_tls_error;
 }  // namespace
 
 constexpr long kDefaultKsplitPixels = 256;
+// expand layers whose unsplit LDS weight image exceeds this also split their
+// hidden channels (keeps every layer within the persistent forward's LDS
+// budget of two workgroups per CU; mirrors KSPLIT_WEIGHT_BYTES in
+// tools/gen_registry.py)
+constexpr size_t kKsplitWeightBytes = 40 * 1024;
 
 struct vss_handle {
   vss_config cfg{};
@@ -115,7 +120,24 @@ struct vss_handle {
   int prof_next = 0;
   std::vector<double> prof_sum;
   int prof_count = 0;
+  double fwd_prof_sum = 0.0;
+  int fwd_prof_count = 0;
   int last_n = 0;
+  // persistent forward (k_forward): the whole network in one launch
+  int want_forward = 0;          // env VSS_FORWARD=1 at create: plan for the persistent forward
+  bool fwd_ok = false;           // every layer of the plan has a k_forward case
+  int use_forward = 0;           // VSS_OPT_FORWARD
+  FwdLayer* d_fwd_layers = nullptr;
+  unsigned* d_fwd_ctl = nullptr;   // kFwdCtlWords (FwdParams::ctl)
+  unsigned* d_fwd_done = nullptr;  // [n_layers][max_batch]
+  int fwd_lds_floats = 0;
+  int fwd_grid = 0;
+  int fwd_order = 0;             // 0 layer-major, 1 diagonal (env VSS_FWD_ORDER=diag)
+  std::map<int, std::pair<FwdTask*, int>> fwd_tasks;  // per batch size n
+  unsigned* fwd_dbg = nullptr;   // env VSS_FWD_DEBUG: host-mapped per-workgroup state
+  unsigned long long* fwd_trace = nullptr;  // env VSS_FWD_TRACE: per-task stamps of the last launch
+  size_t fwd_trace_cap = 0;                 // tasks
+  int fwd_trace_n = 0;                      // tasks of the last traced launch
 };
 
 namespace {
@@ -181,7 +203,7 @@ void set_tile(LayerPlan& l, const BlockEntry* e) {
 // Tile choice among the compiled shapes for this layer (csrc/vss_registry.inc):
 // the largest tile that still gives >= 2 workgroups per CU (256 CUs) at
 // max_batch, preferring <= 64 KiB of LDS; otherwise the most workgroups.
-int choose_tile(vss_handle* h, LayerPlan& l, int N) {
+int choose_tile(vss_handle* h, LayerPlan& l, int N, bool mk_only) {
   int count = 0;
   const BlockEntry* reg = block_registry(&count);
   const int cskip = l.mode == MODE_DEC ? (int)l.rec.chid : 0;
@@ -190,7 +212,7 @@ int choose_tile(vss_handle* h, LayerPlan& l, int N) {
   for (int i = 0; i < count; ++i) {
     const BlockEntry& e = reg[i];
     if (e.mode != l.mode || e.stride != l.stride || e.cin != (int)l.rec.cin || e.cskip != cskip ||
-        e.chid != l.chid / l.ks || e.cout != l.C || e.flags != l.flags)
+        e.chid != l.chid / l.ks || e.cout != l.C || e.flags != l.flags || (mk_only && e.mk < 0))
       continue;
     const long blocks = (long)((l.H + e.TH - 1) / e.TH) * ((l.W + e.TW - 1) / e.TW) * N;
     const size_t lds = block_lds_bytes(l, e.TH, e.TW);
@@ -242,7 +264,13 @@ int load_weights(vss_handle* h) {
   return VSS_OK;
 }
 
-int plan(vss_handle* h) {
+// Bytes of an unsplit expand layer's LDS weight image (block_lds regions w1..b2).
+size_t weight_image_bytes(const LayerPlan& l) {
+  const BlockLds B = block_lds(l.mode, l.stride, 1, 16, (int)l.rec.cin, 0, l.chid, l.C);
+  return (size_t)(B.lr - B.w1) * 4;
+}
+
+int plan_once(vss_handle* h, bool mk_only) {
   const int Hm = h->cfg.model_h, Wm = h->cfg.model_w, N = h->cfg.max_batch;
   const int nl = (int)h->recs.size();
   h->L.assign(nl, LayerPlan{});
@@ -297,18 +325,32 @@ int plan(vss_handle* h) {
     // hidden split: expand layers whose output has at most ksplit_pixels
     // pixels per frame (a function of the model resolution only, so results
     // never depend on the batch or the autotuner)
-    if (l.mode == MODE_IR_EXPAND && (long)l.H * l.W <= h->ksplit_pixels) l.ks = ks_max(l);
+    if (l.mode == MODE_IR_EXPAND &&
+        ((long)l.H * l.W <= h->ksplit_pixels || weight_image_bytes(l) > kKsplitWeightBytes))
+      l.ks = ks_max(l);
     if (r.kind == K_IR || r.kind == K_DEC) l.xp = h->L[r.src].ks;
     if (r.kind == K_DEC) l.sp = h->L[r.skip].ks;
     if (r.kind == K_IR) l.flags = block_flags(0, (r.flags & F_RESIDUAL) != 0, l.xp, 1, l.ks);
     if (r.kind == K_DEC) l.flags = block_flags(h->L[r.src].rec.kind == K_DEC, 0, l.xp, l.sp, 1);
     if (l.mode >= 0) {
-      int rc = choose_tile(h, l, N);
+      int rc = choose_tile(h, l, N, mk_only);
       if (rc) return rc;
     }
   }
   if (nl == 0 || h->recs.back().kind != K_HEAD) return fail(h, VSS_E_UNSUPPORTED, "last layer must be the head");
   return VSS_OK;
+}
+
+// Plan for the persistent forward when every layer has a k_forward case
+// (csrc/vss_mk.inc), else for per-layer launches.
+int plan(vss_handle* h) {
+  h->fwd_ok = h->want_forward != 0;
+  int rc = plan_once(h, h->fwd_ok);
+  if (rc == VSS_E_UNSUPPORTED && h->fwd_ok) {
+    h->fwd_ok = false;
+    rc = plan_once(h, false);
+  }
+  return rc;
 }
 
 int upload(vss_handle* h) {
@@ -458,6 +500,136 @@ BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n, int f0 
   return p;
 }
 
+int n_tasks_per_frame(const LayerPlan& l, int Hm, int Wm) {
+  if (l.rec.kind == K_STEM) return ((l.W + kStemTW - 1) / kStemTW) * ((l.H + kStemTH - 1) / kStemTH);
+  if (l.rec.kind == K_HEAD) return ((Wm + kHeadTW - 1) / kHeadTW) * ((Hm + kHeadTH - 1) / kHeadTH);
+  return l.tiles_x * l.tiles_y * l.ks;
+}
+
+// The persistent forward's layer table (device), counters and launch shape.
+int setup_forward(vss_handle* h) {
+  if (!h->fwd_ok) return VSS_OK;
+  const int Hm = h->cfg.model_h, Wm = h->cfg.model_w, N = h->cfg.max_batch;
+  const int nl = (int)h->L.size();
+  std::vector<FwdLayer> fl(nl);
+  size_t lds = 0;
+  for (int i = 0; i < nl; ++i) {
+    const LayerPlan& l = h->L[i];
+    const Rec& r = l.rec;
+    FwdLayer& f = fl[i];
+    std::memset(&f, 0, sizeof(f));
+    f.dep[0] = f.dep[1] = -1;
+    f.ks = 1;
+    if (r.kind == K_STEM) {
+      f.kind = FWD_STEM;
+      f.tiles_x = (l.W + kStemTW - 1) / kStemTW;
+      f.tiles_y = (l.H + kStemTH - 1) / kStemTH;
+      StemParams& p = f.stem;
+      p.Hm = Hm; p.Wm = Wm;
+      p.w = l.stem_w; p.b = l.stem_b; p.y = l.act;
+      p.Ho = l.H; p.Wo = l.W; p.cout = l.C;
+      p.acc_zero = h->d_acc;
+      p.acc_stride = h->acc_stride;
+      lds = std::max(lds, (size_t)kStemLds * 4);
+    } else if (r.kind == K_IR || r.kind == K_DEC) {
+      f.kind = FWD_BLOCK;
+      f.mk = l.entry->mk;
+      f.tiles_x = l.tiles_x;
+      f.tiles_y = l.tiles_y;
+      f.ks = l.ks;
+      f.block = block_params(h, l, N);
+      f.dep[0] = (int)r.src;
+      if (r.kind == K_DEC) f.dep[1] = (int)r.skip;
+      lds = std::max(lds, l.lds);
+    } else {
+      const LayerPlan& src = h->L[r.src];
+      f.kind = FWD_HEAD;
+      f.tiles_x = (Wm + kHeadTW - 1) / kHeadTW;
+      f.tiles_y = (Hm + kHeadTH - 1) / kHeadTH;
+      HeadParams& p = f.head;
+      p.x = src.act;
+      p.in_acc = h->d_acc + src.acc_off;
+      p.acc_stride = h->acc_stride;
+      p.gamma = src.gamma; p.beta = src.beta; p.eps = h->eps;
+      p.w = l.head_w; p.b = l.head_b;
+      p.N = N; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
+      f.dep[0] = (int)r.src;
+      lds = std::max(lds, (size_t)kHeadLds * 4);
+    }
+    for (int k = 0; k < 2; ++k)
+      if (f.dep[k] >= 0) f.need[k] = n_tasks_per_frame(h->L[f.dep[k]], Hm, Wm);
+  }
+  h->fwd_lds_floats = (int)((lds + 15) / 16 * 4) + 16;  // + the control words
+  int rc = dalloc(h, &h->d_fwd_layers, sizeof(FwdLayer) * nl);
+  if (!rc) rc = dalloc(h, &h->d_fwd_ctl, kFwdCtlWords * sizeof(unsigned));
+  if (!rc) rc = dalloc(h, &h->d_fwd_done, sizeof(unsigned) * nl * N * kFwdLine);
+  if (rc) return rc;
+  HIP_TRY(h, hipMemcpy(h->d_fwd_layers, fl.data(), sizeof(FwdLayer) * nl, hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemset(h->d_fwd_ctl, 0, kFwdCtlWords * sizeof(unsigned)));
+  HIP_TRY(h, hipMemset(h->d_fwd_done, 0, sizeof(unsigned) * nl * N * kFwdLine));
+  const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
+  const FwdFn fn = forward_kernel(prec);
+  const int bytes = h->fwd_lds_floats * 4;
+  HIP_TRY(h, hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  int per_cu = 0;
+  HIP_TRY(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kThreads, bytes));
+  hipDeviceProp_t prop{};
+  HIP_TRY(h, hipGetDeviceProperties(&prop, h->device));
+  if (per_cu < 1) {  // cannot be resident: fall back to layer launches
+    h->fwd_ok = false;
+    return VSS_OK;
+  }
+  h->fwd_grid = per_cu * prop.multiProcessorCount / kFwdQueues * kFwdQueues;
+  if (h->fwd_grid < kFwdQueues) {
+    h->fwd_ok = false;
+    return VSS_OK;
+  }
+  if (const char* ev = std::getenv("VSS_FWD_ORDER")) h->fwd_order = std::strcmp(ev, "diag") == 0 ? 1 : 0;
+  h->use_forward = 1;
+  if (std::getenv("VSS_FWD_DEBUG")) {
+    HIP_TRY(h, hipHostMalloc((void**)&h->fwd_dbg, (size_t)h->fwd_grid * 4 * sizeof(unsigned), hipHostMallocCoherent));
+    std::memset(h->fwd_dbg, 0xFF, (size_t)h->fwd_grid * 4 * sizeof(unsigned));
+  }
+  return VSS_OK;
+}
+
+// Task list of a forward over n frames, in an order where every task's
+// dependencies come earlier (the ticket order is the only scheduling).
+//   layer-major: layer by layer, frame by frame within a layer, tiles in
+//                (slice, row, column) order;
+//   diagonal   : by layer + frame, so frame f runs layer L beside frame f+1's
+//                layer L-1.
+int forward_tasks(vss_handle* h, int n, FwdTask** out, int* count) {
+  auto it = h->fwd_tasks.find(n);
+  if (it == h->fwd_tasks.end()) {
+    const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
+    const int nl = (int)h->L.size();
+    std::vector<FwdTask> t;
+    auto emit = [&](int li, int f) {
+      const int k = n_tasks_per_frame(h->L[li], Hm, Wm);
+      for (int j = 0; j < k; ++j) t.push_back(FwdTask{li, f, j, 0});
+    };
+    const char* only = std::getenv("VSS_FWD_ONLY");  // debug: one layer's tasks, no waits
+    if (only) {
+      for (int f = 0; f < n; ++f) emit(std::atoi(only), f);
+    } else if (h->fwd_order == 1) {
+      for (int d = 0; d < nl + n - 1; ++d)
+        for (int f = std::max(0, d - nl + 1); f <= std::min(n - 1, d); ++f) emit(d - f, f);
+    } else {
+      for (int li = 0; li < nl; ++li)
+        for (int f = 0; f < n; ++f) emit(li, f);
+    }
+    FwdTask* d = nullptr;
+    int rc = dalloc(h, &d, t.size() * sizeof(FwdTask));
+    if (rc) return rc;
+    HIP_TRY(h, hipMemcpy(d, t.data(), t.size() * sizeof(FwdTask), hipMemcpyHostToDevice));
+    it = h->fwd_tasks.emplace(n, std::make_pair(d, (int)t.size())).first;
+  }
+  *out = it->second.first;
+  *count = it->second.second;
+  return VSS_OK;
+}
+
 // Enqueue the whole forward for frames [f0, f0 + n) on stream s (frames and
 // masks point at frame f0; no sync, no alloc: graph-capturable).
 int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs,
@@ -465,6 +637,44 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
   const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
   const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
   const int nl = (int)h->L.size();
+  if (h->use_forward && f0 == 0) {
+    FwdParams fp{};
+    int rc = forward_tasks(h, n, const_cast<FwdTask**>(&fp.tasks), &fp.ntasks);
+    if (rc) return rc;
+    fp.layers = h->d_fwd_layers;
+    fp.max_batch = h->cfg.max_batch;
+    fp.n_layers = nl;
+    fp.ctl = h->d_fwd_ctl;
+    fp.done = h->d_fwd_done;
+    fp.spin_limit = 20000000;  // 200 ms of s_memrealtime (100 MHz)
+    fp.lds_floats = h->fwd_lds_floats;
+    fp.frames = frames; fp.row_stride = (long)rs; fp.frame_stride = (long)fs;
+    fp.fh = fh; fp.fw = fw; fp.fc = fc;
+    fp.ry = (float)((double)fh / (double)Hm);
+    fp.rx = (float)((double)fw / (double)Wm);
+    fp.mask = masks;
+    fp.dbg = h->fwd_dbg;
+    fp.nowait = std::getenv("VSS_FWD_ONLY") ? 1 : 0;
+    if (std::getenv("VSS_FWD_TRACE")) {
+      if ((size_t)fp.ntasks > h->fwd_trace_cap) {
+        if ((rc = dalloc(h, &h->fwd_trace, (size_t)fp.ntasks * 4 * 8))) return rc;
+        h->fwd_trace_cap = (size_t)fp.ntasks;
+      }
+      fp.ttrace = h->fwd_trace;
+      h->fwd_trace_n = fp.ntasks;
+    }
+    // every queue needs a workgroup: round the grid to a multiple of kFwdQueues
+    const dim3 grid(std::min(h->fwd_grid, (fp.ntasks + kFwdQueues - 1) / kFwdQueues * kFwdQueues));
+    const size_t lds = (size_t)h->fwd_lds_floats * 4;
+    if (prof_slot >= 0)
+      hipExtLaunchKernelGGL(forward_kernel(prec), grid, dim3(kThreads), (uint32_t)lds, s,
+                            h->ev[(size_t)prof_slot * nl * 2], h->ev[(size_t)prof_slot * nl * 2 + 1], 0, fp);
+    else
+      hipLaunchKernelGGL(forward_kernel(prec), grid, dim3(kThreads), lds, s, fp);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("k_forward launch: ") + hipGetErrorString(e));
+    return VSS_OK;
+  }
   for (int i = 0; i < nl; ++i) {
     LayerPlan& l = h->L[i];
     const Rec& r = l.rec;
@@ -493,7 +703,7 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       p.trace = h->trace[i];
       h->trace_wgs[i] = ((l.W + 31) / 32) * ((l.H + 7) / 8) * n;
 #endif
-      go(stem_kernel16(), dim3((l.W + 31) / 32, (l.H + 7) / 8, n), 0, p);
+      go(stem_kernel16(), dim3((l.W + kStemTW - 1) / kStemTW, (l.H + kStemTH - 1) / kStemTH, n), kStemLds * 4, p);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
 #ifdef VSS_TRACE
       BlockParams p = block_params(h, l, n, f0);
@@ -516,7 +726,7 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       p.trace = h->trace[i];
       h->trace_wgs[i] = ((Wm + 63) / 64) * ((Hm + 15) / 16) * n;
 #endif
-      go(head_kernel16(), dim3((Wm + 63) / 64, (Hm + 15) / 16, n), 0, p);
+      go(head_kernel16(), dim3((Wm + kHeadTW - 1) / kHeadTW, (Hm + kHeadTH - 1) / kHeadTH, n), kHeadLds * 4, p);
     }
   }
   hipError_t e = hipGetLastError();
@@ -526,6 +736,15 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
 
 int harvest_slot(vss_handle* h, int slot) {
   const int nl = (int)h->L.size();
+  if (h->slot_pending[slot] == 2) {  // one k_forward launch
+    float ms = 0.f;
+    HIP_TRY(h, hipEventSynchronize(h->ev[(size_t)slot * nl * 2 + 1]));
+    HIP_TRY(h, hipEventElapsedTime(&ms, h->ev[(size_t)slot * nl * 2], h->ev[(size_t)slot * nl * 2 + 1]));
+    h->fwd_prof_sum += ms;
+    h->fwd_prof_count++;
+    h->slot_pending[slot] = 0;
+    return VSS_OK;
+  }
   for (int i = 0; i < nl; ++i) {
     float ms = 0.f;
     HIP_TRY(h, hipEventSynchronize(h->ev[((size_t)slot * nl + i) * 2 + 1]));
@@ -548,19 +767,25 @@ int forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc,
       if (rc) return rc;
     }
     int rc = enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, s, slot);
-    if (!rc) h->slot_pending[slot] = 1;
+    if (!rc) h->slot_pending[slot] = h->use_forward ? 2 : 1;
     return rc;
   }
   if (!h->use_graph) return enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, s, -1);
   GraphKey key{frames, masks, n, fh, fw, fc, rs, fs};
   auto it = h->graphs.find(key);
   if (it == h->graphs.end()) {
+    if (h->use_forward) {  // the task table is uploaded outside the capture
+      FwdTask* t = nullptr;
+      int cnt = 0;
+      int rc = forward_tasks(h, n, &t, &cnt);
+      if (rc) return rc;
+    }
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     HIP_TRY(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
     // Independent sub-batches on forked streams: their kernels overlap, which
     // fills the GPU while each chain waits on memory latency.
-    const int nb = std::max(1, std::min(h->branches, n));
+    const int nb = h->use_forward ? 1 : std::max(1, std::min(h->branches, n));
     int rc = VSS_OK;
     if (nb == 1) {
       rc = enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, h->stream, -1);
@@ -645,6 +870,7 @@ void async_done(void* p) {
 // this device and keep the fastest.  The kernels' arithmetic does not depend
 // on the tile (see block_lds), so this changes speed only, never results.
 int autotune(vss_handle* h) {
+  if (h->fwd_ok) return VSS_OK;  // the persistent forward's tiles are fixed (vss_mk.inc)
   const int N = h->cfg.max_batch;
   const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -721,6 +947,7 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
   };
   if (hipSetDevice(h->device) != hipSuccess) return bail(fail(h, VSS_E_HIP, "hipSetDevice failed"));
   if (const char* ev = std::getenv("VSS_KSPLIT_PIXELS")) h->ksplit_pixels = std::atol(ev);
+  if (const char* ev = std::getenv("VSS_FORWARD")) h->want_forward = std::atoi(ev) != 0;
   int rc = load_weights(h);
   if (!rc) rc = plan(h);
   if (!rc) rc = upload(h);
@@ -753,6 +980,7 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
     if (hipEventCreate(&e) != hipSuccess) return bail(fail(h, VSS_E_HIP, "hipEventCreate failed"));
   h->slot_pending.assign(vss_handle::kSlots, 0);
   h->prof_sum.assign(nl, 0.0);
+  if ((rc = setup_forward(h))) return bail(rc);
   if (!(cfg->flags & VSS_CREATE_NO_AUTOTUNE) && (rc = autotune(h))) return bail(rc);
   *out = h;
   return VSS_OK;
@@ -773,6 +1001,7 @@ void vss_destroy(vss_handle* h) {
   for (void* p : h->dev_allocs) (void)hipFree(p);
   if (h->h_frames) (void)hipHostFree(h->h_frames);
   if (h->h_masks) (void)hipHostFree(h->h_masks);
+  if (h->fwd_dbg) (void)hipHostFree(h->fwd_dbg);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -861,6 +1090,16 @@ int vss_synchronize(vss_handle* h) {
 
 int vss_set_option(vss_handle* h, int option, int value) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (option == VSS_OPT_FORWARD) {
+    if (value && !h->fwd_ok)
+      return fail(h, VSS_E_UNSUPPORTED, "this plan has no persistent forward (a layer shape outside vss_mk.inc)");
+    if ((value ? 1 : 0) != h->use_forward) {
+      for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+      h->graphs.clear();
+    }
+    h->use_forward = value ? 1 : 0;
+    return VSS_OK;
+  }
   if (option == VSS_OPT_USE_GRAPH) h->use_graph = value ? 1 : 0;
   else if (option == VSS_OPT_PROFILE) h->profile = value ? 1 : 0;
   else if (option == VSS_OPT_BRANCHES) {
@@ -873,6 +1112,75 @@ int vss_set_option(vss_handle* h, int option, int value) {
   }
   else return fail(h, VSS_E_INVALID_ARG, "unknown option");
   return VSS_OK;
+}
+
+int vss_get_option(vss_handle* h, int option, int* value) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (!value) return fail(h, VSS_E_INVALID_ARG, "null value");
+  switch (option) {
+    case VSS_OPT_USE_GRAPH: *value = h->use_graph; return VSS_OK;
+    case VSS_OPT_PROFILE: *value = h->profile; return VSS_OK;
+    case VSS_OPT_BRANCHES: *value = h->branches; return VSS_OK;
+    case VSS_OPT_FORWARD: *value = h->use_forward; return VSS_OK;
+    case VSS_OPT_FORWARD_FAULTS: {
+      *value = 0;
+      if (!h->d_fwd_ctl) return VSS_OK;
+      HIP_TRY(h, hipSetDevice(h->device));
+      HIP_TRY(h, hipDeviceSynchronize());
+      unsigned w = 0;
+      unsigned* fw = h->d_fwd_ctl + kFwdQueues * kFwdLine + 1;
+      HIP_TRY(h, hipMemcpy(&w, fw, sizeof(w), hipMemcpyDeviceToHost));
+      HIP_TRY(h, hipMemset(fw, 0, sizeof(unsigned)));
+      *value = (int)w;
+      return VSS_OK;
+    }
+    default: return fail(h, VSS_E_INVALID_ARG, "unknown option");
+  }
+}
+
+int vss_forward_kernel(const vss_handle* h, char* buf, int cap) {
+  if (!h || !buf || cap < 1) return VSS_E_INVALID_ARG;
+  if (!h->fwd_ok) return VSS_E_UNSUPPORTED;
+  char tmp[96];
+  std::snprintf(tmp, sizeof(tmp), "void vss::k_forward<%d>(vss::FwdParams)",
+                h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2);
+  std::snprintf(buf, (size_t)cap, "%s", tmp);
+  return (int)std::strlen(tmp);
+}
+
+int vss_profile_read_forward(vss_handle* h, double* ms, int* count) {
+  if (!h || !ms) return fail(h, VSS_E_INVALID_ARG, "null handle/ms");
+  HIP_TRY(h, hipSetDevice(h->device));
+  for (int s = 0; s < vss_handle::kSlots; ++s)
+    if (h->slot_pending[s]) {
+      int rc = harvest_slot(h, s);
+      if (rc) return rc;
+    }
+  *ms = h->fwd_prof_count ? h->fwd_prof_sum / h->fwd_prof_count : 0.0;
+  if (count) *count = h->fwd_prof_count;
+  h->fwd_prof_sum = 0.0;
+  h->fwd_prof_count = 0;
+  return VSS_OK;
+}
+
+// Debug (not in vss.h): per-task stamps of the last VSS_FWD_TRACE launch, [n][4]
+// {taken, deps met, body done, workgroup}; returns the task count.
+int vss_fwd_trace_read(vss_handle* h, unsigned long long* out, int cap) {
+  if (!h || !out || !h->fwd_trace) return VSS_E_INVALID_ARG;
+  HIP_TRY(h, hipDeviceSynchronize());
+  const int n = std::min(cap, h->fwd_trace_n);
+  HIP_TRY(h, hipMemcpy(out, h->fwd_trace, (size_t)n * 4 * 8, hipMemcpyDeviceToHost));
+  return n;
+}
+
+// Debug (not in vss.h): the k_forward per-workgroup state words (VSS_FWD_DEBUG),
+// read WITHOUT synchronising, so a stuck launch can be inspected.
+int vss_fwd_debug(const vss_handle* h, unsigned* out, int cap, int* grid) {
+  if (!h || !out || !h->fwd_dbg) return VSS_E_INVALID_ARG;
+  const int n = std::min(cap, h->fwd_grid * 4);
+  for (int i = 0; i < n; ++i) out[i] = __atomic_load_n(h->fwd_dbg + i, __ATOMIC_RELAXED);
+  if (grid) *grid = h->fwd_grid;
+  return n;
 }
 
 int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww) {

@@ -32,8 +32,48 @@
 namespace vss {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+
+// Activation tensors (and the instance-norm accumulators).  Layer launches use
+// plain loads and stores.  The persistent forward (COH = true) hands them from
+// workgroup to workgroup inside one launch, so there EVERY store and load of
+// them is `sc1` — write-through stores, L1-bypassing loads — through a buffer
+// descriptor built from a wave-uniform base (cdna_hip_programming.md
+// Guideline 16, R1 with the sc1-load consumer form): no release or acquire
+// fence per hand-off.  Indices are in floats; offsets stay below 2 GiB.
+// The same pointer, provably wave-uniform (in SGPRs): the caller guarantees
+// it is uniform; hipcc would otherwise waterfall every buffer op whose
+// descriptor it cannot prove uniform (cdna_hip_programming.md T20).
+__device__ __forceinline__ const void* uniform_ptr(const void* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return reinterpret_cast<const void*>(((unsigned long long)hi << 32) | lo);
+}
+
+template <bool COH>
+struct Gm {
+  const float* b;
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit Gm(const float* base) : b(base) {
+    if constexpr (COH)
+      r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(base)), 0, 0x7FFFFFF0, 0x00020000);
+  }
+  __device__ __forceinline__ f4 ld(long i) const {
+    if constexpr (COH)
+      return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 4), 0, 16));
+    else
+      return *reinterpret_cast<const f4*>(b + i);
+  }
+  __device__ __forceinline__ void st(long i, f4 v) const {
+    if constexpr (COH)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)(i * 4), 0, 16);
+    else
+      *reinterpret_cast<f4*>(const_cast<float*>(b) + i) = v;
+  }
+};
 
 __device__ __forceinline__ float relu6f(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
 __device__ __forceinline__ f4 relu6v(f4 v) {
@@ -124,14 +164,15 @@ __global__ __launch_bounds__(256) void k_prep(PrepParams p) {
 
 // ---------------------------------------------------------------------------
 // Stem: output tile 8 x 32 pixels x 16 channels, one pixel per thread.
-template <int COUT>
-__global__ __launch_bounds__(256) void k_stem(StemParams p) {
-  constexpr int TH = 8, TW = 32, IH = 2 * TH + 1, IW = 2 * TW + 1, IWP = IW + 1;
-  __shared__ float xs[3][IH][IWP];
-  __shared__ __attribute__((aligned(16))) float ws[27 * COUT];  // [tap][c]: 4 channels per LDS read
-  __shared__ float bs[COUT];
+template <int COUT, bool COH>
+__device__ __forceinline__ void stem_body(const StemParams& p, int bx, int by, int n, float* smem) {
+  constexpr int TH = kStemTH, TW = kStemTW, IH = kStemIH, IW = 2 * TW + 1, IWP = kStemIWP;
+  static_assert(COUT == 16, "stem LDS carve (kStemLds) assumes 16 output channels");
+  float (*xs)[IH][IWP] = reinterpret_cast<float (*)[IH][IWP]>(smem);  // [3][IH][IWP]
+  float* ws = smem + r4(3 * IH * IWP);                                 // [tap][c]: 4 channels per LDS read
+  float* bs = ws + 27 * COUT;
   const int tid = threadIdx.x;
-  const int n = blockIdx.z, oy0 = blockIdx.y * TH, ox0 = blockIdx.x * TW;
+  const int oy0 = by * TH, ox0 = bx * TW;
   const uint8_t* f = p.frames + (long)n * p.frame_stride;
   const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
   VSS_STAMP(0);
@@ -169,8 +210,14 @@ __global__ __launch_bounds__(256) void k_stem(StemParams p) {
     }
   }
   // start of the forward: zero this frame's decoder norm accumulators
-  if (blockIdx.x == 0 && blockIdx.y == 0)
-    for (int i = tid; i < p.acc_stride; i += 256) p.acc_zero[(long)n * p.acc_stride + i] = 0ull;
+  // (write-through in the persistent forward: the decoders' atomics follow)
+  if (bx == 0 && by == 0)
+    for (int i = tid; i < p.acc_stride; i += 256) {
+      if constexpr (COH)
+        __hip_atomic_store(p.acc_zero + (long)n * p.acc_stride + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        p.acc_zero[(long)n * p.acc_stride + i] = 0ull;
+    }
 #pragma unroll
   for (int u = 0; u < NW; ++u) {
     const int i = tid + 256 * u;  // p.w is [c][27]
@@ -203,12 +250,19 @@ __global__ __launch_bounds__(256) void k_stem(StemParams p) {
       }
   const int oy = oy0 + ly, ox = ox0 + lx;
   if (oy < p.Ho && ox < p.Wo) {
-    f4* o = reinterpret_cast<f4*>(p.y + (((long)n * p.Ho + oy) * p.Wo + ox) * COUT);
+    const Gm<COH> gy(p.y + (long)n * p.Ho * p.Wo * COUT);
+    const long o = ((long)oy * p.Wo + ox) * COUT;
 #pragma unroll
     for (int q = 0; q < COUT / 4; ++q)
-      o[q] = f4{relu6f(acc[4 * q]), relu6f(acc[4 * q + 1]), relu6f(acc[4 * q + 2]), relu6f(acc[4 * q + 3])};
+      gy.st(o + 4 * q, f4{relu6f(acc[4 * q]), relu6f(acc[4 * q + 1]), relu6f(acc[4 * q + 2]), relu6f(acc[4 * q + 3])});
   }
   VSS_STAMP(3);
+}
+
+template <int COUT>
+__global__ __launch_bounds__(256) void k_stem(StemParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  stem_body<COUT, false>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -353,8 +407,8 @@ __device__ __forceinline__ void commit_sum(const Staged<TOTAL> (&st)[XP], Store 
 //             decoder: per-tile instance-norm partial sums, and the last
 //             workgroup of each frame to arrive reduces them (fixed order) into
 //             the frame's scale/shift for the consumer.
-template <int MODE, int STRIDE, int TH, int TW, int CIN, int CSKIP, int CH, int COUT, int FLAGS, int PREC>
-__global__ __launch_bounds__(256) void k_block(BlockParams p) {
+template <int MODE, int STRIDE, int TH, int TW, int CIN, int CSKIP, int CH, int COUT, int FLAGS, int PREC, bool COH>
+__device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by, int bz, float* smem) {
   constexpr BlockLds L = block_lds(MODE, STRIDE, TH, TW, CIN, CSKIP, CH, COUT);
   constexpr bool NORM_IN = (FLAGS & 1) != 0, RES = (FLAGS & 2) != 0;
   constexpr int XP = flags_xp(FLAGS), SP = flags_sp(FLAGS), KS = flags_ks(FLAGS);
@@ -369,12 +423,11 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   static_assert(!RES || (STRIDE == 1 && CIN == COUT && MODE != MODE_DEC), "residual shape");
   static_assert(MODE != MODE_IR_EXPAND || CS == 4, "expand deals its chunks to the 4 waves");
   static_assert(NPB % PW == 0, "pixel blocks must split evenly over the wave groups");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int n = KS == 1 ? (int)blockIdx.z : (int)blockIdx.z / KS;  // grid z = frame * KS + slice
-  const int ks = KS == 1 ? 0 : (int)blockIdx.z % KS;
-  const int oy0 = blockIdx.y * TH, ox0 = blockIdx.x * TW;
+  const int n = KS == 1 ? bz : bz / KS;  // grid z = frame * KS + slice
+  const int ks = KS == 1 ? 0 : bz % KS;
+  const int oy0 = by * TH, ox0 = bx * TW;
   const int iy0 = STRIDE * oy0 - 1, ix0 = STRIDE * ox0 - 1;
   const int Ho = p.Ho, Wo = p.Wo;
   float* xt = smem + L.xt;
@@ -403,27 +456,29 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
     // src instance norm: every slot of the frame's exact totals (issued first)
     constexpr int NSLOT16 = NORM_IN ? kAccSlots * 2 * CL / 2 : 0;  // 16-B items
     Staged<NSLOT16> st_slots;
-    if constexpr (NORM_IN)
-      st_slots.issue([&](int i) {
-        return reinterpret_cast<const f4*>(p.in_acc + (long)n * p.acc_stride)[i];
-      });
+    const Gm<COH> g_slots(reinterpret_cast<const float*>(p.in_acc + (long)n * p.acc_stride));
+    if constexpr (NORM_IN) st_slots.issue([&](int i) { return g_slots.ld(4L * i); });
     Staged<SR * SC * C4L> st_lr[XP];
     Staged<P_IN_PAD * C4S> st_sk[SP];
     Staged<WIMG_F4> st_w;
 #pragma unroll
-    for (int q = 0; q < XP; ++q)
+    for (int q = 0; q < XP; ++q) {
+      const Gm<COH> gx(xn + q * p.x_part_stride);
       st_lr[q].issue([&](int i) {
         const int pr = i / C4L, c4 = i % C4L;
         const int yy = min(h - 1, sy0 + pr / SC), xx = min(w - 1, sx0 + pr % SC);
-        return *reinterpret_cast<const f4*>(xn + q * p.x_part_stride + ((long)yy * w + xx) * CL + 4 * c4);
+        return gx.ld(((long)yy * w + xx) * CL + 4 * c4);
       });
+    }
 #pragma unroll
-    for (int q = 0; q < SP; ++q)
+    for (int q = 0; q < SP; ++q) {
+      const Gm<COH> gs(sn + q * p.skip_part_stride);
       st_sk[q].issue([&](int i) {
         const int pix = i / C4S, c4 = i % C4S;
         const int yy = min(max(iy0 + pix / IW, 0), Ho - 1), xx = min(max(ix0 + pix % IW, 0), Wo - 1);
-        return *reinterpret_cast<const f4*>(sn + q * p.skip_part_stride + ((long)yy * Wo + xx) * CSKIP + 4 * c4);
+        return gs.ld(((long)yy * Wo + xx) * CSKIP + 4 * c4);
       });
+    }
     st_w.issue([&](int i) { return wsrc[i]; });
     VSS_STAMP(6);  // every load issued
     if constexpr (NORM_IN) st_slots.commit([&](int i, f4 v) { reinterpret_cast<f4*>(work)[i] = v; });
@@ -493,12 +548,14 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
     Staged<P_IN_PAD * C4> st_x[XP];
     Staged<WIMG_F4> st_w;
 #pragma unroll
-    for (int q = 0; q < XP; ++q)
+    for (int q = 0; q < XP; ++q) {
+      const Gm<COH> gx(xn + q * p.x_part_stride);
       st_x[q].issue([&](int i) {
         const int pix = i / C4, c4 = i % C4;
         const int yy = min(max(iy0 + pix / IW, 0), H - 1), xx = min(max(ix0 + pix % IW, 0), W - 1);
-        return *reinterpret_cast<const f4*>(xn + q * p.x_part_stride + ((long)yy * W + xx) * CIN + 4 * c4);
+        return gx.ld(((long)yy * W + xx) * CIN + 4 * c4);
       });
+    }
     st_w.issue([&](int i) { return wsrc[i]; });
     VSS_STAMP(6);  // every load issued
     commit_sum(st_x, [&](int i, f4 v) {
@@ -618,6 +675,7 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   }
   __syncthreads();
   constexpr int C4O = COUT / 4;
+  const Gm<COH> gy(p.y + ks * p.y_part_stride + (long)n * Ho * Wo * COUT);
 #pragma unroll
   for (int k = 0; k < (P_OUT * C4O + 255) / 256; ++k) {
     const int i = tid + 256 * k;
@@ -639,8 +697,7 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
             v = v + *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + 4 * c4);
         }
       }
-      if (valid)
-        *reinterpret_cast<f4*>(p.y + ks * p.y_part_stride + (((long)n * Ho + oy) * Wo + ox) * COUT + 4 * c4) = v;
+      if (valid) gy.st(((long)oy * Wo + ox) * COUT + 4 * c4, v);
       if constexpr (MODE == MODE_DEC)
         *reinterpret_cast<f4*>(work + pix * RS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
     }
@@ -672,7 +729,7 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
       long long t = 0;
 #pragma unroll
       for (int k = 0; k < G; ++k) t += st64[base + k * COUT];
-      const int slot = (blockIdx.y * p.tiles_x + blockIdx.x) % kAccSlots;
+      const int slot = (by * p.tiles_x + bx) % kAccSlots;
       __hip_atomic_fetch_add(p.out_acc + (long)n * p.acc_stride + slot * 2 * COUT + tid, (unsigned long long)t,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -680,34 +737,44 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   VSS_STAMP(3);
 }
 
+template <int MODE, int STRIDE, int TH, int TW, int CIN, int CSKIP, int CH, int COUT, int FLAGS, int PREC>
+__global__ __launch_bounds__(256) void k_block(BlockParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  block_body<MODE, STRIDE, TH, TW, CIN, CSKIP, CH, COUT, FLAGS, PREC, false>(p, blockIdx.x, blockIdx.y, blockIdx.z,
+                                                                             smem);
+}
+
 // ---------------------------------------------------------------------------
 // Head: mask tile 16 x 64; logits over the (10 x 34) low-res region in LDS.
-template <int C>
-__global__ __launch_bounds__(256) void k_head(HeadParams p) {
-  constexpr int OTH = 16, OTW = 64, ZR = 10, ZC = 34, ZCP = 35, NZ = (ZR * ZC + 255) / 256;
-  __shared__ float z[ZR][ZCP];
-  __shared__ float sc[C], sh[C], wv[C];
-  const int tid = threadIdx.x, n = blockIdx.z;
-  const int oy0 = blockIdx.y * OTH, ox0 = blockIdx.x * OTW;
+template <int C, bool COH>
+__device__ __forceinline__ void head_body(const HeadParams& p, int bx, int by, int n, float* smem) {
+  constexpr int OTH = kHeadTH, OTW = kHeadTW, ZR = kHeadZR, ZC = kHeadZC, ZCP = kHeadZCP, NZ = (ZR * ZC + 255) / 256;
+  static_assert(C == 16, "head LDS carve (kHeadLds) assumes 16 channels");
+  unsigned long long* slots = reinterpret_cast<unsigned long long*>(smem);  // [kAccSlots][2][C]
+  float (*z)[ZCP] = reinterpret_cast<float (*)[ZCP]>(smem + kAccSlots * 2 * C * 2);
+  float* sc = smem + kAccSlots * 2 * C * 2 + r4(ZR * ZCP);
+  float* sh = sc + C;
+  float* wv = sh + C;
+  const int tid = threadIdx.x;
+  const int oy0 = by * OTH, ox0 = bx * OTW;
   const int h = p.h, w = p.w_;
   const int zr0 = oy0 / 2 - 1, zc0 = ox0 / 2 - 1;
   VSS_STAMP(0);
   // issue this thread's d3 loads before the statistics reduction
+  const Gm<COH> gx(p.x + (long)n * h * w * C);
   f4 xv[NZ][C / 4];
 #pragma unroll
   for (int u = 0; u < NZ; ++u) {
     const int i = min(tid + 256 * u, ZR * ZC - 1);
     const int zr = i / ZC, zc = i - zr * ZC;
     const int yy = min(max(zr0 + zr, 0), h - 1), xx = min(max(zc0 + zc, 0), w - 1);
-    const f4* px = reinterpret_cast<const f4*>(p.x + (((long)n * h + yy) * w + xx) * C);
 #pragma unroll
-    for (int q = 0; q < C / 4; ++q) xv[u][q] = px[q];
+    for (int q = 0; q < C / 4; ++q) xv[u][q] = gx.ld(((long)yy * w + xx) * C + 4 * q);
   }
   // the d3 norm: all slots of the frame's exact totals (2 x C int64 per slot)
-  __shared__ unsigned long long slots[kAccSlots * 2 * C];
   {
-    const unsigned long long* ia = p.in_acc + (long)n * p.acc_stride;
-    for (int i = tid; i < kAccSlots * 2 * C; i += 256) slots[i] = ia[i];
+    const Gm<COH> ga(reinterpret_cast<const float*>(p.in_acc + (long)n * p.acc_stride));
+    for (int i = tid; i < kAccSlots * C; i += 256) reinterpret_cast<f4*>(slots)[i] = ga.ld(4L * i);
   }
   if (tid < C) wv[tid] = p.w[tid];
   __syncthreads();
@@ -759,16 +826,211 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
   VSS_STAMP(3);
 }
 
+template <int C>
+__global__ __launch_bounds__(256) void k_head(HeadParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  head_body<C, false>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent forward: the whole network in one launch (FwdParams, vss_kernels.h).
+// A dependency wait polls ONE word from ONE lane (relaxed agent loads = sc1,
+// with s_sleep) and gives up after spin_limit ticks, setting the sticky fault
+// word (the host reports it; no wave ever spins forever).
+__device__ __forceinline__ void fwd_wait(unsigned* w, unsigned need, unsigned* fault, long long limit) {
+  if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) return;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    // ~0.5 us between polls: hundreds of waiting workgroups polling the same
+    // few counters otherwise load the memory system every task depends on
+    __builtin_amdgcn_s_sleep(16);
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) return;
+    if (__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > limit) {
+      __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+}
+
+// One task of the persistent forward, each shape its own (non-inlined)
+// function so every body keeps the register allocation of its layer launch
+// instead of sharing one allocation with every other shape.  Arguments of a
+// device function live in VGPRs, so the wave-uniform ones are re-established
+// with readfirstlane (buffer descriptors from divergent bases would be
+// waterfalled).
+
+// The layer table and task list never change during a launch: read them
+// through the constant address space (scalar loads into SGPRs, like kernel
+// arguments) and copy the parameters into registers once per task, instead
+// of re-loading them from global memory after every store.
+template <class T>
+using const_as = const __attribute__((address_space(4))) T;
+template <class T>
+__device__ __forceinline__ const_as<T>* as_const(const T* p) {
+  return (const_as<T>*)(unsigned long long)uniform_ptr(p);
+}
+template <class T>
+__device__ __forceinline__ T load_const(const T* p) {  // dword by dword: scalar loads
+  static_assert(sizeof(T) % 4 == 0, "dword-sized parameter blocks");
+  T out;
+  const_as<unsigned>* src = (const_as<unsigned>*)(unsigned long long)uniform_ptr(p);
+  unsigned* dst = reinterpret_cast<unsigned*>(&out);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = src[i];
+  return out;
+}
+
+template <int M, int S, int TH, int TW, int CI, int CK, int CH, int CO, int FL, int PREC>
+__device__ __noinline__ void fwd_block(const BlockParams* p, int bx, int by, int bz) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const BlockParams pu = load_const(p);
+  block_body<M, S, TH, TW, CI, CK, CH, CO, FL, PREC, true>(pu, __builtin_amdgcn_readfirstlane(bx),
+                                                          __builtin_amdgcn_readfirstlane(by),
+                                                          __builtin_amdgcn_readfirstlane(bz), smem);
+}
+
+__device__ __noinline__ void fwd_stem(const FwdLayer* L, const uint8_t* frames, long rs, long fs, int fh, int fw,
+                                     int fc, float ry, float rx, int bx, int by, int f) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  StemParams sp = load_const(&L->stem);  // + this call's frames
+  sp.frames = static_cast<const uint8_t*>(uniform_ptr(frames));
+  sp.row_stride = (long)uniform_ptr(reinterpret_cast<const void*>(rs));
+  sp.frame_stride = (long)uniform_ptr(reinterpret_cast<const void*>(fs));
+  sp.fh = __builtin_amdgcn_readfirstlane(fh);
+  sp.fw = __builtin_amdgcn_readfirstlane(fw);
+  sp.fc = __builtin_amdgcn_readfirstlane(fc);
+  sp.ry = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ry)));
+  sp.rx = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rx)));
+  stem_body<16, true>(sp, __builtin_amdgcn_readfirstlane(bx), __builtin_amdgcn_readfirstlane(by),
+                      __builtin_amdgcn_readfirstlane(f), smem);
+}
+
+__device__ __noinline__ void fwd_head(const FwdLayer* L, float* mask, int bx, int by, int f) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  HeadParams hp = load_const(&L->head);  // + this call's mask buffer
+  hp.mask = static_cast<float*>(const_cast<void*>(uniform_ptr(mask)));
+  head_body<16, true>(hp, __builtin_amdgcn_readfirstlane(bx), __builtin_amdgcn_readfirstlane(by),
+                      __builtin_amdgcn_readfirstlane(f), smem);
+}
+
+template <int PREC>
+__global__ __launch_bounds__(256, 2) void k_forward(FwdParams fp) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int* slot = reinterpret_cast<int*>(smem + fp.lds_floats - 16);  // [2]: this / next ticket
+  const int tid = threadIdx.x;
+  // tickets: kFwdQueues counters, each on its own 128-B line; workgroup b
+  // serves queue b % kFwdQueues, which holds the tasks t = k * kFwdQueues + q
+  // in order (the host's order is topological, so every queue is too)
+  const int q = (int)blockIdx.x & (kFwdQueues - 1);
+  unsigned* fault = fp.ctl + kFwdQueues * kFwdLine + 1;
+  unsigned* dbg = fp.dbg ? fp.dbg + blockIdx.x * 4 : nullptr;
+  auto trace = [&](int k, unsigned v) {
+    if (dbg && tid == 0) __hip_atomic_store(dbg + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  };
+  trace(1, 1);
+  const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+  const int ntasks = fp.ntasks;
+  auto take = [&]() {  // lane 0 only
+    int t = (int)__hip_atomic_fetch_add(fp.ctl + q * kFwdLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) *
+                kFwdQueues + q;
+    // a launch past its deadline stops taking work (and says so): whatever
+    // went wrong, every workgroup drains
+    if (t < ntasks && (long long)__builtin_amdgcn_s_memrealtime() - t_start > 10 * fp.spin_limit) {
+      __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = ntasks;
+    }
+    return t < ntasks ? t : ntasks;
+  };
+  if (tid == 0) slot[0] = take();
+  for (int it = 0;; ++it) {
+    __syncthreads();
+    const int t = __builtin_amdgcn_readfirstlane(slot[it & 1]);
+    if (t >= ntasks) break;
+    const_as<FwdTask>& tk = as_const(fp.tasks)[t];
+    const int li = __builtin_amdgcn_readfirstlane(tk.layer);
+    const int f = __builtin_amdgcn_readfirstlane(tk.frame);
+    const int tile = __builtin_amdgcn_readfirstlane(tk.tile);
+    const_as<FwdLayer>& L = as_const(fp.layers)[li];
+    unsigned long long* tt = fp.ttrace ? fp.ttrace + 4L * t : nullptr;
+    if (tt && tid == 0) {
+      tt[0] = __builtin_amdgcn_s_memrealtime();
+      tt[3] = blockIdx.x | ((unsigned long long)li << 16) | ((unsigned long long)f << 24);
+    }
+    trace(0, (unsigned)t);
+    trace(2, (unsigned)li);
+    trace(3, (unsigned)f);
+    trace(1, 2);
+    if (tid == 0) {
+      const int tn = take();  // the next ticket: its round trip overlaps this task's wait and body
+      if (!fp.nowait)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          if (L.dep[k] >= 0) fwd_wait(fp.done + (L.dep[k] * fp.max_batch + f) * kFwdLine, (unsigned)L.need[k], fault, fp.spin_limit);
+      slot[(it + 1) & 1] = tn;  // read after the next loop-top barrier
+    }
+    __syncthreads();  // the other waves load only after the polling lane matched
+    if (tt && tid == 0) tt[1] = __builtin_amdgcn_s_memrealtime();
+    trace(1, 3);
+    const int txy = L.tiles_x * L.tiles_y;
+    const int ks = tile / txy, rem = tile - ks * txy;
+    const int by = rem / L.tiles_x, bx = rem - by * L.tiles_x;
+    if (L.kind == FWD_STEM) {
+      fwd_stem(fp.layers + li, fp.frames, fp.row_stride, fp.frame_stride, fp.fh, fp.fw, fp.fc, fp.ry, fp.rx, bx, by, f);
+    } else if (L.kind == FWD_HEAD) {
+      fwd_head(fp.layers + li, fp.mask, bx, by, f);
+    } else {
+      const int bz = f * L.ks + ks;
+      switch (L.mk) {
+#define VSS_MK(ID, M, S, TH, TW, CI, CK, CH, CO, FL)                      \
+  case ID:                                                               \
+    fwd_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC>(&fp.layers[li].block, bx, by, bz); \
+    break;
+#include "vss_mk.inc"
+#undef VSS_MK
+        default:
+          break;
+      }
+    }
+    trace(1, 4);
+    if (tt && tid == 0) tt[2] = __builtin_amdgcn_s_memrealtime();
+    // every storing wave drains its write-through stores (and norm atomics),
+    // then ONE lane signals the task done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(fp.done + (li * fp.max_batch + f) * kFwdLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    trace(1, 5);
+  }
+  trace(1, 6);
+  // the last workgroup out re-arms the counters for the next launch (stream
+  // order puts it before that launch; the fault word stays for the host)
+  if (tid == 0) {
+    unsigned* exits = fp.ctl + kFwdQueues * kFwdLine;
+    const unsigned e = __hip_atomic_fetch_add(exits, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e == gridDim.x - 1) {
+      for (int i = 0; i < fp.n_layers * fp.max_batch; ++i)
+        __hip_atomic_store(fp.done + i * kFwdLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < kFwdQueues; ++k)
+        __hip_atomic_store(fp.ctl + k * kFwdLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host-visible launch table (used by vss_capi.hip): one entry per compiled
 // block shape, generated from the layer table by tools/gen_registry.py.
-#define VSS_BLOCK(M, S, TH, TW, CI, CK, CH, CO, FL)                                    \
-  {M, S, TH, TW, CI, CK, CH, CO, FL,                                                  \
+#define VSS_BLOCK(M, S, TH, TW, CI, CK, CH, CO, FL, MK)                                \
+  {M, S, TH, TW, CI, CK, CH, CO, FL, MK,                                              \
    {k_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC_F32>,                              \
     k_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC_BF16X2>}},
+#ifndef VSS_ONLY_FORWARD  // (quick compile of k_forward alone for resource checks)
 static const BlockEntry kBlocks[] = {
 #include "vss_registry.inc"
 };
+#else
+static const BlockEntry kBlocks[] = {{0}};
+#endif
 #undef VSS_BLOCK
 
 const BlockEntry* block_registry(int* count) {
@@ -779,5 +1041,6 @@ const BlockEntry* block_registry(int* count) {
 void (*stem_kernel16())(StemParams) { return k_stem<16>; }
 void (*head_kernel16())(HeadParams) { return k_head<16>; }
 void (*prep_kernel())(PrepParams) { return k_prep; }
+FwdFn forward_kernel(int prec) { return prec == PREC_F32 ? k_forward<PREC_F32> : k_forward<PREC_BF16X2>; }
 
 }  // namespace vss
