@@ -176,12 +176,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # VSS_BENCH_BACKEND=gloo: rehearse the N > 1 code path with ranks sharing
+    # fewer GPUs than ranks (plumbing check only; RCCL is the measured backend)
+    backend = os.environ.get("VSS_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev if backend != "nccl" else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", gpu if world > 1 else 0)
 
     pkg = _load_pkg()
     import vss_amd.synthetic as syn
@@ -284,7 +292,8 @@ def main():
     costs = cm.layer_costs(recs, hm, wm, fh, fw, 3, pw_weight_bytes=2 if args.dtype == "bf16x2" else 4)
     names = [sess.layer_kernel(i) for i in range(len(ms))]
     per_layer = [{"layer": i, "kind": costs[i]["kind"], "kernel": names[i], "ms": round(m, 5),
-                  "GBps": round(cm.launch_bytes(costs[i], B) / (m * 1e-3) / 1e9, 1)} for i, m in enumerate(ms)]
+                  "GBps": round(cm.launch_bytes(costs[i], B) / (m * 1e-3) / 1e9, 1) if m > 0 else None}
+                 for i, m in enumerate(ms)]
     if persistent:
         # the dominant (only) kernel is the whole forward: every layer's
         # compulsory HBM bytes (each activation written once, read once)

@@ -231,3 +231,24 @@ def test_branches_bitwise(pkg, sess_bf, synthetic, torch_cuda):
         sess_bf.synchronize()
         assert np.array_equal(out.cpu().numpy(), ref), br
     sess_bf.set_option(pkg.VSS_OPT_BRANCHES, 1)
+
+
+def test_stem_fusion_bitwise(pkg, synthetic, torch_cuda):
+    # the stem computed inside b1's prologue (STEM_IN, one launch fewer) gives
+    # bitwise the activations and masks of the separate stem launch
+    f = _frames(synthetic, 5, start=800)
+    with pkg.Session(dtype="bf16x2", max_batch=8) as s:
+        assert s.layer_kernel(0).startswith("(fused into layer 1")
+        a, _, _ = s.segment_frames(f)
+        taps_a = [s.read_layer(li, 5) for li in range(2)]
+    os.environ["VSS_FUSE_STEM"] = "0"
+    try:
+        with pkg.Session(dtype="bf16x2", max_batch=8) as s:
+            assert s.layer_kernel(0) == "void vss::k_stem<16>(vss::StemParams)"
+            b, _, _ = s.segment_frames(f)
+            taps_b = [s.read_layer(li, 5) for li in range(2)]
+    finally:
+        del os.environ["VSS_FUSE_STEM"]
+    assert np.array_equal(a, b)
+    for li in range(2):
+        assert np.array_equal(taps_a[li], taps_b[li]), li

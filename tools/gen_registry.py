@@ -37,7 +37,11 @@ def r4(v):
     return (v + 3) & ~3
 
 
-def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout):
+def stem_in_lds(ih, iw):
+    return r4(3 * (2 * ih + 1) * (2 * iw + 2)) + 27 * 16 + 16
+
+
+def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=False):
     ih = 2 * th + 1 if stride == 2 else th + 2
     iw = 2 * tw + 1 if stride == 2 else tw + 2
     p_in_pad = (ih * iw + 15) & ~15
@@ -58,7 +62,7 @@ def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout):
     f += r4(cout * (chid + 8) // 2) + r4(9 * chid) + r4(chid) + (r4(chid) if mode == 0 else 0) + r4(cout)
     f += (r4(sr * sc * cin) + r4(2 * cin)) if mode == 2 else 0
     f += max(4 * ((p_in_pad + p_out) * 16 if mode == 0 else 256), cs * p_out * (cout + 4),
-             16 * 2 * cin * 2 if mode == 2 else 0)
+             16 * 2 * cin * 2 if mode == 2 else 0, stem_in_lds(ih, iw) if stem_in else 0)
     f += 1024
     return f * 4, nacc
 
@@ -75,8 +79,9 @@ def ks_max(layer):
     return 1
 
 
-def flags_of(norm_in, residual, xp, sp, ks):
-    return (1 if norm_in else 0) | (2 if residual else 0) | ((xp - 1) << 2) | ((sp - 1) << 4) | ((ks - 1) << 6)
+def flags_of(norm_in, residual, xp, sp, ks, stem_in=False):
+    return ((1 if norm_in else 0) | (2 if residual else 0) | ((xp - 1) << 2) | ((sp - 1) << 4) | ((ks - 1) << 6) |
+            (256 if stem_in else 0))
 
 
 def shapes(spec):
@@ -92,6 +97,11 @@ def shapes(spec):
                 for xp in ks_opts[l["src"]]:
                     out.append((l["name"], mode, l["stride"], l["cin"], 0, chid // ks, l["cout"],
                                 flags_of(False, l["residual"], xp, 1, ks)))
+            src = layers[names.index(l["src"])]
+            if src["kind"] == "stem" and not l["expand"] and l["stride"] == 1 and l["cin"] == src["cout"] == 16:
+                # the stem fused into its consumer's prologue (STEM_IN)
+                out.append((l["name"], mode, 1, l["cin"], 0, chid, l["cout"],
+                            flags_of(False, l["residual"], 1, 1, 1, stem_in=True)))
         elif l["kind"] == "dec":
             src = layers[names.index(l["src"])]
             for xp in ks_opts[l["src"]]:
@@ -163,7 +173,7 @@ def main():
     seen = set()
     for name, mode, stride, cin, cskip, chid, cout, flags in shapes(spec):
         for th, tw in CANDIDATES:
-            lds, nacc = block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout)
+            lds, nacc = block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, bool(flags & 256))
             if lds is None or nacc > MAX_ACC or lds > MAX_LDS or (th * tw) % 16:
                 continue
             key = (mode, stride, th, tw, cin, cskip, chid, cout, flags)

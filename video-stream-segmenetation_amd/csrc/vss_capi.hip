@@ -54,6 +54,7 @@ struct LayerPlan {
   long wimg_stride = 0;        // floats between the slices' weight images
   size_t lds = 0;
   const BlockEntry* entry = nullptr;  // compiled shape (registry)
+  bool fused = false;          // computed inside its only consumer's prologue (no launch of its own)
   float* act = nullptr;        // [max_batch][H][W][C]
   int acc_off = -1;            // DEC: offset of its [2][C] norm accumulator in a frame's row of d_acc
   const float* wimg = nullptr;  // LDS weight image (block_lds regions w1..b2)
@@ -133,6 +134,7 @@ struct vss_handle {
   int fwd_lds_floats = 0;
   int fwd_grid = 0;
   int fwd_order = 0;             // 0 layer-major, 1 diagonal (env VSS_FWD_ORDER=diag)
+  int fuse_stem = 1;             // env VSS_FUSE_STEM=0: launch the stem on its own
   std::map<int, std::pair<FwdTask*, int>> fwd_tasks;  // per batch size n
   unsigned* fwd_dbg = nullptr;   // env VSS_FWD_DEBUG: host-mapped per-workgroup state
   unsigned long long* fwd_trace = nullptr;  // env VSS_FWD_TRACE: per-task stamps of the last launch
@@ -177,7 +179,8 @@ uint16_t bf16_bits(float f) {  // pointwise weights are bf16-exact: truncation i
 
 size_t block_lds_bytes(const LayerPlan& l, int TH, int TW) {
   const int cskip = l.mode == MODE_DEC ? (int)l.rec.chid : 0;
-  return (size_t)block_lds(l.mode, l.stride, TH, TW, (int)l.rec.cin, cskip, l.chid / l.ks, l.C).total * 4;
+  return (size_t)block_lds(l.mode, l.stride, TH, TW, (int)l.rec.cin, cskip, l.chid / l.ks, l.C,
+                           flags_stem_in(l.flags)).total * 4;
 }
 
 // Largest hidden split of an expand layer that leaves every wave >= 1 chunk of
@@ -274,6 +277,11 @@ int plan_once(vss_handle* h, bool mk_only) {
   const int Hm = h->cfg.model_h, Wm = h->cfg.model_w, N = h->cfg.max_batch;
   const int nl = (int)h->recs.size();
   h->L.assign(nl, LayerPlan{});
+  std::vector<int> consumers(nl, 0);
+  for (const Rec& r : h->recs) {
+    if (r.kind != K_STEM && r.src < (uint32_t)nl) consumers[r.src]++;
+    if (r.kind == K_DEC && r.skip < (uint32_t)nl) consumers[r.skip]++;
+  }
   for (int i = 0; i < nl; ++i) {
     LayerPlan& l = h->L[i];
     const Rec& r = h->recs[i];
@@ -331,6 +339,12 @@ int plan_once(vss_handle* h, bool mk_only) {
     if (r.kind == K_IR || r.kind == K_DEC) l.xp = h->L[r.src].ks;
     if (r.kind == K_DEC) l.sp = h->L[r.skip].ks;
     if (r.kind == K_IR) l.flags = block_flags(0, (r.flags & F_RESIDUAL) != 0, l.xp, 1, l.ks);
+    // the stem fused into its only consumer, a stride-1 direct block (STEM_IN)
+    if (r.kind == K_IR && !mk_only && h->fuse_stem && l.mode == MODE_IR_DIRECT && l.stride == 1 &&
+        h->L[r.src].rec.kind == K_STEM && consumers[r.src] == 1 && r.cin == 16) {
+      l.flags |= block_flags(0, 0, 1, 1, 1, 1);
+      h->L[r.src].fused = true;
+    }
     if (r.kind == K_DEC) l.flags = block_flags(h->L[r.src].rec.kind == K_DEC, 0, l.xp, l.sp, 1);
     if (l.mode >= 0) {
       int rc = choose_tile(h, l, N, mk_only);
@@ -461,6 +475,22 @@ int check_frames(vss_handle* h, int n, int fh, int fw, int fc, size_t rs, size_t
 }
 
 size_t frame_elems(const LayerPlan& l) { return (size_t)l.H * l.W * l.C; }
+
+// The stem's parameters for this call's frames (frames point at frame f0).
+StemParams stem_params(const vss_handle* h, const LayerPlan& l, const uint8_t* frames, size_t rs, size_t fs, int fh,
+                       int fw, int fc, int f0) {
+  const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
+  StemParams p{};
+  p.frames = frames; p.row_stride = (long)rs; p.frame_stride = (long)fs;
+  p.fh = fh; p.fw = fw; p.fc = fc; p.Hm = Hm; p.Wm = Wm;
+  p.ry = (float)((double)fh / (double)Hm);
+  p.rx = (float)((double)fw / (double)Wm);
+  p.w = l.stem_w; p.b = l.stem_b; p.y = l.act + (size_t)f0 * l.H * l.W * l.C;
+  p.Ho = l.H; p.Wo = l.W; p.cout = l.C;
+  p.acc_zero = h->d_acc + (size_t)f0 * h->acc_stride;
+  p.acc_stride = h->acc_stride;
+  return p;
+}
 
 // Kernel parameters of block layer l for frames [f0, f0 + n) of the batch.
 BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n, int f0 = 0) {
@@ -689,28 +719,25 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       else
         hipLaunchKernelGGL(fn, grid, dim3(kThreads), lds, s, prm);
     };
+    if (l.fused) {  // runs inside its consumer's launch
+#ifdef VSS_TRACE
+      h->trace_wgs[i] = 0;
+#endif
+      continue;
+    }
     if (r.kind == K_STEM) {
-      StemParams p{};
-      p.frames = frames; p.row_stride = (long)rs; p.frame_stride = (long)fs;
-      p.fh = fh; p.fw = fw; p.fc = fc; p.Hm = Hm; p.Wm = Wm;
-      p.ry = (float)((double)fh / (double)Hm);
-      p.rx = (float)((double)fw / (double)Wm);
-      p.w = l.stem_w; p.b = l.stem_b; p.y = l.act + f0 * frame_elems(l);
-      p.Ho = l.H; p.Wo = l.W; p.cout = l.C;
-      p.acc_zero = h->d_acc + (size_t)f0 * h->acc_stride;
-      p.acc_stride = h->acc_stride;
+      StemParams p = stem_params(h, l, frames, rs, fs, fh, fw, fc, f0);
 #ifdef VSS_TRACE
       p.trace = h->trace[i];
       h->trace_wgs[i] = ((l.W + 31) / 32) * ((l.H + 7) / 8) * n;
 #endif
       go(stem_kernel16(), dim3((l.W + kStemTW - 1) / kStemTW, (l.H + kStemTH - 1) / kStemTH, n), kStemLds * 4, p);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
-#ifdef VSS_TRACE
       BlockParams p = block_params(h, l, n, f0);
+      if (flags_stem_in(l.flags)) p.stem = stem_params(h, h->L[r.src], frames, rs, fs, fh, fw, fc, f0);
+#ifdef VSS_TRACE
       p.trace = h->trace[i];
       h->trace_wgs[i] = l.tiles_x * l.tiles_y * n * l.ks;
-#else
-      const BlockParams p = block_params(h, l, n, f0);
 #endif
       go(l.entry->fn[prec == PREC_F32 ? 0 : 1], dim3(l.tiles_x, l.tiles_y, n * l.ks), l.lds, p);
     } else if (r.kind == K_HEAD) {
@@ -747,6 +774,7 @@ int harvest_slot(vss_handle* h, int slot) {
   }
   for (int i = 0; i < nl; ++i) {
     float ms = 0.f;
+    if (h->L[i].fused) continue;  // timed inside its consumer's launch
     HIP_TRY(h, hipEventSynchronize(h->ev[((size_t)slot * nl + i) * 2 + 1]));
     HIP_TRY(h, hipEventElapsedTime(&ms, h->ev[((size_t)slot * nl + i) * 2], h->ev[((size_t)slot * nl + i) * 2 + 1]));
     h->prof_sum[i] += ms;
@@ -888,7 +916,11 @@ int autotune(vss_handle* h) {
       if (hipFuncSetAttribute((const void*)e->fn[pi], hipFuncAttributeMaxDynamicSharedMemorySize, (int)l.lds) !=
           hipSuccess)
         continue;
-      const BlockParams p = block_params(h, l, N);
+      BlockParams p = block_params(h, l, N);
+      if (flags_stem_in(l.flags))  // the staging buffer as frames: any bytes, valid memory
+        p.stem = stem_params(h, h->L[l.rec.src], h->d_frames, (size_t)h->cfg.max_frame_w * 3,
+                             (size_t)h->cfg.max_frame_w * 3 * h->cfg.max_frame_h, h->cfg.max_frame_h,
+                             h->cfg.max_frame_w, 3, 0);
       const dim3 grid(l.tiles_x, l.tiles_y, N * l.ks);
       for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(kThreads), l.lds, h->stream, p);
       (void)hipEventRecord(e0, h->stream);
@@ -948,6 +980,7 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
   if (hipSetDevice(h->device) != hipSuccess) return bail(fail(h, VSS_E_HIP, "hipSetDevice failed"));
   if (const char* ev = std::getenv("VSS_KSPLIT_PIXELS")) h->ksplit_pixels = std::atol(ev);
   if (const char* ev = std::getenv("VSS_FORWARD")) h->want_forward = std::atoi(ev) != 0;
+  if (const char* ev = std::getenv("VSS_FUSE_STEM")) h->fuse_stem = std::atoi(ev) != 0;
   int rc = load_weights(h);
   if (!rc) rc = plan(h);
   if (!rc) rc = upload(h);
@@ -1196,7 +1229,8 @@ int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap) {
   const LayerPlan& l = h->L[layer];
   const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
   char tmp[160];
-  if (l.rec.kind == K_STEM) std::snprintf(tmp, sizeof(tmp), "void vss::k_stem<16>(vss::StemParams)");
+  if (l.fused) std::snprintf(tmp, sizeof(tmp), "(fused into layer %d)", layer + 1);
+  else if (l.rec.kind == K_STEM) std::snprintf(tmp, sizeof(tmp), "void vss::k_stem<16>(vss::StemParams)");
   else if (l.rec.kind == K_HEAD) std::snprintf(tmp, sizeof(tmp), "void vss::k_head<16>(vss::HeadParams)");
   else {
     const BlockEntry* e = l.entry;

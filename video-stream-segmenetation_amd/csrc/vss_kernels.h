@@ -20,7 +20,11 @@ enum Prec : int { PREC_F32 = 0, PREC_BF16X2 = 1, PREC_BF16 = 2 };
 enum BlockMode : int { MODE_IR_EXPAND = 0, MODE_IR_DIRECT = 1, MODE_DEC = 2 };
 
 // k_block FLAGS: bit 0 the decoder's src needs instance norm + ReLU, bit 1
-// residual add, bits 2-3 XP-1, bits 4-5 SP-1, bits 6-7 KS-1 where
+// residual add, bits 2-3 XP-1, bits 4-5 SP-1, bits 6-7 KS-1, bit 8 STEM_IN where
+//   STEM_IN = the block's input is the stem's output, computed in the block's
+//        prologue from the frame (stem fused into its only consumer: one launch
+//        and one HBM round trip fewer); the block still writes the stem
+//        activation's tile so every layer stays readable;
 //   KS = hidden-channel split of this (expand) layer: KS workgroups per tile,
 //        slice s owns hidden channels [s*chid/KS, (s+1)*chid/KS) and writes
 //        its partial project sum to part s of the output (bias and residual
@@ -28,9 +32,11 @@ enum BlockMode : int { MODE_IR_EXPAND = 0, MODE_IR_DIRECT = 1, MODE_DEC = 2 };
 //        the weights per workgroup;
 //   XP / SP = parts of the x / skip input, summed in part order (fixed, so
 //        results never depend on the tiling) as the prologue loads them.
-__host__ __device__ constexpr int block_flags(int norm_in, int residual, int xp, int sp, int ks) {
-  return (norm_in ? 1 : 0) | (residual ? 2 : 0) | ((xp - 1) << 2) | ((sp - 1) << 4) | ((ks - 1) << 6);
+__host__ __device__ constexpr int block_flags(int norm_in, int residual, int xp, int sp, int ks, int stem_in = 0) {
+  return (norm_in ? 1 : 0) | (residual ? 2 : 0) | ((xp - 1) << 2) | ((sp - 1) << 4) | ((ks - 1) << 6) |
+         (stem_in ? 256 : 0);
 }
+__host__ __device__ constexpr bool flags_stem_in(int f) { return (f & 256) != 0; }
 __host__ __device__ constexpr int flags_xp(int f) { return ((f >> 2) & 3) + 1; }
 __host__ __device__ constexpr int flags_sp(int f) { return ((f >> 4) & 3) + 1; }
 __host__ __device__ constexpr int flags_ks(int f) { return ((f >> 6) & 3) + 1; }
@@ -53,8 +59,13 @@ struct BlockLds {
   int slab_stride;  // floats per wave slab = P_out * (cout + 4)
 };
 
+// LDS the fused stem needs (x0 region [3][2*IH+1][2*IW+2] + stem weights), in the work region
+__host__ __device__ constexpr int stem_in_lds(int IH, int IW) {
+  return r4(3 * (2 * IH + 1) * (2 * IW + 2)) + 27 * 16 + 16;
+}
+
 __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, int TW, int cin, int cskip, int chid,
-                                                 int cout) {
+                                                 int cout, int stem_in = 0) {
   BlockLds L{};
   L.IH = stride == 2 ? 2 * TH + 1 : TH + 2;
   L.IW = stride == 2 ? 2 * TW + 1 : TW + 2;
@@ -96,8 +107,9 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   // per-wave scratch during the main loop, reused as the accumulator slabs
   // after it; for the decoder also the staging of the src's norm slots
   L.work = o;
-  o += cmax(cmax(4 * (mode == 0 ? (L.P_in_pad + L.P_out) * 16 : 256), L.CS * L.slab_stride),
-            mode == 2 ? kAccSlots * 2 * cin * 2 : 0);
+  o += cmax(cmax(cmax(4 * (mode == 0 ? (L.P_in_pad + L.P_out) * 16 : 256), L.CS * L.slab_stride),
+                 mode == 2 ? kAccSlots * 2 * cin * 2 : 0),
+            stem_in ? stem_in_lds(L.IH, L.IW) : 0);
   L.stt = o; o += 1024;  // 4 KiB: stats scratch (int64 pairs)
   L.total = o;
   return L;
@@ -133,6 +145,21 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   } while (0)
 #endif
 
+struct StemParams {
+  const uint8_t* frames; // [N] frames, row_stride / frame_stride bytes
+  long row_stride, frame_stride;
+  int fh, fw, fc;        // frame geometry, fc = 3 or 4
+  int Hm, Wm;            // model input resolution
+  float ry, rx;          // (float)((double)fh/Hm), (float)((double)fw/Wm)
+  const float* w;        // [cout][3][3][3]
+  const float* b;
+  float* y;              // [N][Ho][Wo][cout]
+  int Ho, Wo, cout;
+  unsigned long long* acc_zero;  // all decoder norm accumulators [N][acc_stride]: zeroed here
+  int acc_stride;
+  VSS_TRACE_FIELD
+};
+
 struct BlockParams {
   const float* wimg;     // the layer's LDS weight image (block_lds regions w1..b2), built by the host;
                          // with KS > 1 one image per hidden slice, wimg_stride floats apart
@@ -166,6 +193,7 @@ struct BlockParams {
   int TH, TW;            // output tile
   int tiles_x, tiles_y;
   int norm_in;           // DEC: src needs norm+relu
+  StemParams stem;       // STEM_IN: the fused stem (frames of this call, stem weights, its output y)
   VSS_TRACE_FIELD
 };
 
@@ -179,20 +207,6 @@ struct BlockEntry {
 };
 const BlockEntry* block_registry(int* count);
 
-struct StemParams {
-  const uint8_t* frames; // [N] frames, row_stride / frame_stride bytes
-  long row_stride, frame_stride;
-  int fh, fw, fc;        // frame geometry, fc = 3 or 4
-  int Hm, Wm;            // model input resolution
-  float ry, rx;          // (float)((double)fh/Hm), (float)((double)fw/Wm)
-  const float* w;        // [cout][3][3][3]
-  const float* b;
-  float* y;              // [N][Ho][Wo][cout]
-  int Ho, Wo, cout;
-  unsigned long long* acc_zero;  // all decoder norm accumulators [N][acc_stride]: zeroed here
-  int acc_stride;
-  VSS_TRACE_FIELD
-};
 
 struct HeadParams {
   const float* x;        // pre-norm dec output [N][h][w][cin]

@@ -409,7 +409,8 @@ __device__ __forceinline__ void commit_sum(const Staged<TOTAL> (&st)[XP], Store 
 //             the frame's scale/shift for the consumer.
 template <int MODE, int STRIDE, int TH, int TW, int CIN, int CSKIP, int CH, int COUT, int FLAGS, int PREC, bool COH>
 __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by, int bz, float* smem) {
-  constexpr BlockLds L = block_lds(MODE, STRIDE, TH, TW, CIN, CSKIP, CH, COUT);
+  constexpr bool STEM_IN = flags_stem_in(FLAGS);
+  constexpr BlockLds L = block_lds(MODE, STRIDE, TH, TW, CIN, CSKIP, CH, COUT, STEM_IN);
   constexpr bool NORM_IN = (FLAGS & 1) != 0, RES = (FLAGS & 2) != 0;
   constexpr int XP = flags_xp(FLAGS), SP = flags_sp(FLAGS), KS = flags_ks(FLAGS);
   static_assert(KS == 1 || MODE == MODE_IR_EXPAND, "only expand layers split their hidden channels");
@@ -540,6 +541,100 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         }
         *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
       }
+    }
+  } else if constexpr (STEM_IN) {
+    // The input tile is the stem's output region (IH x IW at half model
+    // resolution, halo included), computed here from the frame: resize taps of
+    // its x0 region -> LDS, then the stem's 3x3 s2 conv + ReLU6 -> xt, in the
+    // same operation order as k_stem (bitwise the same activations).
+    static_assert(MODE == MODE_IR_DIRECT && STRIDE == 1 && CIN == 16 && XP == 1, "stem fusion shape");
+    constexpr int IH = L.IH, XH = 2 * IH + 1, XW = 2 * IW + 1, XWP = XW + 1, NX = (XH * XW + 255) / 256;
+    const StemParams& sp = p.stem;
+    const int H = p.H, W = p.W;  // the stem's output = this block's input
+    const uint8_t* fr = sp.frames + (long)n * sp.frame_stride;
+    const int r0 = 2 * iy0 - 1, c0 = 2 * ix0 - 1;  // x0 region origin (model resolution)
+    float* x0s = work;                            // [3][XH][XWP]
+    float* sws = work + r4(3 * XH * XWP);          // [tap][16]
+    float* sbs = sws + 27 * 16;
+    Staged<WIMG_F4> st_w;
+    st_w.issue([&](int i) { return wsrc[i]; });
+    float wr[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) wr[u] = sp.w[min(tid + 256 * u, 27 * 16 - 1)];
+    const float sb = sp.b[min(tid, 15)];
+    uint32_t raw[NX][12];
+    float dys[NX], dxs[NX];
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int i = min(tid + 256 * u, XH * XW - 1);
+      const int ly = i / XW, lx = i - ly * XW;
+      const int yy = min(max(r0 + ly, 0), sp.Hm - 1), xx = min(max(c0 + lx, 0), sp.Wm - 1);
+      const PrepTap t = prep_tap(fr, sp.row_stride, sp.fc, sp.fh, sp.fw, sp.ry, sp.rx, yy, xx);
+      prep_load(t, raw[u]);
+      dys[u] = t.dy;
+      dxs[u] = t.dx;
+    }
+    VSS_STAMP(6);  // every load issued
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int i = tid + 256 * u;
+      if (i < XH * XW) {
+        const int ly = i / XW, lx = i - ly * XW;
+        const int yy = r0 + ly, xx = c0 + lx;
+        float o[3];
+        prep_finish(raw[u], dys[u], dxs[u], o);
+        const bool valid = yy >= 0 && yy < sp.Hm && xx >= 0 && xx < sp.Wm;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x0s[(c * XH + ly) * XWP + lx] = valid ? o[c] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + 256 * u;  // sp.w is [c][27]
+      if (i < 27 * 16) sws[(i % 27) * 16 + i / 27] = wr[u];
+    }
+    if (tid < 16) sbs[tid] = sb;
+    // start of the forward: zero this frame's decoder norm accumulators (the stem's job)
+    if (bx == 0 && by == 0)
+      for (int i = tid; i < sp.acc_stride; i += 256) {
+        if constexpr (COH)
+          __hip_atomic_store(sp.acc_zero + (long)n * sp.acc_stride + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          sp.acc_zero[(long)n * sp.acc_stride + i] = 0ull;
+      }
+    st_w.commit([&](int i, f4 v) { wdst[i] = v; });
+    VSS_STAMP(4);
+    __syncthreads();
+    // stem outputs of the region: one (pixel, 4-channel group) per item
+    const Gm<COH> gst(sp.y + (long)n * H * W * 16);
+    for (int i = tid; i < P_IN_PAD * 4; i += 256) {
+      const int pix = i >> 2, q = i & 3;
+      const int py = pix / IW, px = pix - (pix / IW) * IW;
+      const int yy = iy0 + py, xx = ix0 + px;
+      f4 a = {0.f, 0.f, 0.f, 0.f};
+      if (pix < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        float acc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = sbs[4 * q + c];
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              const float xv = x0s[(ci * XH + 2 * py + ky) * XWP + 2 * px + kx];
+              const f4 w4 = *reinterpret_cast<const f4*>(sws + (ci * 9 + ky * 3 + kx) * 16 + 4 * q);
+              acc[0] = __builtin_fmaf(w4.x, xv, acc[0]);
+              acc[1] = __builtin_fmaf(w4.y, xv, acc[1]);
+              acc[2] = __builtin_fmaf(w4.z, xv, acc[2]);
+              acc[3] = __builtin_fmaf(w4.w, xv, acc[3]);
+            }
+        a = f4{relu6f(acc[0]), relu6f(acc[1]), relu6f(acc[2]), relu6f(acc[3])};
+        // the stem activation itself (its tile centre, written once): what
+        // vss_read_layer reports for the stem
+        if (py >= 1 && py <= TH && px >= 1 && px <= TW) gst.st(((long)yy * W + xx) * 16 + 4 * q, a);
+      }
+      *reinterpret_cast<f4*>(xt + pix * XS + 4 * q) = a;
     }
   } else {
     constexpr int C4 = CIN / 4;
