@@ -1,0 +1,207 @@
+"""Synthetic ONNX models for the GPU ONNX sessions (test infrastructure):
+built with oracle/onnx_ref.py's writer from seeded weights, so every test
+run sees the same bytes.  `modnet_like` follows the public MODNet layout the
+reference's absent model_q4f16.onnx is named after:
+MobileNetV2 inverted residuals with ReLU6 (Clip), an SE block (GAP ->
+Gemm -> Relu -> Gemm -> Sigmoid -> Mul), IBNorm (half the channels
+BatchNormalization, half InstanceNormalization: Split / Concat), bilinear
+Resize x2 with skip Concat, and a sigmoid matte at input resolution."""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import onnx_ref as R  # noqa: E402
+
+
+class Builder:
+    def __init__(self, seed=0):
+        self.rng = np.random.default_rng(seed)
+        self.nodes, self.inits, self.k = [], {}, 0
+
+    def name(self, p="t"):
+        self.k += 1
+        return f"{p}{self.k}"
+
+    def w(self, *shape, scale=None):
+        n = self.name("w")
+        fan = int(np.prod(shape[1:])) if len(shape) > 1 else 1
+        s = scale if scale is not None else (2.0 / max(fan, 1)) ** 0.5
+        self.inits[n] = (self.rng.standard_normal(shape) * s).astype(np.float32)
+        return n
+
+    def const(self, arr):
+        n = self.name("c")
+        self.inits[n] = np.asarray(arr)
+        return n
+
+    def op(self, op, inputs, n_out=1, **attrs):
+        outs = [self.name(op.lower()) for _ in range(n_out)]
+        self.nodes.append(R.make_node(op, inputs, outs, **attrs))
+        return outs[0] if n_out == 1 else outs
+
+    def conv(self, x, cin, cout, k, stride=1, pads=None, group=1, dil=1, bias=True):
+        p = pads if pads is not None else [k // 2 * dil] * 4
+        ins = [x, self.w(cout, cin // group, k, k)]
+        if bias:
+            ins.append(self.w(cout, scale=0.1))
+        return self.op("Conv", ins, kernel_shape=[k, k], strides=[stride, stride], pads=p, group=group,
+                       dilations=[dil, dil])
+
+    def model(self, inputs, outputs, opset=13):
+        return R.make_model(self.nodes, self.inits, inputs, outputs, opset=opset)
+
+
+def conv_zoo():
+    """Every convolution shape class the face models and MODNet use, with the
+    epilogue fusions (BatchNormalization folding, residual Add, activations)."""
+    b = Builder(1)
+    x = "x"
+    a = b.conv(x, 3, 24, 5, stride=2, pads=[1, 1, 2, 2])                  # MediaPipe stem: 5x5 s2 asym pads
+    a = b.op("Relu", [a])
+    d = b.conv(a, 24, 24, 3, group=24)                                     # depthwise 3x3
+    p = b.conv(d, 24, 24, 1)                                               # 1x1
+    r = b.op("Add", [p, a])                                                # residual
+    r = b.op("Relu", [r])
+    s2 = b.conv(r, 24, 24, 3, stride=2, pads=[0, 0, 2, 2], group=24)       # depthwise s2, pads (0,0,2,2)
+    s2 = b.conv(s2, 24, 32, 1)
+    sl = b.w(32, 1, 1, scale=0.3)
+    s2 = b.op("PRelu", [s2, sl])                                           # per-channel PRelu (landmarks)
+    g = b.conv(s2, 32, 32, 3, group=2)                                     # grouped
+    bn = b.op("BatchNormalization", [g, b.const(b.rng.random(32).astype(np.float32) + 0.5),
+                                     b.const(b.rng.standard_normal(32).astype(np.float32) * 0.1),
+                                     b.const(b.rng.standard_normal(32).astype(np.float32) * 0.1),
+                                     b.const(b.rng.random(32).astype(np.float32) + 0.5)], epsilon=1e-5)
+    c6 = b.op("Clip", [bn, b.const(np.array(0, np.float32)), b.const(np.array(6, np.float32))])
+    dl = b.conv(c6, 32, 40, 3, dil=2)                                      # dilated
+    dl = b.op("LeakyRelu", [dl], alpha=0.1)
+    v = b.conv(dl, 40, 16, 3, pads=[0, 0, 0, 0], bias=False)               # valid padding, no bias
+    nb = b.w(16, 40 // 1, 1, 1)
+    v2 = b.op("Conv", [dl, nb], kernel_shape=[1, 1], auto_pad="SAME_UPPER", strides=[2, 2])
+    return b.model([("x", [1, 3, 64, 80])], [(v, [1, 16, 14, 18]), (v2, [1, 16, 8, 10])])
+
+
+def ops_zoo():
+    """The non-convolution operators, incl. the shape arithmetic exporters emit."""
+    b = Builder(2)
+    x = "x"                                                                # [2, 8, 12, 16]
+    mp = b.op("MaxPool", [x], kernel_shape=[2, 2], strides=[2, 2])
+    ap = b.op("AveragePool", [x], kernel_shape=[3, 3], strides=[2, 2], pads=[1, 1, 1, 1], count_include_pad=0)
+    cat = b.op("Concat", [mp, ap], axis=1)                                  # [2, 16, 6, 8]
+    pad = b.op("Pad", [cat, b.const(np.array([0, 0, 1, 0, 0, 4, 0, 2], np.int64)), b.const(np.array(0.5, np.float32))],
+               mode="constant")                                             # channel + spatial pad [2, 20, 7, 10]
+    sp = b.op("Split", [pad, b.const(np.array([5, 15], np.int64))], n_out=2, axis=1)
+    sm = b.op("Sigmoid", [sp[0]])
+    th = b.op("Tanh", [sp[1]])
+    mul = b.op("Mul", [th, b.const(b.rng.standard_normal((15, 1, 1)).astype(np.float32))])
+    sub = b.op("Sub", [mul, b.const(np.array(0.25, np.float32))])
+    div = b.op("Div", [sm, b.const(np.array(192.0, np.float32))])
+    cat2 = b.op("Concat", [div, sub], axis=1)                               # [2, 20, 7, 10]
+    sl = b.op("Slice", [cat2, b.const(np.array([1, 0], np.int64)), b.const(np.array([7, 10], np.int64)),
+                        b.const(np.array([2, 3], np.int64)), b.const(np.array([2, 3], np.int64))])  # [2, 20, 3, 4]
+    tr = b.op("Transpose", [sl], perm=[0, 2, 3, 1])                         # NHWC like the face heads
+    # shape arithmetic: reshape to [N, -1, 4] via Shape -> Gather -> Unsqueeze -> Concat
+    shp = b.op("Shape", [tr])
+    n0 = b.op("Gather", [shp, b.const(np.array(0, np.int64))], axis=0)
+    n0 = b.op("Unsqueeze", [n0, b.const(np.array([0], np.int64))])
+    tgt = b.op("Concat", [n0, b.const(np.array([-1, 4], np.int64))], axis=0)
+    rs = b.op("Reshape", [tr, tgt])                                         # [2, 60, 4]
+    smx = b.op("Softmax", [rs], axis=-1)
+    up = b.op("Resize", [x, "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+              coordinate_transformation_mode="half_pixel")                  # [2, 8, 24, 32]
+    upn = b.op("Resize", [x, "", "", b.const(np.array([2, 8, 18, 24], np.int64))], mode="nearest",
+               coordinate_transformation_mode="asymmetric", nearest_mode="floor")
+    upa = b.op("Resize", [x, "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+               coordinate_transformation_mode="align_corners")
+    inn = b.op("InstanceNormalization", [up, b.const(b.rng.random(8).astype(np.float32) + 0.5),
+                                         b.const(b.rng.standard_normal(8).astype(np.float32))], epsilon=1e-5)
+    gap = b.op("GlobalAveragePool", [x])                                    # [2, 8, 1, 1]
+    fl = b.op("Flatten", [gap], axis=1)                                     # [2, 8]
+    gm = b.op("Gemm", [fl, b.w(12, 8), b.w(12, scale=0.1)], transB=1)      # [2, 12]
+    mm = b.op("MatMul", [gm, b.w(12, 5)])                                   # [2, 5]
+    sq = b.op("Unsqueeze", [mm, b.const(np.array([1], np.int64))])          # [2, 1, 5]
+    sq = b.op("Squeeze", [sq, b.const(np.array([1], np.int64))])            # [2, 5]
+    return b.model([("x", [2, 8, 12, 16])],
+                   [(smx, [2, 60, 4]), (inn, [2, 8, 24, 32]), (upn, [2, 8, 18, 24]), (upa, [2, 8, 24, 32]),
+                    (sq, [2, 5])])
+
+
+def modnet_like(h=64, w=96):
+    """A small MODNet-shaped matting net (see module docstring)."""
+    b = Builder(3)
+    x = "input"
+    s = b.op("Clip", [b.conv(x, 3, 16, 3, stride=2), b.const(np.array(0, np.float32)), b.const(np.array(6, np.float32))])
+
+    def ir(t, cin, cout, stride, e=4):
+        hdn = b.op("Clip", [b.conv(t, cin, cin * e, 1), b.const(np.array(0, np.float32)),
+                            b.const(np.array(6, np.float32))])
+        d = b.op("Clip", [b.conv(hdn, cin * e, cin * e, 3, stride=stride, group=cin * e),
+                          b.const(np.array(0, np.float32)), b.const(np.array(6, np.float32))])
+        o = b.conv(d, cin * e, cout, 1)
+        return b.op("Add", [o, t]) if stride == 1 and cin == cout else o
+
+    e1 = ir(s, 16, 16, 1)          # /2
+    e2 = ir(e1, 16, 24, 2)         # /4
+    e3 = ir(e2, 24, 24, 1)
+    e4 = ir(e3, 24, 32, 2)         # /8
+    # SE block
+    gp = b.op("GlobalAveragePool", [e4])
+    f = b.op("Flatten", [gp])
+    f = b.op("Relu", [b.op("Gemm", [f, b.w(8, 32), b.w(8, scale=0.1)], transB=1)])
+    f = b.op("Sigmoid", [b.op("Gemm", [f, b.w(32, 8), b.w(32, scale=0.1)], transB=1)])
+    f = b.op("Reshape", [f, b.const(np.array([1, 32, 1, 1], np.int64))])
+    se = b.op("Mul", [e4, f])
+    # IBNorm: half BatchNorm, half InstanceNorm
+    c = b.conv(se, 32, 32, 3)
+    parts = b.op("Split", [c, b.const(np.array([16, 16], np.int64))], n_out=2, axis=1)
+    bn = b.op("BatchNormalization", [parts[0], b.const(b.rng.random(16).astype(np.float32) + 0.5),
+                                     b.const(b.rng.standard_normal(16).astype(np.float32) * 0.1),
+                                     b.const(b.rng.standard_normal(16).astype(np.float32) * 0.1),
+                                     b.const(b.rng.random(16).astype(np.float32) + 0.5)])
+    inn = b.op("InstanceNormalization", [parts[1], b.const(np.ones(16, np.float32)), b.const(np.zeros(16, np.float32))])
+    ib = b.op("Relu", [b.op("Concat", [bn, inn], axis=1)])
+    # decoder
+    u = b.op("Resize", [ib, "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+             coordinate_transformation_mode="half_pixel")                  # /4
+    u = b.op("Relu", [b.conv(b.op("Concat", [u, e3], axis=1), 56, 24, 3)])
+    u = b.op("Resize", [u, "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+             coordinate_transformation_mode="half_pixel")                  # /2
+    u = b.op("Relu", [b.conv(b.op("Concat", [u, e1], axis=1), 40, 16, 3)])
+    u = b.op("Resize", [u, "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+             coordinate_transformation_mode="half_pixel")                  # /1
+    m = b.op("Sigmoid", [b.conv(u, 16, 1, 3)])
+    return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])])
+
+
+MODELS = {"conv_zoo": (conv_zoo, {"x": (1, 3, 64, 80)}), "ops_zoo": (ops_zoo, {"x": (2, 8, 12, 16)}),
+          "modnet_like": (modnet_like, {"input": (1, 3, 64, 96)})}
+
+
+def feeds_for(name, seed=0):
+    rng = np.random.default_rng(100 + seed)
+    return {k: rng.random(s, dtype=np.float32) for k, s in MODELS[name][1].items()}
+
+
+def load_golden(path):
+    """(model bytes, feeds, expected outputs, meta) of a tests/golden/*.npz
+    written by tests/golden/make_onnx_golden.py (the ONNX re-encoded from the
+    stored graph with onnx_ref's writer)."""
+    import json
+    z = np.load(path, allow_pickle=False)
+    meta = json.loads(bytes(z["meta"]).decode())
+    nodes = []
+    for nd in meta["nodes"]:
+        attrs = {}
+        for an, av in nd["attrs"].items():
+            attrs[an] = z[av["tensor"]] if "tensor" in av else av["value"]
+        nodes.append(R.make_node(nd["op"], nd["inputs"], nd["outputs"], **attrs))
+    inits = {n: z[f"init_{k}"] for k, n in enumerate(meta["inits"])}
+    model = R.make_model(nodes, inits, [(n, d, e) for n, e, d in meta["inputs"]],
+                         [(n, [v if isinstance(v, int) else 1 for v in d], e) for n, e, d in meta["outputs"]],
+                         opset=meta["opset"])
+    feeds = {n: z[f"feed_{k}"] for k, n in enumerate(meta["feeds"])}
+    want = {n: z[f"want_{k}"] for k, n in enumerate(meta["expected"])}
+    return model, feeds, want, meta

@@ -1,0 +1,133 @@
+// vso_kernels.h — launch parameter blocks of the ONNX-session kernels
+// (vso_kernels.hip), shared with the session planner (vso_model.hip).
+// float32 NCHW tensors; plain structs passed by value.
+#pragma once
+#include <cstdint>
+
+#include <hip/hip_runtime.h>
+
+namespace vso {
+
+constexpr int kMaxDims = 6;
+
+// Activations fused into the producing kernel's epilogue (and the unary kernel).
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_CLIP = 2, ACT_PRELU = 3, ACT_LEAKY = 4, ACT_SIGMOID = 5, ACT_TANH = 6 };
+
+struct Epilogue {
+  const float* bias;   // [M] or null
+  const float* res;    // residual added before the activation (same layout as y) or null
+  int act;             // Act
+  float a0, a1;        // CLIP lo/hi, LEAKY alpha
+  const float* slope;  // PRELU: per output channel ([M]) or one value (slope_stride 0)
+  int slope_stride;
+};
+
+struct ConvParams {
+  const float* x;  // [N][C][H][W]
+  const float* w;  // [M][Cg][kh][kw]
+  float* y;        // [N][M][Ho][Wo]
+  int N, C, H, W, M, Ho, Wo;
+  int G, Cg, Mg;   // groups, input / output channels per group
+  int kh, kw, sh, sw, dh, dw, pt, pl;
+  Epilogue ep;
+};
+
+enum BinOp : int { BIN_ADD = 0, BIN_SUB = 1, BIN_MUL = 2, BIN_DIV = 3, BIN_PRELU = 4 };
+
+struct BinParams {  // y = a (op) b with numpy broadcasting (strides 0 on broadcast dims)
+  const float* a;
+  const float* b;
+  float* y;
+  long n;
+  int nd;
+  int dims[kMaxDims];
+  long sa[kMaxDims], sb[kMaxDims];
+  int op;
+};
+
+struct UnaryParams {
+  const float* x;
+  float* y;
+  long n;
+  int act;
+  float a0, a1;
+};
+
+// dst[dst_base + sum_d i_d * dst_stride_d] = src[src_base + sum_d c_d * src_stride_d]
+// with c_d = i_d * step_d + start_d, or `fill` when some c_d is outside [0, lim_d):
+// Transpose, Slice, Split, Concat (one launch per input), Pad.
+struct CopyParams {
+  const float* src;
+  float* dst;
+  long n;
+  int nd;
+  int size[kMaxDims];
+  long dst_stride[kMaxDims], src_stride[kMaxDims];
+  int start[kMaxDims], step[kMaxDims], lim[kMaxDims];
+  long dst_base, src_base;
+  float fill;
+};
+
+struct PoolParams {
+  const float* x;
+  float* y;
+  int N, C, H, W, Ho, Wo, kh, kw, sh, sw, dh, dw, pt, pl;
+  int max_mode;           // 1 max, 0 average
+  int count_include_pad;
+};
+
+struct RowParams {  // per-row reductions over `inner` contiguous elements (rows = N*C)
+  const float* x;
+  float* y;
+  long rows, inner;
+  const float* scale;  // InstanceNormalization gamma [C] (rows % C), beta
+  const float* shift;
+  int C;
+  float eps;
+};
+
+struct AffineParams {  // y = x * scale[c] + shift[c] over NC(HW)
+  const float* x;
+  float* y;
+  long n, inner;
+  int C;
+  const float* scale;
+  const float* shift;
+};
+
+// Resize of [N][C][H][W] -> [N][C][Ho][Wo]; ctm: 0 half_pixel, 1 pytorch_half_pixel,
+// 2 align_corners, 3 asymmetric; nearest: 0 round_prefer_floor, 1 round_prefer_ceil, 2 floor, 3 ceil
+struct ResizeParams {
+  const float* x;
+  float* y;
+  int N, C, H, W, Ho, Wo;
+  float sy, sx;  // scales (output / input)
+  int linear, ctm, nearest;
+};
+
+struct GemmParams {  // y[b][m][n] = alpha * sum_k A[b][m][k] B[b][k][n] + beta * c
+  const float* a;
+  const float* b;
+  const float* c;     // broadcast over (m, n) with strides cm, cn (0 = broadcast) or null
+  float* y;
+  int batch, M, N, K;
+  long sab, sam, sak;  // A strides (batch, m, k)
+  long sbb, sbk, sbn;  // B strides
+  long scm, scn;
+  float alpha, beta;
+  Epilogue ep;         // act only
+};
+
+void launch_conv(const ConvParams& p, hipStream_t s, const char** name);
+void launch_binary(const BinParams& p, hipStream_t s);
+void launch_unary(const UnaryParams& p, hipStream_t s);
+void launch_copy(const CopyParams& p, hipStream_t s);
+void launch_pool(const PoolParams& p, hipStream_t s);
+void launch_gap(const RowParams& p, hipStream_t s);
+void launch_inorm(const RowParams& p, hipStream_t s);
+void launch_softmax(const RowParams& p, hipStream_t s);
+void launch_affine(const AffineParams& p, hipStream_t s);
+void launch_resize(const ResizeParams& p, hipStream_t s);
+void launch_gemm(const GemmParams& p, hipStream_t s);
+
+}  // namespace vso

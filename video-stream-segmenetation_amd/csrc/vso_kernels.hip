@@ -1,0 +1,394 @@
+// vso_kernels.hip — gfx950 kernels of the ONNX sessions (include/vso.h):
+// the operators of the reference's ORT models (MODNet, MediaPipe face
+// detector and landmarks; client/src/core/model.ts) on float32 NCHW tensors.
+//
+//   k_conv_gemm : dense / grouped convolution as an implicit GEMM per (image,
+//                 group): D[m][p] = sum_k W[m][k] * X^[k][p], k = (c, ky, kx),
+//                 p = output pixel; 64x64 output tile per workgroup, K in
+//                 steps of 16 staged through LDS (the im2col gather happens in
+//                 the staging loads, never in HBM; the next step's loads are in
+//                 flight while the current one computes), four wave64s each
+//                 running 16 rows x 64 columns on v_mfma_f32_16x16x4_f32;
+//                 bias, residual and activation fused into the epilogue.
+//   k_conv_dw   : depthwise convolution (groups == channels), direct.
+//   the rest    : broadcast binary ops, unary activations, one strided
+//                 gather-copy for Transpose / Slice / Split / Concat / Pad,
+//                 pooling, per-row reductions (GlobalAveragePool,
+//                 InstanceNormalization, Softmax), channel affine
+//                 (BatchNormalization), Resize and a small batched GEMM.
+#include <hip/hip_runtime.h>
+
+#include "vso_kernels.h"
+
+namespace vso {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float act_apply(float v, int act, float a0, float a1, const float* slope, int ch,
+                                           int slope_stride) {
+  switch (act) {
+    case ACT_RELU: return fmaxf(v, 0.f);
+    case ACT_CLIP: return fminf(fmaxf(v, a0), a1);
+    case ACT_PRELU: return v < 0.f ? v * slope[ch * slope_stride] : v;
+    case ACT_LEAKY: return v < 0.f ? v * a0 : v;
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    case ACT_TANH: return tanhf(v);
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float epilogue(const Epilogue& e, float v, int ch, long idx) {
+  if (e.bias) v += e.bias[ch];
+  if (e.res) v += e.res[idx];
+  return act_apply(v, e.act, e.a0, e.a1, e.slope, ch, e.slope_stride);
+}
+
+// ---------------------------------------------------------------------------
+constexpr int BM = 64, BP = 64, BK = 16;
+
+__global__ __launch_bounds__(256) void k_conv_gemm(ConvParams p) {
+  __shared__ float As[BM][BK + 1];
+  __shared__ float Bs[BK][BP + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g4 = lane >> 4;
+  const int P = p.Ho * p.Wo;
+  const int p0 = blockIdx.x * BP, m0 = blockIdx.y * BM;
+  const int n = blockIdx.z / p.G, grp = blockIdx.z % p.G;
+  const int khw = p.kh * p.kw;
+  const int K = p.Cg * khw;
+  const float* xg = p.x + ((long)n * p.C + (long)grp * p.Cg) * p.H * p.W;
+  const float* wg = p.w + (long)grp * p.Mg * K;
+  float ra[4], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = tid + 256 * u;
+      {  // A: weights, row m (output channel), 16 consecutive k
+        const int m = idx >> 4, kk = idx & 15;
+        const int gm = m0 + m, k = k0 + kk;
+        ra[u] = (gm < p.Mg && k < K) ? wg[(long)gm * K + k] : 0.f;
+      }
+      {  // B: the im2col element (k, pixel), gathered from the input
+        const int kk = idx >> 6, pp = idx & 63;
+        const int k = k0 + kk, pix = p0 + pp;
+        float v = 0.f;
+        if (k < K && pix < P) {
+          const int c = k / khw, rem = k - c * khw;
+          const int ky = rem / p.kw, kx = rem - ky * p.kw;
+          const int oy = pix / p.Wo, ox = pix - oy * p.Wo;
+          const int iy = oy * p.sh - p.pt + ky * p.dh, ix = ox * p.sw - p.pl + kx * p.dw;
+          if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) v = xg[((long)c * p.H + iy) * p.W + ix];
+        }
+        rb[u] = v;
+      }
+    }
+  };
+  f4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int k0 = 0; k0 < K; k0 += BK) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = tid + 256 * u;
+      As[idx >> 4][idx & 15] = ra[u];
+      Bs[idx >> 6][idx & 63] = rb[u];
+    }
+    __syncthreads();
+    if (k0 + BK < K) load(k0 + BK);  // next step's loads in flight during this step's MFMAs
+#pragma unroll
+    for (int s = 0; s < BK / 4; ++s) {
+      const float a = As[16 * wave + r][4 * s + g4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[4 * s + g4][16 * j + r], acc[j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // acc[j][v] = D[row 16*wave + 4*g4 + v][column 16*j + r]
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int gm = m0 + 16 * wave + 4 * g4 + v;
+    if (gm >= p.Mg) continue;
+    const int ch = grp * p.Mg + gm;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pix = p0 + 16 * j + r;
+      if (pix < P) {
+        const long o = ((long)n * p.M + ch) * P + pix;
+        p.y[o] = epilogue(p.ep, acc[j][v], ch, o);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_conv_dw(ConvParams p) {
+  const long total = (long)p.N * p.M * p.Ho * p.Wo;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    const int ox = (int)(o % p.Wo);
+    const long t = o / p.Wo;
+    const int oy = (int)(t % p.Ho);
+    const long nc = t / p.Ho;
+    const int ch = (int)(nc % p.M);
+    const float* xc = p.x + nc * p.H * p.W;  // depthwise: input channel = output channel
+    const float* wc = p.w + (long)ch * p.kh * p.kw;
+    float acc = 0.f;
+    for (int ky = 0; ky < p.kh; ++ky) {
+      const int iy = oy * p.sh - p.pt + ky * p.dh;
+      if (iy < 0 || iy >= p.H) continue;
+      for (int kx = 0; kx < p.kw; ++kx) {
+        const int ix = ox * p.sw - p.pl + kx * p.dw;
+        if (ix >= 0 && ix < p.W) acc = __builtin_fmaf(wc[ky * p.kw + kx], xc[(long)iy * p.W + ix], acc);
+      }
+    }
+    p.y[o] = epilogue(p.ep, acc, ch, o);
+  }
+}
+
+static int grid_for(long n) { return (int)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536); }
+
+void launch_conv(const ConvParams& p, hipStream_t s, const char** name) {
+  if (p.G == p.C && p.G == p.M) {
+    const long total = (long)p.N * p.M * p.Ho * p.Wo;
+    hipLaunchKernelGGL(k_conv_dw, dim3(grid_for(total)), dim3(256), 0, s, p);
+    if (name) *name = "vso::k_conv_dw(vso::ConvParams)";
+  } else {
+    const dim3 grid((p.Ho * p.Wo + BP - 1) / BP, (p.Mg + BM - 1) / BM, p.N * p.G);
+    hipLaunchKernelGGL(k_conv_gemm, grid, dim3(256), 0, s, p);
+    if (name) *name = "vso::k_conv_gemm(vso::ConvParams)";
+  }
+}
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void unravel(long i, int nd, const int* dims, int* idx) {
+  for (int d = nd - 1; d >= 0; --d) {
+    idx[d] = (int)(i % dims[d]);
+    i /= dims[d];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_binary(BinParams p) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < p.n; i += (long)gridDim.x * 256) {
+    int idx[kMaxDims];
+    unravel(i, p.nd, p.dims, idx);
+    long oa = 0, ob = 0;
+    for (int d = 0; d < p.nd; ++d) {
+      oa += idx[d] * p.sa[d];
+      ob += idx[d] * p.sb[d];
+    }
+    const float a = p.a[oa], b = p.b[ob];
+    float v;
+    switch (p.op) {
+      case BIN_ADD: v = a + b; break;
+      case BIN_SUB: v = a - b; break;
+      case BIN_MUL: v = a * b; break;
+      case BIN_DIV: v = a / b; break;
+      default: v = a < 0.f ? a * b : a; break;  // PRELU
+    }
+    p.y[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unary(UnaryParams p) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < p.n; i += (long)gridDim.x * 256)
+    p.y[i] = act_apply(p.x[i], p.act, p.a0, p.a1, nullptr, 0, 0);
+}
+
+__global__ __launch_bounds__(256) void k_copy(CopyParams p) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < p.n; i += (long)gridDim.x * 256) {
+    int idx[kMaxDims];
+    unravel(i, p.nd, p.size, idx);
+    long od = p.dst_base, os = p.src_base;
+    bool in = true;
+    for (int d = 0; d < p.nd; ++d) {
+      od += idx[d] * p.dst_stride[d];
+      const int c = idx[d] * p.step[d] + p.start[d];
+      in = in && c >= 0 && c < p.lim[d];
+      os += (long)c * p.src_stride[d];
+    }
+    p.dst[od] = in ? p.src[os] : p.fill;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pool(PoolParams p) {
+  const long total = (long)p.N * p.C * p.Ho * p.Wo;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    const int ox = (int)(o % p.Wo);
+    const long t = o / p.Wo;
+    const int oy = (int)(t % p.Ho);
+    const long nc = t / p.Ho;
+    const float* xc = p.x + nc * p.H * p.W;
+    float m = -INFINITY, s = 0.f;
+    int cnt = 0;
+    for (int ky = 0; ky < p.kh; ++ky) {
+      const int iy = oy * p.sh - p.pt + ky * p.dh;
+      if (iy < 0 || iy >= p.H) continue;
+      for (int kx = 0; kx < p.kw; ++kx) {
+        const int ix = ox * p.sw - p.pl + kx * p.dw;
+        if (ix < 0 || ix >= p.W) continue;
+        const float v = xc[(long)iy * p.W + ix];
+        m = fmaxf(m, v);
+        s += v;
+        ++cnt;
+      }
+    }
+    p.y[o] = p.max_mode ? m : s / (float)(p.count_include_pad ? p.kh * p.kw : (cnt > 0 ? cnt : 1));
+  }
+}
+
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int wave = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[wave] = v;
+  __syncthreads();
+  return sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__device__ __forceinline__ float block_max(float v, float* sh) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  const int wave = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[wave] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+}
+
+__global__ __launch_bounds__(256) void k_gap(RowParams p) {
+  __shared__ float sh[4];
+  const float* x = p.x + (long)blockIdx.x * p.inner;
+  float s = 0.f;
+  for (long i = threadIdx.x; i < p.inner; i += 256) s += x[i];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) p.y[blockIdx.x] = s / (float)p.inner;
+}
+
+__global__ __launch_bounds__(256) void k_inorm(RowParams p) {
+  __shared__ float sh[4];
+  const float* x = p.x + (long)blockIdx.x * p.inner;
+  float* y = p.y + (long)blockIdx.x * p.inner;
+  float s = 0.f;
+  for (long i = threadIdx.x; i < p.inner; i += 256) s += x[i];
+  const float mean = block_sum(s, sh) / (float)p.inner;
+  float q = 0.f;
+  for (long i = threadIdx.x; i < p.inner; i += 256) {
+    const float d = x[i] - mean;
+    q += d * d;
+  }
+  const float var = block_sum(q, sh) / (float)p.inner;
+  const int c = (int)(blockIdx.x % p.C);
+  const float sc = p.scale[c] / sqrtf(var + p.eps), sf = p.shift[c];
+  for (long i = threadIdx.x; i < p.inner; i += 256) y[i] = (x[i] - mean) * sc + sf;
+}
+
+__global__ __launch_bounds__(256) void k_softmax(RowParams p) {
+  __shared__ float sh[4];
+  const float* x = p.x + (long)blockIdx.x * p.inner;
+  float* y = p.y + (long)blockIdx.x * p.inner;
+  float m = -INFINITY;
+  for (long i = threadIdx.x; i < p.inner; i += 256) m = fmaxf(m, x[i]);
+  m = block_max(m, sh);
+  float s = 0.f;
+  for (long i = threadIdx.x; i < p.inner; i += 256) s += expf(x[i] - m);
+  s = block_sum(s, sh);
+  for (long i = threadIdx.x; i < p.inner; i += 256) y[i] = expf(x[i] - m) / s;
+}
+
+__global__ __launch_bounds__(256) void k_affine(AffineParams p) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < p.n; i += (long)gridDim.x * 256) {
+    const int c = (int)((i / p.inner) % p.C);
+    p.y[i] = p.x[i] * p.scale[c] + p.shift[c];
+  }
+}
+
+__device__ __forceinline__ float resize_src(int o, float scale, int in, int out, int ctm) {
+  switch (ctm) {
+    case 0: return ((float)o + 0.5f) / scale - 0.5f;
+    case 1: return out > 1 ? ((float)o + 0.5f) / scale - 0.5f : 0.f;
+    case 2: return out > 1 ? (float)o * (float)(in - 1) / (float)(out - 1) : 0.f;
+    default: return (float)o / scale;
+  }
+}
+
+__device__ __forceinline__ int nearest_idx(float v, int mode, int in) {
+  float r;
+  if (mode == 0) r = (v == floorf(v) + 0.5f) ? floorf(v) : rintf(v);        // round_prefer_floor
+  else if (mode == 1) r = floorf(v + 0.5f);                                   // round_prefer_ceil
+  else if (mode == 2) r = floorf(v);
+  else r = ceilf(v);
+  const int i = (int)r;
+  return i < 0 ? 0 : (i > in - 1 ? in - 1 : i);
+}
+
+__global__ __launch_bounds__(256) void k_resize(ResizeParams p) {
+  const long total = (long)p.N * p.C * p.Ho * p.Wo;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    const int ox = (int)(o % p.Wo);
+    const long t = o / p.Wo;
+    const int oy = (int)(t % p.Ho);
+    const long nc = t / p.Ho;
+    const float* xc = p.x + nc * p.H * p.W;
+    const float fy = resize_src(oy, p.sy, p.H, p.Ho, p.ctm), fx = resize_src(ox, p.sx, p.W, p.Wo, p.ctm);
+    if (!p.linear) {
+      p.y[o] = xc[(long)nearest_idx(fy, p.nearest, p.H) * p.W + nearest_idx(fx, p.nearest, p.W)];
+    } else {
+      const float sy = fminf(fmaxf(fy, 0.f), (float)(p.H - 1)), sx = fminf(fmaxf(fx, 0.f), (float)(p.W - 1));
+      const int y0 = (int)sy, x0 = (int)sx;
+      const int y1 = min(y0 + 1, p.H - 1), x1 = min(x0 + 1, p.W - 1);
+      const float ly = sy - (float)y0, lx = sx - (float)x0;
+      const float v00 = xc[(long)y0 * p.W + x0], v01 = xc[(long)y0 * p.W + x1];
+      const float v10 = xc[(long)y1 * p.W + x0], v11 = xc[(long)y1 * p.W + x1];
+      p.y[o] = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gemm(GemmParams p) {
+  const long total = (long)p.batch * p.M * p.N;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    const int nn = (int)(o % p.N);
+    const long t = o / p.N;
+    const int m = (int)(t % p.M);
+    const int b = (int)(t / p.M);
+    const float* a = p.a + b * p.sab + m * p.sam;
+    const float* bb = p.b + b * p.sbb + nn * p.sbn;
+    float acc = 0.f;
+    for (int k = 0; k < p.K; ++k) acc = __builtin_fmaf(a[k * p.sak], bb[k * p.sbk], acc);
+    float v = p.alpha * acc;
+    if (p.c) v += p.beta * p.c[m * p.scm + nn * p.scn];
+    p.y[o] = act_apply(v, p.ep.act, p.ep.a0, p.ep.a1, p.ep.slope, nn, p.ep.slope_stride);
+  }
+}
+
+void launch_binary(const BinParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_binary, dim3(grid_for(p.n)), dim3(256), 0, s, p);
+}
+void launch_unary(const UnaryParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_unary, dim3(grid_for(p.n)), dim3(256), 0, s, p);
+}
+void launch_copy(const CopyParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_copy, dim3(grid_for(p.n)), dim3(256), 0, s, p);
+}
+void launch_pool(const PoolParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_pool, dim3(grid_for((long)p.N * p.C * p.Ho * p.Wo)), dim3(256), 0, s, p);
+}
+void launch_gap(const RowParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_gap, dim3((unsigned)p.rows), dim3(256), 0, s, p);
+}
+void launch_inorm(const RowParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_inorm, dim3((unsigned)p.rows), dim3(256), 0, s, p);
+}
+void launch_softmax(const RowParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_softmax, dim3((unsigned)p.rows), dim3(256), 0, s, p);
+}
+void launch_affine(const AffineParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_affine, dim3(grid_for(p.n)), dim3(256), 0, s, p);
+}
+void launch_resize(const ResizeParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_resize, dim3(grid_for((long)p.N * p.C * p.Ho * p.Wo)), dim3(256), 0, s, p);
+}
+void launch_gemm(const GemmParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_gemm, dim3(grid_for((long)p.batch * p.M * p.N)), dim3(256), 0, s, p);
+}
+
+}  // namespace vso

@@ -1,0 +1,1505 @@
+// vso_model.hip — ONNX sessions (include/vso.h): protobuf reader, shape
+// inference and constant folding at create, a fixed launch list over
+// preallocated HBM tensors at run time (captured once in a hipGraph).
+//
+// What it replaces: onnxruntime-web's InferenceSession as the reference uses
+// it (client/src/core/model.ts:12-67; session.run at frameProcessorTest.ts:91,
+// :406, :478), through the same kind of entry points as ORT-web's wasm
+// exports (_OrtCreateSession / _OrtRun / _OrtGetLastError,
+// client/public/ort-wasm-simd-threaded.mjs:50-53).
+//
+// Planning rules:
+//  * every shape is static once input 0's shape is fixed; nodes whose inputs
+//    are all constants (the exporters' Shape/Gather/Concat/... arithmetic,
+//    weight reshapes) are evaluated on the host at create;
+//  * Reshape / Flatten / Squeeze / Unsqueeze / Identity alias their input;
+//  * Conv absorbs a following BatchNormalization (weights folded), residual
+//    Add and activation (Relu, Clip, PRelu, LeakyRelu, Sigmoid, Tanh) into
+//    one launch when each intermediate has exactly one consumer;
+//  * every other runtime node is one launch (vso_kernels.hip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/vso.h"
+#include "vso_kernels.h"
+
+using namespace vso;
+
+namespace {
+
+thread_local std::string g_err;
+
+enum { DT_FLOAT = 1, DT_UINT8 = 2, DT_INT8 = 3, DT_INT32 = 6, DT_INT64 = 7, DT_BOOL = 9, DT_FLOAT16 = 10,
+       DT_DOUBLE = 11 };
+
+// ---- protobuf wire format ---------------------------------------------------
+struct PB {
+  const uint8_t* p;
+  const uint8_t* e;
+  bool bad = false;
+  bool more() const { return !bad && p < e; }
+  uint64_t varint() {
+    uint64_t r = 0;
+    for (int s = 0; s < 64; s += 7) {
+      if (p >= e) { bad = true; return 0; }
+      const uint8_t c = *p++;
+      r |= (uint64_t)(c & 0x7F) << s;
+      if (c < 0x80) return r;
+    }
+    bad = true;
+    return 0;
+  }
+  bool key(uint32_t& f, uint32_t& wt) {
+    const uint64_t k = varint();
+    f = (uint32_t)(k >> 3);
+    wt = (uint32_t)(k & 7);
+    return !bad;
+  }
+  PB sub() {
+    const uint64_t n = varint();
+    if (bad || n > (uint64_t)(e - p)) { bad = true; return PB{e, e}; }
+    PB s{p, p + n};
+    p += n;
+    return s;
+  }
+  uint32_t fixed32() {
+    if (e - p < 4) { bad = true; return 0; }
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    p += 4;
+    return v;
+  }
+  uint64_t fixed64() {
+    if (e - p < 8) { bad = true; return 0; }
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    p += 8;
+    return v;
+  }
+  std::string str() {
+    PB s = sub();
+    return std::string(reinterpret_cast<const char*>(s.p), s.e - s.p);
+  }
+  void skip(uint32_t wt) {
+    if (wt == 0) varint();
+    else if (wt == 1) fixed64();
+    else if (wt == 2) sub();
+    else if (wt == 5) fixed32();
+    else bad = true;
+  }
+};
+
+void read_int64s(PB& pb, uint32_t wt, std::vector<int64_t>& out) {
+  if (wt == 2) {
+    PB s = pb.sub();
+    while (s.more()) out.push_back((int64_t)s.varint());
+    pb.bad |= s.bad;
+  } else {
+    out.push_back((int64_t)pb.varint());
+  }
+}
+
+void read_floats(PB& pb, uint32_t wt, std::vector<float>& out) {
+  if (wt == 2) {
+    PB s = pb.sub();
+    while (s.more()) {
+      const uint32_t u = s.fixed32();
+      float f;
+      std::memcpy(&f, &u, 4);
+      out.push_back(f);
+    }
+    pb.bad |= s.bad;
+  } else {
+    const uint32_t u = pb.fixed32();
+    float f;
+    std::memcpy(&f, &u, 4);
+    out.push_back(f);
+  }
+}
+
+float half_to_float(uint16_t h) {
+  const uint32_t s = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 31, m = h & 1023;
+  uint32_t u;
+  if (e == 0) {
+    if (m == 0) u = s;
+    else {  // subnormal
+      float f = std::ldexp((float)m, -24);
+      std::memcpy(&u, &f, 4);
+      u |= s;
+    }
+  } else if (e == 31) {
+    u = s | 0x7F800000u | (m << 13);
+  } else {
+    u = s | ((e + 112) << 23) | (m << 13);
+  }
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// A constant tensor (initializer / attribute / folded value).
+struct Const {
+  std::vector<int64_t> dims;
+  bool is_int = false;
+  std::vector<float> f;    // float data (also filled for ints, as doubles would be)
+  std::vector<int64_t> i;  // integer data
+  int64_t numel() const {
+    int64_t n = 1;
+    for (int64_t d : dims) n *= d;
+    return n;
+  }
+};
+
+bool parse_tensor(PB pb, std::string* name, Const* c, std::string* err) {
+  int dt = DT_FLOAT;
+  std::string raw;
+  bool has_raw = false;
+  std::vector<float> fl;
+  std::vector<int64_t> i32, i64;
+  std::vector<double> dbl;
+  uint32_t f, wt;
+  while (pb.more() && pb.key(f, wt)) {
+    if (f == 1) read_int64s(pb, wt, c->dims);
+    else if (f == 2) dt = (int)pb.varint();
+    else if (f == 4) read_floats(pb, wt, fl);
+    else if (f == 5) read_int64s(pb, wt, i32);
+    else if (f == 7) read_int64s(pb, wt, i64);
+    else if (f == 8) *name = pb.str();
+    else if (f == 9) { raw = pb.str(); has_raw = true; }
+    else if (f == 10) {
+      if (wt == 2) {
+        PB s = pb.sub();
+        while (s.more()) { const uint64_t u = s.fixed64(); double d; std::memcpy(&d, &u, 8); dbl.push_back(d); }
+      } else { const uint64_t u = pb.fixed64(); double d; std::memcpy(&d, &u, 8); dbl.push_back(d); }
+    } else if (f == 14) {
+      if (pb.varint() == 1) { *err = "external tensor data is not supported"; return false; }
+    } else pb.skip(wt);
+  }
+  if (pb.bad) { *err = "malformed TensorProto"; return false; }
+  const int64_t n = c->numel();
+  auto set_ints = [&](const std::vector<int64_t>& v) {
+    c->is_int = true;
+    c->i = v;
+    c->f.assign(v.begin(), v.end());
+  };
+  switch (dt) {
+    case DT_FLOAT:
+      if (has_raw) { c->f.resize(raw.size() / 4); std::memcpy(c->f.data(), raw.data(), c->f.size() * 4); }
+      else c->f = fl;
+      break;
+    case DT_FLOAT16: {
+      std::vector<uint16_t> h;
+      if (has_raw) { h.resize(raw.size() / 2); std::memcpy(h.data(), raw.data(), h.size() * 2); }
+      else for (int64_t v : i32) h.push_back((uint16_t)v);
+      for (uint16_t v : h) c->f.push_back(half_to_float(v));
+      break;
+    }
+    case DT_DOUBLE:
+      if (has_raw) { dbl.resize(raw.size() / 8); std::memcpy(dbl.data(), raw.data(), dbl.size() * 8); }
+      c->f.assign(dbl.begin(), dbl.end());
+      break;
+    case DT_INT64:
+      if (has_raw) { std::vector<int64_t> v(raw.size() / 8); std::memcpy(v.data(), raw.data(), v.size() * 8); set_ints(v); }
+      else set_ints(i64);
+      break;
+    case DT_INT32: case DT_INT8: case DT_UINT8: case DT_BOOL: {
+      std::vector<int64_t> v;
+      if (has_raw) {
+        const size_t es = dt == DT_INT32 ? 4 : 1;
+        for (size_t k = 0; k + es <= raw.size(); k += es) {
+          if (dt == DT_INT32) { int32_t x; std::memcpy(&x, raw.data() + k, 4); v.push_back(x); }
+          else if (dt == DT_INT8) v.push_back((int8_t)raw[k]);
+          else v.push_back((uint8_t)raw[k]);
+        }
+      } else v = i32;
+      set_ints(v);
+      break;
+    }
+    default:
+      *err = "tensor data type " + std::to_string(dt) + " is not supported";
+      return false;
+  }
+  if ((int64_t)c->f.size() != n) { *err = "tensor '" + *name + "' size does not match its dims"; return false; }
+  return true;
+}
+
+struct Attr {
+  bool has_f = false, has_i = false, has_s = false, has_t = false;
+  float f = 0.f;
+  int64_t i = 0;
+  std::string s;
+  std::vector<float> fs;
+  std::vector<int64_t> is;
+  Const t;
+};
+
+struct Node {
+  std::string op, name;
+  std::vector<std::string> in, out;
+  std::map<std::string, Attr> attrs;
+  int64_t ai(const char* k, int64_t d) const {
+    auto it = attrs.find(k);
+    return it != attrs.end() && it->second.has_i ? it->second.i : d;
+  }
+  float af(const char* k, float d) const {
+    auto it = attrs.find(k);
+    return it != attrs.end() && it->second.has_f ? it->second.f : d;
+  }
+  std::string as(const char* k, const char* d) const {
+    auto it = attrs.find(k);
+    return it != attrs.end() && it->second.has_s ? it->second.s : std::string(d);
+  }
+  bool has(const char* k) const { return attrs.count(k) != 0; }
+  std::vector<int64_t> ais(const char* k) const {
+    auto it = attrs.find(k);
+    return it != attrs.end() ? it->second.is : std::vector<int64_t>{};
+  }
+};
+
+bool parse_attr(PB pb, std::string* name, Attr* a, std::string* err) {
+  uint32_t f, wt;
+  while (pb.more() && pb.key(f, wt)) {
+    if (f == 1) *name = pb.str();
+    else if (f == 2) { const uint32_t u = pb.fixed32(); std::memcpy(&a->f, &u, 4); a->has_f = true; }
+    else if (f == 3) { a->i = (int64_t)pb.varint(); a->has_i = true; }
+    else if (f == 4) { a->s = pb.str(); a->has_s = true; }
+    else if (f == 5) { std::string tn; if (!parse_tensor(pb.sub(), &tn, &a->t, err)) return false; a->has_t = true; }
+    else if (f == 7) read_floats(pb, wt, a->fs);
+    else if (f == 8) read_int64s(pb, wt, a->is);
+    else pb.skip(wt);
+  }
+  if (pb.bad) { *err = "malformed AttributeProto"; return false; }
+  return true;
+}
+
+struct IO {
+  std::string name;
+  std::vector<int64_t> dims;  // -1 = symbolic
+};
+
+bool parse_value_info(PB pb, IO* io) {
+  uint32_t f, wt;
+  while (pb.more() && pb.key(f, wt)) {
+    if (f == 1) io->name = pb.str();
+    else if (f == 2) {
+      PB tp = pb.sub();
+      uint32_t f2, w2;
+      while (tp.more() && tp.key(f2, w2)) {
+        if (f2 != 1) { tp.skip(w2); continue; }
+        PB tt = tp.sub();
+        uint32_t f3, w3;
+        while (tt.more() && tt.key(f3, w3)) {
+          if (f3 != 2) { tt.skip(w3); continue; }
+          PB sh = tt.sub();
+          uint32_t f4, w4;
+          while (sh.more() && sh.key(f4, w4)) {
+            if (f4 != 1) { sh.skip(w4); continue; }
+            PB dm = sh.sub();
+            int64_t d = -1;
+            uint32_t f5, w5;
+            while (dm.more() && dm.key(f5, w5)) {
+              if (f5 == 1) d = (int64_t)dm.varint();
+              else dm.skip(w5);
+            }
+            io->dims.push_back(d);
+          }
+        }
+      }
+    } else pb.skip(wt);
+  }
+  return !pb.bad;
+}
+
+struct Graph {
+  std::vector<Node> nodes;
+  std::map<std::string, Const> inits;
+  std::vector<IO> inputs, outputs;
+};
+
+bool parse_model(const uint8_t* data, size_t n, Graph* g, std::string* err) {
+  PB m{data, data + n};
+  uint32_t f, wt;
+  bool have_graph = false;
+  while (m.more() && m.key(f, wt)) {
+    if (f != 7) { m.skip(wt); continue; }
+    have_graph = true;
+    PB gp = m.sub();
+    uint32_t f2, w2;
+    while (gp.more() && gp.key(f2, w2)) {
+      if (f2 == 1) {
+        PB np = gp.sub();
+        Node nd;
+        uint32_t f3, w3;
+        while (np.more() && np.key(f3, w3)) {
+          if (f3 == 1) nd.in.push_back(np.str());
+          else if (f3 == 2) nd.out.push_back(np.str());
+          else if (f3 == 3) nd.name = np.str();
+          else if (f3 == 4) nd.op = np.str();
+          else if (f3 == 5) {
+            std::string an;
+            Attr a;
+            if (!parse_attr(np.sub(), &an, &a, err)) return false;
+            nd.attrs[an] = a;
+          } else np.skip(w3);
+        }
+        if (np.bad) { *err = "malformed NodeProto"; return false; }
+        g->nodes.push_back(nd);
+      } else if (f2 == 5) {
+        std::string tn;
+        Const c;
+        if (!parse_tensor(gp.sub(), &tn, &c, err)) return false;
+        g->inits[tn] = c;
+      } else if (f2 == 11 || f2 == 12) {
+        IO io;
+        if (!parse_value_info(gp.sub(), &io)) { *err = "malformed ValueInfoProto"; return false; }
+        (f2 == 11 ? g->inputs : g->outputs).push_back(io);
+      } else gp.skip(w2);
+    }
+    if (gp.bad) { *err = "malformed GraphProto"; return false; }
+  }
+  if (m.bad || !have_graph) { *err = "not an ONNX ModelProto (no graph)"; return false; }
+  // graph inputs that are initializers are constants, not feeds
+  std::vector<IO> feeds;
+  for (const IO& io : g->inputs)
+    if (!g->inits.count(io.name)) feeds.push_back(io);
+  g->inputs = feeds;
+  return true;
+}
+
+}  // namespace
+
+// ---- the session -----------------------------------------------------------
+struct Value {
+  std::vector<int64_t> shape;
+  bool is_const = false;
+  Const c;          // when is_const
+  int buf = -1;     // runtime tensor: device buffer id
+  int64_t numel() const {
+    int64_t n = 1;
+    for (int64_t d : shape) n *= d;
+    return n;
+  }
+};
+
+struct Launch {
+  std::string name;
+  std::function<void(hipStream_t)> fn;
+};
+
+struct vso_session {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::vector<std::string> in_names, out_names;
+  std::vector<std::vector<int64_t>> in_shapes, out_shapes;
+  std::vector<float*> bufs;
+  std::vector<int64_t> buf_elems;
+  std::vector<int> in_bufs, out_bufs;
+  std::vector<void*> allocs;
+  std::vector<Launch> launches;
+  hipGraphExec_t graph = nullptr;
+  std::atomic<int> busy{0};
+};
+
+namespace {
+
+struct Planner {
+  vso_session* s;
+  Graph& g;
+  std::map<std::string, Value> vals;
+  std::map<std::string, int> consumers;
+  std::set<size_t> done;  // node indices absorbed by a fused launch
+  std::map<const void*, float*> dev_consts;
+  std::string err;
+
+  bool fail(const std::string& m) {
+    err = m;
+    return false;
+  }
+
+  template <class T>
+  bool dalloc(T** p, size_t bytes) {
+    void* q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(bytes, 16)) != hipSuccess) return fail("hipMalloc failed");
+    s->allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return true;
+  }
+
+  int new_buf(int64_t elems) {
+    float* d = nullptr;
+    if (!dalloc(&d, (size_t)std::max<int64_t>(elems, 1) * 4)) return -1;
+    s->bufs.push_back(d);
+    s->buf_elems.push_back(elems);
+    return (int)s->bufs.size() - 1;
+  }
+
+  // device copy of a constant's float data (cached per Const)
+  const float* upload(const Const& c) {
+    auto it = dev_consts.find(&c);
+    if (it != dev_consts.end()) return it->second;
+    float* d = nullptr;
+    if (!dalloc(&d, c.f.size() * 4)) return nullptr;
+    if (!c.f.empty() && hipMemcpy(d, c.f.data(), c.f.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      fail("constant upload failed");
+      return nullptr;
+    }
+    dev_consts[&c] = d;
+    return d;
+  }
+  const float* upload_vec(const std::vector<float>& v) {
+    float* d = nullptr;
+    if (!dalloc(&d, v.size() * 4)) return nullptr;
+    if (!v.empty() && hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      fail("constant upload failed");
+      return nullptr;
+    }
+    return d;
+  }
+
+  Value* val(const std::string& n) {
+    if (n.empty()) return nullptr;
+    auto it = vals.find(n);
+    return it == vals.end() ? nullptr : &it->second;
+  }
+  float* dptr(const Value& v) { return s->bufs[v.buf]; }
+  // a runtime pointer for an operand: its buffer, or its uploaded constant
+  const float* operand(Value& v) { return v.is_const ? upload(v.c) : s->bufs[v.buf]; }
+
+  bool set_runtime(const std::string& name, const std::vector<int64_t>& shape, int alias = -1) {
+    Value v;
+    v.shape = shape;
+    v.buf = alias >= 0 ? alias : new_buf(v.numel());
+    if (v.buf < 0) return false;
+    vals[name] = v;
+    return true;
+  }
+  void set_const(const std::string& name, const Const& c) {
+    Value v;
+    v.is_const = true;
+    v.c = c;
+    v.shape = c.dims;
+    vals[name] = v;
+  }
+
+  void add(const char* name, std::function<void(hipStream_t)> fn) { s->launches.push_back(Launch{name, fn}); }
+
+  // ---- constant folding (host) ---------------------------------------------
+  bool fold(const Node& nd, std::vector<Value*>& in) {
+    const std::string& op = nd.op;
+    Const r;
+    auto ints = [](const Const& c) { return c.is_int ? c.i : std::vector<int64_t>(c.f.begin(), c.f.end()); };
+    if (op == "Constant") {
+      auto it = nd.attrs.find("value");
+      if (it != nd.attrs.end() && it->second.has_t) r = it->second.t;
+      else if (nd.has("value_float")) { r.f = {nd.af("value_float", 0)}; }
+      else if (nd.has("value_int")) { r.is_int = true; r.i = {nd.ai("value_int", 0)}; r.f = {(float)r.i[0]}; }
+      else if (nd.has("value_ints")) { r.is_int = true; r.i = nd.ais("value_ints"); r.dims = {(int64_t)r.i.size()}; r.f.assign(r.i.begin(), r.i.end()); }
+      else if (nd.has("value_floats")) { r.f = nd.attrs.at("value_floats").fs; r.dims = {(int64_t)r.f.size()}; }
+      else return fail("Constant without a supported value");
+    } else if (op == "Shape") {
+      r.is_int = true;
+      r.i = in[0]->shape;
+      int64_t st = nd.ai("start", 0), en = nd.ai("end", (int64_t)r.i.size());
+      const int64_t rk = (int64_t)r.i.size();
+      if (st < 0) st += rk;
+      if (en < 0) en += rk;
+      st = std::clamp<int64_t>(st, 0, rk);
+      en = std::clamp<int64_t>(en, 0, rk);
+      r.i = std::vector<int64_t>(r.i.begin() + st, r.i.begin() + std::max(st, en));
+      r.dims = {(int64_t)r.i.size()};
+      r.f.assign(r.i.begin(), r.i.end());
+    } else if (op == "ConstantOfShape") {
+      r.dims = ints(in[0]->c);
+      float v = 0.f;
+      bool is_int = false;
+      auto it = nd.attrs.find("value");
+      if (it != nd.attrs.end() && it->second.has_t && !it->second.t.f.empty()) {
+        v = it->second.t.f[0];
+        is_int = it->second.t.is_int;
+      }
+      r.is_int = is_int;
+      r.f.assign((size_t)r.numel(), v);
+      if (is_int) r.i.assign((size_t)r.numel(), (int64_t)v);
+    } else if (op == "Identity" || op == "Cast" || op == "Floor" || op == "Ceil") {
+      r = in[0]->c;
+      if (op == "Cast") {
+        const int64_t to = nd.ai("to", DT_FLOAT);
+        const bool to_int = to == DT_INT64 || to == DT_INT32 || to == DT_INT8 || to == DT_UINT8 || to == DT_BOOL;
+        if (to_int && !r.is_int) { r.i.clear(); for (float x : r.f) r.i.push_back((int64_t)x); }
+        r.is_int = to_int;
+      } else if (op == "Floor" || op == "Ceil") {
+        for (float& x : r.f) x = op == "Floor" ? std::floor(x) : std::ceil(x);
+      }
+    } else if (op == "Add" || op == "Sub" || op == "Mul" || op == "Div") {
+      const Const &a = in[0]->c, &b = in[1]->c;
+      const bool both_int = a.is_int && b.is_int;
+      // broadcasting on small constant tensors
+      const size_t ra = a.dims.size(), rb = b.dims.size(), rk = std::max(ra, rb);
+      r.dims.assign(rk, 1);
+      for (size_t d = 0; d < rk; ++d) {
+        const int64_t da = d + ra >= rk ? a.dims[d + ra - rk] : 1, db = d + rb >= rk ? b.dims[d + rb - rk] : 1;
+        if (da != db && da != 1 && db != 1) return fail(nd.op + ": incompatible constant shapes");
+        r.dims[d] = std::max(da, db);
+      }
+      const int64_t n = r.numel();
+      r.is_int = both_int;
+      for (int64_t k = 0; k < n; ++k) {
+        int64_t ka = 0, kb = 0, rem = k, sa = 1, sb = 1;
+        for (int d = (int)rk - 1; d >= 0; --d) {
+          const int64_t id = rem % r.dims[d];
+          rem /= r.dims[d];
+          const int64_t da = d + (int)ra >= (int)rk ? a.dims[d + ra - rk] : 1;
+          const int64_t db = d + (int)rb >= (int)rk ? b.dims[d + rb - rk] : 1;
+          if (da > 1) ka += id * sa;
+          if (db > 1) kb += id * sb;
+          sa *= da;
+          sb *= db;
+        }
+        if (both_int) {
+          const int64_t x = a.i[ka], y = b.i[kb];
+          int64_t v = op == "Add" ? x + y : op == "Sub" ? x - y : op == "Mul" ? x * y
+                                                                       : (y ? (int64_t)std::floor((double)x / y) : 0);
+          r.i.push_back(v);
+          r.f.push_back((float)v);
+        } else {
+          const double x = a.f[ka], y = b.f[kb];
+          r.f.push_back((float)(op == "Add" ? x + y : op == "Sub" ? x - y : op == "Mul" ? x * y : x / y));
+        }
+      }
+    } else if (op == "Gather") {
+      const Const &d = in[0]->c, &ix = in[1]->c;
+      int64_t ax = nd.ai("axis", 0);
+      const int64_t rk = (int64_t)d.dims.size();
+      if (ax < 0) ax += rk;
+      int64_t outer = 1, inner = 1;
+      for (int64_t k = 0; k < ax; ++k) outer *= d.dims[k];
+      for (int64_t k = ax + 1; k < rk; ++k) inner *= d.dims[k];
+      const std::vector<int64_t> idx = ints(ix);
+      for (int64_t k = 0; k < ax; ++k) r.dims.push_back(d.dims[k]);
+      for (int64_t v : ix.dims) r.dims.push_back(v);
+      for (int64_t k = ax + 1; k < rk; ++k) r.dims.push_back(d.dims[k]);
+      r.is_int = d.is_int;
+      for (int64_t o = 0; o < outer; ++o)
+        for (int64_t j : idx) {
+          const int64_t jj = j < 0 ? j + d.dims[ax] : j;
+          for (int64_t q = 0; q < inner; ++q) {
+            const int64_t src = (o * d.dims[ax] + jj) * inner + q;
+            r.f.push_back(d.f[src]);
+            if (d.is_int) r.i.push_back(d.i[src]);
+          }
+        }
+    } else if (op == "Unsqueeze" || op == "Squeeze" || op == "Reshape" || op == "Flatten") {
+      r = in[0]->c;
+      std::vector<int64_t> shp;
+      if (!infer_view(nd, in, &shp)) return false;
+      r.dims = shp;
+    } else if (op == "Concat") {
+      int64_t ax = nd.ai("axis", 0);
+      const int64_t rk = (int64_t)in[0]->c.dims.size();
+      if (ax < 0) ax += rk;
+      r.dims = in[0]->c.dims;
+      r.dims[ax] = 0;
+      bool all_int = true;
+      for (Value* v : in) { r.dims[ax] += v->c.dims[ax]; all_int = all_int && v->c.is_int; }
+      int64_t outer = 1;
+      for (int64_t k = 0; k < ax; ++k) outer *= r.dims[k];
+      r.is_int = all_int;
+      for (int64_t o = 0; o < outer; ++o)
+        for (Value* v : in) {
+          const int64_t blk = v->c.numel() / std::max<int64_t>(outer, 1);
+          for (int64_t q = 0; q < blk; ++q) {
+            r.f.push_back(v->c.f[o * blk + q]);
+            if (all_int) r.i.push_back(v->c.i[o * blk + q]);
+          }
+        }
+    } else if (op == "Slice") {
+      const Const& d = in[0]->c;
+      if (d.dims.size() != 1) return fail("Slice of a constant: rank 1 only");
+      const std::vector<int64_t> st = ints(in[1]->c), en = ints(in[2]->c);
+      const std::vector<int64_t> stp = in.size() > 4 && in[4] ? ints(in[4]->c) : std::vector<int64_t>{1};
+      const int64_t L = d.dims[0];
+      int64_t a = st[0] < 0 ? st[0] + L : st[0], b = en[0] < 0 ? en[0] + L : en[0];
+      const int64_t step = stp[0];
+      a = std::clamp<int64_t>(a, 0, L);
+      b = std::clamp<int64_t>(b, step > 0 ? 0 : -1, L);
+      r.is_int = d.is_int;
+      for (int64_t k = a; step > 0 ? k < b : k > b; k += step) {
+        r.f.push_back(d.f[k]);
+        if (d.is_int) r.i.push_back(d.i[k]);
+      }
+      r.dims = {(int64_t)r.f.size()};
+    } else if (op == "Transpose") {
+      const Const& d = in[0]->c;
+      std::vector<int64_t> perm = nd.ais("perm");
+      const size_t rk = d.dims.size();
+      if (perm.empty()) for (size_t k = 0; k < rk; ++k) perm.push_back((int64_t)(rk - 1 - k));
+      r.dims.resize(rk);
+      for (size_t k = 0; k < rk; ++k) r.dims[k] = d.dims[perm[k]];
+      std::vector<int64_t> st(rk, 1);
+      for (int k = (int)rk - 2; k >= 0; --k) st[k] = st[k + 1] * d.dims[k + 1];
+      const int64_t n = r.numel();
+      r.is_int = d.is_int;
+      for (int64_t o = 0; o < n; ++o) {
+        int64_t rem = o, src = 0;
+        for (int k = (int)rk - 1; k >= 0; --k) {
+          src += (rem % r.dims[k]) * st[perm[k]];
+          rem /= r.dims[k];
+        }
+        r.f.push_back(d.f[src]);
+        if (d.is_int) r.i.push_back(d.i[src]);
+      }
+    } else {
+      return fail("cannot evaluate constant " + op + " (node '" + nd.name + "')");
+    }
+    if (r.f.size() != (size_t)r.numel()) return fail("constant " + op + " produced a malformed tensor");
+    set_const(nd.out[0], r);
+    return true;
+  }
+
+  // Output shape of the view ops (Reshape, Flatten, Squeeze, Unsqueeze).
+  bool infer_view(const Node& nd, std::vector<Value*>& in, std::vector<int64_t>* out) {
+    const std::vector<int64_t>& x = in[0]->shape;
+    const int64_t rk = (int64_t)x.size();
+    auto axes_of = [&](int64_t out_rank) -> std::vector<int64_t> {
+      std::vector<int64_t> a = nd.ais("axes");
+      if (a.empty() && in.size() > 1 && in[1]) {
+        const Const& c = in[1]->c;
+        a = c.is_int ? c.i : std::vector<int64_t>(c.f.begin(), c.f.end());
+      }
+      for (int64_t& v : a) if (v < 0) v += out_rank;
+      std::sort(a.begin(), a.end());
+      return a;
+    };
+    if (nd.op == "Reshape") {
+      if (in.size() < 2 || !in[1] || !in[1]->is_const) return fail("Reshape needs a constant shape");
+      const Const& c = in[1]->c;
+      std::vector<int64_t> shp = c.is_int ? c.i : std::vector<int64_t>(c.f.begin(), c.f.end());
+      const bool allowzero = nd.ai("allowzero", 0) != 0;
+      int64_t known = 1, neg = -1;
+      for (size_t k = 0; k < shp.size(); ++k) {
+        if (shp[k] == 0 && !allowzero) shp[k] = k < x.size() ? x[k] : 1;
+        if (shp[k] == -1) neg = (int64_t)k;
+        else known *= shp[k];
+      }
+      int64_t total = 1;
+      for (int64_t d : x) total *= d;
+      if (neg >= 0) shp[neg] = known ? total / known : 0;
+      *out = shp;
+    } else if (nd.op == "Flatten") {
+      int64_t ax = nd.ai("axis", 1);
+      if (ax < 0) ax += rk;
+      int64_t a = 1, b = 1;
+      for (int64_t k = 0; k < rk; ++k) (k < ax ? a : b) *= x[k];
+      *out = {a, b};
+    } else if (nd.op == "Squeeze") {
+      std::vector<int64_t> axes = axes_of(rk);
+      out->clear();
+      for (int64_t k = 0; k < rk; ++k) {
+        const bool drop = axes.empty() ? x[k] == 1 : std::binary_search(axes.begin(), axes.end(), k);
+        if (!drop) out->push_back(x[k]);
+      }
+    } else {  // Unsqueeze
+      std::vector<int64_t> a0 = nd.ais("axes");
+      if (a0.empty() && in.size() > 1 && in[1]) a0 = in[1]->c.is_int ? in[1]->c.i : std::vector<int64_t>{};
+      const int64_t orank = rk + (int64_t)a0.size();
+      std::vector<int64_t> axes = axes_of(orank);
+      out->clear();
+      size_t j = 0;
+      for (int64_t k = 0; k < orank; ++k) {
+        if (std::binary_search(axes.begin(), axes.end(), k)) out->push_back(1);
+        else out->push_back(x[j++]);
+      }
+    }
+    int64_t a = 1, b = 1;
+    for (int64_t d : x) a *= d;
+    for (int64_t d : *out) b *= d;
+    if (a != b) return fail(nd.op + " '" + nd.name + "': element count changes");
+    return true;
+  }
+
+  // ---- runtime ops ---------------------------------------------------------
+  static bool is_act(const std::string& op) {
+    return op == "Relu" || op == "Clip" || op == "PRelu" || op == "LeakyRelu" || op == "Sigmoid" || op == "Tanh";
+  }
+
+  // the single node consuming `name`, if exactly one and `name` is no graph output
+  int sole_consumer(const std::string& name, size_t after) {
+    if (consumers[name] != 1) return -1;
+    for (const IO& o : g.outputs)
+      if (o.name == name) return -1;
+    for (size_t k = after + 1; k < g.nodes.size(); ++k)
+      for (const std::string& i : g.nodes[k].in)
+        if (i == name) return (int)k;
+    return -1;
+  }
+
+  // activation parameters of an activation node (constants only)
+  bool act_of(const Node& nd, Epilogue* ep, int channels) {
+    if (nd.op == "Relu") ep->act = ACT_RELU;
+    else if (nd.op == "Sigmoid") ep->act = ACT_SIGMOID;
+    else if (nd.op == "Tanh") ep->act = ACT_TANH;
+    else if (nd.op == "LeakyRelu") { ep->act = ACT_LEAKY; ep->a0 = nd.af("alpha", 0.01f); }
+    else if (nd.op == "Clip") {
+      float lo = nd.af("min", -INFINITY), hi = nd.af("max", INFINITY);
+      if (nd.in.size() > 1 && !nd.in[1].empty()) { Value* v = val(nd.in[1]); if (!v || !v->is_const) return false; lo = v->c.f[0]; }
+      if (nd.in.size() > 2 && !nd.in[2].empty()) { Value* v = val(nd.in[2]); if (!v || !v->is_const) return false; hi = v->c.f[0]; }
+      ep->act = ACT_CLIP; ep->a0 = lo; ep->a1 = hi;
+    } else if (nd.op == "PRelu") {
+      Value* sl = val(nd.in[1]);
+      if (!sl || !sl->is_const) return false;
+      const int64_t n = sl->c.numel();
+      if (n != 1 && n != channels) return false;
+      // slope must vary along the channel axis only ([C], [C,1,1], [1,C,1,1], or one value)
+      int nontriv = 0;
+      for (int64_t d : sl->c.dims) nontriv += d > 1;
+      if (nontriv > 1) return false;
+      ep->act = ACT_PRELU;
+      ep->slope = upload(sl->c);
+      ep->slope_stride = n == 1 ? 0 : 1;
+    } else return false;
+    return true;
+  }
+
+  bool plan_conv(size_t ni) {
+    const Node& nd = g.nodes[ni];
+    Value* x = val(nd.in[0]);
+    Value* w = val(nd.in[1]);
+    Value* b = nd.in.size() > 2 ? val(nd.in[2]) : nullptr;
+    if (!w || !w->is_const) return fail("Conv '" + nd.name + "': weights must be constant");
+    if (x->shape.size() != 4 || w->c.dims.size() != 4) return fail("Conv '" + nd.name + "': 2D only");
+    ConvParams p{};
+    p.N = (int)x->shape[0]; p.C = (int)x->shape[1]; p.H = (int)x->shape[2]; p.W = (int)x->shape[3];
+    p.M = (int)w->c.dims[0]; p.Cg = (int)w->c.dims[1]; p.kh = (int)w->c.dims[2]; p.kw = (int)w->c.dims[3];
+    p.G = (int)nd.ai("group", 1);
+    if (p.G < 1 || p.C != p.Cg * p.G || p.M % p.G) return fail("Conv '" + nd.name + "': channel/group mismatch");
+    p.Mg = p.M / p.G;
+    std::vector<int64_t> st = nd.ais("strides"), dl = nd.ais("dilations"), pd = nd.ais("pads");
+    p.sh = st.size() > 0 ? (int)st[0] : 1; p.sw = st.size() > 1 ? (int)st[1] : 1;
+    p.dh = dl.size() > 0 ? (int)dl[0] : 1; p.dw = dl.size() > 1 ? (int)dl[1] : 1;
+    int pt = pd.size() == 4 ? (int)pd[0] : 0, pl = pd.size() == 4 ? (int)pd[1] : 0;
+    int pb = pd.size() == 4 ? (int)pd[2] : 0, pr = pd.size() == 4 ? (int)pd[3] : 0;
+    const std::string ap = nd.as("auto_pad", "NOTSET");
+    if (ap == "SAME_UPPER" || ap == "SAME_LOWER") {
+      const int in[2] = {p.H, p.W}, k[2] = {p.kh, p.kw}, s2[2] = {p.sh, p.sw}, d2[2] = {p.dh, p.dw};
+      int lo[2], hi[2];
+      for (int d = 0; d < 2; ++d) {
+        const int o = (in[d] + s2[d] - 1) / s2[d];
+        const int tot = std::max((o - 1) * s2[d] + d2[d] * (k[d] - 1) + 1 - in[d], 0);
+        lo[d] = ap == "SAME_UPPER" ? tot / 2 : tot - tot / 2;
+        hi[d] = tot - lo[d];
+      }
+      pt = lo[0]; pl = lo[1]; pb = hi[0]; pr = hi[1];
+    } else if (ap == "VALID") {
+      pt = pl = pb = pr = 0;
+    }
+    p.pt = pt; p.pl = pl;
+    p.Ho = (p.H + pt + pb - p.dh * (p.kh - 1) - 1) / p.sh + 1;
+    p.Wo = (p.W + pl + pr - p.dw * (p.kw - 1) - 1) / p.sw + 1;
+    if (p.Ho < 1 || p.Wo < 1) return fail("Conv '" + nd.name + "': empty output");
+    std::vector<float> wf = w->c.f;
+    std::vector<float> bias(p.M, 0.f);
+    bool has_bias = false;
+    if (b) {
+      if (!b->is_const || b->c.numel() != p.M) return fail("Conv '" + nd.name + "': bias must be constant [M]");
+      bias = b->c.f;
+      has_bias = true;
+    }
+    // absorb BatchNormalization -> residual Add -> activation
+    std::string out = nd.out[0];
+    size_t last = ni;
+    Epilogue ep{};
+    int c1 = sole_consumer(out, last);
+    if (c1 >= 0 && g.nodes[c1].op == "BatchNormalization") {
+      const Node& bn = g.nodes[c1];
+      Value *sc = val(bn.in[1]), *bb = val(bn.in[2]), *mu = val(bn.in[3]), *vr = val(bn.in[4]);
+      if (sc && bb && mu && vr && sc->is_const && bb->is_const && mu->is_const && vr->is_const &&
+          sc->c.numel() == p.M) {
+        const double eps = bn.af("epsilon", 1e-5f);
+        const int64_t per = (int64_t)p.Cg * p.kh * p.kw;
+        for (int m = 0; m < p.M; ++m) {
+          const double a = sc->c.f[m] / std::sqrt((double)vr->c.f[m] + eps);
+          for (int64_t k = 0; k < per; ++k) wf[m * per + k] = (float)(wf[m * per + k] * a);
+          bias[m] = (float)((bias[m] - mu->c.f[m]) * a + bb->c.f[m]);
+        }
+        has_bias = true;
+        done.insert((size_t)c1);
+        out = bn.out[0];
+        last = (size_t)c1;
+        c1 = sole_consumer(out, last);
+      }
+    }
+    const std::vector<int64_t> oshape = {p.N, p.M, p.Ho, p.Wo};
+    if (c1 >= 0 && g.nodes[c1].op == "Add") {
+      const Node& ad = g.nodes[c1];
+      const std::string& other = ad.in[0] == out ? ad.in[1] : ad.in[0];
+      Value* o = val(other);
+      if (o && !o->is_const && o->shape == oshape && ad.in[0] != ad.in[1]) {
+        ep.res = dptr(*o);
+        done.insert((size_t)c1);
+        out = ad.out[0];
+        last = (size_t)c1;
+        c1 = sole_consumer(out, last);
+      }
+    }
+    if (c1 >= 0 && is_act(g.nodes[c1].op) && act_of(g.nodes[c1], &ep, p.M)) {
+      done.insert((size_t)c1);
+      out = g.nodes[c1].out[0];
+    }
+    if (!err.empty()) return false;
+    p.w = upload_vec(wf);
+    ep.bias = has_bias ? upload_vec(bias) : nullptr;
+    if (!p.w || (has_bias && !ep.bias)) return false;
+    p.ep = ep;
+    p.x = dptr(*x);
+    if (!set_runtime(out, oshape)) return false;
+    p.y = dptr(vals[out]);
+    const char* kname = (p.G == p.C && p.G == p.M) ? "vso::k_conv_dw(vso::ConvParams)" : "vso::k_conv_gemm(vso::ConvParams)";
+    add(kname, [p](hipStream_t st) { launch_conv(p, st, nullptr); });
+    return true;
+  }
+
+  static void fill_strides(const std::vector<int64_t>& shape, std::vector<int64_t>* st) {
+    st->assign(shape.size(), 1);
+    for (int k = (int)shape.size() - 2; k >= 0; --k) (*st)[k] = (*st)[k + 1] * shape[k + 1];
+  }
+
+  bool plan_binary(const Node& nd, Value* a, Value* b, int op) {
+    const size_t ra = a->shape.size(), rb = b->shape.size(), rk = std::max(ra, rb);
+    if (rk > (size_t)kMaxDims) return fail(nd.op + ": rank > 6");
+    std::vector<int64_t> os(rk);
+    for (size_t d = 0; d < rk; ++d) {
+      const int64_t da = d + ra >= rk ? a->shape[d + ra - rk] : 1, db = d + rb >= rk ? b->shape[d + rb - rk] : 1;
+      if (da != db && da != 1 && db != 1) return fail(nd.op + " '" + nd.name + "': shapes do not broadcast");
+      os[d] = std::max(da, db);
+    }
+    std::vector<int64_t> sta, stb;
+    fill_strides(a->shape, &sta);
+    fill_strides(b->shape, &stb);
+    BinParams p{};
+    p.nd = (int)rk;
+    for (size_t d = 0; d < rk; ++d) {
+      p.dims[d] = (int)os[d];
+      const int64_t da = d + ra >= rk ? a->shape[d + ra - rk] : 1, db = d + rb >= rk ? b->shape[d + rb - rk] : 1;
+      p.sa[d] = da == 1 ? 0 : sta[d + ra - rk];
+      p.sb[d] = db == 1 ? 0 : stb[d + rb - rk];
+    }
+    p.op = op;
+    p.a = operand(*a);
+    p.b = operand(*b);
+    if (!p.a || !p.b) return false;
+    if (!set_runtime(nd.out[0], os)) return false;
+    p.y = dptr(vals[nd.out[0]]);
+    p.n = vals[nd.out[0]].numel();
+    add("vso::k_binary(vso::BinParams)", [p](hipStream_t st) { launch_binary(p, st); });
+    return true;
+  }
+
+  bool plan_copy_into(const float* src, const std::vector<int64_t>& src_shape, float* dst,
+                      const std::vector<int64_t>& dst_shape, const std::vector<int64_t>& iter, const std::vector<int64_t>& dst_off,
+                      const std::vector<int64_t>& src_start, const std::vector<int64_t>& src_step,
+                      const std::vector<int64_t>& src_perm, float fill) {
+    const size_t rk = iter.size();
+    if (rk > (size_t)kMaxDims) return fail("copy: rank > 6");
+    std::vector<int64_t> sst, dst_st;
+    fill_strides(src_shape, &sst);
+    fill_strides(dst_shape, &dst_st);
+    CopyParams p{};
+    p.nd = (int)rk;
+    p.n = 1;
+    long base = 0;
+    for (size_t d = 0; d < rk; ++d) {
+      p.size[d] = (int)iter[d];
+      p.n *= iter[d];
+      p.dst_stride[d] = dst_st[d];
+      base += dst_off[d] * dst_st[d];
+      const int64_t sd = src_perm.empty() ? (int64_t)d : src_perm[d];
+      p.src_stride[d] = sst[sd];
+      p.start[d] = (int)src_start[d];
+      p.step[d] = (int)src_step[d];
+      p.lim[d] = (int)src_shape[sd];
+    }
+    p.dst_base = base;
+    p.src_base = 0;
+    p.src = src;
+    p.dst = dst;
+    p.fill = fill;
+    if (p.n == 0) return true;
+    add("vso::k_copy(vso::CopyParams)", [p](hipStream_t st) { launch_copy(p, st); });
+    return true;
+  }
+
+  bool plan_node(size_t ni) {
+    const Node& nd = g.nodes[ni];
+    const std::string& op = nd.op;
+    std::vector<Value*> in;
+    bool all_const = true;
+    for (const std::string& n : nd.in) {
+      if (n.empty()) { in.push_back(nullptr); continue; }
+      Value* v = val(n);
+      if (!v) return fail("node '" + nd.name + "' (" + op + "): input '" + n + "' is not defined");
+      in.push_back(v);
+      all_const = all_const && v->is_const;
+    }
+    if (op == "Shape" || (all_const && !in.empty() && op != "Conv") || op == "Constant") return fold(nd, in);
+    Value* x = in.empty() ? nullptr : in[0];
+    const std::vector<int64_t>& xs = x->shape;
+    if (op == "Conv") return plan_conv(ni);
+    if (op == "Reshape" || op == "Flatten" || op == "Squeeze" || op == "Unsqueeze") {
+      std::vector<int64_t> shp;
+      if (!infer_view(nd, in, &shp)) return false;
+      return set_runtime(nd.out[0], shp, x->buf);
+    }
+    if (op == "Identity" || op == "Dropout" || op == "Cast") {
+      if (op == "Cast" && nd.ai("to", DT_FLOAT) != DT_FLOAT) return fail("Cast of a runtime tensor to a non-float type");
+      return set_runtime(nd.out[0], xs, x->buf);
+    }
+    if (is_act(op)) {
+      Epilogue ep{};
+      if (op == "PRelu") return plan_binary(nd, x, in[1], BIN_PRELU);
+      if (!act_of(nd, &ep, 0)) return fail(op + " '" + nd.name + "': non-constant parameters");
+      UnaryParams p{};
+      p.x = dptr(*x);
+      p.act = ep.act; p.a0 = ep.a0; p.a1 = ep.a1;
+      if (!set_runtime(nd.out[0], xs)) return false;
+      p.y = dptr(vals[nd.out[0]]);
+      p.n = vals[nd.out[0]].numel();
+      add("vso::k_unary(vso::UnaryParams)", [p](hipStream_t st) { launch_unary(p, st); });
+      return true;
+    }
+    if (op == "Add" || op == "Sub" || op == "Mul" || op == "Div")
+      return plan_binary(nd, in[0], in[1], op == "Add" ? BIN_ADD : op == "Sub" ? BIN_SUB : op == "Mul" ? BIN_MUL : BIN_DIV);
+    if (op == "MaxPool" || op == "AveragePool") {
+      if (xs.size() != 4) return fail(op + ": 2D only");
+      std::vector<int64_t> k = nd.ais("kernel_shape"), st = nd.ais("strides"), dl = nd.ais("dilations"), pd = nd.ais("pads");
+      if (k.size() != 2) return fail(op + ": kernel_shape must be 2D");
+      PoolParams p{};
+      p.N = (int)xs[0]; p.C = (int)xs[1]; p.H = (int)xs[2]; p.W = (int)xs[3];
+      p.kh = (int)k[0]; p.kw = (int)k[1];
+      p.sh = st.size() > 0 ? (int)st[0] : 1; p.sw = st.size() > 1 ? (int)st[1] : 1;
+      p.dh = dl.size() > 0 ? (int)dl[0] : 1; p.dw = dl.size() > 1 ? (int)dl[1] : 1;
+      int pt = pd.size() == 4 ? (int)pd[0] : 0, pl = pd.size() == 4 ? (int)pd[1] : 0;
+      int pb = pd.size() == 4 ? (int)pd[2] : 0, pr = pd.size() == 4 ? (int)pd[3] : 0;
+      const std::string ap = nd.as("auto_pad", "NOTSET");
+      if (ap == "SAME_UPPER" || ap == "SAME_LOWER") {
+        const int inn[2] = {p.H, p.W}, kk[2] = {p.kh, p.kw}, ss[2] = {p.sh, p.sw}, dd[2] = {p.dh, p.dw};
+        int lo[2], hi[2];
+        for (int d = 0; d < 2; ++d) {
+          const int o = (inn[d] + ss[d] - 1) / ss[d];
+          const int tot = std::max((o - 1) * ss[d] + dd[d] * (kk[d] - 1) + 1 - inn[d], 0);
+          lo[d] = ap == "SAME_UPPER" ? tot / 2 : tot - tot / 2;
+          hi[d] = tot - lo[d];
+        }
+        pt = lo[0]; pl = lo[1]; pb = hi[0]; pr = hi[1];
+      }
+      p.pt = pt; p.pl = pl;
+      const bool ceil_mode = nd.ai("ceil_mode", 0) != 0;
+      auto osz = [&](int i, int p0, int p1, int kk, int ss, int dd) {
+        const int num = i + p0 + p1 - dd * (kk - 1) - 1;
+        int o = (ceil_mode ? (num + ss - 1) / ss : num / ss) + 1;
+        if (ceil_mode && (o - 1) * ss >= i + p0) --o;
+        return o;
+      };
+      p.Ho = osz(p.H, pt, pb, p.kh, p.sh, p.dh);
+      p.Wo = osz(p.W, pl, pr, p.kw, p.sw, p.dw);
+      p.max_mode = op == "MaxPool";
+      p.count_include_pad = (int)nd.ai("count_include_pad", 0);
+      p.x = dptr(*x);
+      if (!set_runtime(nd.out[0], {xs[0], xs[1], p.Ho, p.Wo})) return false;
+      p.y = dptr(vals[nd.out[0]]);
+      add("vso::k_pool(vso::PoolParams)", [p](hipStream_t st) { launch_pool(p, st); });
+      return true;
+    }
+    if (op == "GlobalAveragePool") {
+      RowParams p{};
+      p.x = dptr(*x);
+      p.rows = xs[0] * xs[1];
+      p.inner = 1;
+      for (size_t d = 2; d < xs.size(); ++d) p.inner *= xs[d];
+      std::vector<int64_t> os = {xs[0], xs[1]};
+      for (size_t d = 2; d < xs.size(); ++d) os.push_back(1);
+      if (!set_runtime(nd.out[0], os)) return false;
+      p.y = dptr(vals[nd.out[0]]);
+      add("vso::k_gap(vso::RowParams)", [p](hipStream_t st) { launch_gap(p, st); });
+      return true;
+    }
+    if (op == "InstanceNormalization") {
+      if (!in[1]->is_const || !in[2]->is_const) return fail("InstanceNormalization: constant scale/B only");
+      RowParams p{};
+      p.x = dptr(*x);
+      p.rows = xs[0] * xs[1];
+      p.inner = 1;
+      for (size_t d = 2; d < xs.size(); ++d) p.inner *= xs[d];
+      p.C = (int)xs[1];
+      p.eps = nd.af("epsilon", 1e-5f);
+      p.scale = upload(in[1]->c);
+      p.shift = upload(in[2]->c);
+      if (!set_runtime(nd.out[0], xs)) return false;
+      p.y = dptr(vals[nd.out[0]]);
+      add("vso::k_inorm(vso::RowParams)", [p](hipStream_t st) { launch_inorm(p, st); });
+      return true;
+    }
+    if (op == "BatchNormalization") {
+      for (int k = 1; k <= 4; ++k)
+        if (!in[k]->is_const) return fail("BatchNormalization: constant parameters only");
+      const int C = (int)xs[1];
+      std::vector<float> sc(C), sh(C);
+      const double eps = nd.af("epsilon", 1e-5f);
+      for (int c = 0; c < C; ++c) {
+        const double a = in[1]->c.f[c] / std::sqrt((double)in[4]->c.f[c] + eps);
+        sc[c] = (float)a;
+        sh[c] = (float)(in[2]->c.f[c] - in[3]->c.f[c] * a);
+      }
+      AffineParams p{};
+      p.x = dptr(*x);
+      p.C = C;
+      p.inner = 1;
+      for (size_t d = 2; d < xs.size(); ++d) p.inner *= xs[d];
+      p.scale = upload_vec(sc);
+      p.shift = upload_vec(sh);
+      if (!set_runtime(nd.out[0], xs)) return false;
+      p.y = dptr(vals[nd.out[0]]);
+      p.n = vals[nd.out[0]].numel();
+      add("vso::k_affine(vso::AffineParams)", [p](hipStream_t st) { launch_affine(p, st); });
+      return true;
+    }
+    if (op == "Softmax") {
+      int64_t ax = nd.ai("axis", -1);
+      if (ax < 0) ax += (int64_t)xs.size();
+      if (ax != (int64_t)xs.size() - 1) return fail("Softmax: last axis only");
+      RowParams p{};
+      p.x = dptr(*x);
+      p.inner = xs.back();
+      p.rows = x->numel() / std::max<int64_t>(p.inner, 1);
+      if (!set_runtime(nd.out[0], xs)) return false;
+      p.y = dptr(vals[nd.out[0]]);
+      add("vso::k_softmax(vso::RowParams)", [p](hipStream_t st) { launch_softmax(p, st); });
+      return true;
+    }
+    if (op == "Transpose") {
+      std::vector<int64_t> perm = nd.ais("perm");
+      const size_t rk = xs.size();
+      if (perm.empty()) for (size_t k = 0; k < rk; ++k) perm.push_back((int64_t)(rk - 1 - k));
+      std::vector<int64_t> os(rk);
+      for (size_t k = 0; k < rk; ++k) os[k] = xs[perm[k]];
+      if (!set_runtime(nd.out[0], os)) return false;
+      return plan_copy_into(dptr(*x), xs, dptr(vals[nd.out[0]]), os, os, std::vector<int64_t>(rk, 0),
+                            std::vector<int64_t>(rk, 0), std::vector<int64_t>(rk, 1), perm, 0.f);
+    }
+    if (op == "Pad") {
+      const std::string mode = nd.as("mode", "constant");
+      if (mode != "constant") return fail("Pad: constant mode only");
+      std::vector<int64_t> pads = nd.ais("pads");
+      if (in.size() > 1 && in[1]) {
+        if (!in[1]->is_const) return fail("Pad: constant pads only");
+        pads = in[1]->c.is_int ? in[1]->c.i : std::vector<int64_t>(in[1]->c.f.begin(), in[1]->c.f.end());
+      }
+      float value = nd.af("value", 0.f);
+      if (in.size() > 2 && in[2]) {
+        if (!in[2]->is_const) return fail("Pad: constant value only");
+        if (!in[2]->c.f.empty()) value = in[2]->c.f[0];
+      }
+      const size_t rk = xs.size();
+      std::vector<int64_t> axes;
+      if (in.size() > 3 && in[3]) axes = in[3]->c.i;
+      std::vector<int64_t> pb(rk, 0), pe(rk, 0);
+      if (axes.empty()) {
+        if (pads.size() != 2 * rk) return fail("Pad: pads length");
+        for (size_t d = 0; d < rk; ++d) { pb[d] = pads[d]; pe[d] = pads[d + rk]; }
+      } else {
+        for (size_t k = 0; k < axes.size(); ++k) {
+          const int64_t a = axes[k] < 0 ? axes[k] + (int64_t)rk : axes[k];
+          pb[a] = pads[k];
+          pe[a] = pads[k + axes.size()];
+        }
+      }
+      std::vector<int64_t> os(rk), start(rk);
+      for (size_t d = 0; d < rk; ++d) { os[d] = xs[d] + pb[d] + pe[d]; start[d] = -pb[d]; }
+      if (!set_runtime(nd.out[0], os)) return false;
+      return plan_copy_into(dptr(*x), xs, dptr(vals[nd.out[0]]), os, os, std::vector<int64_t>(rk, 0), start,
+                            std::vector<int64_t>(rk, 1), {}, value);
+    }
+    if (op == "Concat") {
+      int64_t ax = nd.ai("axis", 0);
+      const size_t rk = xs.size();
+      if (ax < 0) ax += (int64_t)rk;
+      std::vector<int64_t> os = xs;
+      os[ax] = 0;
+      for (Value* v : in) os[ax] += v->shape[ax];
+      if (!set_runtime(nd.out[0], os)) return false;
+      int64_t off = 0;
+      for (Value* v : in) {
+        std::vector<int64_t> doff(rk, 0);
+        doff[ax] = off;
+        off += v->shape[ax];
+        if (!plan_copy_into(operand(*v), v->shape, dptr(vals[nd.out[0]]), os, v->shape, doff,
+                            std::vector<int64_t>(rk, 0), std::vector<int64_t>(rk, 1), {}, 0.f))
+          return false;
+      }
+      return true;
+    }
+    if (op == "Split") {
+      int64_t ax = nd.ai("axis", 0);
+      const size_t rk = xs.size();
+      if (ax < 0) ax += (int64_t)rk;
+      std::vector<int64_t> sp = nd.ais("split");
+      if (in.size() > 1 && in[1]) sp = in[1]->c.i;
+      const int64_t k = (int64_t)nd.out.size();
+      if (sp.empty()) {
+        const int64_t part = (xs[ax] + k - 1) / k;
+        for (int64_t q = 0; q < k; ++q) sp.push_back(std::min(part, xs[ax] - q * part));
+      }
+      int64_t off = 0;
+      for (int64_t q = 0; q < k; ++q) {
+        std::vector<int64_t> os = xs;
+        os[ax] = sp[q];
+        if (!set_runtime(nd.out[q], os)) return false;
+        std::vector<int64_t> start(rk, 0);
+        start[ax] = off;
+        off += sp[q];
+        if (!plan_copy_into(dptr(*x), xs, dptr(vals[nd.out[q]]), os, os, std::vector<int64_t>(rk, 0), start,
+                            std::vector<int64_t>(rk, 1), {}, 0.f))
+          return false;
+      }
+      return true;
+    }
+    if (op == "Slice") {
+      const size_t rk = xs.size();
+      auto ints = [](Value* v) { return v->c.is_int ? v->c.i : std::vector<int64_t>(v->c.f.begin(), v->c.f.end()); };
+      std::vector<int64_t> st, en, axes, steps;
+      if (in.size() >= 3) {
+        for (size_t k = 1; k < in.size(); ++k)
+          if (in[k] && !in[k]->is_const) return fail("Slice: constant starts/ends/axes/steps only");
+        st = ints(in[1]); en = ints(in[2]);
+        if (in.size() > 3 && in[3]) axes = ints(in[3]);
+        if (in.size() > 4 && in[4]) steps = ints(in[4]);
+      } else {
+        st = nd.ais("starts"); en = nd.ais("ends"); axes = nd.ais("axes");
+      }
+      if (axes.empty()) for (size_t k = 0; k < st.size(); ++k) axes.push_back((int64_t)k);
+      if (steps.empty()) steps.assign(st.size(), 1);
+      std::vector<int64_t> os = xs, start(rk, 0), step(rk, 1);
+      for (size_t k = 0; k < st.size(); ++k) {
+        const int64_t a = axes[k] < 0 ? axes[k] + (int64_t)rk : axes[k];
+        const int64_t L = xs[a], s = steps[k];
+        if (s == 0) return fail("Slice: zero step");
+        int64_t b = st[k] < 0 ? st[k] + L : st[k], e = en[k] < 0 ? en[k] + L : en[k];
+        if (s > 0) { b = std::clamp<int64_t>(b, 0, L); e = std::clamp<int64_t>(e, 0, L); os[a] = std::max<int64_t>(0, (e - b + s - 1) / s); }
+        else { b = std::clamp<int64_t>(b, 0, L - 1); e = std::clamp<int64_t>(e, -1, L - 1); os[a] = std::max<int64_t>(0, (b - e - s - 1) / (-s)); }
+        start[a] = b;
+        step[a] = s;
+      }
+      if (!set_runtime(nd.out[0], os)) return false;
+      return plan_copy_into(dptr(*x), xs, dptr(vals[nd.out[0]]), os, os, std::vector<int64_t>(rk, 0), start, step, {}, 0.f);
+    }
+    if (op == "Resize" || op == "Upsample") {
+      if (xs.size() != 4) return fail(op + ": 4D only");
+      std::vector<float> scales;
+      std::vector<int64_t> sizes;
+      if (op == "Upsample") {
+        if (in.size() > 1 && in[1] && in[1]->is_const) scales = in[1]->c.f;
+        else scales = nd.attrs.count("scales") ? nd.attrs.at("scales").fs : std::vector<float>{};
+      } else {
+        if (in.size() > 2 && in[2]) { if (!in[2]->is_const) return fail("Resize: constant scales only"); scales = in[2]->c.f; }
+        if (in.size() > 3 && in[3]) { if (!in[3]->is_const) return fail("Resize: constant sizes only"); sizes = in[3]->c.i; }
+      }
+      ResizeParams p{};
+      p.N = (int)xs[0]; p.C = (int)xs[1]; p.H = (int)xs[2]; p.W = (int)xs[3];
+      if (!sizes.empty()) {
+        if (sizes.size() != 4 || sizes[0] != xs[0] || sizes[1] != xs[1]) return fail("Resize: N, C must not change");
+        p.Ho = (int)sizes[2]; p.Wo = (int)sizes[3];
+        p.sy = (float)p.Ho / p.H; p.sx = (float)p.Wo / p.W;
+      } else {
+        if (scales.size() != 4 || scales[0] != 1.f || scales[1] != 1.f) return fail("Resize: scales on H, W only");
+        p.sy = scales[2]; p.sx = scales[3];
+        p.Ho = (int)std::floor(p.H * (double)p.sy);
+        p.Wo = (int)std::floor(p.W * (double)p.sx);
+      }
+      const std::string mode = nd.as("mode", "nearest");
+      if (mode != "nearest" && mode != "linear" && mode != "bilinear") return fail("Resize: mode " + mode);
+      p.linear = mode != "nearest";
+      const std::string ctm = nd.as("coordinate_transformation_mode", op == "Upsample" ? "asymmetric" : "half_pixel");
+      if (ctm == "half_pixel") p.ctm = 0;
+      else if (ctm == "pytorch_half_pixel") p.ctm = 1;
+      else if (ctm == "align_corners") p.ctm = 2;
+      else if (ctm == "asymmetric") p.ctm = 3;
+      else return fail("Resize: coordinate_transformation_mode " + ctm);
+      const std::string nm = nd.as("nearest_mode", "round_prefer_floor");
+      p.nearest = nm == "round_prefer_floor" ? 0 : nm == "round_prefer_ceil" ? 1 : nm == "floor" ? 2 : 3;
+      p.x = dptr(*x);
+      if (!set_runtime(nd.out[0], {xs[0], xs[1], p.Ho, p.Wo})) return false;
+      p.y = dptr(vals[nd.out[0]]);
+      add("vso::k_resize(vso::ResizeParams)", [p](hipStream_t st) { launch_resize(p, st); });
+      return true;
+    }
+    if (op == "MatMul" || op == "Gemm") {
+      Value* a = in[0];
+      Value* b = in[1];
+      GemmParams p{};
+      p.alpha = 1.f;
+      p.beta = 1.f;
+      std::vector<int64_t> os;
+      if (op == "Gemm") {
+        if (a->shape.size() != 2 || b->shape.size() != 2) return fail("Gemm: 2D operands");
+        const bool ta = nd.ai("transA", 0) != 0, tb = nd.ai("transB", 0) != 0;
+        p.alpha = nd.af("alpha", 1.f);
+        p.beta = nd.af("beta", 1.f);
+        p.batch = 1;
+        p.M = (int)(ta ? a->shape[1] : a->shape[0]);
+        p.K = (int)(ta ? a->shape[0] : a->shape[1]);
+        p.N = (int)(tb ? b->shape[0] : b->shape[1]);
+        if ((tb ? b->shape[1] : b->shape[0]) != p.K) return fail("Gemm: inner dimensions differ");
+        p.sam = ta ? 1 : p.K; p.sak = ta ? p.M : 1;
+        p.sbk = tb ? 1 : p.N; p.sbn = tb ? p.K : 1;
+        if (in.size() > 2 && in[2]) {
+          Value* c = in[2];
+          const std::vector<int64_t>& cs = c->shape;
+          if (cs.size() == 2) { p.scm = cs[0] == 1 ? 0 : cs[1]; p.scn = cs[1] == 1 ? 0 : 1; }
+          else if (cs.size() == 1) { p.scm = 0; p.scn = cs[0] == 1 ? 0 : 1; }
+          else { p.scm = 0; p.scn = 0; }
+          p.c = operand(*c);
+        }
+        os = {p.M, p.N};
+      } else {
+        const std::vector<int64_t>& as_ = a->shape;
+        const std::vector<int64_t>& bs = b->shape;
+        if (as_.size() < 2 || bs.size() < 2) return fail("MatMul: operands of rank >= 2 only");
+        p.M = (int)as_[as_.size() - 2]; p.K = (int)as_.back(); p.N = (int)bs.back();
+        if (bs[bs.size() - 2] != p.K) return fail("MatMul: inner dimensions differ");
+        int64_t ba = 1, bb = 1;
+        for (size_t d = 0; d + 2 < as_.size(); ++d) ba *= as_[d];
+        for (size_t d = 0; d + 2 < bs.size(); ++d) bb *= bs[d];
+        if (bb != 1 && bb != ba) return fail("MatMul: batch broadcast beyond [B] x [1] not supported");
+        p.batch = (int)ba;
+        p.sab = (int64_t)p.M * p.K; p.sam = p.K; p.sak = 1;
+        p.sbb = bb == 1 ? 0 : (int64_t)p.K * p.N; p.sbk = p.N; p.sbn = 1;
+        os = std::vector<int64_t>(as_.begin(), as_.end() - 2);
+        os.push_back(p.M);
+        os.push_back(p.N);
+      }
+      p.a = operand(*a);
+      p.b = operand(*b);
+      if (!p.a || !p.b) return false;
+      if (!set_runtime(nd.out[0], os)) return false;
+      p.y = dptr(vals[nd.out[0]]);
+      add("vso::k_gemm(vso::GemmParams)", [p](hipStream_t st) { launch_gemm(p, st); });
+      return true;
+    }
+    return fail("unsupported operator " + op + " (node '" + nd.name + "')");
+  }
+
+  bool run(const std::vector<std::vector<int64_t>>& in_shapes) {
+    for (const Node& nd : g.nodes)
+      for (const std::string& i : nd.in)
+        if (!i.empty()) consumers[i]++;
+    for (auto& kv : g.inits) set_const(kv.first, kv.second);
+    for (size_t k = 0; k < g.inputs.size(); ++k) {
+      if (!set_runtime(g.inputs[k].name, in_shapes[k])) return false;
+      s->in_names.push_back(g.inputs[k].name);
+      s->in_shapes.push_back(in_shapes[k]);
+      s->in_bufs.push_back(vals[g.inputs[k].name].buf);
+    }
+    for (size_t k = 0; k < g.nodes.size(); ++k) {
+      if (done.count(k)) continue;
+      if (!plan_node(k)) return false;
+    }
+    for (const IO& o : g.outputs) {
+      Value* v = val(o.name);
+      if (!v) return fail("graph output '" + o.name + "' is never produced");
+      if (v->is_const) {  // a constant output: materialise it once
+        const float* d = upload(v->c);
+        if (!d) return false;
+        const int b = new_buf(v->c.numel());
+        if (b < 0) return false;
+        if (hipMemcpy(s->bufs[b], d, v->c.numel() * 4, hipMemcpyDeviceToDevice) != hipSuccess)
+          return fail("constant output copy failed");
+        v->buf = b;
+      }
+      s->out_names.push_back(o.name);
+      s->out_shapes.push_back(v->shape);
+      s->out_bufs.push_back(v->buf);
+    }
+    return true;
+  }
+};
+
+int fail_s(vso_session* s, int code, const std::string& m) {
+  if (s) s->err = m;
+  else g_err = m;
+  return code;
+}
+
+int64_t numel(const std::vector<int64_t>& v) {
+  int64_t n = 1;
+  for (int64_t d : v) n *= d;
+  return n;
+}
+
+int run_graph(vso_session* s, hipStream_t st) {
+  if (!s->graph) {  // capture the launch list once (buffers are the session's own)
+    hipGraph_t g = nullptr;
+    hipStream_t cs = s->stream;
+    if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess)
+      return fail_s(s, VSO_E_HIP, "hipStreamBeginCapture failed");
+    for (const Launch& l : s->launches) l.fn(cs);
+    const hipError_t e = hipStreamEndCapture(cs, &g);
+    if (e != hipSuccess || !g) return fail_s(s, VSO_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    const hipError_t e2 = hipGraphInstantiate(&s->graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e2 != hipSuccess) return fail_s(s, VSO_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e2));
+  }
+  if (hipGraphLaunch(s->graph, st) != hipSuccess) return fail_s(s, VSO_E_HIP, "hipGraphLaunch failed");
+  return VSO_OK;
+}
+
+struct Busy {
+  vso_session* s;
+  bool ok;
+  explicit Busy(vso_session* ss) : s(ss) {
+    int z = 0;
+    ok = s->busy.compare_exchange_strong(z, 1);
+  }
+  ~Busy() { if (ok) s->busy.store(0); }
+};
+
+}  // namespace
+
+extern "C" {
+
+int vso_create(const void* model, size_t bytes, const int64_t* input_dims, int input_ndim, int device_id,
+               vso_session** out) {
+  if (!model || !bytes || !out) return fail_s(nullptr, VSO_E_INVALID_ARG, "null model/out");
+  *out = nullptr;
+  Graph g;
+  std::string err;
+  if (!parse_model(static_cast<const uint8_t*>(model), bytes, &g, &err)) return fail_s(nullptr, VSO_E_PARSE, err);
+  if (g.inputs.empty()) return fail_s(nullptr, VSO_E_UNSUPPORTED, "model has no runtime inputs");
+  std::vector<std::vector<int64_t>> shapes;
+  for (size_t k = 0; k < g.inputs.size(); ++k) {
+    std::vector<int64_t> d = g.inputs[k].dims;
+    if (k == 0 && input_dims && input_ndim > 0) d.assign(input_dims, input_dims + input_ndim);
+    for (int64_t v : d)
+      if (v < 1) return fail_s(nullptr, VSO_E_INVALID_ARG, "input '" + g.inputs[k].name + "' has symbolic dims: pass input_dims");
+    shapes.push_back(d);
+  }
+  vso_session* s = new vso_session();
+  s->device = device_id;
+  if (hipSetDevice(device_id) != hipSuccess) {
+    delete s;
+    return fail_s(nullptr, VSO_E_HIP, "hipSetDevice failed");
+  }
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete s;
+    return fail_s(nullptr, VSO_E_HIP, "hipStreamCreate failed");
+  }
+  Planner pl{s, g};
+  if (!pl.run(shapes)) {
+    const std::string m = pl.err;
+    const bool unsup = m.find("unsupported") != std::string::npos || m.find("only") != std::string::npos;
+    vso_destroy(s);
+    return fail_s(nullptr, unsup ? VSO_E_UNSUPPORTED : VSO_E_INVALID_ARG, m);
+  }
+  *out = s;
+  return VSO_OK;
+}
+
+void vso_destroy(vso_session* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->graph) (void)hipGraphExecDestroy(s->graph);
+  for (void* p : s->allocs) (void)hipFree(p);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+const char* vso_last_error(const vso_session* s) { return s ? s->err.c_str() : g_err.c_str(); }
+
+int vso_io_count(const vso_session* s, int* n_in, int* n_out) {
+  if (!s) return VSO_E_INVALID_ARG;
+  if (n_in) *n_in = (int)s->in_names.size();
+  if (n_out) *n_out = (int)s->out_names.size();
+  return VSO_OK;
+}
+
+static int copy_name(const std::vector<std::string>& v, int i, char* buf, int cap) {
+  if (i < 0 || i >= (int)v.size() || !buf || cap < 1) return VSO_E_INVALID_ARG;
+  std::snprintf(buf, (size_t)cap, "%s", v[i].c_str());
+  return (int)v[i].size();
+}
+
+static int copy_shape(const std::vector<std::vector<int64_t>>& v, int i, int64_t* dims, int cap) {
+  if (i < 0 || i >= (int)v.size() || !dims) return VSO_E_INVALID_ARG;
+  const int n = (int)v[i].size();
+  for (int k = 0; k < n && k < cap; ++k) dims[k] = v[i][k];
+  return n;
+}
+
+int vso_input_name(const vso_session* s, int i, char* buf, int cap) { return s ? copy_name(s->in_names, i, buf, cap) : VSO_E_INVALID_ARG; }
+int vso_output_name(const vso_session* s, int i, char* buf, int cap) { return s ? copy_name(s->out_names, i, buf, cap) : VSO_E_INVALID_ARG; }
+int vso_input_shape(const vso_session* s, int i, int64_t* dims, int cap) { return s ? copy_shape(s->in_shapes, i, dims, cap) : VSO_E_INVALID_ARG; }
+int vso_output_shape(const vso_session* s, int i, int64_t* dims, int cap) { return s ? copy_shape(s->out_shapes, i, dims, cap) : VSO_E_INVALID_ARG; }
+
+int vso_run(vso_session* s, const float* const* inputs, float* const* outputs) {
+  if (!s) return fail_s(nullptr, VSO_E_INVALID_ARG, "null session");
+  if (!inputs || !outputs) return fail_s(s, VSO_E_INVALID_ARG, "null inputs/outputs");
+  Busy b(s);
+  if (!b.ok) return fail_s(s, VSO_E_INVALID_ARG, "a run is already in flight on this session");
+  if (hipSetDevice(s->device) != hipSuccess) return fail_s(s, VSO_E_HIP, "hipSetDevice failed");
+  for (size_t k = 0; k < s->in_bufs.size(); ++k) {
+    if (!inputs[k]) return fail_s(s, VSO_E_INVALID_ARG, "null input " + std::to_string(k));
+    if (hipMemcpyAsync(s->bufs[s->in_bufs[k]], inputs[k], numel(s->in_shapes[k]) * 4, hipMemcpyHostToDevice,
+                       s->stream) != hipSuccess)
+      return fail_s(s, VSO_E_HIP, "input copy failed");
+  }
+  int rc = run_graph(s, s->stream);
+  if (rc) return rc;
+  for (size_t k = 0; k < s->out_bufs.size(); ++k) {
+    if (!outputs[k]) return fail_s(s, VSO_E_INVALID_ARG, "null output " + std::to_string(k));
+    if (hipMemcpyAsync(outputs[k], s->bufs[s->out_bufs[k]], numel(s->out_shapes[k]) * 4, hipMemcpyDeviceToHost,
+                       s->stream) != hipSuccess)
+      return fail_s(s, VSO_E_HIP, "output copy failed");
+  }
+  if (hipStreamSynchronize(s->stream) != hipSuccess) return fail_s(s, VSO_E_HIP, "run failed");
+  return VSO_OK;
+}
+
+int vso_run_device(vso_session* s, const float* const* d_inputs, float* const* d_outputs, void* stream) {
+  if (!s) return fail_s(nullptr, VSO_E_INVALID_ARG, "null session");
+  if (!d_inputs || !d_outputs) return fail_s(s, VSO_E_INVALID_ARG, "null inputs/outputs");
+  Busy b(s);
+  if (!b.ok) return fail_s(s, VSO_E_INVALID_ARG, "a run is already in flight on this session");
+  if (hipSetDevice(s->device) != hipSuccess) return fail_s(s, VSO_E_HIP, "hipSetDevice failed");
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
+  for (size_t k = 0; k < s->in_bufs.size(); ++k)
+    if (hipMemcpyAsync(s->bufs[s->in_bufs[k]], d_inputs[k], numel(s->in_shapes[k]) * 4, hipMemcpyDeviceToDevice,
+                       st) != hipSuccess)
+      return fail_s(s, VSO_E_HIP, "input copy failed");
+  int rc = run_graph(s, st);
+  if (rc) return rc;
+  for (size_t k = 0; k < s->out_bufs.size(); ++k)
+    if (hipMemcpyAsync(d_outputs[k], s->bufs[s->out_bufs[k]], numel(s->out_shapes[k]) * 4, hipMemcpyDeviceToDevice,
+                       st) != hipSuccess)
+      return fail_s(s, VSO_E_HIP, "output copy failed");
+  return VSO_OK;
+}
+
+int vso_launch_count(const vso_session* s) { return s ? (int)s->launches.size() : VSO_E_INVALID_ARG; }
+
+int vso_launch_name(const vso_session* s, int k, char* buf, int cap) {
+  if (!s || k < 0 || k >= (int)s->launches.size() || !buf || cap < 1) return VSO_E_INVALID_ARG;
+  std::snprintf(buf, (size_t)cap, "%s", s->launches[k].name.c_str());
+  return (int)s->launches[k].name.size();
+}
+
+}  // extern "C"
