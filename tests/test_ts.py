@@ -104,3 +104,66 @@ def test_node_post_chain_matches_oracle_and_python_host(addon_built, pkg, oracle
     # compositing after reset + default config: the RGBA canvases of the same frames
     rgba = np.fromfile(str(op) + "_rgba.u8", np.uint8).reshape(n, h, w, 4)
     assert np.array_equal(rgba, oracle.composite(frames, want_u))
+
+
+def test_node_tensor_and_session_errors(addon_built):
+    """ort.Tensor validates like onnxruntime-web's (float32 only here); a
+    garbage model rejects InferenceSession.create with the vso error code."""
+    script = r"""
+const ort = require(process.argv[1]);
+const r = {};
+try { new ort.Tensor('int64', new BigInt64Array(1), [1]); } catch (e) { r.int64 = e instanceof TypeError; }
+try { new ort.Tensor('float32', new Float32Array(5), [2, 3]); } catch (e) { r.size = e instanceof RangeError; }
+const t = new ort.Tensor('float32', new Float32Array(6), [2, 3]);
+r.tensor = [t.type, t.size, t.dims];
+ort.InferenceSession.create(new Uint8Array([8, 1, 18, 4, 110, 111, 112, 101]), {})
+  .then(() => { r.created = true; }, (e) => { r.createCode = e.code; })
+  .then(() => console.log(JSON.stringify(r)));
+"""
+    out = subprocess.run([NODE, "-e", script, os.path.join(TS, "segment.js")], capture_output=True, text=True,
+                         timeout=60)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["int64"] and r["size"] and r["tensor"] == ["float32", 6, [2, 3]]
+    assert "created" not in r and r["createCode"] in ("-3", "-2")  # VSO_E_PARSE (or VSO_E_HIP with no GPU)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["modnet_like", "mediapipe_face_detector"])
+def test_node_onnx_session_matches_oracle_and_python_host(addon_built, pkg, tmp_path, key):
+    """InferenceSession.create/run from TypeScript == the ONNX oracle (within
+    the 1e-4 relative bar of tests/test_gpu_onnx.py) and == the Python host's
+    session bit for bit; concurrent runs serialise, bad feeds reject."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import onnx_models as M
+    import onnx_ref as R
+    if key == "modnet_like":
+        model = M.modnet_like()
+        feeds = M.feeds_for(key)
+        want = R.run(R.load(model), feeds)
+    else:
+        model, feeds, want, _ = M.load_golden(os.path.join(ROOT, "tests", "golden", key + ".npz"))
+    bad = R.make_model([R.make_node("Einsum", ["x", "x"], ["y"], equation="ij,jk->ik")], {},
+                       [("x", [4, 4])], [("y", [4, 4])])
+    mp, ip, bp = tmp_path / "model.onnx", tmp_path / "inputs.bin", tmp_path / "bad.onnx"
+    mp.write_bytes(model)
+    bp.write_bytes(bad)
+    np.concatenate([np.ascontiguousarray(v, np.float32).ravel() for v in feeds.values()]).tofile(ip)
+    out = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "run_onnx.js"), str(mp), str(ip),
+                          str(tmp_path / "out"), str(bp)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    assert info["inputNames"] == list(feeds) and info["outputNames"] == list(want)
+    assert info["replaySame"] and info["badDimsRejected"] and info["afterReject"] and info["releasedRejects"]
+    assert info["unsupported"]["code"] == "-4" and "Einsum" in info["unsupported"]["message"]
+    from vss_amd import ort as pyort
+    with pyort.InferenceSession(model) as s:
+        py = s.run(feeds)
+    for k, (name, w) in enumerate(want.items()):
+        assert info["outputDims"][k] == list(w.shape) and info["outputTypes"][k] == "float32"
+        got = np.fromfile(tmp_path / f"out_{k}.bin", np.float32).reshape(w.shape)
+        err = float(np.abs(got - w).max())
+        assert err <= 1e-4 * max(1.0, float(np.abs(w).max())), (name, err)
+        assert np.array_equal(got, py[name]), name

@@ -20,6 +20,11 @@
 //       -> Promise<{alpha: Float32Array, alphaU8: Uint8Array}>   (processFrame :78-169)
 //   segmentComposite(handle, post, frames, n, height, width, channels, rowStride)
 //       -> Promise<Uint8Array>   RGBA output canvases, n * height * width * 4 (:78-178)
+//   ortCreate(modelBytes: Uint8Array, inputDims: number[] | null, deviceId) -> session
+//       ONNX sessions (include/vso.h) behind InferenceSession.create (model.ts:14, :38, :61)
+//   ortInfo(session) -> {inputNames, outputNames, inputShapes, outputShapes}
+//   ortRun(session, inputs: Float32Array[]) -> Promise<Float32Array[]>   (session.run)
+//   ortDestroy(session)
 // segment runs vss_segment on a libuv worker thread (napi_create_async_work),
 // so the event loop is not blocked — as `await session.run` does not block.
 #include <node_api.h>
@@ -30,6 +35,7 @@
 #include <string>
 #include <vector>
 
+#include "../../../include/vso.h"
 #include "../../../include/vss.h"
 
 namespace {
@@ -469,6 +475,253 @@ napi_value Segment(napi_env env, napi_callback_info info) { return SegmentImpl(e
 napi_value SegmentPost(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, true); }
 napi_value SegmentComposite(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, true, true); }
 
+// ---- ONNX sessions (include/vso.h) -------------------------------------------
+struct OrtSess {
+  vso_session* s = nullptr;
+  std::vector<std::string> in_names, out_names;
+  std::vector<std::vector<int64_t>> in_shapes, out_shapes;
+};
+
+void finalize_ort(napi_env, void* data, void*) {
+  OrtSess* o = static_cast<OrtSess*>(data);
+  if (o->s) vso_destroy(o->s);
+  delete o;
+}
+
+OrtSess* get_ort(napi_env env, napi_value v) {
+  void* p = nullptr;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, nullptr, "expected an ONNX session");
+    return nullptr;
+  }
+  OrtSess* o = static_cast<OrtSess*>(p);
+  if (!o->s) {
+    napi_throw_error(env, nullptr, "ONNX session already released");
+    return nullptr;
+  }
+  return o;
+}
+
+size_t elem_count(const std::vector<int64_t>& d) {
+  size_t n = 1;
+  for (int64_t v : d) n *= (size_t)v;
+  return n;
+}
+
+napi_value OrtCreate(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  bool is_ta = false;
+  if (argc < 1 || napi_is_typedarray(env, argv[0], &is_ta) != napi_ok || !is_ta) {
+    napi_throw_type_error(env, nullptr, "ortCreate(modelBytes: Uint8Array, inputDims?: number[], deviceId?: number)");
+    return nullptr;
+  }
+  napi_typedarray_type tt;
+  size_t len = 0, off = 0;
+  void* data = nullptr;
+  napi_value buf;
+  NAPI_OK(env, napi_get_typedarray_info(env, argv[0], &tt, &len, &data, &buf, &off));
+  std::vector<int64_t> dims;
+  bool is_arr = false;
+  if (argc >= 2 && napi_is_array(env, argv[1], &is_arr) == napi_ok && is_arr) {
+    uint32_t n = 0;
+    napi_get_array_length(env, argv[1], &n);
+    for (uint32_t k = 0; k < n; ++k) {
+      napi_value e;
+      double d = 0;
+      napi_get_element(env, argv[1], k, &e);
+      napi_get_value_double(env, e, &d);
+      dims.push_back((int64_t)d);
+    }
+  }
+  int device = 0;
+  if (argc >= 3) napi_get_value_int32(env, argv[2], &device);
+  vso_session* s = nullptr;
+  const int rc = vso_create(data, len, dims.empty() ? nullptr : dims.data(), (int)dims.size(), device, &s);
+  if (rc != VSO_OK) {
+    throw_vss(env, "vso_create", rc, vso_last_error(nullptr));
+    return nullptr;
+  }
+  OrtSess* o = new OrtSess();
+  o->s = s;
+  int ni = 0, no = 0;
+  vso_io_count(s, &ni, &no);
+  char name[512];
+  int64_t d[16];
+  for (int k = 0; k < ni; ++k) {
+    vso_input_name(s, k, name, sizeof(name));
+    o->in_names.push_back(name);
+    const int r = vso_input_shape(s, k, d, 16);
+    o->in_shapes.emplace_back(d, d + std::max(0, std::min(r, 16)));
+  }
+  for (int k = 0; k < no; ++k) {
+    vso_output_name(s, k, name, sizeof(name));
+    o->out_names.push_back(name);
+    const int r = vso_output_shape(s, k, d, 16);
+    o->out_shapes.emplace_back(d, d + std::max(0, std::min(r, 16)));
+  }
+  napi_value ext;
+  NAPI_OK(env, napi_create_external(env, o, finalize_ort, nullptr, &ext));
+  return ext;
+}
+
+napi_value names_array(napi_env env, const std::vector<std::string>& v) {
+  napi_value a, e;
+  napi_create_array_with_length(env, v.size(), &a);
+  for (size_t k = 0; k < v.size(); ++k) {
+    napi_create_string_utf8(env, v[k].c_str(), NAPI_AUTO_LENGTH, &e);
+    napi_set_element(env, a, (uint32_t)k, e);
+  }
+  return a;
+}
+
+napi_value shapes_array(napi_env env, const std::vector<std::vector<int64_t>>& v) {
+  napi_value a, row, e;
+  napi_create_array_with_length(env, v.size(), &a);
+  for (size_t k = 0; k < v.size(); ++k) {
+    napi_create_array_with_length(env, v[k].size(), &row);
+    for (size_t j = 0; j < v[k].size(); ++j) {
+      napi_create_double(env, (double)v[k][j], &e);
+      napi_set_element(env, row, (uint32_t)j, e);
+    }
+    napi_set_element(env, a, (uint32_t)k, row);
+  }
+  return a;
+}
+
+napi_value OrtInfo(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  OrtSess* o = argc >= 1 ? get_ort(env, argv[0]) : nullptr;
+  if (!o) return nullptr;
+  napi_value r;
+  NAPI_OK(env, napi_create_object(env, &r));
+  napi_set_named_property(env, r, "inputNames", names_array(env, o->in_names));
+  napi_set_named_property(env, r, "outputNames", names_array(env, o->out_names));
+  napi_set_named_property(env, r, "inputShapes", shapes_array(env, o->in_shapes));
+  napi_set_named_property(env, r, "outputShapes", shapes_array(env, o->out_shapes));
+  return r;
+}
+
+struct OrtWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  vso_session* s = nullptr;
+  std::vector<napi_ref> in_refs, out_refs;  // inputs and output buffers held until done
+  std::vector<const float*> ins;
+  std::vector<float*> outs;
+  std::vector<size_t> out_counts;
+  int rc = 0;
+  std::string err;
+};
+
+void OrtExecute(napi_env, void* data) {  // libuv worker thread: no JS calls here
+  OrtWork* w = static_cast<OrtWork*>(data);
+  w->rc = vso_run(w->s, w->ins.data(), w->outs.data());
+  if (w->rc != VSO_OK) w->err = vso_last_error(w->s);
+}
+
+void OrtComplete(napi_env env, napi_status, void* data) {
+  OrtWork* w = static_cast<OrtWork*>(data);
+  if (w->rc == VSO_OK) {
+    napi_value a;
+    napi_create_array_with_length(env, w->outs.size(), &a);
+    for (size_t k = 0; k < w->outs.size(); ++k) {
+      napi_value ab, ta;
+      napi_get_reference_value(env, w->out_refs[k], &ab);
+      napi_create_typedarray(env, napi_float32_array, w->out_counts[k], ab, 0, &ta);
+      napi_set_element(env, a, (uint32_t)k, ta);
+    }
+    napi_resolve_deferred(env, w->deferred, a);
+  } else {
+    napi_value msg, code, e;
+    const std::string m = "vso_run failed (" + std::to_string(w->rc) + "): " + w->err;
+    napi_create_string_utf8(env, m.c_str(), m.size(), &msg);
+    napi_create_string_utf8(env, std::to_string(w->rc).c_str(), NAPI_AUTO_LENGTH, &code);
+    napi_create_error(env, code, msg, &e);
+    napi_reject_deferred(env, w->deferred, e);
+  }
+  for (napi_ref r : w->in_refs) napi_delete_reference(env, r);
+  for (napi_ref r : w->out_refs) napi_delete_reference(env, r);
+  napi_delete_async_work(env, w->work);
+  delete w;
+}
+
+napi_value OrtRun(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  OrtSess* o = argc >= 1 ? get_ort(env, argv[0]) : nullptr;
+  if (!o) return nullptr;
+  bool is_arr = false;
+  uint32_t n = 0;
+  if (argc < 2 || napi_is_array(env, argv[1], &is_arr) != napi_ok || !is_arr ||
+      napi_get_array_length(env, argv[1], &n) != napi_ok || n != o->in_names.size()) {
+    napi_throw_type_error(env, nullptr, "ortRun(session, inputs: Float32Array[]): one array per model input");
+    return nullptr;
+  }
+  // validate every input before anything is allocated or referenced
+  std::vector<napi_value> elems(n);
+  std::vector<const float*> ptrs(n);
+  for (uint32_t k = 0; k < n; ++k) {
+    napi_value buf;
+    bool ta = false;
+    napi_typedarray_type tt;
+    size_t len = 0, off = 0;
+    void* data = nullptr;
+    napi_get_element(env, argv[1], k, &elems[k]);
+    if (napi_is_typedarray(env, elems[k], &ta) != napi_ok || !ta ||
+        napi_get_typedarray_info(env, elems[k], &tt, &len, &data, &buf, &off) != napi_ok ||
+        tt != napi_float32_array || len != elem_count(o->in_shapes[k])) {
+      const std::string m = "input '" + o->in_names[k] + "' must be a Float32Array of " +
+                            std::to_string(elem_count(o->in_shapes[k])) + " elements";
+      napi_throw_range_error(env, nullptr, m.c_str());
+      return nullptr;
+    }
+    ptrs[k] = static_cast<const float*>(data);
+  }
+  OrtWork* w = new OrtWork();
+  w->s = o->s;
+  w->ins = ptrs;
+  for (uint32_t k = 0; k < n; ++k) {
+    napi_ref r;
+    napi_create_reference(env, elems[k], 1, &r);
+    w->in_refs.push_back(r);
+  }
+  for (size_t k = 0; k < o->out_names.size(); ++k) {
+    const size_t cnt = elem_count(o->out_shapes[k]);
+    napi_value ab;
+    void* out = nullptr;
+    NAPI_OK(env, napi_create_arraybuffer(env, cnt * 4, &out, &ab));
+    napi_ref r;
+    napi_create_reference(env, ab, 1, &r);
+    w->out_refs.push_back(r);
+    w->outs.push_back(static_cast<float*>(out));
+    w->out_counts.push_back(cnt);
+  }
+  napi_value promise, name;
+  NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
+  napi_create_string_utf8(env, "vso_run", NAPI_AUTO_LENGTH, &name);
+  NAPI_OK(env, napi_create_async_work(env, nullptr, name, OrtExecute, OrtComplete, w, &w->work));
+  NAPI_OK(env, napi_queue_async_work(env, w->work));
+  return promise;
+}
+
+napi_value OrtDestroy(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  void* p = nullptr;
+  if (argc >= 1 && napi_get_value_external(env, argv[0], &p) == napi_ok && p) {
+    OrtSess* o = static_cast<OrtSess*>(p);
+    if (o->s) vso_destroy(o->s);
+    o->s = nullptr;
+  }
+  return nullptr;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   const napi_property_descriptor props[] = {
       {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -482,6 +735,10 @@ napi_value Init(napi_env env, napi_value exports) {
       {"postDestroy", nullptr, PostDestroy, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"segmentPost", nullptr, SegmentPost, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"segmentComposite", nullptr, SegmentComposite, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"ortCreate", nullptr, OrtCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"ortInfo", nullptr, OrtInfo, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"ortRun", nullptr, OrtRun, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"ortDestroy", nullptr, OrtDestroy, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;
