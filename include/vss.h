@@ -170,6 +170,13 @@ int vss_read_layer(vss_handle* h, int layer, int n, float* host_out);
  * flags, precision).  Returns the string length, or a negative code. */
 int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap);
 
+/* The output tiles compiled for `layer`'s shape (csrc/vss_registry.inc), as
+ * (tile h, tile w) pairs in th[k], tw[k]; returns how many (0 for the stem
+ * and the head), at most `cap` written.  Any of them can be pinned with the
+ * environment variable VSS_TILE="layer:THxTW[,...]" at vss_create; results
+ * do not depend on the tile (bitwise). */
+int vss_layer_tiles(const vss_handle* h, int layer, int* th, int* tw, int cap);
+
 /* Kernel times from VSS_OPT_PROFILE runs: per layer, the mean over `count`
  * forwards (ms).  Resets the accumulators. */
 int vss_profile_read(vss_handle* h, double* ms_per_layer, int cap, int* count);

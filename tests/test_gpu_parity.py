@@ -146,7 +146,8 @@ def test_graph_vs_eager_and_profile(pkg, sess_bf, synthetic):
         assert cnt == 1 and ms > 0
     else:
         ms, cnt = sess_bf.profile_read()
-        assert cnt == 1 and all(m > 0 for m in ms)
+        fused = ["fused" in sess_bf.layer_kernel(i) for i in range(len(ms))]
+        assert cnt == 1 and all((m == 0) if fu else (m > 0) for m, fu in zip(ms, fused)), (ms, fused)
 
 
 def test_device_path_row_stride(pkg, sess_bf, synthetic, torch_cuda):
@@ -252,3 +253,28 @@ def test_stem_fusion_bitwise(pkg, synthetic, torch_cuda):
     assert np.array_equal(a, b)
     for li in range(2):
         assert np.array_equal(taps_a[li], taps_b[li]), li
+
+
+def test_every_compiled_tile_bitwise(pkg, synthetic):
+    """Every compiled tile of every block layer (pinned with VSS_TILE) gives
+    bitwise the activations and masks of the planner's choice."""
+    f = _frames(synthetic, 3, start=900)
+    with pkg.Session(dtype="bf16x2", max_batch=3, autotune=False) as s:
+        ref, _, _ = s.segment_frames(f)
+        ref_layers = [s.read_layer(li, 3) for li in range(s.n_layers - 1)]  # (the head's output is the mask)
+        tiles = {li: s.layer_tiles(li) for li in range(s.n_layers)}
+        chosen = [s.layer_kernel(li) for li in range(s.n_layers)]
+    bad = []
+    for li, ts in tiles.items():
+        for th, tw in ts:
+            os.environ["VSS_TILE"] = f"{li}:{th}x{tw}"
+            try:
+                with pkg.Session(dtype="bf16x2", max_batch=3, autotune=False) as s:
+                    got, _, _ = s.segment_frames(f)
+                    first = next((k for k in range(s.n_layers - 1)
+                                  if not np.array_equal(s.read_layer(k, 3), ref_layers[k])), None)
+                    if first is not None or not np.array_equal(got, ref):
+                        bad.append((li, th, tw, first, s.layer_kernel(li)))
+            finally:
+                del os.environ["VSS_TILE"]
+    assert not bad, (bad, chosen)

@@ -29,8 +29,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SPEC = os.path.join(ROOT, "video-stream-segmenetation_amd", "model", "spec.json")
-CANDIDATES = [(8, 16), (4, 16), (8, 8), (4, 8), (2, 16), (2, 8), (1, 16)]
+CANDIDATES = [(8, 16), (6, 16), (4, 16), (3, 16), (8, 8), (6, 8), (4, 8), (2, 16), (2, 8), (1, 16)]
 MAX_ACC, MAX_LDS = 16, 160 * 1024
+SHARDS = 6  # compile units for the block shapes (csrc/Makefile: VSS_SHARDS)
 
 
 def r4(v):
@@ -60,10 +61,11 @@ def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=False)
     f += r4(p_out * cin) if (mode == 0 and stride == 1 and cin == cout) else 0
     f += r4(chid * (cin + 8) // 2) if mode == 0 else 0
     f += r4(cout * (chid + 8) // 2) + r4(9 * chid) + r4(chid) + (r4(chid) if mode == 0 else 0) + r4(cout)
-    f += (r4(sr * sc * cin) + r4(2 * cin)) if mode == 2 else 0
-    f += max(4 * ((p_in_pad + p_out) * 16 if mode == 0 else 256), cs * p_out * (cout + 4),
-             16 * 2 * cin * 2 if mode == 2 else 0, stem_in_lds(ih, iw) if stem_in else 0)
-    f += 1024
+    f += r4(2 * cin) if mode == 2 else 0
+    # work: expand scratch / slabs / (decoder) the low-res src region; the
+    # decoder's norm slots and stats scratch live in xt
+    f += max(4 * p_in_pad * 16 if mode == 0 else 1024, cs * p_out * (cout + 4),
+             r4(sr * sc * cin) if mode == 2 else 0, stem_in_lds(ih, iw) if stem_in else 0)
     return f * 4, nacc
 
 
@@ -204,6 +206,12 @@ def main():
         mk_lines.append(f"VSS_MK({i}, " + ", ".join(str(v) for v in key) + ")")
     csrc = os.path.join(ROOT, "video-stream-segmenetation_amd", "csrc")
     open(os.path.join(csrc, "vss_registry.inc"), "w").write("\n".join(lines) + "\n")
+    # the same lines dealt round-robin to the shard files the Makefile compiles in parallel
+    for k in range(SHARDS):
+        part = [head + f" (shard {k} of {SHARDS})"] + lines[1 + k::SHARDS]
+        open(os.path.join(csrc, f"vss_registry_{k}.inc"), "w").write("\n".join(part) + "\n")
+    open(os.path.join(csrc, "vss_registry_shards.inc"), "w").write(
+        "\n".join([head] + [f"VSS_SHARD_FN({k})" for k in range(SHARDS)]) + "\n")
     open(os.path.join(csrc, "vss_mk.inc"), "w").write("\n".join(mk_lines) + "\n")
 
 

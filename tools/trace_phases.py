@@ -55,12 +55,15 @@ def main():
             buf = np.zeros((200000, 16), np.uint64)
             k = L.vss_trace_read(s._h, i, buf.ctypes.data, buf.shape[0])
             stamps.append(buf[:k].astype(np.int64))
-        t0 = min(int(x[:, 0].min()) for x in stamps)
+        t0 = min(int(x[:, 0].min()) for x in stamps if len(x))
         prev_end = None
         print(f"\n== batch {n} ({a.dtype}); times in us (s_memrealtime 10 ns ticks)")
         print(f"{'layer':>5} {'wgs':>5} {'span':>6} {'gap':>5} {'skew':>5} {'pro':>5} {'proMx':>5} {'main':>5} "
               f"{'mainMx':>6} {'epi':>5} {'wg':>5} {'iss':>5} {'land':>5} {'norm':>5} {'MHz':>5}  kernel")
         for i, x in enumerate(stamps):
+            if not len(x):  # fused into its consumer (the stem with VSS_FUSE_STEM)
+                print(f"{i:>5}     - (fused into layer {i + 1})")
+                continue
             us = (x - t0) / 100.0
             span = us[:, 3].max() - us[:, 0].min()
             gap = (us[:, 0].min() - prev_end) if prev_end is not None else 0.0

@@ -125,6 +125,7 @@ def lib() -> ctypes.CDLL:
                 "vss_read_layer": ([P, I, I, P], I),
                 "vss_profile_read": ([P, ctypes.POINTER(ctypes.c_double), I, ctypes.POINTER(I)], I),
                 "vss_layer_kernel": ([P, I, ctypes.c_char_p, I], I),
+                "vss_layer_tiles": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I), I], I),
                 "vss_post_config_default": ([ctypes.POINTER(PostConfig)], None),
                 "vss_post_create": ([P, ctypes.POINTER(PostConfig), ctypes.POINTER(P)], I),
                 "vss_post_destroy": ([P], None),
@@ -283,6 +284,14 @@ class Session:
         c, h, w = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _check(lib().vss_layer_shape(self._h, layer, ctypes.byref(c), ctypes.byref(h), ctypes.byref(w)), self._h)
         return c.value, h.value, w.value
+
+    def layer_tiles(self, layer: int):
+        """The compiled output tiles (th, tw) of `layer`'s shape ([] for stem / head)."""
+        th, tw = (ctypes.c_int * 64)(), (ctypes.c_int * 64)()
+        n = lib().vss_layer_tiles(self._h, layer, th, tw, 64)
+        if n < 0:
+            _check(n, self._h)
+        return [(th[k], tw[k]) for k in range(n)]
 
     def layer_kernel(self, layer: int) -> str:
         """The kernel running `layer`, named as rocprofv3 reports it."""

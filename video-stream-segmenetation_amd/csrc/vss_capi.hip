@@ -270,7 +270,7 @@ int load_weights(vss_handle* h) {
 // Bytes of an unsplit expand layer's LDS weight image (block_lds regions w1..b2).
 size_t weight_image_bytes(const LayerPlan& l) {
   const BlockLds B = block_lds(l.mode, l.stride, 1, 16, (int)l.rec.cin, 0, l.chid, l.C);
-  return (size_t)(B.lr - B.w1) * 4;
+  return (size_t)(B.wimg_end - B.w1) * 4;
 }
 
 int plan_once(vss_handle* h, bool mk_only) {
@@ -398,7 +398,7 @@ int upload(vss_handle* h) {
     const int cskip = l.mode == MODE_DEC ? (int)r.chid : 0;
     const int cs = l.chid / l.ks;  // hidden channels per slice
     const BlockLds B = block_lds(l.mode, l.stride, 1, 16, (int)r.cin, cskip, cs, l.C);
-    const size_t span = (size_t)(B.lr - B.w1);  // one slice's image (floats, multiple of 4)
+    const size_t span = (size_t)(B.wimg_end - B.w1);  // one slice's image (floats, multiple of 4)
     img_off[i] = img.size();
     img_len[i] = span;
     for (int sl = 0; sl < l.ks; ++sl) {
@@ -945,6 +945,32 @@ int autotune(vss_handle* h) {
   return rc;
 }
 
+// Pin layers to given compiled tiles (after the planner and the autotuner):
+// the tile-invariance tests run every compiled tile of every layer this way.
+int force_tiles(vss_handle* h, const char* spec) {
+  if (h->fwd_ok) return VSS_OK;  // the persistent forward's tiles are fixed (vss_mk.inc)
+  const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
+  const char* s = spec;
+  while (*s) {
+    int layer = -1, th = 0, tw = 0, used = 0;
+    if (std::sscanf(s, "%d:%dx%d%n", &layer, &th, &tw, &used) != 3 || layer < 0 || layer >= (int)h->L.size())
+      return fail(h, VSS_E_INVALID_ARG, std::string("VSS_TILE: bad entry in '") + spec + "'");
+    LayerPlan& l = h->L[layer];
+    const BlockEntry* pick = nullptr;
+    if (l.mode >= 0)
+      for (const BlockEntry* e : tile_candidates(l))
+        if (e->TH == th && e->TW == tw) pick = e;
+    if (!pick)
+      return fail(h, VSS_E_UNSUPPORTED, "VSS_TILE: layer " + std::to_string(layer) + " has no compiled " +
+                                            std::to_string(th) + "x" + std::to_string(tw) + " tile");
+    set_tile(l, pick);
+    HIP_TRY(h, hipFuncSetAttribute((const void*)pick->fn[pi], hipFuncAttributeMaxDynamicSharedMemorySize, (int)l.lds));
+    s += used;
+    if (*s == ',') ++s;
+  }
+  return VSS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1015,6 +1041,8 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
   h->prof_sum.assign(nl, 0.0);
   if ((rc = setup_forward(h))) return bail(rc);
   if (!(cfg->flags & VSS_CREATE_NO_AUTOTUNE) && (rc = autotune(h))) return bail(rc);
+  if (const char* ev = std::getenv("VSS_TILE"))  // tests / scans: "layer:THxTW[,layer:THxTW...]"
+    if ((rc = force_tiles(h, ev))) return bail(rc);
   *out = h;
   return VSS_OK;
 }
@@ -1222,6 +1250,21 @@ int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww) {
   if (hh) *hh = h->L[layer].H;
   if (ww) *ww = h->L[layer].W;
   return VSS_OK;
+}
+
+int vss_layer_tiles(const vss_handle* h, int layer, int* th, int* tw, int cap) {
+  if (!h || layer < 0 || layer >= (int)h->L.size() || cap < 0 || (cap > 0 && (!th || !tw))) return VSS_E_INVALID_ARG;
+  const LayerPlan& l = h->L[layer];
+  if (l.mode < 0) return 0;
+  int n = 0;
+  for (const BlockEntry* e : tile_candidates(l)) {
+    if (n < cap) {
+      th[n] = e->TH;
+      tw[n] = e->TW;
+    }
+    ++n;
+  }
+  return std::min(n, cap);
 }
 
 int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap) {

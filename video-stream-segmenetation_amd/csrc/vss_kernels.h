@@ -55,7 +55,7 @@ __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 struct BlockLds {
   int IH, IW, P_in, P_in_pad, P_out, CX, XS, LD1, LD2, SR, SC;
   int NCB, NPB, NCHUNK, PW, CS, NPBW, NACC;  // CS = chunk groups, PW = pixel-block groups
-  int xt, xr, w1, w2, wdw, bdw, b1, b2, lr, nrm, work, stt, total;
+  int xt, xr, w1, w2, wdw, bdw, b1, b2, wimg_end, lr, nrm, work, stt, total;  // [w1, wimg_end): the weight image
   int slab_stride;  // floats per wave slab = P_out * (cout + 4)
 };
 
@@ -102,15 +102,21 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   L.bdw = o; o += r4(chid);
   L.b1 = o;  o += mode == 0 ? r4(chid) : 0;
   L.b2 = o;  o += r4(cout);
-  L.lr = o;  o += mode == 2 ? r4(L.SR * L.SC * cin) : 0;
-  L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;
-  // per-wave scratch during the main loop, reused as the accumulator slabs
-  // after it; for the decoder also the staging of the src's norm slots
+  L.wimg_end = o;
+  // per-wave scratch during the main loop (expand: each wave's hidden chunk
+  // over the input tile), reused as the accumulator slabs after it.  The
+  // decoder's main loop needs no scratch, so its low-res src region (read
+  // only in the prologue) shares the space with the slabs (written only in
+  // the epilogue); the decoder stages the src's norm slots and, in the
+  // epilogue, its own stats scratch (int64 pairs) in xt, which is dead at
+  // both points (before the input tile is committed / after the main loop).
   L.work = o;
-  o += cmax(cmax(cmax(4 * (mode == 0 ? (L.P_in_pad + L.P_out) * 16 : 256), L.CS * L.slab_stride),
-                 mode == 2 ? kAccSlots * 2 * cin * 2 : 0),
+  L.lr = o;
+  o += cmax(cmax(cmax(mode == 0 ? 4 * L.P_in_pad * 16 : 1024, L.CS * L.slab_stride),
+                 mode == 2 ? r4(L.SR * L.SC * cin) : 0),
             stem_in ? stem_in_lds(L.IH, L.IW) : 0);
-  L.stt = o; o += 1024;  // 4 KiB: stats scratch (int64 pairs)
+  L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;
+  L.stt = L.xt;
   L.total = o;
   return L;
 }

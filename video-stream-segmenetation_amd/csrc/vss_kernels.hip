@@ -27,6 +27,8 @@
 //              (frameProcessorTest.ts:85) — bit-exact with the oracle.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "vss_kernels.h"
 
 namespace vss {
@@ -145,6 +147,7 @@ __device__ __forceinline__ void prep_sample(const uint8_t* __restrict__ f, long 
   r = out[0]; g = out[1]; b = out[2];
 }
 
+#if !defined(VSS_SHARD) || VSS_SHARD == 0  // (one definition across the shard objects)
 __global__ __launch_bounds__(256) void k_prep(PrepParams p) {
   const long plane = (long)p.Hm * p.Wm;
   const long total = plane * p.N;
@@ -161,6 +164,7 @@ __global__ __launch_bounds__(256) void k_prep(PrepParams p) {
     o[2 * plane] = b;
   }
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Stem: output tile 8 x 32 pixels x 16 channels, one pixel per thread.
@@ -424,6 +428,9 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   static_assert(!RES || (STRIDE == 1 && CIN == COUT && MODE != MODE_DEC), "residual shape");
   static_assert(MODE != MODE_IR_EXPAND || CS == 4, "expand deals its chunks to the 4 waves");
   static_assert(NPB % PW == 0, "pixel blocks must split evenly over the wave groups");
+  static_assert(MODE != MODE_DEC || (L.xt == L.stt && r4(P_IN_PAD * XS) >= 1024 &&
+                                     r4(P_IN_PAD * XS) >= (NORM_IN ? kAccSlots * 2 * CIN * 2 : 0)),
+                "decoder: xt holds the src's norm slots (prologue) and the stats scratch (epilogue)");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n = KS == 1 ? bz : bz / KS;  // grid z = frame * KS + slice
@@ -443,7 +450,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   VSS_STAMP(0);
 
   // ---- prologue: issue every load, then commit to LDS ----
-  constexpr int WIMG_F4 = (L.lr - L.w1) / 4;
+  constexpr int WIMG_F4 = (L.wimg_end - L.w1) / 4;
   const f4* wsrc = reinterpret_cast<const f4*>(p.wimg + ks * p.wimg_stride);
   f4* wdst = reinterpret_cast<f4*>(smem + L.w1);
   if constexpr (MODE == MODE_DEC) {
@@ -482,8 +489,34 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     }
     st_w.issue([&](int i) { return wsrc[i]; });
     VSS_STAMP(6);  // every load issued
-    if constexpr (NORM_IN) st_slots.commit([&](int i, f4 v) { reinterpret_cast<f4*>(work)[i] = v; });
-    commit_sum(st_lr, [&](int i, f4 v) { reinterpret_cast<f4*>(lr)[i] = v; });
+    if constexpr (NORM_IN) {
+      // sum the slots (exact, any order) -> the src's scale/shift; the slots
+      // are staged in xt, whose contents are committed only after this
+      const float gam = p.in_gamma[min(tid, CL - 1)], bet = p.in_beta[min(tid, CL - 1)];
+      st_slots.commit([&](int i, f4 v) { reinterpret_cast<f4*>(xt)[i] = v; });
+      __syncthreads();
+      const unsigned long long* sl = reinterpret_cast<const unsigned long long*>(xt);
+      if (tid < CL) {
+        unsigned long long s_fx = 0, q_fx = 0;
+#pragma unroll
+        for (int k = 0; k < kAccSlots; ++k) {
+          s_fx += sl[k * 2 * CL + tid];
+          q_fx += sl[k * 2 * CL + CL + tid];
+        }
+        norm_affine(s_fx, q_fx, p.in_hw, p.eps, gam, bet, nrm + tid, nrm + CL + tid);
+      }
+      __syncthreads();
+      VSS_STAMP(5);
+    }
+    // the low-res src region; with norm_in, relu(src * scale + shift) applied
+    // once per element as it is committed
+    commit_sum(st_lr, [&](int i, f4 v) {
+      if constexpr (NORM_IN) {
+        const int c4 = i % C4L;
+        v = reluv(v * *reinterpret_cast<const f4*>(nrm + 4 * c4) + *reinterpret_cast<const f4*>(nrm + CL + 4 * c4));
+      }
+      reinterpret_cast<f4*>(lr)[i] = v;
+    });
     commit_sum(st_sk, [&](int i, f4 v) {
       const int pix = i / C4S, c4 = i % C4S;
       const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
@@ -493,28 +526,6 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     VSS_STAMP(4);
     __syncthreads();
-    if constexpr (NORM_IN) {
-      // sum the slots (exact, any order) -> the src's scale/shift
-      const unsigned long long* sl = reinterpret_cast<const unsigned long long*>(work);
-      if (tid < CL) {
-        unsigned long long s_fx = 0, q_fx = 0;
-#pragma unroll
-        for (int k = 0; k < kAccSlots; ++k) {
-          s_fx += sl[k * 2 * CL + tid];
-          q_fx += sl[k * 2 * CL + CL + tid];
-        }
-        norm_affine(s_fx, q_fx, p.in_hw, p.eps, p.in_gamma[tid], p.in_beta[tid], nrm + tid, nrm + CL + tid);
-      }
-      __syncthreads();
-      VSS_STAMP(5);
-      // relu(src * scale + shift) once per low-res element, in place
-      for (int i = tid; i < SR * SC * C4L; i += 256) {
-        const int c4 = i % C4L;
-        f4* v = reinterpret_cast<f4*>(lr) + i;
-        *v = reluv(*v * *reinterpret_cast<const f4*>(nrm + 4 * c4) + *reinterpret_cast<const f4*>(nrm + CL + 4 * c4));
-      }
-      __syncthreads();
-    }
     // upsampled channels: PyTorch upsample_bilinear2d(scale 2, align_corners=False)
     // of relu(src * scale + shift) (the src's instance norm, applied per tap)
 #pragma unroll
@@ -681,7 +692,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   const int pw = wave % PW, cw = wave / PW;
 
   if constexpr (MODE == MODE_IR_EXPAND) {
-    float* hid = work + wave * (P_IN_PAD + P_OUT) * 16;
+    float* hid = work + wave * P_IN_PAD * 16;
     constexpr int NK = CIN / 16;
     for (int ck = wave; ck < NCHUNK; ck += 4) {
       const int c0 = ck << 4;
@@ -1114,28 +1125,61 @@ __global__ __launch_bounds__(256, 2) void k_forward(FwdParams fp) {
 
 // ---------------------------------------------------------------------------
 // Host-visible launch table (used by vss_capi.hip): one entry per compiled
-// block shape, generated from the layer table by tools/gen_registry.py.
+// block shape, generated from the layer table by tools/gen_registry.py and
+// dealt to kRegistryShards files (vss_registry_<k>.inc) so that the shapes
+// compile in parallel: this file is compiled once per shard with
+// -DVSS_SHARD=<k>; shard 0 also holds k_forward, the stem, head and
+// preprocessing kernels and the concatenated table.
+#ifndef VSS_SHARD
+#define VSS_SHARD 0
+#endif
 #define VSS_BLOCK(M, S, TH, TW, CI, CK, CH, CO, FL, MK)                                \
   {M, S, TH, TW, CI, CK, CH, CO, FL, MK,                                              \
    {k_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC_F32>,                              \
     k_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC_BF16X2>}},
+#define VSS_STR2(x) #x
+#define VSS_STR(x) VSS_STR2(x)
+#define VSS_CAT2(a, b) a##b
+#define VSS_CAT(a, b) VSS_CAT2(a, b)
 #ifndef VSS_ONLY_FORWARD  // (quick compile of k_forward alone for resource checks)
-static const BlockEntry kBlocks[] = {
-#include "vss_registry.inc"
+static const BlockEntry kShardBlocks[] = {
+#include VSS_STR(VSS_CAT(vss_registry_, VSS_SHARD).inc)
 };
 #else
-static const BlockEntry kBlocks[] = {{0}};
+static const BlockEntry kShardBlocks[] = {{0}};
 #endif
 #undef VSS_BLOCK
 
+const BlockEntry* VSS_CAT(registry_shard_, VSS_SHARD)(int* count) {
+  *count = (int)(sizeof(kShardBlocks) / sizeof(kShardBlocks[0]));
+  return kShardBlocks;
+}
+
+#if VSS_SHARD == 0
+#define VSS_SHARD_FN(k) const BlockEntry* registry_shard_##k(int* count);
+#include "vss_registry_shards.inc"
+#undef VSS_SHARD_FN
+
 const BlockEntry* block_registry(int* count) {
-  *count = (int)(sizeof(kBlocks) / sizeof(kBlocks[0]));
-  return kBlocks;
+  static const std::vector<BlockEntry> all = [] {
+    std::vector<BlockEntry> v;
+    int n = 0;
+    const BlockEntry* part = nullptr;
+#define VSS_SHARD_FN(k)                              \
+    part = registry_shard_##k(&n);                   \
+    v.insert(v.end(), part, part + n);
+#include "vss_registry_shards.inc"
+#undef VSS_SHARD_FN
+    return v;
+  }();
+  *count = (int)all.size();
+  return all.data();
 }
 
 void (*stem_kernel16())(StemParams) { return k_stem<16>; }
 void (*head_kernel16())(HeadParams) { return k_head<16>; }
 void (*prep_kernel())(PrepParams) { return k_prep; }
 FwdFn forward_kernel(int prec) { return prec == PREC_F32 ? k_forward<PREC_F32> : k_forward<PREC_BF16X2>; }
+#endif
 
 }  // namespace vss
