@@ -743,25 +743,33 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     }
   } else {
     // dw 3x3 straight into the project MFMA's B layout (lane (r, g): pixel r
-    // of the block, channels c0+4g..c0+4g+3); no LDS round trip, no syncs
+    // of the block, channels c0+4g..c0+4g+3); no LDS round trip, no syncs.
+    // Chunk-outer: the chunk's dw taps and project fragments are read from
+    // LDS once and reused for every pixel block of the wave (each
+    // accumulator still sums its chunks in the same order).
+    for (int ck = cw; ck < NCHUNK; ck += CS) {
+      const int c0 = ck << 4;
+      f4 wk[9];
 #pragma unroll
-    for (int i = 0; i < NPBW; ++i) {
-      const int pix = (pw + i * PW) * 16 + r;
-      const int ly = pix / TW, lx = pix % TW;
-      for (int ck = cw; ck < NCHUNK; ck += CS) {
-        const int c0 = ck << 4;
-        f4 a = *reinterpret_cast<const f4*>(bdws + c0 + 4 * g);
+      for (int t = 0; t < 9; ++t) wk[t] = *reinterpret_cast<const f4*>(wdws + t * CH + c0 + 4 * g);
+      const f4 bb = *reinterpret_cast<const f4*>(bdws + c0 + 4 * g);
+      typename AFrag<PREC>::T a2[NCB];
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) a2[cb] = lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g);
+#pragma unroll
+      for (int i = 0; i < NPBW; ++i) {
+        const int pix = (pw + i * PW) * 16 + r;
+        const int ly = pix / TW, lx = pix % TW;
+        f4 a = bb;
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx)
-            a = *reinterpret_cast<const f4*>(wdws + (ky * 3 + kx) * CH + c0 + 4 * g) *
-                    *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx + kx) * XS + c0 + 4 * g) + a;
+            a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx + kx) * XS + c0 + 4 * g) + a;
         if constexpr (MODE == MODE_IR_DIRECT) a = relu6v(a);
         const f4 b = to_operand<PREC>(a);
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb)
-          acc[i * NCB + cb] = mma16_op<PREC>(acc[i * NCB + cb], lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g), b);
+        for (int cb = 0; cb < NCB; ++cb) acc[i * NCB + cb] = mma16_op<PREC>(acc[i * NCB + cb], a2[cb], b);
       }
     }
   }
