@@ -23,8 +23,13 @@
  * Resize/Upsample (nearest, linear; half_pixel, pytorch_half_pixel,
  * align_corners, asymmetric), InstanceNormalization, BatchNormalization,
  * MatMul, Gemm, Softmax, and Shape, Gather, Constant, ConstantOfShape,
- * Floor, Ceil, Cast on constants.  Anything else fails vso_create with
- * VSO_E_UNSUPPORTED naming the node.
+ * Floor, Ceil, Cast on constants.  For q4f16 exports (model_q4f16.onnx's
+ * form): float16 initializers, Cast to FLOAT16 (values rounded to halves and
+ * kept as f32; later ops compute in f32), DequantizeLinear of int8 / uint8 /
+ * int4 / uint4 weights (per tensor, per axis, opset-21 blocks; folded at
+ * create) and com.microsoft MatMulNBits (4-bit blocks, packed uint8 zero
+ * points, bias; dequantised once at create).  Anything else fails vso_create
+ * with VSO_E_UNSUPPORTED naming the node.
  *
  * Errors: int returns are 0 or a negative code, message in vso_last_error
  * (thread-local when the session is NULL), like _OrtGetLastError (:50).

@@ -18,7 +18,11 @@ operator specification (opset <= 18) for the subset:
   Resize/Upsample (nearest, linear), InstanceNormalization,
   BatchNormalization, MatMul, Gemm, Softmax,
   and the shape arithmetic exporters emit (Shape, Gather, Constant,
-  ConstantOfShape, Floor, Ceil) on constants.
+  ConstantOfShape, Floor, Ceil) on constants; for q4f16 exports (the form
+  of the reference's absent model_q4f16.onnx): Cast to FLOAT16 (values rounded
+  to halves), float16 initializers, DequantizeLinear (opset 21: int8 / uint8 /
+  int4 / uint4, per tensor / axis / block) and com.microsoft MatMulNBits
+  (4-bit blocks, onnxruntime's contrib-op schema).
 
 Float math is float64 inside each op, cast to float32 at every op boundary
 (so the oracle is the exactly rounded value of each op on float32 inputs,
@@ -33,8 +37,9 @@ import numpy as np
 # ---------------------------------------------------------------------------
 # protobuf wire format
 DT_FLOAT, DT_UINT8, DT_INT8, DT_INT32, DT_INT64, DT_BOOL, DT_FLOAT16, DT_DOUBLE = 1, 2, 3, 6, 7, 9, 10, 11
+DT_UINT4, DT_INT4 = 21, 22  # two per byte, low nibble first (held here as int8 / uint8 arrays)
 _NP = {DT_FLOAT: np.float32, DT_UINT8: np.uint8, DT_INT8: np.int8, DT_INT32: np.int32, DT_INT64: np.int64,
-       DT_BOOL: np.bool_, DT_FLOAT16: np.float16, DT_DOUBLE: np.float64}
+       DT_BOOL: np.bool_, DT_FLOAT16: np.float16, DT_DOUBLE: np.float64, DT_UINT4: np.uint8, DT_INT4: np.int8}
 
 
 def _varint(b, i):
@@ -107,6 +112,13 @@ def parse_tensor(b):
         elif f == 14 and v == 1:
             raise ValueError("external tensor data is not supported")
     npdt = _NP[dt]
+    if dt in (DT_UINT4, DT_INT4):
+        n = int(np.prod(dims)) if dims else 1
+        packed = np.frombuffer(raw, np.uint8) if raw is not None else np.array(i32, np.uint8)
+        q = np.stack([packed & 15, packed >> 4], axis=1).reshape(-1)[:n].astype(np.int16)
+        if dt == DT_INT4:
+            q = np.where(q >= 8, q - 16, q)
+        return name, q.astype(npdt).reshape(dims)
     if raw is not None:
         a = np.frombuffer(raw, dtype=npdt).copy()
     elif dt == DT_FLOAT:
@@ -259,10 +271,27 @@ def _str(f, s):
     return _len(f, s.encode())
 
 
+class Packed4:
+    """An int4 / uint4 initializer for the writer: `values` (ints in range),
+    stored two per byte, low nibble first."""
+
+    def __init__(self, values, signed: bool):
+        self.values = np.asarray(values)
+        self.signed = signed
+
+
 def make_tensor(name, arr):
+    if isinstance(arr, Packed4):
+        v = arr.values.astype(np.int16).reshape(-1) & 15
+        if v.size % 2:
+            v = np.append(v, 0)
+        raw = (v[0::2] | (v[1::2] << 4)).astype(np.uint8).tobytes()
+        b = b"".join(_key(1, 0) + _enc_varint(int(d)) for d in arr.values.shape)
+        return b + _key(2, 0) + _enc_varint(DT_INT4 if arr.signed else DT_UINT4) + _str(8, name) + _len(9, raw)
     arr = np.asarray(arr)
     dt = {np.dtype(np.float32): DT_FLOAT, np.dtype(np.int64): DT_INT64, np.dtype(np.float16): DT_FLOAT16,
-          np.dtype(np.int32): DT_INT32, np.dtype(np.float64): DT_DOUBLE, np.dtype(np.uint8): DT_UINT8}[arr.dtype]
+          np.dtype(np.int32): DT_INT32, np.dtype(np.float64): DT_DOUBLE, np.dtype(np.uint8): DT_UINT8,
+          np.dtype(np.int8): DT_INT8}[arr.dtype]
     b = b"".join(_key(1, 0) + _enc_varint(int(d)) for d in arr.shape)
     b += _key(2, 0) + _enc_varint(dt) + _str(8, name) + _len(9, np.ascontiguousarray(arr).tobytes())
     return b
@@ -285,10 +314,12 @@ def make_attr(name, v):
     raise TypeError(f"attribute {name}: {type(v)}")
 
 
-def make_node(op, inputs, outputs, **attrs):
+def make_node(op, inputs, outputs, domain="", **attrs):
     b = b"".join(_str(1, i) for i in inputs) + b"".join(_str(2, o) for o in outputs) + _str(4, op)
     for k, v in attrs.items():
         b += _len(5, make_attr(k, v))
+    if domain:
+        b += _str(7, domain)
     return b
 
 
@@ -445,6 +476,48 @@ def _f32(v):
     return np.asarray(v).astype(np.float32)
 
 
+def _dequantize_linear(x, scale, zp, attrs):
+    """ONNX DequantizeLinear (opset 21): y = (x - zero_point) * scale, per
+    tensor, per axis, or in blocks of `block_size` along the axis; the result
+    has the scale's type."""
+    ax = attrs.get("axis", 1)
+    bs = attrs.get("block_size", 0)
+    xx = x.astype(np.float64)
+    s = scale.astype(np.float64)
+    z = zp.astype(np.float64) if zp is not None else np.zeros_like(s)
+    if s.size != 1:
+        ax = ax % x.ndim
+        if bs:
+            s = np.repeat(s, bs, axis=ax).take(range(x.shape[ax]), axis=ax)
+            z = np.repeat(z, bs, axis=ax).take(range(x.shape[ax]), axis=ax)
+        else:
+            shp = [1] * x.ndim
+            shp[ax] = x.shape[ax]
+            s, z = s.reshape(shp), z.reshape(shp)
+    y = ((xx - z) * s).astype(np.float32)
+    return y.astype(np.float16) if scale.dtype == np.float16 else y
+
+
+def _dequant_nbits(bq, scales, zp, attrs):
+    """com.microsoft MatMulNBits weights (4 bits): B [N][k_blocks][blob] uint8,
+    element k of row n in nibble k%2 (low first) of byte k/2 of its block;
+    W[n][k] = (q - zp) * scale[n][k // block_size], zp packed two blocks per byte
+    (default 8).  Returns W [N][K] (float16 when the scales are)."""
+    K, N, bs = attrs["K"], attrs["N"], attrs["block_size"]
+    assert attrs.get("bits", 4) == 4
+    kb = (K + bs - 1) // bs
+    b = np.asarray(bq, np.uint8).reshape(N, kb, bs // 2)
+    q = np.stack([b & 15, b >> 4], axis=3).reshape(N, kb * bs)[:, :K].astype(np.float64)
+    s = np.asarray(scales).astype(np.float64).reshape(N, kb)
+    if zp is not None:
+        zb = np.asarray(zp, np.uint8).reshape(N, -1)
+        z = np.stack([zb & 15, zb >> 4], axis=2).reshape(N, -1)[:, :kb].astype(np.float64)
+    else:
+        z = np.full((N, kb), 8.0)
+    w = ((q - np.repeat(z, bs, axis=1)[:, :K]) * np.repeat(s, bs, axis=1)[:, :K]).astype(np.float32)
+    return w.astype(np.float16) if np.asarray(scales).dtype == np.float16 else w
+
+
 def run(model: Model, feeds: dict, want=None) -> dict:
     """Evaluate the graph on numpy feeds; returns {output name: array} (or
     every value named in `want`)."""
@@ -534,7 +607,8 @@ def run(model: Model, feeds: dict, want=None) -> dict:
         elif op in ("Identity", "Dropout"):
             y = x
         elif op == "Cast":
-            y = x.astype(_NP[a["to"]])
+            with np.errstate(over="ignore"):  # beyond the float16 range -> inf, as specified
+                y = x.astype(_NP[a["to"]])
         elif op in ("Resize", "Upsample"):
             if op == "Upsample":
                 y = _resize(x, ins[1], None, a)
@@ -564,6 +638,14 @@ def run(model: Model, feeds: dict, want=None) -> dict:
             if len(ins) > 2 and ins[2] is not None:
                 r = r + a.get("beta", 1.0) * ins[2].astype(np.float64)
             y = _f32(r)
+        elif op == "DequantizeLinear":
+            y = _dequantize_linear(ins[0], ins[1], ins[2] if len(ins) > 2 else None, a)
+        elif op == "MatMulNBits":
+            w = _dequant_nbits(ins[1], ins[2], ins[3] if len(ins) > 3 else None, a)
+            r = x.astype(np.float64).reshape(-1, a["K"]) @ w.astype(np.float64).T
+            if len(ins) > 5 and ins[5] is not None:
+                r = r + ins[5].astype(np.float64)
+            y = _f32(r).reshape(tuple(x.shape[:-1]) + (a["N"],))
         elif op == "Softmax":
             ax = a.get("axis", -1)
             e = np.exp(x.astype(np.float64) - x.max(axis=ax, keepdims=True))

@@ -176,8 +176,64 @@ def modnet_like(h=64, w=96):
     return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])])
 
 
+def q4f16_like(h=64, w=96):
+    """A MODNet-shaped net in the form of a q4f16 export (the reference's
+    absent model_q4f16.onnx, model.ts:13): float32 input Cast to float16,
+    float16 weights and biases, a convolution whose weights are int4 blocks
+    behind DequantizeLinear (opset 21, block_size along the input channels),
+    the SE block's fully connected layers as com.microsoft MatMulNBits (4-bit
+    blocks with packed zero points, a partial last block, a bias), and a
+    float32 Cast of the matte."""
+    b = Builder(4)
+    rng = b.rng
+    x = "input"
+
+    def w16(*shape, scale=None):
+        n = b.w(*shape, scale=scale)
+        b.inits[n] = b.inits[n].astype(np.float16)
+        return n
+
+    def conv16(t, cin, cout, k, stride=1, group=1, wname=None):
+        ins = [t, wname or w16(cout, cin // group, k, k), w16(cout, scale=0.1)]
+        return b.op("Conv", ins, kernel_shape=[k, k], strides=[stride, stride], pads=[k // 2] * 4, group=group)
+
+    def relu6(t):
+        return b.op("Clip", [t, b.const(np.array(0, np.float16)), b.const(np.array(6, np.float16))])
+
+    def nbits(t, K, N, bs, bias):
+        kb = -(-K // bs)
+        n = b.name("q")
+        b.inits[n] = rng.integers(0, 256, (N, kb, bs // 2), dtype=np.uint8)
+        sc = b.const((rng.random(N * kb) * 0.1 + 0.02).astype(np.float16))
+        zp = b.const(rng.integers(0, 256, (N * (-(-kb // 2)),), dtype=np.uint8))
+        ins = [t, n, sc, zp] + (["", b.const((rng.standard_normal(N) * 0.1).astype(np.float16))] if bias else [])
+        return b.op("MatMulNBits", ins, domain="com.microsoft", K=K, N=N, bits=4, block_size=bs)
+
+    h16 = b.op("Cast", [x], to=R.DT_FLOAT16)
+    s = relu6(conv16(h16, 3, 16, 3, stride=2))                               # /2
+    qn = b.name("qw")
+    b.inits[qn] = R.Packed4(rng.integers(-8, 8, (24, 16, 3, 3)), signed=True)
+    dq = b.op("DequantizeLinear", [qn, b.const((rng.random((24, 2, 3, 3)) * 0.05 + 0.01).astype(np.float16))],
+              axis=1, block_size=8)
+    e = relu6(conv16(s, 16, 24, 3, stride=2, wname=dq))                      # /4
+    e = relu6(conv16(e, 24, 24, 3, group=24))
+    gp = b.op("Flatten", [b.op("GlobalAveragePool", [e])])                   # [1, 24]
+    f = b.op("Relu", [nbits(gp, 24, 8, 16, bias=False)])                     # K 24 = 16 + partial 8
+    f = b.op("Sigmoid", [nbits(f, 8, 24, 16, bias=True)])                    # one partial block
+    f = b.op("Reshape", [f, b.const(np.array([1, 24, 1, 1], np.int64))])
+    e = b.op("Mul", [e, f])
+    u = b.op("Resize", [e, "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+             coordinate_transformation_mode="half_pixel")                    # /2
+    u = b.op("Relu", [conv16(b.op("Concat", [u, s], axis=1), 40, 16, 3)])
+    u = b.op("Resize", [u, "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+             coordinate_transformation_mode="half_pixel")                    # /1
+    m = b.op("Cast", [b.op("Sigmoid", [conv16(u, 16, 1, 3)])], to=R.DT_FLOAT)
+    return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])], opset=21)
+
+
 MODELS = {"conv_zoo": (conv_zoo, {"x": (1, 3, 64, 80)}), "ops_zoo": (ops_zoo, {"x": (2, 8, 12, 16)}),
-          "modnet_like": (modnet_like, {"input": (1, 3, 64, 96)})}
+          "modnet_like": (modnet_like, {"input": (1, 3, 64, 96)}),
+          "q4f16_like": (q4f16_like, {"input": (1, 3, 64, 96)})}
 
 
 def feeds_for(name, seed=0):

@@ -113,3 +113,19 @@ def test_errors(ort):
         with pytest.raises(ort.VsoError) as e:
             s.run({"input": np.zeros((1, 3, 10, 10), np.float32)})
         assert e.value.code == ort.VSO_E_INVALID_ARG
+
+
+def test_cast_float16_bitwise(ort):
+    # the GPU's Cast to FLOAT16 rounds exactly as numpy (nearest, ties to even,
+    # subnormals, overflow to inf)
+    rng = np.random.default_rng(4)
+    v = np.concatenate([np.array([1 + 2 ** -11, 1 + 3 * 2 ** -11, 65519.0, 65520.0, -70000.0, 2 ** -25,
+                                  3 * 2 ** -25, 6.1e-5, 0.0, -0.0], np.float32),
+                        (rng.standard_normal(1014) * 10.0 ** rng.integers(-7, 5, 1014)).astype(np.float32)])
+    m = R.make_model([R.make_node("Cast", ["v"], ["h"], to=R.DT_FLOAT16),
+                      R.make_node("Cast", ["h"], ["y"], to=R.DT_FLOAT)], {}, [("v", [1024])], [("y", [1024])])
+    with ort.InferenceSession(m) as s:
+        got = s.run({"v": v})["y"]
+    with np.errstate(over="ignore"):
+        want = v.astype(np.float16).astype(np.float32)
+    assert np.array_equal(got, want)

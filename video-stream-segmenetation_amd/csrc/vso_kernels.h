@@ -11,7 +11,8 @@ namespace vso {
 constexpr int kMaxDims = 6;
 
 // Activations fused into the producing kernel's epilogue (and the unary kernel).
-enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_CLIP = 2, ACT_PRELU = 3, ACT_LEAKY = 4, ACT_SIGMOID = 5, ACT_TANH = 6 };
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_CLIP = 2, ACT_PRELU = 3, ACT_LEAKY = 4, ACT_SIGMOID = 5, ACT_TANH = 6,
+                 ACT_F16 = 7 /* Cast to float16: round to the nearest half (ties to even), kept as f32 */ };
 
 struct Epilogue {
   const float* bias;   // [M] or null

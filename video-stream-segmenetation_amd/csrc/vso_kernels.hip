@@ -16,6 +16,7 @@
 //                 pooling, per-row reductions (GlobalAveragePool,
 //                 InstanceNormalization, Softmax), channel affine
 //                 (BatchNormalization), Resize and a small batched GEMM.
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
 #include "vso_kernels.h"
@@ -33,6 +34,7 @@ __device__ __forceinline__ float act_apply(float v, int act, float a0, float a1,
     case ACT_LEAKY: return v < 0.f ? v * a0 : v;
     case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
     case ACT_TANH: return tanhf(v);
+    case ACT_F16: return __half2float(__float2half_rn(v));
     default: return v;
   }
 }

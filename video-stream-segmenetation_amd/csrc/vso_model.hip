@@ -40,7 +40,7 @@ namespace {
 thread_local std::string g_err;
 
 enum { DT_FLOAT = 1, DT_UINT8 = 2, DT_INT8 = 3, DT_INT32 = 6, DT_INT64 = 7, DT_BOOL = 9, DT_FLOAT16 = 10,
-       DT_DOUBLE = 11 };
+       DT_DOUBLE = 11, DT_UINT4 = 21, DT_INT4 = 22 };
 
 // ---- protobuf wire format ---------------------------------------------------
 struct PB {
@@ -147,10 +147,28 @@ float half_to_float(uint16_t h) {
   return f;
 }
 
+// f -> the nearest float16 value (ties to even), as a float: what a Cast to
+// FLOAT16 or a float16-typed result holds (the GPU's __float2half_rn).
+float round_half(float f) {
+  const float a = std::fabs(f);
+  if (!(a < INFINITY)) return f;  // inf / nan
+  float q;
+  if (a >= 65520.f) q = INFINITY;
+  else if (a < 6.103515625e-05f) q = std::nearbyint(a * 16777216.f) / 16777216.f;  // subnormal: quantum 2^-24
+  else {
+    int e = 0;
+    (void)std::frexp(a, &e);  // a in [2^(e-1), 2^e): 11 significant bits
+    const float sc = std::ldexp(1.f, 11 - e);
+    q = std::nearbyint(a * sc) / sc;
+  }
+  return std::copysign(q, f);
+}
+
 // A constant tensor (initializer / attribute / folded value).
 struct Const {
   std::vector<int64_t> dims;
   bool is_int = false;
+  bool f16 = false;        // float16-typed (values are exact halves)
   std::vector<float> f;    // float data (also filled for ints, as doubles would be)
   std::vector<int64_t> i;  // integer data
   int64_t numel() const {
@@ -202,6 +220,24 @@ bool parse_tensor(PB pb, std::string* name, Const* c, std::string* err) {
       if (has_raw) { h.resize(raw.size() / 2); std::memcpy(h.data(), raw.data(), h.size() * 2); }
       else for (int64_t v : i32) h.push_back((uint16_t)v);
       for (uint16_t v : h) c->f.push_back(half_to_float(v));
+      c->f16 = true;
+      break;
+    }
+    case DT_UINT4: case DT_INT4: {  // two per byte, low nibble first
+      std::vector<int64_t> v;
+      const std::string& src = has_raw ? raw : std::string();
+      for (int64_t k = 0; k < n; ++k) {
+        int q = 0;
+        if (has_raw) {
+          if ((size_t)(k / 2) >= src.size()) break;
+          q = ((uint8_t)src[k / 2] >> ((k & 1) * 4)) & 15;
+        } else {
+          if ((size_t)(k / 2) >= i32.size()) break;
+          q = ((int)i32[k / 2] >> ((k & 1) * 4)) & 15;
+        }
+        v.push_back(dt == DT_INT4 && q >= 8 ? q - 16 : q);
+      }
+      set_ints(v);
       break;
     }
     case DT_DOUBLE:
@@ -538,6 +574,9 @@ struct Planner {
         const bool to_int = to == DT_INT64 || to == DT_INT32 || to == DT_INT8 || to == DT_UINT8 || to == DT_BOOL;
         if (to_int && !r.is_int) { r.i.clear(); for (float x : r.f) r.i.push_back((int64_t)x); }
         r.is_int = to_int;
+        r.f16 = to == DT_FLOAT16;
+        if (r.f16)
+          for (float& x : r.f) x = round_half(x);
       } else if (op == "Floor" || op == "Ceil") {
         for (float& x : r.f) x = op == "Floor" ? std::floor(x) : std::ceil(x);
       }
@@ -577,6 +616,42 @@ struct Planner {
           r.f.push_back((float)(op == "Add" ? x + y : op == "Sub" ? x - y : op == "Mul" ? x * y : x / y));
         }
       }
+    } else if (op == "DequantizeLinear") {
+      // y = (x - zero_point) * scale: per tensor, per axis, or blocked along
+      // the axis (opset 21 block_size); int8/uint8/int4/uint4 weights
+      const Const& x = in[0]->c;
+      const Const& sc = in[1]->c;
+      const Const* zp = in.size() > 2 && in[2] ? &in[2]->c : nullptr;
+      if (!x.is_int) return fail("DequantizeLinear: integer input expected");
+      const int64_t rk = (int64_t)x.dims.size();
+      int64_t ax = nd.ai("axis", 1);
+      if (ax < 0) ax += rk;
+      const int64_t bs = nd.ai("block_size", 0);
+      const int64_t n = x.numel(), ns = sc.numel();
+      int64_t inner = 1;
+      for (int64_t k = ax + 1; k < rk; ++k) inner *= x.dims[k];
+      const int64_t da = rk > 0 && ax < rk ? x.dims[ax] : 1;
+      const int64_t sda = bs > 0 && ax < (int64_t)sc.dims.size() ? sc.dims[ax] : 1;
+      if (ns != 1 && (ax < 0 || ax >= rk)) return fail("DequantizeLinear: bad axis");
+      if (ns != 1 && bs == 0 && ns != da) return fail("DequantizeLinear: per-axis scale size mismatch");
+      if (bs > 0 && (sda != (da + bs - 1) / bs || ns != n / da * sda))
+        return fail("DequantizeLinear: blocked scale shape mismatch");
+      if (zp && zp->numel() != ns) return fail("DequantizeLinear: zero point shape differs from the scale's");
+      r.dims = x.dims;
+      r.f.resize((size_t)n);
+      for (int64_t k = 0; k < n; ++k) {
+        int64_t si = 0;
+        if (ns != 1) {
+          const int64_t ia = (k / inner) % da;
+          if (bs == 0) si = ia;
+          else si = ((k / (inner * da)) * sda + ia / bs) * inner + k % inner;
+        }
+        const double q = (double)x.i[k] - (zp ? (double)zp->i[si] : 0.0);
+        float v = (float)(q * (double)sc.f[si]);
+        if (sc.f16) v = round_half(v);
+        r.f[k] = v;
+      }
+      r.f16 = sc.f16;
     } else if (op == "Gather") {
       const Const &d = in[0]->c, &ix = in[1]->c;
       int64_t ax = nd.ai("axis", 0);
@@ -960,6 +1035,18 @@ struct Planner {
       if (!infer_view(nd, in, &shp)) return false;
       return set_runtime(nd.out[0], shp, x->buf);
     }
+    if (op == "Cast" && nd.ai("to", DT_FLOAT) == DT_FLOAT16) {
+      // float16 storage semantics: round to the nearest half (the values stay
+      // f32 in HBM; later ops compute in f32, a superset of the f16 precision)
+      UnaryParams p{};
+      p.x = dptr(*x);
+      p.act = ACT_F16;
+      if (!set_runtime(nd.out[0], xs)) return false;
+      p.y = dptr(vals[nd.out[0]]);
+      p.n = vals[nd.out[0]].numel();
+      add("vso::k_unary(vso::UnaryParams)", [p](hipStream_t st) { launch_unary(p, st); });
+      return true;
+    }
     if (op == "Identity" || op == "Dropout" || op == "Cast") {
       if (op == "Cast" && nd.ai("to", DT_FLOAT) != DT_FLOAT) return fail("Cast of a runtime tensor to a non-float type");
       return set_runtime(nd.out[0], xs, x->buf);
@@ -1295,7 +1382,63 @@ struct Planner {
       add("vso::k_gemm(vso::GemmParams)", [p](hipStream_t st) { launch_gemm(p, st); });
       return true;
     }
+    if (op == "MatMulNBits") return plan_matmul_nbits(nd, in);
     return fail("unsupported operator " + op + " (node '" + nd.name + "')");
+  }
+
+  // com.microsoft MatMulNBits (the q4 layers of a q4f16 export): Y = A @ W^T
+  // (+ bias), W [N][K] dequantised once at create from 4-bit blocks:
+  // W[n][k] = (q - zp) * scale[n][k / block_size], q the k-th nibble of row
+  // n (low nibble first), zp the packed per-block zero point (default 8).
+  bool plan_matmul_nbits(const Node& nd, std::vector<Value*>& in) {
+    auto opt = [&](size_t k) { return in.size() > k ? in[k] : nullptr; };
+    Value *a = in[0], *bq = opt(1), *sc = opt(2), *zp = opt(3), *gidx = opt(4), *bias = opt(5);
+    if (!bq || !bq->is_const || !sc || !sc->is_const || (zp && !zp->is_const) || (bias && !bias->is_const))
+      return fail("MatMulNBits '" + nd.name + "': B, scales, zero_points and bias must be initializers");
+    if (gidx) return fail("MatMulNBits '" + nd.name + "': g_idx is not supported");
+    const int64_t K = nd.ai("K", 0), N = nd.ai("N", 0), bits = nd.ai("bits", 4), bs = nd.ai("block_size", 0);
+    if (bits != 4 || bs < 16 || K <= 0 || N <= 0) return fail("MatMulNBits '" + nd.name + "': 4-bit blocks only");
+    const int64_t kb = (K + bs - 1) / bs, blob = bs * bits / 8, zpb = (kb * bits + 7) / 8;
+    if (bq->c.numel() != N * kb * blob || sc->c.numel() != N * kb)
+      return fail("MatMulNBits '" + nd.name + "': B / scales sizes do not match K, N, block_size");
+    if (zp && (!zp->c.is_int || zp->c.numel() != N * zpb))
+      return fail("MatMulNBits '" + nd.name + "': only packed uint8 zero points are supported");
+    if (a->shape.empty() || a->shape.back() != K) return fail("MatMulNBits '" + nd.name + "': A's last dim is not K");
+    std::vector<float> w((size_t)(N * K));
+    for (int64_t n = 0; n < N; ++n)
+      for (int64_t b = 0; b < kb; ++b) {
+        const double s = sc->c.f[n * kb + b];
+        const int z = zp ? (int)((zp->c.i[n * zpb + b / 2] >> ((b & 1) * 4)) & 15) : 8;
+        for (int64_t j = 0; j < bs && b * bs + j < K; ++j) {
+          const int q = (int)((bq->c.i[(n * kb + b) * blob + j / 2] >> ((j & 1) * 4)) & 15);
+          float v = (float)((double)(q - z) * s);
+          if (sc->c.f16) v = round_half(v);
+          w[n * K + b * bs + j] = v;
+        }
+      }
+    GemmParams p{};
+    p.alpha = 1.f;
+    p.beta = 1.f;
+    p.batch = 1;
+    p.K = (int)K;
+    p.N = (int)N;
+    p.M = (int)(a->numel() / K);
+    p.sam = K; p.sak = 1;
+    p.sbn = K; p.sbk = 1;  // W stored [N][K]
+    p.a = operand(*a);
+    p.b = upload_vec(w);
+    if (bias) {
+      if (bias->c.numel() != N) return fail("MatMulNBits '" + nd.name + "': bias must have N elements");
+      p.c = operand(*bias);
+      p.scm = 0; p.scn = 1;
+    }
+    if (!p.a || !p.b || (bias && !p.c)) return false;
+    std::vector<int64_t> os(a->shape.begin(), a->shape.end() - 1);
+    os.push_back(N);
+    if (!set_runtime(nd.out[0], os)) return false;
+    p.y = dptr(vals[nd.out[0]]);
+    add("vso::k_gemm(vso::GemmParams)", [p](hipStream_t st) { launch_gemm(p, st); });
+    return true;
   }
 
   bool run(const std::vector<std::vector<int64_t>>& in_shapes) {
