@@ -47,7 +47,11 @@ enum {
 };
 
 /* Mask resolution: model (the reference's seam, frameProcessorTest.ts:96-97). */
-enum { VSS_OUT_MODEL = 0 };
+/* out_mode of vss_segment / vss_segment_async: masks at model resolution
+ * (the seam triple, n * mask_h * mask_w floats), or upsampled on the GPU to
+ * the frames' resolution (n * height * width floats; half-pixel bilinear —
+ * the canvas drawImage upscale of :177 defined as in vss_composite_device). */
+enum { VSS_OUT_MODEL = 0, VSS_OUT_FRAME = 1 };
 
 /* Options for vss_set_option. */
 enum {
@@ -113,12 +117,19 @@ const char* vss_last_error(const vss_handle* h);
 
 int vss_get_info(const vss_handle* h, vss_info* info);
 
+/* The model-res masks of vss_segment_device upsampled to frame_h x frame_w
+ * (what VSS_OUT_FRAME returns): d_out [n][frame_h][frame_w] f32, enqueued on
+ * `stream`.  Replaces the canvas scaling of the mask, frameProcessorTest.ts:177. */
+int vss_mask_to_frame_device(vss_handle* h, const float* d_masks, int n, int frame_h, int frame_w, float* d_out,
+                             void* stream);
+
 /* Synchronous host-memory call.  Replaces frameProcessorTest.ts:79-97
  * (fromPixels .. session.run .. squeezeMaskTo2D) for n frames at once:
  * frames: n frames of h rows, row_stride bytes per row, frames packed
  *         back to back (frame stride = h*row_stride), channels 3 (RGB) or 4
  *         (RGBA; alpha dropped as tf.browser.fromPixels does, :79);
- * masks_out: n * mask_h * mask_w floats, row-major per frame, in [0,1]. */
+ * masks_out: n * mask_h * mask_w floats (VSS_OUT_MODEL) or n * height * width
+ *            (VSS_OUT_FRAME), row-major per frame, in [0,1]. */
 int vss_segment(vss_handle* h, const uint8_t* frames, int n, int height, int width, int channels,
                 size_t row_stride, float* masks_out, int out_mode);
 

@@ -40,6 +40,8 @@ def lib():
         L.vsso_post_guide.restype = I
         L.vsso_composite.argtypes = [P, I, I, I, I, Lg, Lg, P, I, I, P]
         L.vsso_composite.restype = I
+        L.vsso_upsample_mask.argtypes = [P, I, I, I, I, I, P]
+        L.vsso_upsample_mask.restype = I
         L.vsso_bf16_round.argtypes = [ctypes.c_float]
         L.vsso_bf16_round.restype = ctypes.c_float
         _lib = L
@@ -149,4 +151,14 @@ def composite(frames: np.ndarray, alpha_u8: np.ndarray) -> np.ndarray:
     out = np.empty((n, fh, fw, 4), np.uint8)
     if lib().vsso_composite(_ptr(frames), n, fh, fw, c, fw * c, fh * fw * c, _ptr(alpha_u8), H, W, _ptr(out)):
         raise ValueError("vsso_composite")
+    return out
+
+
+def upsample_mask(masks: np.ndarray, fh: int, fw: int) -> np.ndarray:
+    """VSS_OUT_FRAME's masks: [n][H][W] f32 -> [n][fh][fw] (vsso_upsample_mask)."""
+    m = np.ascontiguousarray(masks, np.float32)
+    n, H, W = m.shape
+    out = np.empty((n, fh, fw), np.float32)
+    if lib().vsso_upsample_mask(_ptr(m), n, H, W, fh, fw, _ptr(out)):
+        raise ValueError("vsso_upsample_mask")
     return out

@@ -559,3 +559,29 @@ int vsso_composite(const uint8_t* frames, int n, int fh, int fw, int fc, long ro
   }
   return 0;
 }
+
+/* VSS_OUT_FRAME: model-res f32 masks [n][H][W] -> frame-res [n][fh][fw] with
+ * the compositing upscale's half-pixel bilinear (up_coord above), f32 lerps as
+ * fmaf (the canvas drawImage scaling of frameProcessorTest.ts:177, defined). */
+int vsso_upsample_mask(const float* masks, int n, int H, int W, int fh, int fw, float* out) {
+  if (!masks || !out || n < 0 || H < 1 || W < 1 || fh < 1 || fw < 1) return -1;
+  const float sy = (float)H / (float)fh, sx = (float)W / (float)fw;
+  for (int t = 0; t < n; ++t) {
+    const float* a = masks + (long)t * H * W;
+    for (int y = 0; y < fh; ++y) {
+      int y0, y1;
+      float ly;
+      up_coord(y, sy, H, &y0, &y1, &ly);
+      float* o = out + ((long)t * fh + y) * fw;
+      for (int x = 0; x < fw; ++x) {
+        int x0, x1;
+        float lx;
+        up_coord(x, sx, W, &x0, &x1, &lx);
+        const float top = fmaf(a[y0 * W + x1] - a[y0 * W + x0], lx, a[y0 * W + x0]);
+        const float bot = fmaf(a[y1 * W + x1] - a[y1 * W + x0], lx, a[y1 * W + x0]);
+        o[x] = fmaf(bot - top, ly, top);
+      }
+    }
+  }
+  return 0;
+}

@@ -23,8 +23,15 @@ async function main() {
   const out = Buffer.from(batch.masks.buffer, batch.masks.byteOffset, batch.masks.byteLength);
   fs.writeFileSync(outPath, out);
   const same = single.mask.every((v, i) => v === batch.masks[i]);
+  // outputSize 'frame': masks at the frames' resolution (written next to the model-res ones)
+  const sf = new seg.Segmenter({ dtype: dtype, maxBatch: N, maxFrameWidth: W, maxFrameHeight: H, outputSize: 'frame' });
+  const fr = await sf.segmentFrames(frames);
+  fs.writeFileSync(outPath + '.frame', Buffer.from(fr.masks.buffer, fr.masks.byteOffset, fr.masks.byteLength));
+  sf.close();
+  const frameDims = [fr.width, fr.height, fr.masks.length];
   console.log(JSON.stringify({ width: batch.width, height: batch.height, count: batch.count,
-                               singleMatchesBatch: same, oversizeRejected: rejected, version: seg.version() }));
+                               singleMatchesBatch: same, oversizeRejected: rejected, version: seg.version(),
+                               frameDims: frameDims }));
   s.close();
 }
 main().catch((e) => { console.error(e); process.exit(1); });

@@ -278,3 +278,25 @@ def test_every_compiled_tile_bitwise(pkg, synthetic):
             finally:
                 del os.environ["VSS_TILE"]
     assert not bad, (bad, chosen)
+
+
+@pytest.mark.parametrize("h,w,c", [(480, 640, 3), (720, 1280, 4), (60, 100, 3)])
+def test_output_frame_size(pkg, oracle, synthetic, torch_cuda, h, w, c):
+    """VSS_OUT_FRAME: the masks upsampled on the GPU to the frames' size are the
+    oracle's upsample (vsso_upsample_mask) of the model-res masks, bit for bit,
+    from the host call and from the device call."""
+    torch = torch_cuda
+    f = np.stack([synthetic.make_frame(950 + i, h, w, c) for i in range(2)])
+    with pkg.Session(dtype="bf16x2", max_batch=2, max_frame_h=max(h, 480), max_frame_w=max(w, 640)) as s:
+        m, mw, mh = s.segment_frames(f)
+        fm, fw_, fh_ = s.segment_frames(f, output_size="frame")
+        assert (fw_, fh_) == (w, h) and fm.shape == (2, h * w)
+        want = oracle.upsample_mask(m.reshape(2, mh, mw), h, w)
+        assert np.array_equal(fm.reshape(2, h, w), want)
+        dm = torch.from_numpy(m).cuda()
+        out = torch.empty((2, h, w), dtype=torch.float32, device="cuda")
+        s.mask_to_frame_device(dm.data_ptr(), 2, h, w, out.data_ptr(), 0)
+        s.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want)
+        with pytest.raises(pkg.VssError):
+            s.segment_frames(f, output_size="canvas")

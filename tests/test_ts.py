@@ -61,10 +61,13 @@ def test_node_segment_matches_oracle_and_python_host(addon_built, pkg, oracle, b
     assert out.returncode == 0, out.stderr
     info = json.loads(out.stdout.strip().splitlines()[-1])
     assert info == {"width": 256, "height": 144, "count": 3, "singleMatchesBatch": True,
-                    "oversizeRejected": True, "version": 10000}
+                    "oversizeRejected": True, "version": 10000, "frameDims": [640, 480, 3 * 480 * 640]}
     masks = np.fromfile(op, np.float32).reshape(3, -1)
     ref = oracle.forward(blob, frames, 144, 256, mode=0).reshape(3, -1)
     assert np.abs(masks - ref).max() <= 1e-3
+    # outputSize 'frame' = the model-res masks upsampled (oracle restatement, bitwise)
+    fmasks = np.fromfile(str(op) + ".frame", np.float32).reshape(3, 480, 640)
+    assert np.array_equal(fmasks, oracle.upsample_mask(masks.reshape(3, 144, 256), 480, 640))
     with pkg.Session(dtype=dtype, max_batch=3, max_frame_h=480, max_frame_w=640) as s:
         py, _, _ = s.segment_frames(frames)
     assert np.array_equal(masks, py)

@@ -35,7 +35,7 @@ VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_I
 DTYPES = {"f32": 0, "bf16x2": 1}
 VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_BRANCHES, VSS_OPT_FORWARD, VSS_OPT_FORWARD_FAULTS = 1, 2, 3, 4, 5
 VSS_CREATE_NO_AUTOTUNE = 1
-VSS_OUT_MODEL = 0
+VSS_OUT_MODEL, VSS_OUT_FRAME = 0, 1
 
 
 class VssError(RuntimeError):
@@ -116,6 +116,7 @@ def lib() -> ctypes.CDLL:
                 "vss_segment_async": ([P, P, I, I, I, I, S, P, I, CALLBACK, P], I),
                 "vss_segment_device": ([P, P, I, I, I, I, S, S, P, P], I),
                 "vss_preprocess_device": ([P, P, I, I, I, I, S, S, P, P], I),
+                "vss_mask_to_frame_device": ([P, P, I, I, I, P, P], I),
                 "vss_synchronize": ([P], I),
                 "vss_set_option": ([P, I, I], I),
                 "vss_get_option": ([P, I, ctypes.POINTER(I)], I),
@@ -206,14 +207,18 @@ class Session:
         self.close()
 
     # -- the seam -----------------------------------------------------------
-    def segment_frames(self, frames: np.ndarray):
-        """frames [N,H,W,3|4] uint8 -> (masks float32 [N, maskH*maskW], maskW, maskH)."""
+    def segment_frames(self, frames: np.ndarray, output_size: str = "model"):
+        """frames [N,H,W,3|4] uint8 -> (masks float32 [N, maskH*maskW], maskW, maskH); with
+        output_size="frame" the masks come upsampled on the GPU: ([N, H*W], W, H)."""
         f = _as_frames(frames)
         n, hh, ww, c = f.shape
-        out = np.empty((n, self.mask_h * self.mask_w), np.float32)
-        _check(lib().vss_segment(self._h, f.ctypes.data, n, hh, ww, c, ww * c, out.ctypes.data, VSS_OUT_MODEL),
-               self._h)
-        return out, self.mask_w, self.mask_h
+        if output_size not in ("model", "frame"):
+            raise VssError(VSS_E_INVALID_ARG, "output_size must be 'model' or 'frame'")
+        frame = output_size == "frame"
+        out = np.empty((n, hh * ww if frame else self.mask_h * self.mask_w), np.float32)
+        _check(lib().vss_segment(self._h, f.ctypes.data, n, hh, ww, c, ww * c, out.ctypes.data,
+                                 VSS_OUT_FRAME if frame else VSS_OUT_MODEL), self._h)
+        return (out, ww, hh) if frame else (out, self.mask_w, self.mask_h)
 
     def segment_frame(self, frame: np.ndarray):
         """One frame -> (alphaRaw float32[maskH*maskW], maskW, maskH)  (frameProcessorTest.ts:95-97)."""
@@ -240,6 +245,12 @@ class Session:
                        masks_ptr: int, stream: int = 0):
         _check(lib().vss_segment_device(self._h, frames_ptr, n, h, w, c, row_stride, frame_stride, masks_ptr,
                                         stream or None), self._h)
+
+    def mask_to_frame_device(self, masks_ptr: int, n: int, frame_h: int, frame_w: int, out_ptr: int,
+                             stream: int = 0):
+        """HBM masks [n][maskH][maskW] -> [n][frame_h][frame_w] (VSS_OUT_FRAME's upsample)."""
+        _check(lib().vss_mask_to_frame_device(self._h, masks_ptr, n, frame_h, frame_w, out_ptr, stream or None),
+               self._h)
 
     def preprocess_device(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int,
                           frame_stride: int, out_ptr: int, stream: int = 0):

@@ -96,6 +96,11 @@ struct vss_handle {
   size_t frame_cap = 0;
   uint8_t* h_frames = nullptr;  // pinned staging
   float* h_masks = nullptr;
+  float* d_fmasks = nullptr;  // VSS_OUT_FRAME: masks at frame resolution (allocated on first use)
+  float* h_fmasks = nullptr;
+  size_t fmask_cap = 0;       // floats
+  const float* out_src = nullptr;  // what the last staged call left for the host copy
+  size_t out_bytes = 0;
 #ifdef VSS_TRACE
   std::vector<unsigned long long*> trace;  // per layer, [grid][4] stamps
   std::vector<int> trace_wgs;              // workgroups of the layer's last launch
@@ -860,27 +865,58 @@ struct Busy {
   ~Busy() { release(); }
 };
 
+void enqueue_upmask(const vss_handle* h, const float* d_masks, int n, int fh, int fw, float* d_out, hipStream_t s) {
+  UpmaskParams p{};
+  p.masks = d_masks;
+  p.H = h->cfg.model_h;
+  p.W = h->cfg.model_w;
+  p.sy = (float)p.H / (float)fh;
+  p.sx = (float)p.W / (float)fw;
+  p.out = d_out;
+  p.fh = fh;
+  p.fw = fw;
+  launch_upmask(p, n, s);
+}
+
 int stage_in(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, float* masks_out,
              int out_mode) {
   if (!frames || !masks_out) return fail(h, VSS_E_INVALID_ARG, "null frames/masks_out");
-  if (out_mode != VSS_OUT_MODEL) return fail(h, VSS_E_UNSUPPORTED, "only VSS_OUT_MODEL masks are supported");
+  if (out_mode != VSS_OUT_MODEL && out_mode != VSS_OUT_FRAME)
+    return fail(h, VSS_E_INVALID_ARG, "out_mode must be VSS_OUT_MODEL or VSS_OUT_FRAME");
   int rc = check_frames(h, n, fh, fw, fc, rs, rs * (size_t)fh);
   if (rc) return rc;
   const size_t bytes = (size_t)n * fh * rs;
   if (bytes > h->frame_cap)
     return fail(h, VSS_E_INVALID_ARG, "frames exceed the handle's staging capacity (max_frame_h/w)");
+  if (out_mode == VSS_OUT_FRAME && !h->d_fmasks) {  // sized for max_batch frames of the largest size
+    const size_t cap = (size_t)h->cfg.max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w;
+    if ((rc = dalloc(h, &h->d_fmasks, cap * 4))) return rc;
+    HIP_TRY(h, hipHostMalloc((void**)&h->h_fmasks, cap * 4, hipHostMallocDefault));
+    h->fmask_cap = cap;
+  }
+  if (out_mode == VSS_OUT_FRAME && (size_t)n * fh * fw > h->fmask_cap)
+    return fail(h, VSS_E_INVALID_ARG, "frame-size masks exceed max_batch * max_frame_h * max_frame_w");
   std::memcpy(h->h_frames, frames, bytes);
   HIP_TRY(h, hipMemcpyAsync(h->d_frames, h->h_frames, bytes, hipMemcpyHostToDevice, h->stream));
   rc = forward(h, h->d_frames, n, fh, fw, fc, rs, rs * (size_t)fh, h->d_masks, h->stream);
   if (rc) return rc;
-  const size_t mbytes = (size_t)n * h->cfg.model_h * h->cfg.model_w * 4;
-  HIP_TRY(h, hipMemcpyAsync(h->h_masks, h->d_masks, mbytes, hipMemcpyDeviceToHost, h->stream));
+  if (out_mode == VSS_OUT_FRAME) {
+    enqueue_upmask(h, h->d_masks, n, fh, fw, h->d_fmasks, h->stream);
+    h->out_src = h->h_fmasks;
+    h->out_bytes = (size_t)n * fh * fw * 4;
+    HIP_TRY(h, hipMemcpyAsync(h->h_fmasks, h->d_fmasks, h->out_bytes, hipMemcpyDeviceToHost, h->stream));
+  } else {
+    h->out_src = h->h_masks;
+    h->out_bytes = (size_t)n * h->cfg.model_h * h->cfg.model_w * 4;
+    HIP_TRY(h, hipMemcpyAsync(h->h_masks, h->d_masks, h->out_bytes, hipMemcpyDeviceToHost, h->stream));
+  }
   return VSS_OK;
 }
 
 struct AsyncCtx {
   vss_handle* h;
   float* out;
+  const float* src;
   size_t bytes;
   vss_callback cb;
   void* user;
@@ -888,7 +924,7 @@ struct AsyncCtx {
 
 void async_done(void* p) {
   AsyncCtx* c = static_cast<AsyncCtx*>(p);
-  std::memcpy(c->out, c->h->h_masks, c->bytes);
+  std::memcpy(c->out, c->src, c->bytes);
   c->h->busy.store(0);
   if (c->cb) c->cb(c->user, VSS_OK);
   delete c;
@@ -1062,6 +1098,7 @@ void vss_destroy(vss_handle* h) {
   for (void* p : h->dev_allocs) (void)hipFree(p);
   if (h->h_frames) (void)hipHostFree(h->h_frames);
   if (h->h_masks) (void)hipHostFree(h->h_masks);
+  if (h->h_fmasks) (void)hipHostFree(h->h_fmasks);
   if (h->fwd_dbg) (void)hipHostFree(h->fwd_dbg);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1086,7 +1123,7 @@ int vss_segment(vss_handle* h, const uint8_t* frames, int n, int height, int wid
   int rc = stage_in(h, frames, n, height, width, channels, row_stride, masks_out, out_mode);
   if (rc) return rc;
   HIP_TRY(h, hipStreamSynchronize(h->stream));
-  std::memcpy(masks_out, h->h_masks, (size_t)n * h->cfg.model_h * h->cfg.model_w * 4);
+  std::memcpy(masks_out, h->out_src, h->out_bytes);
   return VSS_OK;
 }
 
@@ -1098,7 +1135,7 @@ int vss_segment_async(vss_handle* h, const uint8_t* frames, int n, int height, i
   HIP_TRY(h, hipSetDevice(h->device));
   int rc = stage_in(h, frames, n, height, width, channels, row_stride, masks_out, out_mode);
   if (rc) return rc;
-  AsyncCtx* c = new AsyncCtx{h, masks_out, (size_t)n * h->cfg.model_h * h->cfg.model_w * 4, cb, user};
+  AsyncCtx* c = new AsyncCtx{h, masks_out, h->out_src, h->out_bytes, cb, user};
   hipError_t e = hipLaunchHostFunc(h->stream, async_done, c);
   if (e != hipSuccess) {
     delete c;
@@ -1119,6 +1156,18 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
   HIP_TRY(h, hipSetDevice(h->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
   return forward(h, d_frames, n, height, width, channels, row_stride, frame_stride, d_masks, s);
+}
+
+int vss_mask_to_frame_device(vss_handle* h, const float* d_masks, int n, int frame_h, int frame_w, float* d_out,
+                             void* stream) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (!d_masks || !d_out) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
+  if (n < 1 || n > h->cfg.max_batch || frame_h < 1 || frame_w < 1)
+    return fail(h, VSS_E_INVALID_ARG, "n must be 1..max_batch and the frame size positive");
+  HIP_TRY(h, hipSetDevice(h->device));
+  enqueue_upmask(h, d_masks, n, frame_h, frame_w, d_out, stream ? static_cast<hipStream_t>(stream) : h->stream);
+  HIP_TRY(h, hipGetLastError());
+  return VSS_OK;
 }
 
 int vss_preprocess_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width, int channels,

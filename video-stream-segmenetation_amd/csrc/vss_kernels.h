@@ -347,6 +347,17 @@ struct CompositeParams {
 };
 void launch_composite(const CompositeParams& p, int n, hipStream_t s);
 
+// VSS_OUT_FRAME: the f32 model-res masks upsampled to frame resolution with
+// the same half-pixel bilinear as the compositing alpha (k_composite).
+struct UpmaskParams {
+  const float* masks;  // [n][H][W]
+  int H, W;
+  float sy, sx;        // (float)H / fh, (float)W / fw
+  float* out;          // [n][fh][fw]
+  int fh, fw;
+};
+void launch_upmask(const UpmaskParams& p, int n, hipStream_t s);
+
 void launch_post_ema(const PostEmaParams& p, hipStream_t s);
 void launch_post_filter(const PostFilterParams& p, int n, hipStream_t s);
 

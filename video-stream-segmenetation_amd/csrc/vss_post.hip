@@ -219,6 +219,40 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
   }
 }
 
+// 4 output pixels per thread, one 16-B store; the taps' rows are L2-resident.
+__global__ __launch_bounds__(256) void k_upmask(UpmaskParams p) {
+#pragma clang fp contract(off)
+  const int t = blockIdx.z;
+  const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int x0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
+  if (y >= p.fh || x0 >= p.fw) return;
+  int ya, yb;
+  float ly;
+  up_coord(y, p.sy, p.H, ya, yb, ly);
+  const float* ra = p.masks + ((long)t * p.H + ya) * p.W;
+  const float* rb = p.masks + ((long)t * p.H + yb) * p.W;
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int x = min(x0 + k, p.fw - 1);
+    int xa, xb;
+    float lx;
+    up_coord(x, p.sx, p.W, xa, xb, lx);
+    const float top = __builtin_fmaf(ra[xb] - ra[xa], lx, ra[xa]), bot = __builtin_fmaf(rb[xb] - rb[xa], lx, rb[xa]);
+    v[k] = __builtin_fmaf(bot - top, ly, top);
+  }
+  float* o = p.out + ((long)t * p.fh + y) * p.fw + x0;
+  if (x0 + 4 <= p.fw && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (int k = 0; k < 4 && x0 + k < p.fw; ++k) o[k] = v[k];
+  }
+}
+
+void launch_upmask(const UpmaskParams& p, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_upmask, dim3((p.fw + 255) / 256, (p.fh + 3) / 4, n), dim3(256), 0, s, p);
+}
+
 void launch_composite(const CompositeParams& p, int n, hipStream_t s) {
   hipLaunchKernelGGL(k_composite, dim3((p.fw + 255) / 256, (p.fh + 3) / 4, n), dim3(256), 0, s, p);
 }

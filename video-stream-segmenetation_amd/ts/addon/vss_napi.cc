@@ -8,8 +8,9 @@
 //   create(opts) -> handle            (opts: modelH, modelW, dtype, deviceId, maxBatch,
 //                                       maxFrameH, maxFrameW, weightsPath, autotune)
 //   info(handle) -> {maskW, maskH, nLayers, deviceBytes}
-//   segment(handle, frames: Uint8Array|Uint8ClampedArray, n, height, width, channels, rowStride)
-//       -> Promise<Float32Array>      (n * maskH * maskW masks; rejects with Error(vss_last_error))
+//   segment(handle, frames: Uint8Array|Uint8ClampedArray, n, height, width, channels, rowStride, outMode?)
+//       -> Promise<Float32Array>      (n * maskH * maskW masks, or n * height * width with
+//                                      outMode 1 = VSS_OUT_FRAME; rejects with Error(vss_last_error))
 //   destroy(handle)
 //   postCreate(handle, config?) -> post     (config keys as the reference's `config`:
 //                                             EMA, NOISE_CUTOFF, HIGH_THRESHOLD, GAMMA,
@@ -332,7 +333,7 @@ struct SegmentWork {
   const uint8_t* frames = nullptr;
   float* out = nullptr;
   uint8_t* out_u8 = nullptr;
-  int n = 0, height = 0, width = 0, channels = 0;
+  int n = 0, height = 0, width = 0, channels = 0, out_mode = VSS_OUT_MODEL;
   size_t row_stride = 0, out_count = 0;
   int rc = 0;
   std::string err;
@@ -347,8 +348,7 @@ void SegmentExecute(napi_env, void* data) {  // libuv worker thread: no JS calls
     w->rc = vss_segment_post(w->h, w->post, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out,
                              w->out_u8);
   else
-    w->rc =
-        vss_segment(w->h, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out, VSS_OUT_MODEL);
+    w->rc = vss_segment(w->h, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out, w->out_mode);
   if (w->rc != VSS_OK) w->err = vss_last_error(w->h);
 }
 
@@ -394,8 +394,8 @@ void SegmentComplete(napi_env env, napi_status, void* data) {
 
 // segment(handle, frames, ...) and segmentPost(handle, post, frames, ...)
 napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post, bool composite = false) {
-  size_t argc = 8;
-  napi_value all[8];
+  size_t argc = 9;
+  napi_value all[9];
   NAPI_OK(env, napi_get_cb_info(env, info, &argc, all, nullptr, nullptr));
   const size_t need = with_post ? 8 : 7;
   if (argc < need) {
@@ -447,7 +447,9 @@ napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post, bo
   w->h = hd->h;
   w->post = ps ? ps->st : nullptr;
   w->frames = static_cast<const uint8_t*>(data);
-  w->out_count = (size_t)w->n * hd->mask_h * hd->mask_w;
+  if (!with_post && argc >= 8) napi_get_value_int32(env, argv[7], &w->out_mode);
+  w->out_count = w->out_mode == VSS_OUT_FRAME ? (size_t)w->n * w->height * w->width
+                                              : (size_t)w->n * hd->mask_h * hd->mask_w;
   napi_value ab;
   void* out = nullptr;
   NAPI_OK(env, napi_create_arraybuffer(env, w->out_count * 4, &out, &ab));
