@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SPEC = os.path.join(ROOT, "video-stream-segmenetation_amd", "model", "spec.json")
 CANDIDATES = [(8, 16), (6, 16), (4, 16), (3, 16), (8, 8), (6, 8), (4, 8), (2, 16), (2, 8), (1, 16)]
 MAX_ACC, MAX_LDS = 16, 160 * 1024
+HID_STRIDE = 20  # kHidStride in csrc/vss_kernels.h
 SHARDS = 6  # compile units for the block shapes (csrc/Makefile: VSS_SHARDS)
 
 
@@ -64,7 +65,7 @@ def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=False)
     f += r4(2 * cin) if mode == 2 else 0
     # work: expand scratch / slabs / (decoder) the low-res src region; the
     # decoder's norm slots and stats scratch live in xt
-    f += max(4 * p_in_pad * 16 if mode == 0 else 1024, cs * p_out * (cout + 4),
+    f += max(4 * p_in_pad * HID_STRIDE if mode == 0 else 1024, cs * p_out * (cout + 4),
              r4(sr * sc * cin) if mode == 2 else 0, stem_in_lds(ih, iw) if stem_in else 0)
     return f * 4, nacc
 

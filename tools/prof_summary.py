@@ -34,7 +34,7 @@ def main():
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
     pmc = defaultdict(lambda: defaultdict(list))
-    for kind in ("fetch", "write"):
+    for kind in ("fetch", "write", "mfma"):
         p = os.path.join(src, kind, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -54,6 +54,14 @@ def main():
         traffic[name] = {"avg_ns": avg_ns, "calls": int(s["Calls"]), "fetch_bytes": fetch_b,
                          "write_bytes": write_b, "traffic_bytes": tb,
                          "traffic_GBps": (tb / avg_ns) if tb else None}
+        mf = {c: sum(v) / len(v) for c, v in pmc.get(name, {}).items() if c not in ("FETCH_SIZE", "WRITE_SIZE") and v}
+        if mf:
+            traffic[name]["sq"] = mf
+            g = mf.get("GRBM_GUI_ACTIVE")
+            if g and "SQ_VALU_MFMA_BUSY_CYCLES" in mf:
+                # MFMA pipe busy over every SIMD's active cycles: GRBM_GUI_ACTIVE is
+                # summed over the 8 XCDs (MI355X_MICROARCH.md), 32 CUs x 4 SIMDs each
+                traffic[name]["mfma_util"] = mf["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8.0 * 256 * 4)
     json.dump(traffic, open(os.path.join(out, f"{tag}_traffic.json"), "w"), indent=1)
     log = open(os.path.join(src, "trace.log")).read().strip().splitlines()
     bench_line = next((l for l in reversed(log) if l.startswith("{")), "")
@@ -62,11 +70,18 @@ def main():
         fh.write("Command: `bash tools/prof_run.sh " + tag + " ...` (kernel trace + stats pass; separate FETCH_SIZE "
                  "and WRITE_SIZE PMC passes).  HBM bytes = 2 x FETCH_SIZE KiB + WRITE_SIZE KiB (gfx950 "
                  "correction); memory-side counters include Infinity-Cache hits.\n\n")
-        fh.write("| kernel | calls | mean us | HBM read MB/launch | HBM write MB/launch | GB/s (PMC) |\n")
-        fh.write("|---|---|---|---|---|---|\n")
+        fh.write("| kernel | calls | mean us | HBM read MB/launch | HBM write MB/launch | GB/s (PMC) | MFMA util | "
+                 "MFMA insts | VALU insts | LDS insts | LDS bank conflicts |\n")
+        fh.write("|---|---|---|---|---|---|---|---|---|---|---|\n")
         for name, calls, ns, fb, wb, tb in rows:
+            t = traffic[name]
+            sq = t.get("sq", {})
+            mu = t.get("mfma_util")
+            fmt = lambda k: f"{sq[k]:.0f}" if k in sq else "-"
             fh.write(f"| `{name}` | {calls} | {ns / 1e3:.2f} | {fb / 1e6 if fb else 0:.3f} | "
-                     f"{wb / 1e6 if wb else 0:.3f} | {tb / ns if tb else 0:.0f} |\n")
+                     f"{wb / 1e6 if wb else 0:.3f} | {tb / ns if tb else 0:.0f} | "
+                     f"{'-' if mu is None else f'{100 * mu:.2f}%'} | {fmt('SQ_INSTS_MFMA')} | {fmt('SQ_INSTS_VALU')} | "
+                     f"{fmt('SQ_INSTS_LDS')} | {fmt('SQ_LDS_BANK_CONFLICT')} |\n")
         if bench_line:
             fh.write("\nbench line of the traced run:\n\n```\n" + bench_line + "\n```\n")
     print(open(os.path.join(out, f"{tag}_summary.md")).read())

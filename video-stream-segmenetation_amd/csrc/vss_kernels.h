@@ -43,6 +43,9 @@ __host__ __device__ constexpr int flags_ks(int f) { return ((f >> 6) & 3) + 1; }
 
 constexpr int kThreads = 256;       // 4 wave64 per workgroup
 constexpr int kMaxAcc = 16;         // 16x16 project accumulators per wave
+constexpr int kHidStride = 20;      // floats per pixel of an expand wave's hidden chunk in LDS: 16
+                                    // channels + 4 pad, so the 16 lanes of one 16-B LDS access
+                                    // (lane = pixel) hit 16 distinct bank quads (stride 16: 4-way)
 constexpr int kAccSlots = 16;       // instance-norm accumulator slots per frame and layer
                                     // (spreads the producers' atomics over 16x the cache lines)
 
@@ -112,7 +115,7 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   // both points (before the input tile is committed / after the main loop).
   L.work = o;
   L.lr = o;
-  o += cmax(cmax(cmax(mode == 0 ? 4 * L.P_in_pad * 16 : 1024, L.CS * L.slab_stride),
+  o += cmax(cmax(cmax(mode == 0 ? 4 * L.P_in_pad * kHidStride : 1024, L.CS * L.slab_stride),
                  mode == 2 ? r4(L.SR * L.SC * cin) : 0),
             stem_in ? stem_in_lds(L.IH, L.IW) : 0);
   L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;

@@ -692,7 +692,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   const int pw = wave % PW, cw = wave / PW;
 
   if constexpr (MODE == MODE_IR_EXPAND) {
-    float* hid = work + wave * P_IN_PAD * 16;
+    float* hid = work + wave * P_IN_PAD * kHidStride;
     constexpr int NK = CIN / 16;
     for (int ck = wave; ck < NCHUNK; ck += 4) {
       const int c0 = ck << 4;
@@ -709,7 +709,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         for (int s = 0; s < NK; ++s) d = mma16_op<PREC>(d, aw[s], *reinterpret_cast<const f4*>(xt + pix * XS + 16 * s + 4 * g));
         const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
         const bool valid = pix < P_IN && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
-        *reinterpret_cast<f4*>(hid + pix * 16 + 4 * g) = valid ? relu6v(d + bias) : f4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(hid + pix * kHidStride + 4 * g) = valid ? relu6v(d + bias) : f4{0.f, 0.f, 0.f, 0.f};
       }
       wave_sync();
       // dw 3x3 computed straight into the project MFMA's B layout: lane (r, g)
@@ -732,7 +732,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
               const int sp = (STRIDE * ly + ky) * IW + (STRIDE * lx + kx);
-              a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(hid + sp * 16 + 4 * g) + a;
+              a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(hid + sp * kHidStride + 4 * g) + a;
             }
           const f4 b = to_operand<PREC>(relu6v(a));
 #pragma unroll
