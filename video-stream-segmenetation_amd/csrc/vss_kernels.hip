@@ -75,6 +75,12 @@ struct Gm {
     else
       *reinterpret_cast<f4*>(const_cast<float*>(b) + i) = v;
   }
+  __device__ __forceinline__ void st1(long i, float v) const {
+    if constexpr (COH)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)(i * 4), 0, 16);
+    else
+      const_cast<float*>(b)[i] = v;
+  }
 };
 
 __device__ __forceinline__ float relu6f(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
@@ -167,7 +173,41 @@ __global__ __launch_bounds__(256) void k_prep(PrepParams p) {
 #endif
 
 // ---------------------------------------------------------------------------
-// Stem: output tile 8 x 32 pixels x 16 channels, one pixel per thread.
+// The stem's 3x3 stride-2 conv (3 -> 16 channels) for a block of 16 output
+// pixels on the MFMA (v_mfma_f32_16x16x4_f32): D[pixel][channel] = bias +
+// sum over the 27 taps k = ci*9 + ky*3 + kx of x0[pixel][k] * w[channel][k],
+// K padded to 28 with a zero weight, in 7 MFMAs of K = 4.  Lane (r, g) hands
+// A[pixel r][tap 4s+g] (one LDS read) and B[tap 4s+g][channel r] (a register)
+// and gets back D[pixel 4g+i][channel r].  Each output depends only on its own
+// pixel's taps, so k_stem and the STEM_IN prologue (any tile) give bitwise the
+// same activations.  (A per-lane FMA chain over the taps read 27 f4 weights
+// and 27 x0 values from LDS per 4 outputs: LDS-bandwidth bound, 2.6 us.)
+struct StemTaps {
+  int off[7];  // LDS offset of tap 4s+g from the pixel's x0 corner (2py, 2px)
+  float w[7];  // w[channel r][tap 4s+g]
+};
+
+__device__ __forceinline__ StemTaps stem_taps(const float* ws /* [tap][16] */, int r, int g, int plane, int row) {
+  StemTaps t;
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    const int k = 4 * s + g;
+    const int ci = k / 9, ky = (k % 9) / 3, kx = k % 3;
+    t.off[s] = k < 27 ? ci * plane + ky * row + kx : 0;
+    t.w[s] = k < 27 ? ws[min(k, 26) * 16 + r] : 0.f;
+  }
+  return t;
+}
+
+__device__ __forceinline__ f4 stem_mfma(const StemTaps& t, const float* x0, float bias) {
+  f4 acc = {bias, bias, bias, bias};
+#pragma unroll
+  for (int s = 0; s < 7; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[t.off[s]], t.w[s], acc, 0, 0, 0);
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// Stem: output tile 8 x 32 pixels x 16 channels, 16-pixel blocks on the MFMA.
 template <int COUT, bool COH>
 __device__ __forceinline__ void stem_body(const StemParams& p, int bx, int by, int n, float* smem) {
   constexpr int TH = kStemTH, TW = kStemTW, IH = kStemIH, IW = 2 * TW + 1, IWP = kStemIWP;
@@ -231,34 +271,20 @@ __device__ __forceinline__ void stem_body(const StemParams& p, int bx, int by, i
   __syncthreads();
   VSS_STAMP(1);
   VSS_STAMP(2);
-  const int ly = tid / TW, lx = tid - ly * TW;
-  float acc[COUT];
+  const int lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const StemTaps taps = stem_taps(ws, r, g, IH * IWP, IWP);
+  const float bias = bs[r];
+  const Gm<COH> gy(p.y + (long)n * p.Ho * p.Wo * COUT);
 #pragma unroll
-  for (int c = 0; c < COUT; ++c) acc[c] = bs[c];
+  for (int blk = wave; blk < TH * TW / 16; blk += 4) {
+    const int pa = blk * 16 + r, ly = pa / TW, lx = pa % TW;
+    const f4 acc = stem_mfma(taps, &xs[0][2 * ly][2 * lx], bias);
 #pragma unroll
-  for (int ci = 0; ci < 3; ++ci)
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const float xv = xs[ci][2 * ly + ky][2 * lx + kx];
-        const f4* wt = reinterpret_cast<const f4*>(ws + (ci * 9 + ky * 3 + kx) * COUT);
-#pragma unroll
-        for (int q = 0; q < COUT / 4; ++q) {
-          const f4 w4 = wt[q];
-          acc[4 * q] = __builtin_fmaf(w4.x, xv, acc[4 * q]);
-          acc[4 * q + 1] = __builtin_fmaf(w4.y, xv, acc[4 * q + 1]);
-          acc[4 * q + 2] = __builtin_fmaf(w4.z, xv, acc[4 * q + 2]);
-          acc[4 * q + 3] = __builtin_fmaf(w4.w, xv, acc[4 * q + 3]);
-        }
-      }
-  const int oy = oy0 + ly, ox = ox0 + lx;
-  if (oy < p.Ho && ox < p.Wo) {
-    const Gm<COH> gy(p.y + (long)n * p.Ho * p.Wo * COUT);
-    const long o = ((long)oy * p.Wo + ox) * COUT;
-#pragma unroll
-    for (int q = 0; q < COUT / 4; ++q)
-      gy.st(o + 4 * q, f4{relu6f(acc[4 * q]), relu6f(acc[4 * q + 1]), relu6f(acc[4 * q + 2]), relu6f(acc[4 * q + 3])});
+    for (int i = 0; i < 4; ++i) {  // D[pixel 4g+i][channel r]
+      const int pp = blk * 16 + 4 * g + i;
+      const int oy = oy0 + pp / TW, ox = ox0 + pp % TW;
+      if (oy < p.Ho && ox < p.Wo) gy.st1(((long)oy * p.Wo + ox) * COUT + r, relu6f(acc[i]));
+    }
   }
   VSS_STAMP(3);
 }
@@ -616,37 +642,25 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     VSS_STAMP(4);
     __syncthreads();
-    // stem outputs of the region: one (pixel, 4-channel group) per item
-    const Gm<COH> gst(sp.y + (long)n * H * W * 16);
-    for (int i = tid; i < P_IN_PAD * 4; i += 256) {
-      const int pix = i >> 2, q = i & 3;
-      const int py = pix / IW, px = pix - (pix / IW) * IW;
-      const int yy = iy0 + py, xx = ix0 + px;
-      f4 a = {0.f, 0.f, 0.f, 0.f};
-      if (pix < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        float acc[4];
+    VSS_STAMP(5);  // resized region in LDS: the stem conv starts
+    // stem outputs of the region, 16-pixel blocks on the MFMA (stem_mfma,
+    // bitwise k_stem's), zero outside the image
+    {
+      const StemTaps taps = stem_taps(sws, r, g, XH * XWP, XWP);
+      const float bias = sbs[r];
+      for (int blk = wave; blk < P_IN_PAD / 16; blk += 4) {
+        const int pa = min(blk * 16 + r, P_IN - 1), py = pa / IW, px = pa - py * IW;
+        const f4 acc = stem_mfma(taps, x0s + 2 * py * XWP + 2 * px, bias);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = sbs[4 * q + c];
-#pragma unroll
-        for (int ci = 0; ci < 3; ++ci)
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-              const float xv = x0s[(ci * XH + 2 * py + ky) * XWP + 2 * px + kx];
-              const f4 w4 = *reinterpret_cast<const f4*>(sws + (ci * 9 + ky * 3 + kx) * 16 + 4 * q);
-              acc[0] = __builtin_fmaf(w4.x, xv, acc[0]);
-              acc[1] = __builtin_fmaf(w4.y, xv, acc[1]);
-              acc[2] = __builtin_fmaf(w4.z, xv, acc[2]);
-              acc[3] = __builtin_fmaf(w4.w, xv, acc[3]);
-            }
-        a = f4{relu6f(acc[0]), relu6f(acc[1]), relu6f(acc[2]), relu6f(acc[3])};
-        // the stem activation itself (its tile centre, written once): what
-        // vss_read_layer reports for the stem
-        if (py >= 1 && py <= TH && px >= 1 && px <= TW) gst.st(((long)yy * W + xx) * 16 + 4 * q, a);
+        for (int i = 0; i < 4; ++i) {  // D[pixel 4g+i][channel r]
+          const int pp = blk * 16 + 4 * g + i, qy = pp / IW, qx = pp - qy * IW;
+          const int yy = iy0 + qy, xx = ix0 + qx;
+          const bool valid = pp < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+          xt[pp * XS + r] = valid ? relu6f(acc[i]) : 0.f;
+        }
       }
-      *reinterpret_cast<f4*>(xt + pix * XS + 4 * q) = a;
     }
+
   } else {
     constexpr int C4 = CIN / 4;
     const int H = p.H, W = p.W;
@@ -788,10 +802,13 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       }
   }
   __syncthreads();
-  constexpr int C4O = COUT / 4;
+  constexpr int C4O = COUT / 4, NOUT = (P_OUT * C4O + 255) / 256;
   const Gm<COH> gy(p.y + ks * p.y_part_stride + (long)n * Ho * Wo * COUT);
+  // the decoder keeps its outputs in registers until its stats are done: a
+  // workgroup barrier waits for every store issued before it (vmcnt(0))
+  f4 outv[MODE == MODE_DEC ? NOUT : 1];
 #pragma unroll
-  for (int k = 0; k < (P_OUT * C4O + 255) / 256; ++k) {
+  for (int k = 0; k < NOUT; ++k) {
     const int i = tid + 256 * k;
     if (i < P_OUT * C4O) {
       const int pix = i / C4O, c4 = i % C4O;
@@ -811,9 +828,12 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
             v = v + *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + 4 * c4);
         }
       }
-      if (valid) gy.st(((long)oy * Wo + ox) * COUT + 4 * c4, v);
-      if constexpr (MODE == MODE_DEC)
+      if constexpr (MODE == MODE_DEC) {
+        outv[k] = v;
         *reinterpret_cast<f4*>(work + pix * RS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+      } else if (valid) {
+        gy.st(((long)oy * Wo + ox) * COUT + 4 * c4, v);
+      }
     }
   }
   if constexpr (MODE == MODE_DEC) {
@@ -847,7 +867,31 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       __hip_atomic_fetch_add(p.out_acc + (long)n * p.acc_stride + slot * 2 * COUT + tid, (unsigned long long)t,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) {
+      const int i = tid + 256 * k;
+      if (i < P_OUT * C4O) {
+        const int pix = i / C4O, c4 = i % C4O;
+        const int oy = oy0 + pix / TW, ox = ox0 + pix % TW;
+        if (oy < Ho && ox < Wo) gy.st(((long)oy * Wo + ox) * COUT + 4 * c4, outv[k]);
+      }
+    }
   }
+#ifndef VSS_EXP_NO_STEM_STORE
+  if constexpr (STEM_IN) {
+    // the stem activation itself (the tile centre of xt, intact through the
+    // epilogue): what vss_read_layer reports for the stem; last, so that no
+    // barrier waits for these stores
+    const Gm<COH> gst(p.stem.y + (long)n * p.H * p.W * 16);
+    for (int i = tid; i < TH * TW * 4; i += 256) {
+      const int pix = i >> 2, q = i & 3;
+      const int yy = oy0 + pix / TW, xx = ox0 + pix % TW;
+      if (yy < p.H && xx < p.W)
+        gst.st(((long)yy * p.W + xx) * 16 + 4 * q,
+               *reinterpret_cast<const f4*>(xt + ((pix / TW + 1) * IW + pix % TW + 1) * XS + 4 * q));
+    }
+  }
+#endif
   VSS_STAMP(3);
 }
 
