@@ -230,6 +230,32 @@ int vss_postprocess_device(vss_post_state* st, const uint8_t* d_frames, int n, i
                            int channels, size_t row_stride, size_t frame_stride, const float* d_masks,
                            float* d_alpha, uint8_t* d_alpha_u8, void* stream);
 
+/* §8(f) row 4: the face stabiliser's inputs to the post chain, per frame
+ * (processFrame's opts.lastAffine and its face detection,
+ * frameProcessorTest.ts:99-114, :131-166):
+ *   has_affine: warp prevAlpha by the affine (warpAffineNearest :335 with
+ *               invertAffine :323) and blend it 0.3 / 0.7 into the mask
+ *               before the EMA (:102-113);
+ *   has_box:    the elliptical face prior of the detection box (facePriorMask
+ *               :697-741) -> a 3x3 closing inside it after the opening
+ *               (morphologicalClosingInPrior :743-787) and the prior's clamp
+ *               in refineAlphaOnce (:297-307).
+ * Doubles, as the reference's JS numbers; video_w/h = the video size the box
+ * is in (0 = the frames' size). */
+typedef struct vss_face_frame {
+  int has_affine;
+  double affine[6];   /* a11, a12, tx, a21, a22, ty (estimateAffineFromLandmarks's form, :455-563) */
+  int has_box;
+  double box[4];      /* x0, y0, x1, y1 in video pixels (runFaceDetector's box, :396-452) */
+  int video_w, video_h;
+} vss_face_frame;
+
+/* The face inputs of the NEXT vss_postprocess_device / vss_segment_post call on
+ * this state, one per frame of that call (n must match it); consumed by it.
+ * d_faces: the same from device memory (e.g. written by the GPU face stage). */
+int vss_post_set_faces(vss_post_state* st, const vss_face_frame* faces, int n);
+int vss_post_set_faces_device(vss_post_state* st, const vss_face_frame* d_faces, int n);
+
 /* Host-memory convenience: seam + post chain for n consecutive frames of the
  * state's stream (replaces frameProcessorTest.ts:78-169 up to putImageData). */
 int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, int n, int height, int width,

@@ -40,6 +40,8 @@ def lib():
         L.vsso_post_guide.restype = I
         L.vsso_composite.argtypes = [P, I, I, I, I, Lg, Lg, P, I, I, P]
         L.vsso_composite.restype = I
+        L.vsso_post_face.argtypes = [P, I, I, I, P, I, I, I, Lg, Lg, P, P, P, P, P, P]
+        L.vsso_post_face.restype = I
         L.vsso_upsample_mask.argtypes = [P, I, I, I, I, I, P]
         L.vsso_upsample_mask.restype = I
         L.vsso_bf16_round.argtypes = [ctypes.c_float]
@@ -125,8 +127,27 @@ class PostState:
         self.valid = ctypes.c_int(0)
 
 
-def post(masks: np.ndarray, frames: np.ndarray, state: PostState, cfg: PostConfig | None = None):
-    """(refined alpha [n][H][W] f32, alpha bytes [n][H][W] u8) for consecutive frames of one stream."""
+class Face(ctypes.Structure):
+    """Mirror of vsso_face / vss_face_frame: one frame's face inputs."""
+    _fields_ = [("has_affine", ctypes.c_int), ("affine", ctypes.c_double * 6), ("has_box", ctypes.c_int),
+                ("box", ctypes.c_double * 4), ("video_w", ctypes.c_int), ("video_h", ctypes.c_int)]
+
+    @classmethod
+    def make(cls, affine=None, box=None, video_wh=(0, 0)):
+        f = cls()
+        if affine is not None:
+            f.has_affine = 1
+            f.affine[:] = [float(v) for v in affine]
+        if box is not None:
+            f.has_box = 1
+            f.box[:] = [float(v) for v in box]
+        f.video_w, f.video_h = video_wh
+        return f
+
+
+def post(masks: np.ndarray, frames: np.ndarray, state: PostState, cfg: PostConfig | None = None, faces=None):
+    """(refined alpha [n][H][W] f32, alpha bytes [n][H][W] u8) for consecutive frames of one stream;
+    faces: a list of n Face (the stabiliser's inputs) or None."""
     masks = np.ascontiguousarray(masks, np.float32)
     frames = np.ascontiguousarray(frames)
     n, H, W = masks.shape
@@ -134,8 +155,9 @@ def post(masks: np.ndarray, frames: np.ndarray, state: PostState, cfg: PostConfi
     cfg = cfg or PostConfig.default()
     a = np.empty((n, H, W), np.float32)
     u = np.empty((n, H, W), np.uint8)
-    rc = lib().vsso_post(_ptr(masks), n, H, W, _ptr(frames), fh, fw, c, fw * c, fh * fw * c, ctypes.byref(cfg),
-                         _ptr(state.alpha), ctypes.byref(state.valid), _ptr(a), _ptr(u))
+    fa = (Face * n)(*faces) if faces is not None else None
+    rc = lib().vsso_post_face(_ptr(masks), n, H, W, _ptr(frames), fh, fw, c, fw * c, fh * fw * c,
+                              ctypes.byref(cfg), _ptr(state.alpha), ctypes.byref(state.valid), fa, _ptr(a), _ptr(u))
     if rc:
         raise ValueError(f"vsso_post rc={rc}")
     return a, u

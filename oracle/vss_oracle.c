@@ -397,6 +397,49 @@ static uint8_t guide_px(const uint8_t* f, long rs, int c, int h, int w, float ry
   return (uint8_t)floorf(val + 0.5f);
 }
 
+/* §8(f) row 4: per-frame face inputs (the layout of vss_face_frame, include/vss.h):
+ * opts.lastAffine -> warpAffineNearest :335-353 (invertAffine :323-333) of
+ * prevAlpha blended 0.3/0.7 before the EMA (:102-113); the detection box ->
+ * facePriorMask :697-741 -> morphologicalClosingInPrior :743-787 after the
+ * opening, and the prior's clamp in refineAlphaOnce :297-307.  Doubles. */
+typedef struct {
+  int has_affine;
+  double affine[6];
+  int has_box;
+  double box[4];
+  int video_w, video_h;
+} vsso_face;
+
+static double js_round(double x) {  /* Math.round: nearest, ties toward +infinity */
+  double r = floor(x);
+  return x - r >= 0.5 ? r + 1.0 : r;
+}
+
+static void face_prior(const vsso_face* f, int W, int H, int fw, int fh, float* out) {
+  double vw = f->video_w > 0 ? f->video_w : fw, vh = f->video_h > 0 ? f->video_h : fh;
+  double sx = (double)W / vw, sy = (double)H / vh;
+  double x0 = floor(f->box[0] * sx), y0 = floor(f->box[1] * sy);
+  double x1 = ceil(f->box[2] * sx), y1 = ceil(f->box[3] * sy);
+  double cx = (x0 + x1) / 2, cy = (y0 + y1) / 2;
+  double rx = (x1 - x0) * 0.56, ry = (y1 - y0) * 0.70;
+  double pad = fmax(4.0, floor((double)(W < H ? W : H) * 0.02));
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) {
+      double dx = (x - cx) / fmax(1e-6, rx), dy = (y - cy) / fmax(1e-6, ry);
+      double d2 = dx * dx + dy * dy, v = 0;
+      if (d2 <= 1) {
+        double t = sqrt(fmax(0.0, fmin(1.0, d2)));
+        v = 0.5 - 0.5 * cos(3.141592653589793 * (1 - t)); /* Math.PI */
+        if (d2 > 1 - (pad / fmax(rx, ry))) v = fmax(v, 0.25);
+      }
+      out[y * W + x] = (float)v;
+    }
+}
+
+int vsso_post_face(const float* masks, int n, int H, int W, const uint8_t* frames, int fh, int fw, int fc,
+                   long row_stride, long frame_stride, const vsso_post_cfg* cfg, float* state, int* state_valid,
+                   const vsso_face* faces, float* out_alpha, uint8_t* out_u8);
+
 /* Post-process n consecutive frames of ONE video stream.
  * masks: [n][H][W] raw seam masks; frames: the n source frames (for the guide);
  * state: [H][W] prevAlpha, *state_valid 0 before the stream's first frame;
@@ -404,6 +447,14 @@ static uint8_t guide_px(const uint8_t* f, long rs, int c, int h, int w, float ry
 int vsso_post(const float* masks, int n, int H, int W, const uint8_t* frames, int fh, int fw, int fc,
               long row_stride, long frame_stride, const vsso_post_cfg* cfg, float* state, int* state_valid,
               float* out_alpha, uint8_t* out_u8) {
+  return vsso_post_face(masks, n, H, W, frames, fh, fw, fc, row_stride, frame_stride, cfg, state, state_valid, NULL,
+                        out_alpha, out_u8);
+}
+
+/* vsso_post with per-frame face inputs (NULL: none). */
+int vsso_post_face(const float* masks, int n, int H, int W, const uint8_t* frames, int fh, int fw, int fc,
+                   long row_stride, long frame_stride, const vsso_post_cfg* cfg, float* state, int* state_valid,
+                   const vsso_face* faces, float* out_alpha, uint8_t* out_u8) {
   if (!masks || !frames || !cfg || !state || !state_valid || n < 0 || H < 3 || W < 3) return -1;
   long P = (long)H * W;
   float* ema = (float*)malloc(sizeof(float) * P);
@@ -411,9 +462,30 @@ int vsso_post(const float* masks, int n, int H, int W, const uint8_t* frames, in
   float* op = (float*)malloc(sizeof(float) * P);
   float* gd = (float*)malloc(sizeof(float) * P);
   uint8_t* guide = (uint8_t*)malloc(4 * P);
+  float* base = (float*)malloc(sizeof(float) * P);
+  float* prior = (float*)malloc(sizeof(float) * P);
+  float* dil = (float*)malloc(sizeof(float) * P);
+  float* clo = (float*)malloc(sizeof(float) * P);
   float ry = (float)((double)fh / (double)H), rx = (float)((double)fw / (double)W);
   for (int t = 0; t < n; ++t) {
     const float* cur = masks + (long)t * P;
+    const vsso_face* fc_t = faces ? faces + t : NULL;
+    /* the warp of prevAlpha by lastAffine, blended 0.3 / 0.7 (:102-113) */
+    if (fc_t && fc_t->has_affine && *state_valid) {
+      const double* A = fc_t->affine;
+      double det = A[0] * A[4] - A[1] * A[3];
+      double d = det != 0 ? det : 1e-6;
+      double ia11 = A[4] / d, ia12 = -A[1] / d, ia21 = -A[3] / d, ia22 = A[0] / d;
+      double itx = -(ia11 * A[2] + ia12 * A[5]), ity = -(ia21 * A[2] + ia22 * A[5]);
+      for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+          double sxv = ia11 * x + ia12 * y + itx, syv = ia21 * x + ia22 * y + ity;
+          double xi = js_round(sxv), yi = js_round(syv);
+          float w = (xi >= 0 && xi < W && yi >= 0 && yi < H) ? state[(long)yi * W + (long)xi] : 0.f;
+          base[y * W + x] = (float)((double)w * 0.3 + (double)cur[y * W + x] * (1 - 0.3));
+        }
+      cur = base;
+    }
     /* temporalEMA :218-227 */
     if (!*state_valid) {
       memcpy(state, cur, sizeof(float) * P);
@@ -446,6 +518,32 @@ int vsso_post(const float* masks, int n, int H, int W, const uint8_t* frames, in
           }
         op[y * W + x] = m;
       }
+    /* the face prior and the closing inside it (:136, :157) */
+    int has_prior = fc_t && fc_t->has_box;
+    if (has_prior) {
+      face_prior(fc_t, W, H, fw, fh, prior);
+      memset(dil, 0, sizeof(float) * P);
+      memset(clo, 0, sizeof(float) * P);
+      for (int y = 1; y < H - 1; ++y)
+        for (int x = 1; x < W - 1; ++x) {
+          long c = (long)y * W + x;
+          if (prior[c] <= 0) { dil[c] = op[c]; continue; }
+          float m = 0.0f;
+          for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) { float v = op[(y + dy) * W + x + dx]; if (v > m) m = v; }
+          dil[c] = m;
+        }
+      for (int y = 1; y < H - 1; ++y)
+        for (int x = 1; x < W - 1; ++x) {
+          long c = (long)y * W + x;
+          if (prior[c] <= 0) { clo[c] = dil[c]; continue; }
+          float m = 1.0f;
+          for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) { float v = dil[(y + dy) * W + x + dx]; if (v < m) m = v; }
+          clo[c] = m;
+        }
+      memcpy(op, clo, sizeof(float) * P);
+    }
     /* jointBilateral3x3 :230-266 with the guide of :315-321 */
     const float* a = op;
     if (cfg->use_bilateral) {
@@ -477,7 +575,7 @@ int vsso_post(const float* masks, int n, int H, int W, const uint8_t* frames, in
         }
       a = gd;
     }
-    /* refineAlphaOnce :270-313 (prior undefined) and alphaToImageData :204-216 */
+    /* refineAlphaOnce :270-313 (with the prior clamp when a box is given) and alphaToImageData :204-216 */
     double lo = cfg->noise_cutoff, hi = cfg->high_threshold;
     double denom = hi - lo > 1e-6 ? hi - lo : 1e-6;
     for (long i = 0; i < P; ++i) {
@@ -485,6 +583,11 @@ int vsso_post(const float* masks, int n, int H, int W, const uint8_t* frames, in
       if (v <= lo) v = 0;
       else if (v >= hi) v = 1;
       else v = pow((v - lo) / denom, cfg->gamma);
+      if (has_prior) {
+        double pv = prior[i];
+        if (pv > 0.25) v = fmax(v, fmin(1.0, 0.55 * pv + 0.15));
+        else if (pv > 0) v = fmin(v, 0.35 + 0.15 * pv);
+      }
       float vf = (float)v;
       if (out_alpha) out_alpha[(long)t * P + i] = vf;
       if (out_u8) {
@@ -493,7 +596,7 @@ int vsso_post(const float* masks, int n, int H, int W, const uint8_t* frames, in
       }
     }
   }
-  free(ema); free(er); free(op); free(gd); free(guide);
+  free(ema); free(er); free(op); free(gd); free(guide); free(base); free(prior); free(dil); free(clo);
   return 0;
 }
 

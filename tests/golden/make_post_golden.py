@@ -2,7 +2,7 @@
 OWN CODE run under Node in this container.
 
 Run from the repo root (needs /root/reference and node):
-    python tests/golden/make_post_golden.py
+    python tests/golden/make_post_golden.py     (post_chain.npz and post_face.npz)
 
 The five pure functions the reference applies to the seam's mask
 (/root/reference/client/src/core/frameProcessorTest.ts):
@@ -129,5 +129,118 @@ console.log(JSON.stringify(config));
     print(path, os.path.getsize(path), "bytes; config", cfg, "alpha mean", float(ref_a.mean()))
 
 
+FACE_FUNCS = ["invertAffine", "warpAffineNearest", "facePriorMask", "morphologicalClosingInPrior"]
+
+# per-frame face inputs of the fixture (mask 48x64, video 160x120): the first
+# frame's affine cannot act (no prevAlpha yet), the last frame has none
+FACES = [
+    {"affine": [1.05 * np.cos(0.1), -1.05 * np.sin(0.1), 2.5, 1.05 * np.sin(0.1), 1.05 * np.cos(0.1), -1.5],
+     "box": [40.0, 20.0, 100.0, 90.0]},
+    {"affine": [0.97, 0.05, -1.25, -0.05, 0.97, 3.0], "box": [52.5, 14.25, 118.75, 101.5]},
+    {"affine": [1.0, 0.0, 4.0, 0.0, 1.0, 0.0], "box": None},
+    {"affine": None, "box": None},
+]
+
+
+def main_face():
+    """tests/golden/post_face.npz: the same chain with the face stabiliser's
+    inputs (§8(f) row 4): processFrame's warp-and-blend block (:102-113) cut
+    from the reference as text, warpAffineNearest / invertAffine,
+    facePriorMask, morphologicalClosingInPrior and refineAlphaOnce's prior clamp,
+    in processFrame's order (:99-169)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("strip_types", os.path.join(
+        ROOT, "video-stream-segmenetation_amd", "ts", "strip_types.py"))
+    st = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(st)
+    from conftest import load_pkg
+    pkg = load_pkg()
+    import oracle_py
+    import vss_amd.synthetic as syn
+
+    src = open(REF).read()
+    lines = src.split("\n")
+    cfg_block = "\n".join(lines[11:30]).replace("export const", "const").replace("export let", "let")
+    prev = "let prevAlpha = null;"
+    funcs = "\n\n".join(extract(src, f) for f in FUNCS + FACE_FUNCS)
+    # the warp-and-blend block of processFrame, as written there
+    i = src.index("if (opts.lastAffine && prevAlpha")
+    j = src.index("{", i)
+    depth = 0
+    for k in range(j, len(src)):
+        depth += {"{": 1, "}": -1}.get(src[k], 0)
+        if depth == 0:
+            break
+    warp_block = src[i:k + 1]
+    body = st.strip(cfg_block + "\n" + prev + "\n" + funcs)
+    body = body.replace("'use strict';\n", "")
+    warp_block = st.strip(warp_block).replace("'use strict';\n", "").split("\n", 1)[1]  # drop the header line
+
+    n, H, W, fh, fw = 4, 48, 64, 120, 160
+    frames = np.stack([syn.make_frame(900 + (t % 2), fh, fw, 3) for t in range(n)])
+    blob = open(pkg.ensure_weights(), "rb").read()
+    masks = oracle_py.forward(blob, frames, H, W, mode=0)
+    masks = np.ascontiguousarray(masks.astype(np.float32))
+    guide = oracle_py.post_guide(frames, H, W)
+
+    harness = body + r"""
+class ImageData { constructor(w, h) { this.width = w; this.height = h; this.data = new Uint8ClampedArray(w * h * 4); } }
+const fs = require('fs');
+const [mp, gp, fp, n, H, W, VW, VH, op] = process.argv.slice(2);
+const N = +n, h = +H, w = +W, P = h * w;
+const mb = fs.readFileSync(mp), gb = fs.readFileSync(gp);
+const faces = JSON.parse(fs.readFileSync(fp, 'utf8'));
+const outA = new Float32Array(N * P), outU = new Uint8Array(N * P);
+for (let t = 0; t < N; t++) {
+  const alphaRaw = new Float32Array(mb.buffer.slice(mb.byteOffset + t * P * 4, mb.byteOffset + (t + 1) * P * 4));
+  const guide = new Uint8ClampedArray(P * 4);
+  for (let i = 0; i < P; i++) { for (let c = 0; c < 3; c++) guide[i * 4 + c] = gb[(t * P + i) * 3 + c]; guide[i * 4 + 3] = 255; }
+  const f = faces[t];
+  const opts = { lastAffine: f.affine ? { a11: f.affine[0], a12: f.affine[1], tx: f.affine[2],
+                                          a21: f.affine[3], a22: f.affine[4], ty: f.affine[5] } : null };
+  const maskW = w, maskH = h;
+  // processFrame :99-169 with the face inputs
+  let baseAlpha = alphaRaw;
+""" + warp_block + r"""
+  const emaAlpha = temporalEMA(baseAlpha);
+  const openedAlpha = morphologicalOpening(emaAlpha, w, h);
+  const facePrior = f.box ? facePriorMask({ x0: f.box[0], y0: f.box[1], x1: f.box[2], y1: f.box[3] }, +VW, +VH, w, h) : null;
+  const openedClosedAlpha = morphologicalClosingInPrior(openedAlpha, facePrior, w, h);
+  const guidedAlpha = config.USE_BILATERAL ? jointBilateral3x3(openedClosedAlpha, guide, w, h) : openedClosedAlpha;
+  const refinedAlpha = refineAlphaOnce(guidedAlpha, config.NOISE_CUTOFF, config.HIGH_THRESHOLD, config.GAMMA, facePrior ?? undefined);
+  const img = alphaToImageData(refinedAlpha, w, h);
+  outA.set(refinedAlpha, t * P);
+  for (let i = 0; i < P; i++) outU[t * P + i] = img.data[i * 4 + 3];
+}
+fs.writeFileSync(op + '.f32', Buffer.from(outA.buffer));
+fs.writeFileSync(op + '.u8', Buffer.from(outU.buffer));
+console.log(JSON.stringify(config));
+"""
+    # Node 12 has no `??`: the reference's one use in this glue is rewritten as ||-free explicit form
+    harness = harness.replace("facePrior ?? undefined", "(facePrior === null ? undefined : facePrior)")
+    faces = [{"affine": None if f["affine"] is None else [float(v) for v in f["affine"]],
+              "box": f["box"]} for f in FACES]
+    with tempfile.TemporaryDirectory() as td:
+        js = os.path.join(td, "post_face.js")
+        open(js, "w").write(harness)
+        masks.tofile(os.path.join(td, "m.bin"))
+        guide.tofile(os.path.join(td, "g.bin"))
+        open(os.path.join(td, "f.json"), "w").write(json.dumps(faces))
+        out = subprocess.run(["node", js, os.path.join(td, "m.bin"), os.path.join(td, "g.bin"),
+                              os.path.join(td, "f.json"), str(n), str(H), str(W), str(fw), str(fh),
+                              os.path.join(td, "o")], capture_output=True, text=True)
+        if out.returncode:
+            raise RuntimeError(out.stderr)
+        cfg = json.loads(out.stdout.strip().splitlines()[-1])
+        ref_a = np.fromfile(os.path.join(td, "o.f32"), np.float32).reshape(n, H, W)
+        ref_u = np.fromfile(os.path.join(td, "o.u8"), np.uint8).reshape(n, H, W)
+    path = os.path.join(HERE, "post_face.npz")
+    np.savez_compressed(path, seeds=np.array([900 + (t % 2) for t in range(n)]), frame_hw=np.array([fh, fw]),
+                        masks=masks, guide=guide, config=np.array(json.dumps(cfg)), faces=np.array(json.dumps(faces)),
+                        alpha=ref_a, alpha_u8=ref_u)
+    print(path, os.path.getsize(path), "bytes; alpha mean", float(ref_a.mean()))
+
+
 if __name__ == "__main__":
     main()
+    main_face()

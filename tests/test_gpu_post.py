@@ -196,3 +196,41 @@ def test_segment_composite_end_to_end(pkg, torch_cuda, synthetic, oracle):
             assert np.array_equal(got, want), f"call {call}: {(got != want).sum()} bytes differ"
         with pytest.raises(pkg.VssError):  # more output than the handle holds
             chain.composite(np.zeros((4, 1080, 1920, 3), np.uint8))
+
+
+def test_face_chain_vs_reference_js_golden(pkg, torch_cuda, synthetic):
+    """§8(f) row 4 on the GPU: the stabilised EMA (warp of prevAlpha + blend),
+    the face prior, the closing inside it and the clamped refine against the
+    reference's own JS (tests/golden/post_face.npz); faces given from the host
+    and from device memory; a call with no faces after them is the plain chain."""
+    g = np.load(os.path.join(GOLDEN, "post_face.npz"), allow_pickle=False)
+    import json
+    n, H, W = g["masks"].shape
+    fh, fw = (int(v) for v in g["frame_hw"])
+    frames = _frames(synthetic, g["seeds"], fh, fw)
+    faces = [pkg.FaceFrame.make(affine=f["affine"], box=f["box"], video_wh=(fw, fh))
+             for f in json.loads(str(g["faces"]))]
+    with pkg.Session(model_h=H, model_w=W, dtype="f32", max_batch=8, autotune=False) as s:
+        chain = pkg.PostChain(s)
+        chain.set_faces(faces)
+        a, u = _run_device(torch_cuda, chain, frames, g["masks"])
+        _cmp("face golden", a, u, g["alpha"], g["alpha_u8"])
+        # the same from device memory, frame by frame (state carried across calls)
+        chain.reset()
+        raw = bytes((pkg.FaceFrame * n)(*faces))
+        dfaces = torch_cuda.frombuffer(bytearray(raw), dtype=torch_cuda.uint8).cuda()
+        size = len(raw) // n
+        parts = []
+        for t in range(n):
+            chain.set_faces_device(dfaces.data_ptr() + t * size, 1)
+            parts.append(_run_device(torch_cuda, chain, frames[t:t + 1], g["masks"][t:t + 1]))
+        _cmp("face golden, per frame, device faces", np.concatenate([p[0] for p in parts]),
+             np.concatenate([p[1] for p in parts]), g["alpha"], g["alpha_u8"])
+        # faces are consumed by one call: the next call is the plain chain (no prior, no warp)
+        chain.reset()
+        a2, u2 = _run_device(torch_cuda, chain, frames, g["masks"])
+        plain = np.load(os.path.join(GOLDEN, "post_chain.npz"), allow_pickle=False)
+        _cmp("plain after faces", a2, u2, plain["alpha"], plain["alpha_u8"])
+        with pytest.raises(pkg.VssError):  # face count must match the call's frames
+            chain.set_faces(faces[:2])
+            _run_device(torch_cuda, chain, frames, g["masks"])

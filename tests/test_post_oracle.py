@@ -97,3 +97,22 @@ def test_composite_oracle_identity_and_transparency(oracle):
     out2 = oracle.composite(np.ascontiguousarray(np.repeat(np.repeat(rgba, 3, 1), 2, 2)),
                             np.full((2, 12, 20), 200, np.uint8))
     assert np.all(out2[..., 3] == 200)
+
+
+def test_face_chain_bitexact_vs_reference_js(oracle, synthetic):
+    """§8(f) row 4: warp + blend of prevAlpha, the elliptical face prior, the
+    closing inside it and refine's prior clamp — vsso_post_face against the
+    reference's own functions run under Node (tests/golden/post_face.npz)."""
+    g = np.load(os.path.join(GOLDEN, "post_face.npz"), allow_pickle=False)
+    frames = _golden_frames(synthetic, g)
+    n, H, W = g["masks"].shape
+    fh, fw = (int(v) for v in g["frame_hw"])
+    faces = [oracle.Face.make(affine=f["affine"], box=f["box"], video_wh=(fw, fh))
+             for f in json.loads(str(g["faces"]))]
+    st = oracle.PostState(H, W)
+    a, u = oracle.post(g["masks"], frames, st, faces=faces)
+    assert np.array_equal(a, g["alpha"]), np.abs(a - g["alpha"]).max()
+    assert np.array_equal(u, g["alpha_u8"])
+    # the face inputs change every frame of the fixture (the last through the EMA state)
+    plain, _ = oracle.post(g["masks"], frames, oracle.PostState(H, W))
+    assert all((plain[t] != a[t]).sum() > 100 for t in range(n))

@@ -132,6 +132,8 @@ def lib() -> ctypes.CDLL:
                 "vss_post_destroy": ([P], None),
                 "vss_post_reset": ([P], I),
                 "vss_post_set_config": ([P, ctypes.POINTER(PostConfig)], I),
+                "vss_post_set_faces": ([P, P, I], I),
+                "vss_post_set_faces_device": ([P, P, I], I),
                 "vss_postprocess_device": ([P, P, I, I, I, I, S, S, P, P, P, P], I),
                 "vss_segment_post": ([P, P, P, I, I, I, I, S, P, P], I),
                 "vss_composite_device": ([P, P, I, I, I, I, S, S, P, P, S, S, P], I),
@@ -327,6 +329,26 @@ class Session:
         return list(arr), cnt.value
 
 
+class FaceFrame(ctypes.Structure):
+    """vss_face_frame: one frame's face-stabiliser inputs (processFrame's
+    opts.lastAffine and its detection box, frameProcessorTest.ts:99-114, :131-166)."""
+    _fields_ = [("has_affine", ctypes.c_int), ("affine", ctypes.c_double * 6), ("has_box", ctypes.c_int),
+                ("box", ctypes.c_double * 4), ("video_w", ctypes.c_int), ("video_h", ctypes.c_int)]
+
+    @classmethod
+    def make(cls, affine=None, box=None, video_wh=(0, 0)):
+        """affine = (a11, a12, tx, a21, a22, ty) or None; box = (x0, y0, x1, y1) video pixels or None."""
+        f = cls()
+        if affine is not None:
+            f.has_affine = 1
+            f.affine[:] = [float(v) for v in affine]
+        if box is not None:
+            f.has_box = 1
+            f.box[:] = [float(v) for v in box]
+        f.video_w, f.video_h = (int(v) for v in video_wh)
+        return f
+
+
 class PostChain:
     """The reference's per-stream mask post-processing (processFrame
     frameProcessorTest.ts:115-169: temporalEMA -> morphologicalOpening ->
@@ -385,6 +407,15 @@ class PostChain:
         _check(lib().vss_segment_composite(s._h, self._st, f.ctypes.data, n, hh, ww, c, ww * c, out.ctypes.data),
                s._h)
         return out
+
+    def set_faces(self, faces):
+        """The face inputs (a list of FaceFrame, one per frame) of the NEXT call."""
+        arr = (FaceFrame * len(faces))(*faces)
+        _check(lib().vss_post_set_faces(self._st, arr, len(faces)), self.session._h)
+
+    def set_faces_device(self, faces_ptr: int, n: int):
+        """The same from a device array of n vss_face_frame (e.g. the GPU face stage's output)."""
+        _check(lib().vss_post_set_faces_device(self._st, faces_ptr, n), self.session._h)
 
     def process_device(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int, frame_stride: int,
                        masks_ptr: int, alpha_ptr: int = 0, alpha_u8_ptr: int = 0, stream: int = 0):

@@ -1380,6 +1380,10 @@ struct vss_post_state {
   float* state = nullptr;   // [P] prevAlpha
   int* valid = nullptr;     // device flag: 0 before the stream's first frame
   float* ema = nullptr;     // [max_batch][P]
+  float* state2 = nullptr;  // [P] the other prevAlpha buffer (the stabilised EMA reads one, writes the other)
+  FaceFrame* d_faces = nullptr;       // [max_batch] face inputs set by vss_post_set_faces
+  const FaceFrame* faces = nullptr;   // the next call's face inputs (d_faces or a caller's device array)
+  int faces_n = 0;                    // ... for this many frames (0: none)
   double* rtab = nullptr;   // exp(-r / (2 sigma_r^2)), r in [0, 3*255^2]
   double sw[3] = {0, 0, 0};
   double tab_sigma = -1.0;
@@ -1417,17 +1421,46 @@ int post_enqueue(vss_post_state* st, const uint8_t* d_frames, int n, int fh, int
                  const float* d_masks, float* d_alpha, uint8_t* d_u8, hipStream_t s) {
   vss_handle* h = st->h;
   const int H = h->cfg.model_h, W = h->cfg.model_w;
-  PostEmaParams pe{};
-  pe.masks = d_masks;
-  pe.ema = st->ema;
-  pe.state = st->state;
-  pe.valid = st->valid;
-  pe.n = n;
-  pe.P = (long)H * W;
-  pe.a = st->cfg.ema;
-  launch_post_ema(pe, s);
+  const FaceFrame* faces = nullptr;
+  if (st->faces_n) {
+    if (st->faces_n != n)
+      return post_fail(st, VSS_E_INVALID_ARG, "vss_post_set_faces was given " + std::to_string(st->faces_n) +
+                                                  " frames, this call has " + std::to_string(n));
+    faces = st->faces;
+    st->faces_n = 0;  // consumed
+    st->faces = nullptr;
+  }
+  if (faces) {
+    // the stabilised EMA, one frame at a time (the warp reads prevAlpha at other pixels)
+    for (int t = 0; t < n; ++t) {
+      PostFaceEmaParams pe{};
+      pe.mask = d_masks + (long)t * H * W;
+      pe.prev = st->state;
+      pe.next = st->state2;
+      pe.ema = st->ema + (long)t * H * W;
+      pe.valid = st->valid;
+      pe.first = t == 0;
+      pe.face = faces + t;
+      pe.H = H;
+      pe.W = W;
+      pe.a = st->cfg.ema;
+      launch_post_face_ema(pe, s);
+      std::swap(st->state, st->state2);
+    }
+  } else {
+    PostEmaParams pe{};
+    pe.masks = d_masks;
+    pe.ema = st->ema;
+    pe.state = st->state;
+    pe.valid = st->valid;
+    pe.n = n;
+    pe.P = (long)H * W;
+    pe.a = st->cfg.ema;
+    launch_post_ema(pe, s);
+  }
   HIP_TRY(h, hipMemsetAsync(st->valid, 1, sizeof(int), s));  // the stream has seen its first frame
   PostFilterParams pf{};
+  pf.faces = faces;
   pf.ema = st->ema;
   pf.frames = d_frames;
   pf.row_stride = (long)rs;
@@ -1481,7 +1514,8 @@ int vss_post_create(vss_handle* h, const vss_post_config* cfg, vss_post_state** 
   };
   HIP_TRY(h, hipSetDevice(h->device));
   if (hipMalloc(&st->state, P * 4) != hipSuccess || hipMalloc(&st->valid, 16) != hipSuccess ||
-      hipMalloc(&st->ema, P * 4 * h->cfg.max_batch) != hipSuccess ||
+      hipMalloc(&st->ema, P * 4 * h->cfg.max_batch) != hipSuccess || hipMalloc(&st->state2, P * 4) != hipSuccess ||
+      hipMalloc(&st->d_faces, sizeof(FaceFrame) * h->cfg.max_batch) != hipSuccess ||
       hipMalloc(&st->rtab, (size_t)kRangeTab * 8) != hipSuccess)
     return bail(fail(h, VSS_E_OOM, "post: hipMalloc failed"));
   if (hipMemset(st->valid, 0, 16) != hipSuccess || hipMemset(st->state, 0, P * 4) != hipSuccess)
@@ -1501,6 +1535,8 @@ void vss_post_destroy(vss_post_state* st) {
   if (st->state) (void)hipFree(st->state);
   if (st->valid) (void)hipFree(st->valid);
   if (st->ema) (void)hipFree(st->ema);
+  if (st->state2) (void)hipFree(st->state2);
+  if (st->d_faces) (void)hipFree(st->d_faces);
   if (st->rtab) (void)hipFree(st->rtab);
   delete st;
 }
@@ -1510,6 +1546,29 @@ int vss_post_reset(vss_post_state* st) {
   HIP_TRY(st->h, hipSetDevice(st->h->device));
   HIP_TRY(st->h, hipStreamSynchronize(st->h->stream));
   HIP_TRY(st->h, hipMemset(st->valid, 0, sizeof(int)));
+  st->faces_n = 0;
+  st->faces = nullptr;
+  return VSS_OK;
+}
+
+static_assert(sizeof(FaceFrame) == sizeof(vss_face_frame), "FaceFrame mirrors vss_face_frame");
+
+int vss_post_set_faces(vss_post_state* st, const vss_face_frame* faces, int n) {
+  if (!st) return VSS_E_INVALID_ARG;
+  if (!faces || n < 1 || n > st->h->cfg.max_batch) return post_fail(st, VSS_E_INVALID_ARG, "faces: 1..max_batch frames");
+  HIP_TRY(st->h, hipSetDevice(st->h->device));
+  HIP_TRY(st->h, hipMemcpyAsync(st->d_faces, faces, sizeof(FaceFrame) * n, hipMemcpyHostToDevice, st->h->stream));
+  st->faces = st->d_faces;
+  st->faces_n = n;
+  return VSS_OK;
+}
+
+int vss_post_set_faces_device(vss_post_state* st, const vss_face_frame* d_faces, int n) {
+  if (!st) return VSS_E_INVALID_ARG;
+  if (!d_faces || n < 1 || n > st->h->cfg.max_batch)
+    return post_fail(st, VSS_E_INVALID_ARG, "faces: a device array of 1..max_batch frames");
+  st->faces = reinterpret_cast<const FaceFrame*>(d_faces);
+  st->faces_n = n;
   return VSS_OK;
 }
 

@@ -322,7 +322,33 @@ struct PostEmaParams {
   double a;            // config.EMA
 };
 
+// Per-frame face inputs of the post chain (the same layout as vss_face_frame, include/vss.h)
+struct FaceFrame {
+  int has_affine;
+  double affine[6];
+  int has_box;
+  double box[4];
+  int video_w, video_h;
+};
+
+// One frame of the stabilised EMA: base = mask (+ 0.3 * warp(prevAlpha) when the
+// frame has an affine), then the EMA; prevAlpha double-buffered (the warp reads
+// other pixels' prevAlpha).
+struct PostFaceEmaParams {
+  const float* mask;     // [P] this frame's raw mask
+  const float* prev;     // [P] prevAlpha
+  float* next;           // [P] the new prevAlpha (= this frame's EMA)
+  float* ema;            // [P] this frame's EMA output
+  const int* valid;      // 0 before the stream's first frame
+  int first;             // this is the call's first frame
+  const FaceFrame* face; // this frame's face inputs (device)
+  int H, W;
+  double a;
+};
+void launch_post_face_ema(const PostFaceEmaParams& p, hipStream_t s);
+
 struct PostFilterParams {
+  const FaceFrame* faces;  // [n] per-frame face inputs (device) or null: no prior
   const float* ema;      // [n][H][W]
   const uint8_t* frames; // the n source frames (guide)
   long row_stride, frame_stride;
