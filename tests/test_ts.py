@@ -170,3 +170,38 @@ def test_node_onnx_session_matches_oracle_and_python_host(addon_built, pkg, tmp_
         err = float(np.abs(got - w).max())
         assert err <= 1e-4 * max(1.0, float(np.abs(w).max())), (name, err)
         assert np.array_equal(got, py[name]), name
+
+
+@pytest.mark.gpu
+def test_node_face_inputs_match_python_host(addon_built, pkg, synthetic, tmp_path):
+    """PostChain.processFrames(frames, faces) from TypeScript == the Python
+    host's PostChain with the same FaceFrame inputs, bit for bit (the chain
+    itself is pinned against the reference's JS in tests/test_gpu_post.py)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n, h, w = 4, 240, 320
+    frames = np.stack([synthetic.make_frame(820 + i, h, w, 3) for i in range(n)])
+    faces = [{"box": [90.0, 40.0, 210.0, 200.0]},
+             {"affine": [0.99, 0.04, 1.5, -0.04, 0.99, -2.0], "box": [95.5, 42.25, 214.0, 205.75]},
+             {"affine": [1.0, 0.0, -3.0, 0.0, 1.0, 1.0]},
+             None]
+    fp, jp, op = tmp_path / "frames.bin", tmp_path / "faces.json", tmp_path / "face"
+    frames.tofile(fp)
+    jp.write_text(json.dumps(faces))
+    out = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "run_face.js"), str(fp), str(n), str(h), str(w),
+                          "3", str(jp), str(op)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    assert info == {"count": n, "width": 256, "height": 144, "mismatchRejected": True}
+    alpha = np.fromfile(str(op) + ".f32", np.float32).reshape(n, -1)
+    u8 = np.fromfile(str(op) + ".u8", np.uint8).reshape(n, -1)
+    with pkg.Session(dtype="bf16x2", max_batch=n, max_frame_h=h, max_frame_w=w) as s:
+        chain = pkg.PostChain(s)
+        chain.set_faces([pkg.FaceFrame.make(affine=f.get("affine") if f else None, box=f.get("box") if f else None)
+                         for f in faces])
+        pa, pu, _, _ = chain.segment(frames)
+        plain = pkg.PostChain(s)
+        qa, _, _, _ = plain.segment(frames)
+    assert np.array_equal(alpha, pa) and np.array_equal(u8, pu)
+    assert all((alpha[t] != qa[t]).any() for t in range(n))  # the faces act on every frame

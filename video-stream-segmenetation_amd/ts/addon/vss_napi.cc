@@ -17,6 +17,9 @@
 //                                             USE_BILATERAL, BILATERAL_SIGMA_SPATIAL,
 //                                             BILATERAL_SIGMA_RANGE; frameProcessorTest.ts:12-30)
 //   postSetConfig(post, config), postReset(post), postDestroy(post)
+//   postSetFaces(post, faces: {affine?: number[6], box?: number[4], videoW?, videoH?}[])
+//       the face stabiliser's inputs of the next segmentPost / segmentComposite call, one per frame
+//       (processFrame's opts.lastAffine and detection box, :99-166)
 //   segmentPost(handle, post, frames, n, height, width, channels, rowStride)
 //       -> Promise<{alpha: Float32Array, alphaU8: Uint8Array}>   (processFrame :78-169)
 //   segmentComposite(handle, post, frames, n, height, width, channels, rowStride)
@@ -310,6 +313,55 @@ napi_value PostReset(napi_env env, napi_callback_info info) {
   if (!p) return nullptr;
   const int rc = vss_post_reset(p->st);
   if (rc != VSS_OK) throw_vss(env, "vss_post_reset", rc, vss_last_error(p->hd->h));
+  return nullptr;
+}
+
+bool get_doubles(napi_env env, napi_value obj, const char* key, double* out, uint32_t n) {
+  bool has = false;
+  if (napi_has_named_property(env, obj, key, &has) != napi_ok || !has) return false;
+  napi_value v;
+  napi_get_named_property(env, obj, key, &v);
+  bool is_arr = false;
+  uint32_t len = 0;
+  if (napi_is_array(env, v, &is_arr) != napi_ok || !is_arr || napi_get_array_length(env, v, &len) != napi_ok ||
+      len != n)
+    return false;
+  for (uint32_t k = 0; k < n; ++k) {
+    napi_value e;
+    napi_get_element(env, v, k, &e);
+    if (napi_get_value_double(env, e, out + k) != napi_ok) return false;
+  }
+  return true;
+}
+
+napi_value PostSetFaces(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Post* p = argc >= 2 ? get_post(env, argv[0]) : nullptr;
+  if (!p) return nullptr;
+  bool is_arr = false;
+  uint32_t n = 0;
+  if (napi_is_array(env, argv[1], &is_arr) != napi_ok || !is_arr || napi_get_array_length(env, argv[1], &n) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "postSetFaces(post, faces[]): an array, one entry per frame");
+    return nullptr;
+  }
+  std::vector<vss_face_frame> faces(n);
+  for (uint32_t k = 0; k < n; ++k) {
+    napi_value f;
+    napi_get_element(env, argv[1], k, &f);
+    vss_face_frame& o = faces[k];
+    std::memset(&o, 0, sizeof(o));
+    napi_valuetype t;
+    napi_typeof(env, f, &t);
+    if (t != napi_object) continue;  // null / undefined: no face inputs for this frame
+    o.has_affine = get_doubles(env, f, "affine", o.affine, 6) ? 1 : 0;
+    o.has_box = get_doubles(env, f, "box", o.box, 4) ? 1 : 0;
+    get_int_prop(env, f, "videoW", &o.video_w);
+    get_int_prop(env, f, "videoH", &o.video_h);
+  }
+  const int rc = vss_post_set_faces(p->st, faces.data(), (int)n);
+  if (rc != VSS_OK) throw_vss(env, "vss_post_set_faces", rc, vss_last_error(p->hd->h));
   return nullptr;
 }
 
@@ -735,6 +787,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"postSetConfig", nullptr, PostSetConfig, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"postReset", nullptr, PostReset, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"postDestroy", nullptr, PostDestroy, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"postSetFaces", nullptr, PostSetFaces, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"segmentPost", nullptr, SegmentPost, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"segmentComposite", nullptr, SegmentComposite, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"ortCreate", nullptr, OrtCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
