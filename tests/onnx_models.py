@@ -231,6 +231,51 @@ def q4f16_like(h=64, w=96):
     return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])], opset=21)
 
 
+def face_detector_like(S=256, A=896, score_bias=3.0, seed=5):
+    """A stand-in with the I/O of the reference's face detector
+    (MediaPipeFaceDetector.onnx: image [1,3,S,S] -> box_coords [1,A,16],
+    box_scores [1,A,1]) whose best anchor is a confident, frame-dependent box:
+    the image's channel means through a Gemm onto seeded per-anchor boxes.
+    Drives the face stage through its has-box path, which the real detector
+    does not reach on synthetic frames."""
+    b = Builder(seed)
+    rng = b.rng
+    gp = b.op("Flatten", [b.op("GlobalAveragePool", ["image"])])             # [1, 3]
+    cx, cy = rng.uniform(0.3, 0.7, A), rng.uniform(0.3, 0.7, A)
+    sw, sh = rng.uniform(0.1, 0.3, A), rng.uniform(0.1, 0.3, A)
+    cb = rng.uniform(0, 1, (A, 16))
+    cb[:, 0], cb[:, 1], cb[:, 2], cb[:, 3] = cx - sw / 2, cy - sh / 2, cx + sw / 2, cy + sh / 2
+    wc = b.const((rng.standard_normal((A * 16, 3)) * 0.05).astype(np.float32))
+    co = b.op("Gemm", [gp, wc, b.const(cb.reshape(-1).astype(np.float32))], transB=1)
+    sb = rng.standard_normal(A) - 2.0
+    sb[A // 2 + 17] = score_bias
+    ws = b.const((rng.standard_normal((A, 3)) * 0.2).astype(np.float32))
+    sc = b.op("Sigmoid", [b.op("Gemm", [gp, ws, b.const(sb.astype(np.float32))], transB=1)])
+    b.nodes.append(R.make_node("Reshape", [co, b.const(np.array([1, A, 16], np.int64))], ["box_coords"]))
+    b.nodes.append(R.make_node("Reshape", [sc, b.const(np.array([1, A, 1], np.int64))], ["box_scores"]))
+    return b.model([("image", [1, 3, S, S])], [("box_coords", [1, A, 16]), ("box_scores", [1, A, 1])])
+
+
+def face_landmarks_like(LH=192, LW=192, score_bias=2.0, seed=6):
+    """A stand-in with the I/O of the reference's landmark model
+    (MediaPipeFaceLandmarkDetector.onnx: image [1,3,LH,LW] -> scores [1],
+    landmarks [1,468,3]): seeded points, the five anchors the affine uses
+    near their face positions, moved by the ROI's channel means."""
+    b = Builder(seed)
+    rng = b.rng
+    gp = b.op("Flatten", [b.op("GlobalAveragePool", ["image"])])             # [1, 3]
+    pts = rng.uniform(0.2, 0.8, (468, 3))
+    for i, (x, y) in zip((33, 263, 1, 13, 14), ((0.3, 0.4), (0.7, 0.41), (0.5, 0.56), (0.6, 0.72), (0.41, 0.7))):
+        pts[i, :2] = (x, y)
+    wl = b.const((rng.standard_normal((1404, 3)) * 0.05).astype(np.float32))
+    lm = b.op("Gemm", [gp, wl, b.const(pts.reshape(-1).astype(np.float32))], transB=1)
+    ws = b.const((rng.standard_normal((1, 3)) * 0.2).astype(np.float32))
+    sc = b.op("Sigmoid", [b.op("Gemm", [gp, ws, b.const(np.array([score_bias], np.float32))], transB=1)])
+    b.nodes.append(R.make_node("Reshape", [sc, b.const(np.array([1], np.int64))], ["scores"]))
+    b.nodes.append(R.make_node("Reshape", [lm, b.const(np.array([1, 468, 3], np.int64))], ["landmarks"]))
+    return b.model([("image", [1, 3, LH, LW])], [("scores", [1]), ("landmarks", [1, 468, 3])])
+
+
 MODELS = {"conv_zoo": (conv_zoo, {"x": (1, 3, 64, 80)}), "ops_zoo": (ops_zoo, {"x": (2, 8, 12, 16)}),
           "modnet_like": (modnet_like, {"input": (1, 3, 64, 96)}),
           "q4f16_like": (q4f16_like, {"input": (1, 3, 64, 96)})}

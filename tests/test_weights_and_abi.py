@@ -39,10 +39,10 @@ def test_blob_regenerates_bit_identically(pkg, blob, tmp_path):
 
 def _declared_symbols():
     syms = set()
-    for h in ("vss.h", "vso.h"):
+    for h in ("vss.h", "vso.h", "vsf.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        syms |= set(re.findall(r"\b(vs[so]_[a-z_]+)\s*\(", src))
+        syms |= set(re.findall(r"\b(vs[sof]_[a-z_]+)\s*\(", src))
     return sorted(syms)
 
 
@@ -50,7 +50,7 @@ def test_library_exports_header_symbols(pkg):
     pkg.build()
     L = ctypes.CDLL(pkg.LIB_PATH)
     syms = _declared_symbols()
-    assert len(syms) >= 14 + 12
+    assert len(syms) >= 14 + 12 + 9
     for s in syms:
         assert hasattr(L, s), f"libvss.so does not export {s}"
 
