@@ -205,3 +205,46 @@ def test_node_face_inputs_match_python_host(addon_built, pkg, synthetic, tmp_pat
         qa, _, _, _ = plain.segment(frames)
     assert np.array_equal(alpha, pa) and np.array_equal(u8, pu)
     assert all((alpha[t] != qa[t]).any() for t in range(n))  # the faces act on every frame
+
+
+@pytest.mark.gpu
+def test_node_face_tracker_matches_python_host(addon_built, pkg, synthetic, tmp_path):
+    """FaceTracker.track (TypeScript, over two InferenceSessions) == the Python
+    host's FaceTracker, number for number, across two calls; its faces drive
+    PostChain.processFrames exactly as the Python host's do."""
+    import ctypes  # noqa: F401
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import onnx_models as M
+    import vss_amd.face as face
+    import vss_amd.ort as ort
+    n, h, w = 7, 120, 160
+    frames = np.stack([synthetic.make_frame(700 + i, h, w, 3) for i in range(n)])
+    det_b, lmk_b = M.face_detector_like(), M.face_landmarks_like()
+    dp, lp, fp, op = tmp_path / "det.onnx", tmp_path / "lmk.onnx", tmp_path / "frames.bin", tmp_path / "alpha"
+    dp.write_bytes(det_b)
+    lp.write_bytes(lmk_b)
+    frames.tofile(fp)
+    out = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "run_face_tracker.js"), str(dp), str(lp),
+                          str(fp), str(n), str(h), str(w), "3", str(op)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    assert info["releaseBlocked"] and info["releasedRejects"]
+    with ort.InferenceSession(det_b) as ds, ort.InferenceSession(lmk_b) as ls, \
+            pkg.Session(model_h=48, model_w=64, dtype="f32", max_batch=8, autotune=False) as s:
+        tr = face.FaceTracker(ds, ls, interval=3)
+        want = tr.track(frames[:4], (s.mask_w, s.mask_h)) + tr.track(frames[4:], (s.mask_w, s.mask_h))
+        tr.close()
+        for f, g in zip(info["faces"], want):
+            assert (f["affine"] is not None) == bool(g.has_affine) and (f["box"] is not None) == bool(g.has_box)
+            if g.has_affine:
+                assert f["affine"] == list(g.affine)
+            if g.has_box:
+                assert f["box"] == list(g.box)
+            assert (f["videoW"], f["videoH"]) == (w, h)
+        chain = pkg.PostChain(s)
+        chain.set_faces(want)
+        pa, _, _, _ = chain.segment(frames)
+    assert np.array_equal(np.fromfile(str(op) + ".f32", np.float32).reshape(n, -1), pa)
+    assert sum(f["box"] is not None for f in info["faces"]) == 3

@@ -1,7 +1,11 @@
 """Time the GPU ONNX sessions (include/vso.h) on the reference's two real
 MediaPipe models (tests/golden/*.npz) and the MODNet-shaped synthetic net:
 inputs and outputs resident in HBM, one vso_run_device (hipGraph replay) per
-iteration, HIP events on the session's stream.  Prints one JSON line per model.
+iteration, HIP events on the session's stream.  Prints one JSON line per model,
+then one for the whole face stage (include/vsf.h: letterbox -> detector ->
+decode -> ROI -> landmarks -> affine -> scan) on 640x480 frames in HBM, every
+frame a face frame (interval 1), and its cost amortised over the reference's
+LANDMARK_INTERVAL of 6.
 
     python tools/bench_onnx.py [--iters 200] [--modnet 256x256]
 """
@@ -53,6 +57,44 @@ def main():
             ms = e0.elapsed_time(e1) / args.iters
             print(json.dumps({"model": name, "input": [list(x) for x in s.input_shapes], "ms_per_run": round(ms, 4),
                               "runs_per_s": round(1000.0 / ms, 1), "launches": len(s.launches())}), flush=True)
+    face_stage(args, torch, ort, M)
+
+
+def face_stage(args, torch, ort, M):
+    import ctypes
+    import vss_amd as pkg
+    import vss_amd.face as face
+    import vss_amd.synthetic as syn
+    import numpy as np
+    det = M.load_golden(os.path.join(ROOT, "tests", "golden", "mediapipe_face_detector.npz"))[0]
+    lmk = M.load_golden(os.path.join(ROOT, "tests", "golden", "mediapipe_face_landmarks.npz"))[0]
+    n, fh, fw = 8, 480, 640
+    frames = np.stack([syn.make_frame(900 + t, fh, fw, 3) for t in range(n)])
+    with ort.InferenceSession(det) as ds, ort.InferenceSession(lmk) as ls:
+        tr = face.FaceTracker(ds, ls, interval=1)
+        dfr = torch.from_numpy(frames).cuda()
+        dfaces = torch.zeros(n * ctypes.sizeof(pkg.FaceFrame), dtype=torch.uint8, device="cuda")
+        st = torch.cuda.Stream()
+
+        def call():
+            tr.track_device(dfr.data_ptr(), n, fh, fw, 3, fw * 3, fh * fw * 3, (256, 144), dfaces.data_ptr(),
+                            st.cuda_stream)
+
+        for _ in range(max(2, args.warmup // 4)):
+            call()
+        st.synchronize()
+        iters = max(5, args.iters // 8)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(iters):
+            call()
+        e1.record(st)
+        st.synchronize()
+        ms = e0.elapsed_time(e1) / (iters * n)
+        print(json.dumps({"model": "face_stage_mediapipe", "frame": [fh, fw], "ms_per_face_frame": round(ms, 4),
+                          "face_frames_per_s": round(1000.0 / ms, 1),
+                          "amortised_ms_per_frame_interval6": round(ms / 6, 4)}), flush=True)
+        tr.close()
 
 
 if __name__ == "__main__":

@@ -28,7 +28,14 @@
 //       ONNX sessions (include/vso.h) behind InferenceSession.create (model.ts:14, :38, :61)
 //   ortInfo(session) -> {inputNames, outputNames, inputShapes, outputShapes}
 //   ortRun(session, inputs: Float32Array[]) -> Promise<Float32Array[]>   (session.run)
-//   ortDestroy(session)
+//   ortDestroy(session)              (throws while a face tracker uses the session)
+//   faceCreate(detector, landmarks, config?, deviceId?) -> tracker
+//       the GPU face stage (include/vsf.h) over two ONNX sessions; config keys
+//       interval, warpGain, faceScoreThresh, landmarkScoreThresh, roiPad
+//   faceTrack(tracker, frames, n, height, width, channels, rowStride, maskW, maskH)
+//       -> Promise<{affine: number[6] | null, box: number[4] | null, videoW, videoH}[]>
+//       (the postSetFaces form, one entry per frame)
+//   faceReset(tracker), faceDestroy(tracker)
 // segment runs vss_segment on a libuv worker thread (napi_create_async_work),
 // so the event loop is not blocked — as `await session.run` does not block.
 #include <node_api.h>
@@ -39,6 +46,7 @@
 #include <string>
 #include <vector>
 
+#include "../../../include/vsf.h"
 #include "../../../include/vso.h"
 #include "../../../include/vss.h"
 
@@ -532,6 +540,7 @@ napi_value SegmentComposite(napi_env env, napi_callback_info info) { return Segm
 // ---- ONNX sessions (include/vso.h) -------------------------------------------
 struct OrtSess {
   vso_session* s = nullptr;
+  int users = 0;  // face trackers driving this session
   std::vector<std::string> in_names, out_names;
   std::vector<std::vector<int64_t>> in_shapes, out_shapes;
 };
@@ -770,8 +779,235 @@ napi_value OrtDestroy(napi_env env, napi_callback_info info) {
   void* p = nullptr;
   if (argc >= 1 && napi_get_value_external(env, argv[0], &p) == napi_ok && p) {
     OrtSess* o = static_cast<OrtSess*>(p);
+    if (o->users > 0) {
+      napi_throw_error(env, nullptr, "ONNX session in use by a face tracker: destroy the tracker first");
+      return nullptr;
+    }
     if (o->s) vso_destroy(o->s);
     o->s = nullptr;
+  }
+  return nullptr;
+}
+
+// ---- GPU face stage (include/vsf.h) ------------------------------------------
+struct Face {
+  vsf_tracker* t = nullptr;
+  OrtSess* det = nullptr;
+  OrtSess* lmk = nullptr;
+  napi_ref det_ref = nullptr, lmk_ref = nullptr;  // the sessions outlive the tracker
+  int inflight = 0;                                 // faceTrack calls not yet completed
+};
+
+void release_face(napi_env env, Face* f) {
+  if (f->t) vsf_destroy(f->t);
+  f->t = nullptr;
+  if (f->det) f->det->users--;
+  if (f->lmk) f->lmk->users--;
+  f->det = f->lmk = nullptr;
+  if (env && f->det_ref) napi_delete_reference(env, f->det_ref);
+  if (env && f->lmk_ref) napi_delete_reference(env, f->lmk_ref);
+  f->det_ref = f->lmk_ref = nullptr;
+}
+
+void finalize_face(napi_env env, void* data, void*) {
+  Face* f = static_cast<Face*>(data);
+  release_face(env, f);
+  delete f;
+}
+
+Face* get_face(napi_env env, napi_value v) {
+  void* p = nullptr;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, nullptr, "expected a face tracker");
+    return nullptr;
+  }
+  Face* f = static_cast<Face*>(p);
+  if (!f->t) {
+    napi_throw_error(env, nullptr, "face tracker already destroyed");
+    return nullptr;
+  }
+  return f;
+}
+
+napi_value FaceCreate(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  if (argc < 2) {
+    napi_throw_type_error(env, nullptr, "faceCreate(detector, landmarks, config?, deviceId?)");
+    return nullptr;
+  }
+  OrtSess* det = get_ort(env, argv[0]);
+  if (!det) return nullptr;
+  OrtSess* lmk = get_ort(env, argv[1]);
+  if (!lmk) return nullptr;
+  vsf_config c;
+  vsf_config_default(&c);
+  napi_valuetype t = napi_undefined;
+  if (argc >= 3) napi_typeof(env, argv[2], &t);
+  if (t == napi_object) {
+    get_int_prop(env, argv[2], "interval", &c.interval);
+    get_double_prop(env, argv[2], "warpGain", &c.warp_gain);
+    get_double_prop(env, argv[2], "faceScoreThresh", &c.face_score_thresh);
+    get_double_prop(env, argv[2], "landmarkScoreThresh", &c.landmark_score_thresh);
+    get_double_prop(env, argv[2], "roiPad", &c.roi_pad);
+  }
+  int device = 0;
+  if (argc >= 4) napi_get_value_int32(env, argv[3], &device);
+  vsf_tracker* tr = nullptr;
+  const int rc = vsf_create(det->s, lmk->s, &c, device, &tr);
+  if (rc != VSS_OK) {
+    throw_vss(env, "vsf_create", rc, vsf_last_error(nullptr));
+    return nullptr;
+  }
+  Face* f = new Face();
+  f->t = tr;
+  f->det = det;
+  f->lmk = lmk;
+  det->users++;
+  lmk->users++;
+  napi_create_reference(env, argv[0], 1, &f->det_ref);
+  napi_create_reference(env, argv[1], 1, &f->lmk_ref);
+  napi_value ext;
+  NAPI_OK(env, napi_create_external(env, f, finalize_face, nullptr, &ext));
+  return ext;
+}
+
+struct FaceWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  napi_ref frames_ref = nullptr, face_ref = nullptr;
+  Face* f = nullptr;
+  vsf_tracker* t = nullptr;
+  const uint8_t* frames = nullptr;
+  int n = 0, h = 0, w = 0, c = 0, mask_w = 0, mask_h = 0;
+  size_t rs = 0;
+  std::vector<vss_face_frame> out;
+  int rc = 0;
+  std::string err;
+};
+
+void FaceExecute(napi_env, void* data) {  // libuv worker thread
+  FaceWork* w = static_cast<FaceWork*>(data);
+  w->rc = vsf_track(w->t, w->frames, w->n, w->h, w->w, w->c, w->rs, w->mask_w, w->mask_h, w->out.data());
+  if (w->rc != VSS_OK) w->err = vsf_last_error(w->t);
+}
+
+napi_value doubles_array(napi_env env, const double* v, int n) {
+  napi_value a, e;
+  napi_create_array_with_length(env, n, &a);
+  for (int k = 0; k < n; ++k) {
+    napi_create_double(env, v[k], &e);
+    napi_set_element(env, a, (uint32_t)k, e);
+  }
+  return a;
+}
+
+void FaceComplete(napi_env env, napi_status, void* data) {
+  FaceWork* w = static_cast<FaceWork*>(data);
+  if (w->rc == VSS_OK) {
+    napi_value a, nul;
+    napi_get_null(env, &nul);
+    napi_create_array_with_length(env, w->out.size(), &a);
+    for (size_t k = 0; k < w->out.size(); ++k) {
+      const vss_face_frame& f = w->out[k];
+      napi_value o, v;
+      napi_create_object(env, &o);
+      napi_set_named_property(env, o, "affine", f.has_affine ? doubles_array(env, f.affine, 6) : nul);
+      napi_set_named_property(env, o, "box", f.has_box ? doubles_array(env, f.box, 4) : nul);
+      napi_create_int32(env, f.video_w, &v);
+      napi_set_named_property(env, o, "videoW", v);
+      napi_create_int32(env, f.video_h, &v);
+      napi_set_named_property(env, o, "videoH", v);
+      napi_set_element(env, a, (uint32_t)k, o);
+    }
+    napi_resolve_deferred(env, w->deferred, a);
+  } else {
+    napi_value msg, code, e;
+    const std::string m = "vsf_track failed (" + std::to_string(w->rc) + "): " + w->err;
+    napi_create_string_utf8(env, m.c_str(), m.size(), &msg);
+    napi_create_string_utf8(env, std::to_string(w->rc).c_str(), NAPI_AUTO_LENGTH, &code);
+    napi_create_error(env, code, msg, &e);
+    napi_reject_deferred(env, w->deferred, e);
+  }
+  w->f->inflight--;
+  napi_delete_reference(env, w->frames_ref);
+  napi_delete_reference(env, w->face_ref);
+  napi_delete_async_work(env, w->work);
+  delete w;
+}
+
+napi_value FaceTrack(napi_env env, napi_callback_info info) {
+  size_t argc = 9;
+  napi_value argv[9];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Face* f = argc >= 1 ? get_face(env, argv[0]) : nullptr;
+  if (!f) return nullptr;
+  int v[7] = {0, 0, 0, 0, 0, 0, 0};  // n, h, w, c, rowStride, maskW, maskH
+  bool ta = false;
+  napi_typedarray_type tt;
+  size_t len = 0, off = 0;
+  void* data = nullptr;
+  napi_value buf;
+  bool ok = argc >= 9 && napi_is_typedarray(env, argv[1], &ta) == napi_ok && ta &&
+            napi_get_typedarray_info(env, argv[1], &tt, &len, &data, &buf, &off) == napi_ok &&
+            (tt == napi_uint8_array || tt == napi_uint8_clamped_array);
+  for (int k = 0; ok && k < 7; ++k) ok = napi_get_value_int32(env, argv[2 + k], &v[k]) == napi_ok;
+  if (!ok) {
+    napi_throw_type_error(env, nullptr,
+                          "faceTrack(tracker, frames: Uint8Array, n, height, width, channels, rowStride, maskW, maskH)");
+    return nullptr;
+  }
+  if (v[0] < 0 || v[1] < 1 || v[4] < 1 || (size_t)v[0] * v[1] * v[4] > len) {
+    napi_throw_range_error(env, nullptr, "faceTrack: frames buffer smaller than n * height * rowStride");
+    return nullptr;
+  }
+  FaceWork* w = new FaceWork();
+  w->t = f->t;
+  w->frames = static_cast<const uint8_t*>(data);
+  w->n = v[0];
+  w->h = v[1];
+  w->w = v[2];
+  w->c = v[3];
+  w->rs = (size_t)v[4];
+  w->mask_w = v[5];
+  w->mask_h = v[6];
+  w->out.resize((size_t)v[0]);
+  w->f = f;
+  f->inflight++;
+  napi_create_reference(env, argv[1], 1, &w->frames_ref);
+  napi_create_reference(env, argv[0], 1, &w->face_ref);  // the tracker outlives the call
+  napi_value promise, name;
+  NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
+  napi_create_string_utf8(env, "vsf_track", NAPI_AUTO_LENGTH, &name);
+  NAPI_OK(env, napi_create_async_work(env, nullptr, name, FaceExecute, FaceComplete, w, &w->work));
+  NAPI_OK(env, napi_queue_async_work(env, w->work));
+  return promise;
+}
+
+napi_value FaceReset(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Face* f = argc >= 1 ? get_face(env, argv[0]) : nullptr;
+  if (!f) return nullptr;
+  const int rc = vsf_reset(f->t);
+  if (rc != VSS_OK) throw_vss(env, "vsf_reset", rc, vsf_last_error(f->t));
+  return nullptr;
+}
+
+napi_value FaceDestroy(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  void* p = nullptr;
+  if (argc >= 1 && napi_get_value_external(env, argv[0], &p) == napi_ok && p) {
+    Face* f = static_cast<Face*>(p);
+    if (f->inflight > 0) {
+      napi_throw_error(env, nullptr, "faceDestroy: a faceTrack call is still running on this tracker");
+      return nullptr;
+    }
+    release_face(env, f);
   }
   return nullptr;
 }
@@ -794,6 +1030,10 @@ napi_value Init(napi_env env, napi_value exports) {
       {"ortInfo", nullptr, OrtInfo, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"ortRun", nullptr, OrtRun, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"ortDestroy", nullptr, OrtDestroy, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"faceCreate", nullptr, FaceCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"faceTrack", nullptr, FaceTrack, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"faceReset", nullptr, FaceReset, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"faceDestroy", nullptr, FaceDestroy, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;
