@@ -119,6 +119,7 @@ struct GemmParams {  // y[b][m][n] = alpha * sum_k A[b][m][k] B[b][k][n] + beta 
   Epilogue ep;         // act only
 };
 
+const char* conv_kernel_name(const ConvParams& p);
 void launch_conv(const ConvParams& p, hipStream_t s, const char** name);
 void launch_binary(const BinParams& p, hipStream_t s);
 void launch_unary(const UnaryParams& p, hipStream_t s);

@@ -124,6 +124,102 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvParams p) {
   }
 }
 
+// Small convolutions (few 64x64 tiles: the deep layers of the face models ran
+// 8-22 workgroups of k_conv_gemm, each walking its K serially through LDS —
+// latency bound at 13-36 us).  Here a 16 (output channels) x 16 (output
+// pixels) tile reads its A / B operands straight from global memory into
+// registers (lane (r, g) supplies W[m r][k 4s+g] and the im2col element
+// X^[k 4s+g][pixel r]; 16 consecutive pixels per k are one coalesced 64-B
+// read) and runs v_mfma_f32_16x16x4f32 on them: CH MFMAs per chunk, all of a
+// chunk's loads in flight together and the next chunk's issued before this
+// one's MFMAs.  No LDS, no barriers, 4-16x the workgroups of k_conv_gemm.
+//   SPLIT = false: one wave per tile, the wave walks all of K;
+//   SPLIT = true : one workgroup per tile, its four waves take a quarter of K
+//                  each and reduce through LDS (K > 128: a quarter of the
+//                  serial load latency).
+// PW: 1x1 stride-1 unpadded (the im2col element is X[k][pixel]).
+template <bool PW, int CH, bool SPLIT>
+__global__ __launch_bounds__(256) void k_conv_small(ConvParams p, int tiles_m, int tiles_p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long tile = SPLIT ? (long)blockIdx.x : (long)blockIdx.x * 4 + wave;
+  const long per_img = (long)tiles_m * tiles_p;
+  if (tile >= per_img * p.N * p.G) return;  // SPLIT: uniform per workgroup
+  const int ng = (int)(tile / per_img);
+  const int rem = (int)(tile - (long)ng * per_img);
+  const int tm = rem / tiles_p, tp = rem - tm * tiles_p;  // neighbouring tiles: same weights
+  const int n = ng / p.G, grp = ng - n * p.G;
+  const int r = lane & 15, g = lane >> 4;
+  const int P = p.Ho * p.Wo;
+  const int khw = p.kh * p.kw;
+  const int K = p.Cg * khw;
+  // this wave's K range
+  const int kq = SPLIT ? ((K + 15) / 16) * 4 : K;
+  const int kbeg = SPLIT ? wave * kq : 0;
+  const int kend = SPLIT ? min(K, kbeg + kq) : K;
+  const float* xg = p.x + ((long)n * p.C + (long)grp * p.Cg) * p.H * p.W;
+  const int m = tm * 16 + r, pix = tp * 16 + r;
+  const bool m_ok = m < p.Mg, pix_ok = pix < P;
+  const float* wrow = p.w + ((long)grp * p.Mg + (m_ok ? m : 0)) * K;
+  const int oy = pix / p.Wo, ox = pix - oy * p.Wo;
+  const int iy0 = oy * p.sh - p.pt, ix0 = ox * p.sw - p.pl;
+  auto bval = [&](int k) -> float {
+    if (!pix_ok || k >= kend) return 0.f;
+    if (PW) return xg[(long)k * P + pix];
+    const int c = k / khw, rr = k - c * khw;
+    const int ky = rr / p.kw, kx = rr - ky * p.kw;
+    const int iy = iy0 + ky * p.dh, ix = ix0 + kx * p.dw;
+    return (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? xg[((long)c * p.H + iy) * p.W + ix] : 0.f;
+  };
+  float a[CH], b[CH];
+#pragma unroll
+  for (int s = 0; s < CH; ++s) {
+    const int k = kbeg + 4 * s + g;
+    a[s] = (m_ok && k < kend) ? wrow[k] : 0.f;
+    b[s] = bval(k);
+  }
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kbeg; k0 < kend; k0 += 4 * CH) {
+    const bool more = k0 + 4 * CH < kend;
+    float an[CH], bn[CH];
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {  // the next chunk's loads, in flight during this chunk's MFMAs
+        const int k = k0 + 4 * CH + 4 * s + g;
+        an[s] = (m_ok && k < kend) ? wrow[k] : 0.f;
+        bn[s] = bval(k);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < CH; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        a[s] = an[s];
+        b[s] = bn[s];
+      }
+    }
+  }
+  if (SPLIT) {  // sum the four waves' partial tiles (fixed order: deterministic)
+    __shared__ f4 part[4][64];
+    part[wave][lane] = acc;
+    __syncthreads();
+    if (wave != 0) return;
+    acc = part[0][lane];
+#pragma unroll
+    for (int w2 = 1; w2 < 4; ++w2) acc += part[w2][lane];
+  }
+  // acc[v] = D[channel 16 tm + 4g + v][pixel 16 tp + r]
+  if (!pix_ok) return;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int gm = tm * 16 + 4 * g + v;
+    if (gm >= p.Mg) continue;
+    const int ch = grp * p.Mg + gm;
+    const long o = ((long)n * p.M + ch) * P + pix;
+    p.y[o] = epilogue(p.ep, acc[v], ch, o);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_conv_dw(ConvParams p) {
   const long total = (long)p.N * p.M * p.Ho * p.Wo;
   for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
@@ -149,15 +245,71 @@ __global__ __launch_bounds__(256) void k_conv_dw(ConvParams p) {
 
 static int grid_for(long n) { return (int)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536); }
 
+enum ConvKind { CONV_DW, CONV_SMALL_PW, CONV_SMALL, CONV_GEMM };
+
+static ConvKind conv_kind(const ConvParams& p) {
+  if (p.G == p.C && p.G == p.M) return CONV_DW;
+  const long P = (long)p.Ho * p.Wo;
+  const long tiles64 = ((P + BP - 1) / BP) * ((p.Mg + BM - 1) / BM) * p.N * p.G;
+  if (tiles64 >= 1024) return CONV_GEMM;  // enough 64x64 tiles to fill 256 CUs
+  const bool pw = p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.pt == 0 && p.pl == 0 && p.Ho == p.H &&
+                  p.Wo == p.W;
+  return pw ? CONV_SMALL_PW : CONV_SMALL;
+}
+
+const char* conv_kernel_name(const ConvParams& p) {
+  switch (conv_kind(p)) {
+    case CONV_DW: return "vso::k_conv_dw(vso::ConvParams)";
+    case CONV_SMALL_PW:
+    case CONV_SMALL: {
+      static const char* names[2][4] = {
+          {"void vso::k_conv_small<false, 8, false>(vso::ConvParams, int, int)",
+           "void vso::k_conv_small<false, 16, false>(vso::ConvParams, int, int)",
+           "void vso::k_conv_small<false, 32, false>(vso::ConvParams, int, int)",
+           "void vso::k_conv_small<false, 16, true>(vso::ConvParams, int, int)"},
+          {"void vso::k_conv_small<true, 8, false>(vso::ConvParams, int, int)",
+           "void vso::k_conv_small<true, 16, false>(vso::ConvParams, int, int)",
+           "void vso::k_conv_small<true, 32, false>(vso::ConvParams, int, int)",
+           "void vso::k_conv_small<true, 16, true>(vso::ConvParams, int, int)"}};
+      const int K = p.Cg * p.kh * p.kw;
+      return names[conv_kind(p) == CONV_SMALL_PW][K <= 32 ? 0 : K <= 64 ? 1 : K <= 128 ? 2 : 3];
+    }
+    default: return "vso::k_conv_gemm(vso::ConvParams)";
+  }
+}
+
 void launch_conv(const ConvParams& p, hipStream_t s, const char** name) {
-  if (p.G == p.C && p.G == p.M) {
+  const ConvKind kind = conv_kind(p);
+  if (name) *name = conv_kernel_name(p);
+  if (kind == CONV_DW) {
     const long total = (long)p.N * p.M * p.Ho * p.Wo;
     hipLaunchKernelGGL(k_conv_dw, dim3(grid_for(total)), dim3(256), 0, s, p);
-    if (name) *name = "vso::k_conv_dw(vso::ConvParams)";
-  } else {
+  } else if (kind == CONV_GEMM) {
     const dim3 grid((p.Ho * p.Wo + BP - 1) / BP, (p.Mg + BM - 1) / BM, p.N * p.G);
     hipLaunchKernelGGL(k_conv_gemm, grid, dim3(256), 0, s, p);
-    if (name) *name = "vso::k_conv_gemm(vso::ConvParams)";
+  } else {  // 16x16 tiles: one wave each, or one workgroup each with K split four ways
+    const int tm = (p.Mg + 15) / 16, tp = (p.Ho * p.Wo + 15) / 16;
+    const long tiles = (long)tm * tp * p.N * p.G;
+    const int K = p.Cg * p.kh * p.kw;
+    const bool pw = kind == CONV_SMALL_PW;
+    if (K > 128) {
+      const dim3 grid((unsigned)tiles);
+      if (pw)
+        hipLaunchKernelGGL((k_conv_small<true, 16, true>), grid, dim3(256), 0, s, p, tm, tp);
+      else
+        hipLaunchKernelGGL((k_conv_small<false, 16, true>), grid, dim3(256), 0, s, p, tm, tp);
+    } else {  // a chunk just covers K (no MFMAs on zero padding)
+      const dim3 grid((unsigned)((tiles + 3) / 4));
+#define VSO_SMALL(PWV, CHV) hipLaunchKernelGGL((k_conv_small<PWV, CHV, false>), grid, dim3(256), 0, s, p, tm, tp)
+      if (K <= 32) {
+        if (pw) VSO_SMALL(true, 8); else VSO_SMALL(false, 8);
+      } else if (K <= 64) {
+        if (pw) VSO_SMALL(true, 16); else VSO_SMALL(false, 16);
+      } else {
+        if (pw) VSO_SMALL(true, 32); else VSO_SMALL(false, 32);
+      }
+#undef VSO_SMALL
+    }
   }
 }
 

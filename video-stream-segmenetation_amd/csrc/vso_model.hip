@@ -930,6 +930,7 @@ struct Planner {
     if (c1 >= 0 && is_act(g.nodes[c1].op) && act_of(g.nodes[c1], &ep, p.M)) {
       done.insert((size_t)c1);
       out = g.nodes[c1].out[0];
+      last = (size_t)c1;
     }
     if (!err.empty()) return false;
     p.w = upload_vec(wf);
@@ -939,8 +940,7 @@ struct Planner {
     p.x = dptr(*x);
     if (!set_runtime(out, oshape)) return false;
     p.y = dptr(vals[out]);
-    const char* kname = (p.G == p.C && p.G == p.M) ? "vso::k_conv_dw(vso::ConvParams)" : "vso::k_conv_gemm(vso::ConvParams)";
-    add(kname, [p](hipStream_t st) { launch_conv(p, st, nullptr); });
+    add(conv_kernel_name(p), [p](hipStream_t st) { launch_conv(p, st, nullptr); });
     return true;
   }
 
