@@ -220,15 +220,28 @@ __global__ __launch_bounds__(256) void k_conv_small(ConvParams p, int tiles_m, i
   }
 }
 
-__global__ __launch_bounds__(256) void k_conv_dw(ConvParams p) {
-  const long total = (long)p.N * p.M * p.Ho * p.Wo;
-  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
-    const int ox = (int)(o % p.Wo);
-    const long t = o / p.Wo;
-    const int oy = (int)(t % p.Ho);
-    const long nc = t / p.Ho;
-    const int ch = (int)(nc % p.M);
-    const float* xc = p.x + nc * p.H * p.W;  // depthwise: input channel = output channel
+// Index arithmetic in 32 bits whenever the tensor allows (I = int): a 64-bit
+// division is a ~40-instruction software sequence on CDNA, a 32-bit one a few
+// VALU ops; the elementwise kernels below choose per launch (uniform branch).
+template <typename I>
+__device__ __forceinline__ void unravel(I i, int nd, const int* dims, int* idx) {
+  for (int d = nd - 1; d >= 0; --d) {
+    idx[d] = (int)(i % (I)dims[d]);
+    i /= (I)dims[d];
+  }
+}
+
+constexpr long kIdx32 = 1L << 30;  // totals below this index in int (grid-stride steps cannot overflow)
+
+template <typename I>
+__device__ __forceinline__ void conv_dw_body(const ConvParams& p, I total) {
+  for (I o = (I)blockIdx.x * 256 + (I)threadIdx.x; o < total; o += (I)gridDim.x * 256) {
+    const int ox = (int)(o % (I)p.Wo);
+    const I t = o / (I)p.Wo;
+    const int oy = (int)(t % (I)p.Ho);
+    const I nc = t / (I)p.Ho;
+    const int ch = (int)(nc % (I)p.M);
+    const float* xc = p.x + (long)nc * p.H * p.W;  // depthwise: input channel = output channel
     const float* wc = p.w + (long)ch * p.kh * p.kw;
     float acc = 0.f;
     for (int ky = 0; ky < p.kh; ++ky) {
@@ -239,8 +252,14 @@ __global__ __launch_bounds__(256) void k_conv_dw(ConvParams p) {
         if (ix >= 0 && ix < p.W) acc = __builtin_fmaf(wc[ky * p.kw + kx], xc[(long)iy * p.W + ix], acc);
       }
     }
-    p.y[o] = epilogue(p.ep, acc, ch, o);
+    p.y[o] = epilogue(p.ep, acc, ch, (long)o);
   }
+}
+
+__global__ __launch_bounds__(256) void k_conv_dw(ConvParams p) {
+  const long total = (long)p.N * p.M * p.Ho * p.Wo;
+  if (total < kIdx32) conv_dw_body<int>(p, (int)total);
+  else conv_dw_body<long>(p, total);
 }
 
 static int grid_for(long n) { return (int)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536); }
@@ -314,17 +333,12 @@ void launch_conv(const ConvParams& p, hipStream_t s, const char** name) {
 }
 
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void unravel(long i, int nd, const int* dims, int* idx) {
-  for (int d = nd - 1; d >= 0; --d) {
-    idx[d] = (int)(i % dims[d]);
-    i /= dims[d];
-  }
-}
 
-__global__ __launch_bounds__(256) void k_binary(BinParams p) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < p.n; i += (long)gridDim.x * 256) {
+template <typename I>
+__device__ __forceinline__ void binary_body(const BinParams& p) {
+  for (I i = (I)blockIdx.x * 256 + (I)threadIdx.x; i < (I)p.n; i += (I)gridDim.x * 256) {
     int idx[kMaxDims];
-    unravel(i, p.nd, p.dims, idx);
+    unravel<I>(i, p.nd, p.dims, idx);
     long oa = 0, ob = 0;
     for (int d = 0; d < p.nd; ++d) {
       oa += idx[d] * p.sa[d];
@@ -343,15 +357,21 @@ __global__ __launch_bounds__(256) void k_binary(BinParams p) {
   }
 }
 
+__global__ __launch_bounds__(256) void k_binary(BinParams p) {
+  if (p.n < kIdx32) binary_body<int>(p);
+  else binary_body<long>(p);
+}
+
 __global__ __launch_bounds__(256) void k_unary(UnaryParams p) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < p.n; i += (long)gridDim.x * 256)
     p.y[i] = act_apply(p.x[i], p.act, p.a0, p.a1, nullptr, 0, 0);
 }
 
-__global__ __launch_bounds__(256) void k_copy(CopyParams p) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < p.n; i += (long)gridDim.x * 256) {
+template <typename I>
+__device__ __forceinline__ void copy_body(const CopyParams& p) {
+  for (I i = (I)blockIdx.x * 256 + (I)threadIdx.x; i < (I)p.n; i += (I)gridDim.x * 256) {
     int idx[kMaxDims];
-    unravel(i, p.nd, p.size, idx);
+    unravel<I>(i, p.nd, p.size, idx);
     long od = p.dst_base, os = p.src_base;
     bool in = true;
     for (int d = 0; d < p.nd; ++d) {
@@ -364,14 +384,19 @@ __global__ __launch_bounds__(256) void k_copy(CopyParams p) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_pool(PoolParams p) {
-  const long total = (long)p.N * p.C * p.Ho * p.Wo;
-  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
-    const int ox = (int)(o % p.Wo);
-    const long t = o / p.Wo;
-    const int oy = (int)(t % p.Ho);
-    const long nc = t / p.Ho;
-    const float* xc = p.x + nc * p.H * p.W;
+__global__ __launch_bounds__(256) void k_copy(CopyParams p) {
+  if (p.n < kIdx32) copy_body<int>(p);
+  else copy_body<long>(p);
+}
+
+template <typename I>
+__device__ __forceinline__ void pool_body(const PoolParams& p, I total) {
+  for (I o = (I)blockIdx.x * 256 + (I)threadIdx.x; o < total; o += (I)gridDim.x * 256) {
+    const int ox = (int)(o % (I)p.Wo);
+    const I t = o / (I)p.Wo;
+    const int oy = (int)(t % (I)p.Ho);
+    const I nc = t / (I)p.Ho;
+    const float* xc = p.x + (long)nc * p.H * p.W;
     float m = -INFINITY, s = 0.f;
     int cnt = 0;
     for (int ky = 0; ky < p.kh; ++ky) {
@@ -388,6 +413,12 @@ __global__ __launch_bounds__(256) void k_pool(PoolParams p) {
     }
     p.y[o] = p.max_mode ? m : s / (float)(p.count_include_pad ? p.kh * p.kw : (cnt > 0 ? cnt : 1));
   }
+}
+
+__global__ __launch_bounds__(256) void k_pool(PoolParams p) {
+  const long total = (long)p.N * p.C * p.Ho * p.Wo;
+  if (total < kIdx32) pool_body<int>(p, (int)total);
+  else pool_body<long>(p, total);
 }
 
 __device__ __forceinline__ float block_sum(float v, float* sh) {
