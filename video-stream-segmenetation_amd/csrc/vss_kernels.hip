@@ -562,12 +562,13 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
         f4 v = {0.f, 0.f, 0.f, 0.f};
         if (pix < P_IN && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo) {
-          const float sy = fmaxf(((float)yy + 0.5f) * 0.5f - 0.5f, 0.f);
-          const int y0 = (int)sy, y1 = y0 + (y0 < h - 1 ? 1 : 0);
-          const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
-          const float sx = fmaxf(((float)xx + 0.5f) * 0.5f - 0.5f, 0.f);
-          const int x0 = (int)sx, x1 = x0 + (x0 < w - 1 ? 1 : 0);
-          const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
+          // source coordinate max((o + 0.5) / 2 - 0.5, 0) in integers: o = 0 -> (0, 0);
+          // odd o -> ((o - 1) / 2, 0.25); even o > 0 -> (o / 2 - 1, 0.75) — the
+          // same floats the float formula gives, without its converts
+          const int y0 = yy > 0 ? (yy - 1) >> 1 : 0, y1 = y0 + (y0 < h - 1 ? 1 : 0);
+          const float ly1 = yy > 0 ? ((yy & 1) ? 0.25f : 0.75f) : 0.f, ly0 = 1.f - ly1;
+          const int x0 = xx > 0 ? (xx - 1) >> 1 : 0, x1 = x0 + (x0 < w - 1 ? 1 : 0);
+          const float lx1 = xx > 0 ? ((xx & 1) ? 0.25f : 0.75f) : 0.f, lx0 = 1.f - lx1;
           const int r0 = min(max(y0 - sy0, 0), SR - 1), r1 = min(max(y1 - sy0, 0), SR - 1);
           const int q0 = min(max(x0 - sx0, 0), SC - 1), q1 = min(max(x1 - sx0, 0), SC - 1);
           const f4 v00 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q0) * CL + 4 * c4);
