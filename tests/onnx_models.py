@@ -55,9 +55,11 @@ class Builder:
         return R.make_model(self.nodes, self.inits, inputs, outputs, opset=opset)
 
 
-def conv_zoo():
+def conv_zoo(h=64, w=80):
     """Every convolution shape class the face models and MODNet use, with the
-    epilogue fusions (BatchNormalization folding, residual Add, activations)."""
+    epilogue fusions (BatchNormalization folding, residual Add, activations).
+    At 64x80 every convolution runs as k_conv_small; at 512x512 the first two
+    have >= 1024 64x64 tiles and run as k_conv_gemm (test_gpu_onnx checks both)."""
     b = Builder(1)
     x = "x"
     a = b.conv(x, 3, 24, 5, stride=2, pads=[1, 1, 2, 2])                  # MediaPipe stem: 5x5 s2 asym pads
@@ -81,7 +83,8 @@ def conv_zoo():
     v = b.conv(dl, 40, 16, 3, pads=[0, 0, 0, 0], bias=False)               # valid padding, no bias
     nb = b.w(16, 40 // 1, 1, 1)
     v2 = b.op("Conv", [dl, nb], kernel_shape=[1, 1], auto_pad="SAME_UPPER", strides=[2, 2])
-    return b.model([("x", [1, 3, 64, 80])], [(v, [1, 16, 14, 18]), (v2, [1, 16, 8, 10])])
+    h2, w2 = (h // 2 - 1) // 2 + 1, (w // 2 - 1) // 2 + 1
+    return b.model([("x", [1, 3, h, w])], [(v, [1, 16, h2 - 2, w2 - 2]), (v2, [1, 16, (h2 + 1) // 2, (w2 + 1) // 2])])
 
 
 def ops_zoo():
@@ -276,7 +279,9 @@ def face_landmarks_like(LH=192, LW=192, score_bias=2.0, seed=6):
     return b.model([("image", [1, 3, LH, LW])], [("scores", [1]), ("landmarks", [1, 468, 3])])
 
 
-MODELS = {"conv_zoo": (conv_zoo, {"x": (1, 3, 64, 80)}), "ops_zoo": (ops_zoo, {"x": (2, 8, 12, 16)}),
+MODELS = {"conv_zoo": (conv_zoo, {"x": (1, 3, 64, 80)}),
+          "conv_zoo_512": (lambda: conv_zoo(512, 512), {"x": (1, 3, 512, 512)}),
+          "ops_zoo": (ops_zoo, {"x": (2, 8, 12, 16)}),
           "modnet_like": (modnet_like, {"input": (1, 3, 64, 96)}),
           "q4f16_like": (q4f16_like, {"input": (1, 3, 64, 96)})}
 

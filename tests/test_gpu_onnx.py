@@ -129,3 +129,19 @@ def test_cast_float16_bitwise(ort):
     with np.errstate(over="ignore"):
         want = v.astype(np.float16).astype(np.float32)
     assert np.array_equal(got, want)
+
+
+def test_conv_kernel_choice(ort):
+    """k_conv_small takes convolutions with < 1024 64x64 output tiles (every
+    conv_zoo layer at 64x80, incl. the K > 128 split-K form), k_conv_gemm the
+    large ones (conv_zoo at 512x512: the stem and the first 1x1); both forms are
+    checked against the oracle by test_synthetic_models."""
+    with ort.InferenceSession(M.conv_zoo()) as s:
+        small = s.launches()
+    with ort.InferenceSession(M.conv_zoo(512, 512)) as s:
+        large = s.launches()
+    assert not any("k_conv_gemm" in n for n in small), small
+    assert any("k_conv_small<false, 16, true>" in n for n in small)  # split-K (K = 288, 360)
+    assert any("k_conv_small<true, 8, false>" in n for n in small)   # 1x1, K = 24
+    assert sum("k_conv_gemm" in n for n in large) == 2, large
+    assert any("k_conv_small" in n for n in large)
