@@ -145,3 +145,17 @@ def test_conv_kernel_choice(ort):
     assert any("k_conv_small<true, 8, false>" in n for n in small)   # 1x1, K = 24
     assert sum("k_conv_gemm" in n for n in large) == 2, large
     assert any("k_conv_small" in n for n in large)
+
+
+def test_residual_source_fusion(ort):
+    """MaxPool(2x2 s2) -> [channel Pad] -> Add(Conv) is read by the conv's
+    epilogue (no pool / pad launch): all three of the detector's, four of the
+    landmark net's five (the fifth feeds two Adds).  Values: test_reference_mediapipe_models."""
+    names = {}
+    for key in ("mediapipe_face_detector", "mediapipe_face_landmarks"):
+        model = M.load_golden(os.path.join(GOLDEN, key + ".npz"))[0]
+        with ort.InferenceSession(model) as s:
+            names[key] = s.launches()
+    assert sum("k_pool" in n for n in names["mediapipe_face_detector"]) == 0
+    assert sum("k_pool" in n for n in names["mediapipe_face_landmarks"]) == 1
+    assert len(names["mediapipe_face_detector"]) == 77 and len(names["mediapipe_face_landmarks"]) == 48

@@ -21,6 +21,11 @@ struct Epilogue {
   float a0, a1;        // CLIP lo/hi, LEAKY alpha
   const float* slope;  // PRELU: per output channel ([M]) or one value (slope_stride 0)
   int slope_stride;
+  // res_mode 1: res is [N][res_c][Ho][Wo], channels >= res_c add 0 (an ONNX Pad
+  // of the channel axis, fused); 2: res is [N][res_c][res_h][res_w] and the
+  // value added is its 2x2 stride-2 max (a MaxPool, fused, then that Pad)
+  int res_mode, res_c, res_h, res_w;
+  int out_c, out_hw, out_w;  // the output's M, Ho*Wo, Wo (res_mode != 0)
 };
 
 struct ConvParams {

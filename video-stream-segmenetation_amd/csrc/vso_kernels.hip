@@ -39,9 +39,24 @@ __device__ __forceinline__ float act_apply(float v, int act, float a0, float a1,
   }
 }
 
-__device__ __forceinline__ float epilogue(const Epilogue& e, float v, int ch, long idx) {
+// n / pix: the output's image and pixel (the conv kernels know them; the
+// fused residual sources of res_mode 1 / 2 are addressed by them)
+__device__ __forceinline__ float epilogue(const Epilogue& e, float v, int ch, long idx, int n, int pix) {
   if (e.bias) v += e.bias[ch];
-  if (e.res) v += e.res[idx];
+  if (e.res) {
+    if (e.res_mode == 0) {
+      v += e.res[idx];
+    } else if (ch < e.res_c) {
+      const long plane = (long)n * e.res_c + ch;
+      if (e.res_mode == 1) {
+        v += e.res[plane * e.out_hw + pix];
+      } else {
+        const int y = pix / e.out_w, x = pix - y * e.out_w;
+        const float* b = e.res + (plane * e.res_h + 2 * y) * e.res_w + 2 * x;
+        v += fmaxf(fmaxf(b[0], b[1]), fmaxf(b[e.res_w], b[e.res_w + 1]));
+      }
+    }
+  }
   return act_apply(v, e.act, e.a0, e.a1, e.slope, ch, e.slope_stride);
 }
 
@@ -118,7 +133,7 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvParams p) {
       const int pix = p0 + 16 * j + r;
       if (pix < P) {
         const long o = ((long)n * p.M + ch) * P + pix;
-        p.y[o] = epilogue(p.ep, acc[j][v], ch, o);
+        p.y[o] = epilogue(p.ep, acc[j][v], ch, o, n, pix);
       }
     }
   }
@@ -216,7 +231,7 @@ __global__ __launch_bounds__(256) void k_conv_small(ConvParams p, int tiles_m, i
     if (gm >= p.Mg) continue;
     const int ch = grp * p.Mg + gm;
     const long o = ((long)n * p.M + ch) * P + pix;
-    p.y[o] = epilogue(p.ep, acc[v], ch, o);
+    p.y[o] = epilogue(p.ep, acc[v], ch, o, n, pix);
   }
 }
 
@@ -252,7 +267,7 @@ __device__ __forceinline__ void conv_dw_body(const ConvParams& p, I total) {
         if (ix >= 0 && ix < p.W) acc = __builtin_fmaf(wc[ky * p.kw + kx], xc[(long)iy * p.W + ix], acc);
       }
     }
-    p.y[o] = epilogue(p.ep, acc, ch, (long)o);
+    p.y[o] = epilogue(p.ep, acc, ch, (long)o, (int)(nc / (I)p.M), oy * p.Wo + ox);
   }
 }
 

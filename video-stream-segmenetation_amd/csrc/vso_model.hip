@@ -455,6 +455,13 @@ struct Planner {
   std::map<std::string, Value> vals;
   std::map<std::string, int> consumers;
   std::set<size_t> done;  // node indices absorbed by a fused launch
+  // Add operands computed inside the consuming convolution's epilogue instead
+  // of by their own launches: MaxPool(2x2, s2) -> [Pad of the channel axis] -> Add
+  struct ResFuse {
+    std::string src;  // the MaxPool's input, or the Pad's input
+    int mode;         // Epilogue::res_mode
+  };
+  std::map<std::string, ResFuse> res_fuse;
   std::map<const void*, float*> dev_consts;
   std::string err;
 
@@ -915,7 +922,28 @@ struct Planner {
       }
     }
     const std::vector<int64_t> oshape = {p.N, p.M, p.Ho, p.Wo};
-    if (c1 >= 0 && g.nodes[c1].op == "Add") {
+    if (c1 >= 0 && g.nodes[c1].op == "Add" && res_fuse.count(g.nodes[c1].in[0] == out ? g.nodes[c1].in[1]
+                                                                                   : g.nodes[c1].in[0])) {
+      const Node& ad = g.nodes[c1];
+      const ResFuse& rf = res_fuse[ad.in[0] == out ? ad.in[1] : ad.in[0]];
+      Value* sv = val(rf.src);
+      if (!sv || sv->is_const || sv->shape.size() != 4 || sv->shape[0] != p.N || sv->shape[1] > p.M ||
+          (rf.mode == 1 && (sv->shape[2] != p.Ho || sv->shape[3] != p.Wo)) ||
+          (rf.mode == 2 && (sv->shape[2] / 2 != p.Ho || sv->shape[3] / 2 != p.Wo)))
+        return fail("Conv '" + nd.name + "': internal: fused residual shape");
+      ep.res = dptr(*sv);
+      ep.res_mode = rf.mode;
+      ep.res_c = (int)sv->shape[1];
+      ep.res_h = (int)sv->shape[2];
+      ep.res_w = (int)sv->shape[3];
+      ep.out_c = p.M;
+      ep.out_hw = p.Ho * p.Wo;
+      ep.out_w = p.Wo;
+      done.insert((size_t)c1);
+      out = ad.out[0];
+      last = (size_t)c1;
+      c1 = sole_consumer(out, last);
+    } else if (c1 >= 0 && g.nodes[c1].op == "Add") {
       const Node& ad = g.nodes[c1];
       const std::string& other = ad.in[0] == out ? ad.in[1] : ad.in[0];
       Value* o = val(other);
@@ -1441,6 +1469,77 @@ struct Planner {
     return true;
   }
 
+  int producer(const std::string& name) const {
+    for (size_t k = 0; k < g.nodes.size(); ++k)
+      for (const std::string& o : g.nodes[k].out)
+        if (o == name) return (int)k;
+    return -1;
+  }
+
+  // MaxPool(2x2, stride 2, unpadded, floor) -> [Pad: zeros appended on the
+  // channel axis only] -> Add(x, Conv(...)) where the Conv's output feeds only
+  // that Add (so plan_conv absorbs the Add): the Pad / MaxPool launches are
+  // dropped and the conv's epilogue reads the pool input (BlazeFace's and the
+  // landmark net's strided residual path: 5 + 8 launches).
+  void find_residual_fusions() {
+    for (size_t a = 0; a < g.nodes.size(); ++a) {
+      const Node& ad = g.nodes[a];
+      if (ad.op != "Add" || ad.in.size() != 2 || ad.in[0] == ad.in[1]) continue;
+      for (int side = 0; side < 2; ++side) {
+        const std::string& cv = ad.in[side];
+        const std::string& o = ad.in[1 - side];
+        const int pc = producer(cv);
+        if (pc < 0 || g.nodes[pc].op != "Conv" || sole_consumer(cv, (size_t)pc) != (int)a) continue;
+        int pn = producer(o);
+        if (pn < 0 || sole_consumer(o, (size_t)pn) != (int)a) continue;
+        int mode = 0, pad_node = -1;
+        std::string cur = o;
+        if (g.nodes[pn].op == "Pad" && channel_pad_only(g.nodes[pn])) {
+          pad_node = pn;
+          cur = g.nodes[pn].in[0];
+          mode = 1;
+          pn = producer(cur);
+          if (pn >= 0 && sole_consumer(cur, (size_t)pn) != pad_node) pn = -1;
+        }
+        int pool_node = -1;
+        if (pn >= 0 && g.nodes[pn].op == "MaxPool" && pool_2x2(g.nodes[pn])) {
+          pool_node = pn;
+          cur = g.nodes[pn].in[0];
+          mode = 2;
+        }
+        if (mode == 0) continue;
+        if (pad_node >= 0) done.insert((size_t)pad_node);
+        if (pool_node >= 0) done.insert((size_t)pool_node);
+        res_fuse[o] = ResFuse{cur, mode};
+        break;
+      }
+    }
+  }
+
+  bool channel_pad_only(const Node& nd) {
+    if (nd.as("mode", "constant") != "constant" || nd.in.size() < 2) return false;
+    Value* pv = val(nd.in[1]);
+    if (!pv || !pv->is_const || !pv->c.is_int || pv->c.i.size() != 8) return false;
+    if (nd.in.size() > 2 && !nd.in[2].empty()) {
+      Value* cv = val(nd.in[2]);
+      if (!cv || !cv->is_const || (!cv->c.f.empty() && cv->c.f[0] != 0.f)) return false;
+    }
+    if (nd.in.size() > 3 && !nd.in[3].empty()) return false;  // axes
+    const std::vector<int64_t>& q = pv->c.i;
+    for (int d = 0; d < 8; ++d)
+      if (d != 5 && q[d] != 0) return false;
+    return q[5] >= 0;
+  }
+
+  static bool pool_2x2(const Node& nd) {
+    const std::vector<int64_t> k = nd.ais("kernel_shape"), st = nd.ais("strides"), pd = nd.ais("pads"),
+                               dl = nd.ais("dilations");
+    if (k != std::vector<int64_t>{2, 2} || st != std::vector<int64_t>{2, 2}) return false;
+    for (int64_t v : pd) if (v != 0) return false;
+    for (int64_t v : dl) if (v != 1) return false;
+    return nd.ai("ceil_mode", 0) == 0 && nd.as("auto_pad", "NOTSET") == "NOTSET";
+  }
+
   bool run(const std::vector<std::vector<int64_t>>& in_shapes) {
     for (const Node& nd : g.nodes)
       for (const std::string& i : nd.in)
@@ -1452,6 +1551,7 @@ struct Planner {
       s->in_shapes.push_back(in_shapes[k]);
       s->in_bufs.push_back(vals[g.inputs[k].name].buf);
     }
+    find_residual_fusions();
     for (size_t k = 0; k < g.nodes.size(); ++k) {
       if (done.count(k)) continue;
       if (!plan_node(k)) return false;
