@@ -390,6 +390,7 @@ Geometry letterbox(int S, int w, int h) {
 
 int ensure_slots(vsf_tracker* t, int k) {
   if (k <= t->slots) return 0;
+  VSF_HIP(t, hipDeviceSynchronize());  // earlier calls' kernels may still use the old arena
   if (t->arena) (void)hipFree(t->arena);
   if (t->d_dets) (void)hipFree(t->d_dets);
   t->arena = nullptr;
