@@ -58,8 +58,9 @@ class Builder:
 def conv_zoo(h=64, w=80):
     """Every convolution shape class the face models and MODNet use, with the
     epilogue fusions (BatchNormalization folding, residual Add, activations).
-    At 64x80 every convolution runs as k_conv_small; at 512x512 the first two
-    have >= 1024 64x64 tiles and run as k_conv_gemm (test_gpu_onnx checks both)."""
+    At 64x80 the two depthwise -> 1x1 pairs run as k_conv_dwpw and the rest as
+    k_conv_small; at 512x512 the stem has >= 1024 64x64 tiles and runs as
+    k_conv_gemm (test_gpu_onnx checks the choice)."""
     b = Builder(1)
     x = "x"
     a = b.conv(x, 3, 24, 5, stride=2, pads=[1, 1, 2, 2])                  # MediaPipe stem: 5x5 s2 asym pads

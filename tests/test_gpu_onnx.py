@@ -132,19 +132,21 @@ def test_cast_float16_bitwise(ort):
 
 
 def test_conv_kernel_choice(ort):
-    """k_conv_small takes convolutions with < 1024 64x64 output tiles (every
+    """A depthwise conv feeding a 1x1 one runs with it as k_conv_dwpw;
+    k_conv_small takes convolutions with < 1024 64x64 output tiles (every other
     conv_zoo layer at 64x80, incl. the K > 128 split-K form), k_conv_gemm the
-    large ones (conv_zoo at 512x512: the stem and the first 1x1); both forms are
-    checked against the oracle by test_synthetic_models."""
+    large ones (conv_zoo at 512x512: the stem); all forms are checked against
+    the oracle by test_synthetic_models."""
     with ort.InferenceSession(M.conv_zoo()) as s:
         small = s.launches()
     with ort.InferenceSession(M.conv_zoo(512, 512)) as s:
         large = s.launches()
     assert not any("k_conv_gemm" in n for n in small), small
     assert any("k_conv_small<false, 16, true>" in n for n in small)  # split-K (K = 288, 360)
-    assert any("k_conv_small<true, 8, false>" in n for n in small)   # 1x1, K = 24
-    assert sum("k_conv_gemm" in n for n in large) == 2, large
-    assert any("k_conv_small" in n for n in large)
+    assert sum("k_conv_dwpw" in n for n in small) == 2               # both depthwise -> 1x1 pairs
+    assert not any("k_conv_dw(" in n for n in small)
+    assert sum("k_conv_gemm" in n for n in large) == 1, large          # the 5x5 stem at 256x256 outputs
+    assert sum("k_conv_dwpw" in n for n in large) == 2 and any("k_conv_small" in n for n in large)
 
 
 def test_residual_source_fusion(ort):
@@ -158,4 +160,8 @@ def test_residual_source_fusion(ort):
             names[key] = s.launches()
     assert sum("k_pool" in n for n in names["mediapipe_face_detector"]) == 0
     assert sum("k_pool" in n for n in names["mediapipe_face_landmarks"]) == 1
-    assert len(names["mediapipe_face_detector"]) == 77 and len(names["mediapipe_face_landmarks"]) == 48
+    # and every depthwise conv runs inside its 1x1 consumer (k_conv_dwpw): 32 and 20 launches fewer
+    for key, dw in (("mediapipe_face_detector", 32), ("mediapipe_face_landmarks", 20)):
+        assert sum("k_conv_dwpw" in n for n in names[key]) == dw
+        assert not any("k_conv_dw(" in n for n in names[key])
+    assert len(names["mediapipe_face_detector"]) == 45 and len(names["mediapipe_face_landmarks"]) == 28

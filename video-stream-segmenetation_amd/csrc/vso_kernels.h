@@ -28,6 +28,17 @@ struct Epilogue {
   int out_c, out_hw, out_w;  // the output's M, Ho*Wo, Wo (res_mode != 0)
 };
 
+// A depthwise convolution fused in front of a 1x1 one (k_conv_dwpw): `x` is
+// the depthwise conv's input; its output — the 1x1's input — exists only in
+// LDS.  Same FMA order and epilogue as k_conv_dw: the values k_conv_dw would
+// have stored, bit for bit.
+struct DwPre {
+  const float* w;  // [C][kh][kw]; null: no fused producer
+  int H, W;        // the depthwise input's size
+  int kh, kw, sh, sw, dh, dw, pt, pl;
+  Epilogue ep;     // bias / activation (no residual)
+};
+
 struct ConvParams {
   const float* x;  // [N][C][H][W]
   const float* w;  // [M][Cg][kh][kw]
@@ -36,7 +47,10 @@ struct ConvParams {
   int G, Cg, Mg;   // groups, input / output channels per group
   int kh, kw, sh, sw, dh, dw, pt, pl;
   Epilogue ep;
+  DwPre pre;       // k_conv_dwpw only (x is then the depthwise input)
 };
+
+constexpr int kDwPwMaxC = 256;  // channels a fused depthwise -> 1x1 pair may have
 
 enum BinOp : int { BIN_ADD = 0, BIN_SUB = 1, BIN_MUL = 2, BIN_DIV = 3, BIN_PRELU = 4 };
 

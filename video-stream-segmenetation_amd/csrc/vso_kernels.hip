@@ -139,6 +139,106 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvParams p) {
   }
 }
 
+// Depthwise -> 1x1 pair in one launch (the face models' 32 / 20 dw layers each
+// paid a whole launch, ~4.6 us, for a few MFLOP).  A workgroup owns 16 output
+// pixels and 64 output channels: its 256 threads first compute the depthwise
+// outputs of those pixels for all C channels into LDS (k_conv_dw's arithmetic:
+// the same floats), then each wave runs one 16x16 MFMA tile of the 1x1 over
+// them (A = weights from global / L1, B = the LDS tile), in k order as
+// k_conv_small does.  Only the final output reaches HBM.
+__global__ __launch_bounds__(256) void k_conv_dwpw(ConvParams p) {
+  __shared__ float bs[kDwPwMaxC][17];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int P = p.Ho * p.Wo, K = p.C;
+  const int tp = blockIdx.x, n = blockIdx.z;
+  const DwPre& q = p.pre;
+  // phase 1: depthwise outputs of pixels 16 tp .. 16 tp + 15, channels 0 .. K-1.
+  // 3x3: four outputs per thread per pass, all 36 taps' loads issued together
+  // (an absent tap loads nothing and adds 0: the value of k_conv_dw's skip,
+  // up to the sign of a zero)
+  if (q.kh == 3 && q.kw == 3) {
+    for (int e0 = tid; e0 < K * 16; e0 += 1024) {
+      float t[4][9], wv[4][9];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 256 * u, c = min(e >> 4, K - 1), pix = tp * 16 + (e & 15);
+        const int oy = pix / p.Wo, ox = pix - oy * p.Wo;
+        const float* xc = p.x + ((long)n * K + c) * q.H * q.W;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int iy = oy * q.sh - q.pt + (k / 3) * q.dh, ix = ox * q.sw - q.pl + (k % 3) * q.dw;
+          const bool in = e < K * 16 && pix < P && iy >= 0 && iy < q.H && ix >= 0 && ix < q.W;
+          t[u][k] = in ? xc[(long)iy * q.W + ix] : 0.f;
+          wv[u][k] = q.w[(long)c * 9 + k];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 256 * u;
+        if (e >= K * 16) break;
+        const int c = e >> 4, pl = e & 15, pix = tp * 16 + pl;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc = __builtin_fmaf(wv[u][k], t[u][k], acc);
+        bs[c][pl] = pix < P ? epilogue(q.ep, acc, c, 0, n, pix) : 0.f;
+      }
+    }
+  } else {
+    for (int e = tid; e < K * 16; e += 256) {
+      const int c = e >> 4, pl = e & 15, pix = tp * 16 + pl;
+      float v = 0.f;
+      if (pix < P) {
+        const int oy = pix / p.Wo, ox = pix - oy * p.Wo;
+        const float* xc = p.x + ((long)n * K + c) * q.H * q.W;
+        const float* wc = q.w + (long)c * q.kh * q.kw;
+        float acc = 0.f;
+        for (int ky = 0; ky < q.kh; ++ky) {
+          const int iy = oy * q.sh - q.pt + ky * q.dh;
+          if (iy < 0 || iy >= q.H) continue;
+          for (int kx = 0; kx < q.kw; ++kx) {
+            const int ix = ox * q.sw - q.pl + kx * q.dw;
+            if (ix >= 0 && ix < q.W) acc = __builtin_fmaf(wc[ky * q.kw + kx], xc[(long)iy * q.W + ix], acc);
+          }
+        }
+        v = epilogue(q.ep, acc, c, 0, n, pix);
+      }
+      bs[c][pl] = v;
+    }
+  }
+  __syncthreads();
+  // phase 2: this wave's 16 output channels x the 16 pixels
+  const int m0 = blockIdx.y * 64 + wave * 16;
+  if (m0 >= p.M) return;
+  const int m = m0 + r;
+  const bool m_ok = m < p.M;
+  const float* wrow = p.w + (long)(m_ok ? m : 0) * K;
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  constexpr int CH = 8;
+  for (int k0 = 0; k0 < K; k0 += 4 * CH) {
+    float a[CH];
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const int k = k0 + 4 * s + g;
+      a[s] = (m_ok && k < K) ? wrow[k] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const int k = k0 + 4 * s + g;
+      if (k0 + 4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], k < K ? bs[k][r] : 0.f, acc, 0, 0, 0);
+    }
+  }
+  const int pix = tp * 16 + r;
+  if (pix >= P) return;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int ch = m0 + 4 * g + v;
+    if (ch >= p.M) continue;
+    const long o = ((long)n * p.M + ch) * P + pix;
+    p.y[o] = epilogue(p.ep, acc[v], ch, o, n, pix);
+  }
+}
+
 // Small convolutions (few 64x64 tiles: the deep layers of the face models ran
 // 8-22 workgroups of k_conv_gemm, each walking its K serially through LDS —
 // latency bound at 13-36 us).  Here a 16 (output channels) x 16 (output
@@ -292,6 +392,7 @@ static ConvKind conv_kind(const ConvParams& p) {
 }
 
 const char* conv_kernel_name(const ConvParams& p) {
+  if (p.pre.w) return "vso::k_conv_dwpw(vso::ConvParams)";
   switch (conv_kind(p)) {
     case CONV_DW: return "vso::k_conv_dw(vso::ConvParams)";
     case CONV_SMALL_PW:
@@ -313,8 +414,13 @@ const char* conv_kernel_name(const ConvParams& p) {
 }
 
 void launch_conv(const ConvParams& p, hipStream_t s, const char** name) {
-  const ConvKind kind = conv_kind(p);
   if (name) *name = conv_kernel_name(p);
+  if (p.pre.w) {
+    const dim3 grid((unsigned)((p.Ho * p.Wo + 15) / 16), (unsigned)((p.M + 63) / 64), (unsigned)p.N);
+    hipLaunchKernelGGL(k_conv_dwpw, grid, dim3(256), 0, s, p);
+    return;
+  }
+  const ConvKind kind = conv_kind(p);
   if (kind == CONV_DW) {
     const long total = (long)p.N * p.M * p.Ho * p.Wo;
     hipLaunchKernelGGL(k_conv_dw, dim3(grid_for(total)), dim3(256), 0, s, p);

@@ -462,6 +462,7 @@ struct Planner {
     int mode;         // Epilogue::res_mode
   };
   std::map<std::string, ResFuse> res_fuse;
+  std::map<std::string, std::pair<const float*, DwPre>> pending_dw;  // dw outputs computed in their 1x1 consumer (input, producer)
   std::map<const void*, float*> dev_consts;
   std::string err;
 
@@ -968,7 +969,34 @@ struct Planner {
     p.x = dptr(*x);
     if (!set_runtime(out, oshape)) return false;
     p.y = dptr(vals[out]);
+    if (p.G == p.C && p.G == p.M && !ep.res && p.C <= kDwPwMaxC && feeds_pointwise(out, last, p.M)) {
+      pending_dw[out] = {p.x, DwPre{p.w, p.H, p.W, p.kh, p.kw, p.sh, p.sw, p.dh, p.dw, p.pt, p.pl, ep}};
+      return true;  // no launch: its 1x1 consumer computes it (k_conv_dwpw)
+    }
+    auto pre = pending_dw.find(nd.in[0]);
+    if (pre != pending_dw.end()) {
+      if (p.G != 1 || p.kh != 1 || p.kw != 1 || p.sh != 1 || p.sw != 1 || p.pt || p.pl || p.Ho != p.H || p.Wo != p.W)
+        return fail("Conv '" + nd.name + "': internal: fused depthwise producer");
+      p.x = pre->second.first;
+      p.pre = pre->second.second;
+    }
     add(conv_kernel_name(p), [p](hipStream_t st) { launch_conv(p, st, nullptr); });
+    return true;
+  }
+
+  // The output of a depthwise conv feeds exactly one Conv, 1x1 / stride 1 /
+  // unpadded / ungrouped, on all its channels: the pair runs as k_conv_dwpw.
+  bool feeds_pointwise(const std::string& out, size_t last, int channels) {
+    const int c = sole_consumer(out, last);
+    if (c < 0 || g.nodes[c].op != "Conv" || g.nodes[c].in.empty() || g.nodes[c].in[0] != out) return false;
+    const Node& pw = g.nodes[c];
+    Value* w = val(pw.in[1]);
+    if (!w || !w->is_const || w->c.dims.size() != 4 || w->c.dims[1] != channels || w->c.dims[2] != 1 ||
+        w->c.dims[3] != 1 || pw.ai("group", 1) != 1 || pw.as("auto_pad", "NOTSET") != "NOTSET")
+      return false;
+    for (int64_t v : pw.ais("strides")) if (v != 1) return false;
+    for (int64_t v : pw.ais("pads")) if (v != 0) return false;
+    for (int64_t v : pw.ais("dilations")) if (v != 1) return false;
     return true;
   }
 
