@@ -67,9 +67,14 @@ enum {
                             the handle was created with env VSS_FORWARD=1 (the planner then
                             restricts tiles to the persistent forward's table and skips the
                             autotuner).  Results are bitwise identical either way. */
-  VSS_OPT_FORWARD_FAULTS = 5 /* vss_get_option only: dependency waits of k_forward that gave up
+  VSS_OPT_FORWARD_FAULTS = 5, /* vss_get_option only: dependency waits of k_forward that gave up
                                 (bounded spins; 0 in a correct run).  Synchronises the device
                                 and clears the count. */
+  VSS_OPT_KEEP_STEM = 6  /* 1: the stem fused into layer 1 also stores its activation, so
+                            vss_read_layer(0) can report it (a debugging aid: 4.7 MB of HBM
+                            writes per batch of 8 at 144x256 that no layer reads).  Default 0:
+                            the forward writes only what a later layer or the caller reads;
+                            vss_read_layer(0) then fails with VSS_E_INVALID_ARG. */
 };
 
 typedef struct vss_handle vss_handle;

@@ -66,6 +66,7 @@ def test_forward_default_bitwise_vs_layer_launches(pkg, oracle, blob, synthetic,
 def test_forward_every_layer_bitwise(pkg, synthetic, torch_cuda):
     with pkg.Session(dtype="bf16x2", max_batch=4) as s:
         f = _frames(synthetic, 4, start=950)
+        s.set_option(pkg.VSS_OPT_KEEP_STEM, 1)
         s.set_option(pkg.VSS_OPT_FORWARD, 0)
         s.segment_frames(f)
         want = [s.read_layer(li, 4) for li in range(s.n_layers - 1)]

@@ -31,6 +31,7 @@ def torch_cuda():
 @pytest.fixture(scope="module")
 def sess_f32(pkg, torch_cuda):
     s = pkg.Session(dtype="f32", max_batch=8)
+    s.set_option(pkg.VSS_OPT_KEEP_STEM, 1)  # test_layers_f32 reads the fused stem
     yield s
     s.close()
 
@@ -240,6 +241,7 @@ def test_stem_fusion_bitwise(pkg, synthetic, torch_cuda):
     f = _frames(synthetic, 5, start=800)
     with pkg.Session(dtype="bf16x2", max_batch=8) as s:
         assert s.layer_kernel(0).startswith("(fused into layer 1")
+        s.set_option(pkg.VSS_OPT_KEEP_STEM, 1)
         a, _, _ = s.segment_frames(f)
         taps_a = [s.read_layer(li, 5) for li in range(2)]
     os.environ["VSS_FUSE_STEM"] = "0"
@@ -255,11 +257,33 @@ def test_stem_fusion_bitwise(pkg, synthetic, torch_cuda):
         assert np.array_equal(taps_a[li], taps_b[li]), li
 
 
+def test_keep_stem_option(pkg, synthetic, torch_cuda):
+    # by default the fused stem's activation is not stored (no layer reads it);
+    # VSS_OPT_KEEP_STEM stores it for vss_read_layer(0), masks unchanged
+    f = _frames(synthetic, 3, start=860)
+    with pkg.Session(dtype="bf16x2", max_batch=4) as s:
+        assert s.layer_kernel(0).startswith("(fused into layer 1")
+        assert s.get_option(pkg.VSS_OPT_KEEP_STEM) == 0
+        a, _, _ = s.segment_frames(f)
+        with pytest.raises(pkg.VssError, match="VSS_OPT_KEEP_STEM"):
+            s.read_layer(0, 3)
+        l1 = s.read_layer(1, 3)
+        s.set_option(pkg.VSS_OPT_KEEP_STEM, 1)
+        b, _, _ = s.segment_frames(f)
+        stem = s.read_layer(0, 3)
+        assert np.array_equal(a, b) and np.array_equal(l1, s.read_layer(1, 3))
+        assert np.isfinite(stem).all() and stem.max() > 0
+        s.set_option(pkg.VSS_OPT_KEEP_STEM, 0)
+        c, _, _ = s.segment_frames(f)
+        assert np.array_equal(a, c)
+
+
 def test_every_compiled_tile_bitwise(pkg, synthetic):
     """Every compiled tile of every block layer (pinned with VSS_TILE) gives
     bitwise the activations and masks of the planner's choice."""
     f = _frames(synthetic, 3, start=900)
     with pkg.Session(dtype="bf16x2", max_batch=3, autotune=False) as s:
+        s.set_option(pkg.VSS_OPT_KEEP_STEM, 1)
         ref, _, _ = s.segment_frames(f)
         ref_layers = [s.read_layer(li, 3) for li in range(s.n_layers - 1)]  # (the head's output is the mask)
         tiles = {li: s.layer_tiles(li) for li in range(s.n_layers)}
@@ -270,6 +294,7 @@ def test_every_compiled_tile_bitwise(pkg, synthetic):
             os.environ["VSS_TILE"] = f"{li}:{th}x{tw}"
             try:
                 with pkg.Session(dtype="bf16x2", max_batch=3, autotune=False) as s:
+                    s.set_option(pkg.VSS_OPT_KEEP_STEM, 1)
                     got, _, _ = s.segment_frames(f)
                     first = next((k for k in range(s.n_layers - 1)
                                   if not np.array_equal(s.read_layer(k, 3), ref_layers[k])), None)

@@ -34,6 +34,7 @@ VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_I
     0, -1, -2, -3, -4, -5, -6, -7)
 DTYPES = {"f32": 0, "bf16x2": 1}
 VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_BRANCHES, VSS_OPT_FORWARD, VSS_OPT_FORWARD_FAULTS = 1, 2, 3, 4, 5
+VSS_OPT_KEEP_STEM = 6
 VSS_CREATE_NO_AUTOTUNE = 1
 VSS_OUT_MODEL, VSS_OUT_FRAME = 0, 1
 

@@ -140,6 +140,7 @@ struct vss_handle {
   int fwd_grid = 0;
   int fwd_order = 0;             // 0 layer-major, 1 diagonal (env VSS_FWD_ORDER=diag)
   int fuse_stem = 1;             // env VSS_FUSE_STEM=0: launch the stem on its own
+  int keep_stem = 0;             // VSS_OPT_KEEP_STEM: the fused stem also stores its activation
   std::map<int, std::pair<FwdTask*, int>> fwd_tasks;  // per batch size n
   unsigned* fwd_dbg = nullptr;   // env VSS_FWD_DEBUG: host-mapped per-workgroup state
   unsigned long long* fwd_trace = nullptr;  // env VSS_FWD_TRACE: per-task stamps of the last launch
@@ -739,7 +740,10 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       go(stem_kernel16(), dim3((l.W + kStemTW - 1) / kStemTW, (l.H + kStemTH - 1) / kStemTH, n), kStemLds * 4, p);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
       BlockParams p = block_params(h, l, n, f0);
-      if (flags_stem_in(l.flags)) p.stem = stem_params(h, h->L[r.src], frames, rs, fs, fh, fw, fc, f0);
+      if (flags_stem_in(l.flags)) {
+        p.stem = stem_params(h, h->L[r.src], frames, rs, fs, fh, fw, fc, f0);
+        if (!h->keep_stem) p.stem.y = nullptr;  // no layer reads it (vss_read_layer(0) only)
+      }
 #ifdef VSS_TRACE
       p.trace = h->trace[i];
       h->trace_wgs[i] = l.tiles_x * l.tiles_y * n * l.ks;
@@ -965,6 +969,7 @@ int autotune(vss_handle* h) {
           p.stem = stem_params(h, h->L[l.rec.src], h->d_frames, (size_t)h->cfg.max_frame_w * 3,
                                (size_t)h->cfg.max_frame_w * 3 * h->cfg.max_frame_h, h->cfg.max_frame_h,
                                h->cfg.max_frame_w, 3, 0);
+        if (flags_stem_in(l.flags)) p.stem.y = nullptr;  // timed as the forward runs it by default
         const dim3 grid(l.tiles_x, l.tiles_y, N * l.ks);
         for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(kThreads), l.lds, h->stream, p);
         (void)hipEventRecord(e0, h->stream);
@@ -1223,6 +1228,14 @@ int vss_set_option(vss_handle* h, int option, int value) {
     h->use_forward = value ? 1 : 0;
     return VSS_OK;
   }
+  if (option == VSS_OPT_KEEP_STEM) {
+    if ((value ? 1 : 0) != h->keep_stem) {  // the captured graphs hold the stem pointer
+      for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+      h->graphs.clear();
+    }
+    h->keep_stem = value ? 1 : 0;
+    return VSS_OK;
+  }
   if (option == VSS_OPT_USE_GRAPH) h->use_graph = value ? 1 : 0;
   else if (option == VSS_OPT_PROFILE) h->profile = value ? 1 : 0;
   else if (option == VSS_OPT_BRANCHES) {
@@ -1245,6 +1258,7 @@ int vss_get_option(vss_handle* h, int option, int* value) {
     case VSS_OPT_PROFILE: *value = h->profile; return VSS_OK;
     case VSS_OPT_BRANCHES: *value = h->branches; return VSS_OK;
     case VSS_OPT_FORWARD: *value = h->use_forward; return VSS_OK;
+    case VSS_OPT_KEEP_STEM: *value = h->keep_stem; return VSS_OK;
     case VSS_OPT_FORWARD_FAULTS: {
       *value = 0;
       if (!h->d_fwd_ctl) return VSS_OK;
@@ -1353,6 +1367,11 @@ int vss_read_layer(vss_handle* h, int layer, int n, float* host_out) {
     return fail(h, VSS_E_INVALID_ARG, "bad layer/n/out");
   const LayerPlan& l = h->L[layer];
   if (l.rec.kind == K_HEAD) return fail(h, VSS_E_INVALID_ARG, "the head's output is the mask buffer");
+  if (l.rec.kind == K_STEM && !h->keep_stem)
+    for (const LayerPlan& c : h->L)
+      if (flags_stem_in(c.flags))
+        return fail(h, VSS_E_INVALID_ARG,
+                    "the stem is fused into layer 1 and not stored: set VSS_OPT_KEEP_STEM before the forward");
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipDeviceSynchronize());
   const size_t cnt = (size_t)n * l.H * l.W * l.C;

@@ -878,13 +878,13 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       }
     }
   }
-#ifndef VSS_EXP_NO_STEM_STORE
   if constexpr (STEM_IN) {
     // the stem activation itself (the tile centre of xt, intact through the
-    // epilogue): what vss_read_layer reports for the stem; last, so that no
-    // barrier waits for these stores
+    // epilogue), only under VSS_OPT_KEEP_STEM (null otherwise: no layer reads
+    // it): what vss_read_layer reports for the stem; last, so that no barrier
+    // waits for these stores
     const Gm<COH> gst(p.stem.y + (long)n * p.H * p.W * 16);
-    for (int i = tid; i < TH * TW * 4; i += 256) {
+    for (int i = tid; p.stem.y != nullptr && i < TH * TW * 4; i += 256) {
       const int pix = i >> 2, q = i & 3;
       const int yy = oy0 + pix / TW, xx = ox0 + pix % TW;
       if (yy < p.H && xx < p.W)
@@ -892,7 +892,6 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
                *reinterpret_cast<const f4*>(xt + ((pix / TW + 1) * IW + pix % TW + 1) * XS + 4 * q));
     }
   }
-#endif
   VSS_STAMP(3);
 }
 
