@@ -131,6 +131,19 @@ __device__ __forceinline__ void prep_load(const PrepTap& t, uint32_t v[12]) {
   }
 }
 
+// v / 255.0f, correctly rounded, without the IEEE division sequence (div_scale,
+// rcp, four FMAs, div_fmas, div_fixup): the reciprocal product corrected by one
+// FMA residual.  Equal to the division for EVERY float in [0, 256] (and by
+// symmetry [-256, 0]) — checked exhaustively, all 1,132,462,081 of them, by
+// tools/div255_check.c (tests/test_div255.py); the resize's lerps of bytes
+// never leave [0, 255].
+__device__ __forceinline__ float div255(float v) {
+#pragma clang fp contract(off)
+  constexpr float kInv = 1.0f / 255.0f;
+  const float q = v * kInv;
+  return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, v), kInv, q);
+}
+
 __device__ __forceinline__ void prep_finish(const uint32_t v[12], float dy, float dx, float out[3]) {
 #pragma clang fp contract(off)
 #pragma unroll
@@ -139,7 +152,7 @@ __device__ __forceinline__ void prep_finish(const uint32_t v[12], float dy, floa
     const float top = __builtin_fmaf(tr - tl, dx, tl);
     const float bot = __builtin_fmaf(br - bl, dx, bl);
     const float val = __builtin_fmaf(bot - top, dy, top);
-    out[c] = val / 255.0f;
+    out[c] = div255(val);
   }
 }
 
