@@ -997,7 +997,9 @@ __device__ __forceinline__ void head_body(const HeadParams& p, int bx, int by, i
       const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
       const float v = ly0 * (lx0 * z[y0 - zr0][x0 - zc0] + lx1 * z[y0 - zr0][x1 - zc0]) +
                       ly1 * (lx0 * z[y1 - zr0][x0 - zc0] + lx1 * z[y1 - zr0][x1 - zc0]);
-      p.mask[((long)n * p.Hm + oy) * p.Wm + ox] = 1.0f / (1.0f + expf(-v));
+      // sigmoid from the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32: ~1e-7
+      // off the libm form, against the 1e-3 mask tolerance)
+      p.mask[((long)n * p.Hm + oy) * p.Wm + ox] = __builtin_amdgcn_rcpf(1.0f + __expf(-v));
     }
   }
   VSS_STAMP(3);
