@@ -72,6 +72,25 @@ def cpu_baseline(blob, frames, hm, wm, budget_s):
                       f"{threads} threads; 4 threads: {res['4'][1]} frames in {res['4'][2]:.1f} s"}
 
 
+def host_leg(sess, frames, d_masks, B, steps):
+    """PCIe-inclusive rate of the host-buffer entry point (vss_segment, what the
+    N-API addon calls): host u8 frames -> pinned staging -> H2D -> forward ->
+    D2H into the caller's f32 masks, synchronous per call.  Never `value`."""
+    import numpy as np
+    n_iter = max(10, min(steps, 100))
+    for _ in range(3):
+        masks, _, _ = sess.segment_frames(frames)
+    t0 = time.perf_counter()
+    for _ in range(n_iter):
+        masks, _, _ = sess.segment_frames(frames)
+    el = time.perf_counter() - t0
+    same = bool(np.array_equal(masks, d_masks.cpu().numpy()))
+    return {"value": round(B * n_iter / el, 1), "unit": "frames/s", "ms_per_batch": round(el * 1e3 / n_iter, 4),
+            "iters": n_iter, "h2d_bytes_per_batch": int(frames.nbytes), "d2h_bytes_per_batch": int(masks.nbytes),
+            "masks_equal_device_path": same,
+            "entry": "vss_segment (host frames -> host masks, synchronous, PCIe-inclusive)"}
+
+
 def post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, steps, warmup, cpu_s):
     """Time the post chain on the seam's masks; check it against the oracle."""
     import torch
@@ -163,6 +182,7 @@ def main():
     ap.add_argument("--cpu-budget-s", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-post", action="store_true", help="skip the post-processing leg")
+    ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host-buffer leg")
     ap.add_argument("--persistent", action="store_true",
                     help="run the forward as ONE persistent k_forward launch (VSS_FORWARD=1) instead of "
                          "one launch per layer")
@@ -319,6 +339,10 @@ def main():
         post = post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, args.steps,
                         args.warmup, 0.0 if args.no_cpu else 2.0)
 
+    host = None
+    if rank == 0 and not args.no_host:
+        host = host_leg(sess, frames, d_masks, B, args.steps)
+
     out = None
     if rank == 0:
         masks = d_masks.cpu().numpy()
@@ -378,6 +402,7 @@ def main():
             "layer_launches_sum_ms": round(float(sum(ms)), 5),
             "cpu_baseline": cpu,
             "post": post,
+            "host_path": host,
         }
         print(json.dumps(out), flush=True)
     sess.close()

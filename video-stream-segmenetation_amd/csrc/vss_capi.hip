@@ -900,8 +900,16 @@ int stage_in(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc
   }
   if (out_mode == VSS_OUT_FRAME && (size_t)n * fh * fw > h->fmask_cap)
     return fail(h, VSS_E_INVALID_ARG, "frame-size masks exceed max_batch * max_frame_h * max_frame_w");
-  std::memcpy(h->h_frames, frames, bytes);
-  HIP_TRY(h, hipMemcpyAsync(h->d_frames, h->h_frames, bytes, hipMemcpyHostToDevice, h->stream));
+  // staged in 1 MiB pieces, each piece's DMA queued as soon as it is in the
+  // pinned buffer, so the copy engine runs under the next piece's memcpy
+  // (the staging buffer is free: the previous call on this handle has
+  // finished — Busy — before this one starts)
+  constexpr size_t kStageChunk = size_t(1) << 20;
+  for (size_t off = 0; off < bytes; off += kStageChunk) {
+    const size_t len = std::min(kStageChunk, bytes - off);
+    std::memcpy(h->h_frames + off, frames + off, len);
+    HIP_TRY(h, hipMemcpyAsync(h->d_frames + off, h->h_frames + off, len, hipMemcpyHostToDevice, h->stream));
+  }
   rc = forward(h, h->d_frames, n, fh, fw, fc, rs, rs * (size_t)fh, h->d_masks, h->stream);
   if (rc) return rc;
   if (out_mode == VSS_OUT_FRAME) {
