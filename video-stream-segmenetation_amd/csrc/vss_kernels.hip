@@ -914,36 +914,6 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   VSS_STAMP(3);
 }
 
-// XCD-aware tile order for the layer launches.  Workgroups are dealt
-// round-robin over the 8 XCDs (block b shares an XCD, and its L2, with b + 8;
-// MI355X_MICROARCH.md, workgroup dispatch), so with the grid's natural order
-// horizontally adjacent tiles — which read the same halo columns of the input
-// and, in the decoders, the same low-res src columns — sit on different XCDs
-// and each XCD fetches the shared lines again.  Remap: the workgroups of one
-// XCD (b % 8) take one contiguous eighth of the logical (x, y, z) tile order,
-// i.e. whole rows of tiles of one frame (with 8 frames, one frame per XCD),
-// so neighbours share an L2.  A bijection on the grid (any remainder past the
-// last full eighth keeps its own index); results do not depend on which
-// workgroup computes which tile (tile-invariant, order-free norm sums).
-#ifndef VSS_XCD_REMAP
-#define VSS_XCD_REMAP 1
-#endif
-struct TileIdx {
-  int x, y, z;
-};
-__device__ __forceinline__ TileIdx xcd_tile() {
-  if constexpr (VSS_XCD_REMAP) {
-    const int gx = (int)gridDim.x, gy = (int)gridDim.y;
-    const int L = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
-    const int per = (gx * gy * (int)gridDim.z) >> 3;
-    const int T = L < (per << 3) ? (L & 7) * per + (L >> 3) : L;
-    const int zy = T / gx;
-    return {T - zy * gx, zy % gy, zy / gy};
-  } else {
-    return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
-  }
-}
-
 template <int MODE, int STRIDE, int TH, int TW, int CIN, int CSKIP, int CH, int COUT, int FLAGS, int PREC>
 __global__ __launch_bounds__(256) void k_block(BlockParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
