@@ -19,7 +19,10 @@ Also measured in the same run:
   * post: the GPU post-processing chain (EMA ->
     opening -> joint bilateral -> refine -> u8 alpha) over the same batch as
     consecutive frames of one stream: frames/s, its HBM roofline and parity
-    with the oracle (rank 0, outside the headline's timed region).
+    with the oracle (rank 0, outside the headline's timed region);
+  * host_path: the PCIe-inclusive rate of the host-buffer entry point
+    (vss_segment: host frames -> pinned staging -> H2D -> forward -> D2H),
+    never `value` (rank 0, outside the timed region).
 """
 from __future__ import annotations
 
