@@ -58,7 +58,7 @@ __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 struct BlockLds {
   int IH, IW, P_in, P_in_pad, P_out, CX, XS, LD1, LD2, SR, SC;
   int NCB, NPB, NCHUNK, PW, CS, NPBW, NACC;  // CS = chunk groups, PW = pixel-block groups
-  int xt, xr, w1, w2, wdw, bdw, b1, b2, wimg_end, lr, nrm, work, stt, total;  // [w1, wimg_end): the weight image
+  int xt, xr, w1, w2, wdw, bdw, b1, b2, wimg_end, lr, nrm, uc, work, stt, total;  // [w1, wimg_end): the weight image
   int slab_stride;  // floats per wave slab = P_out * (cout + 4)
 };
 
@@ -119,6 +119,9 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
                  mode == 2 ? r4(L.SR * L.SC * cin) : 0),
             stem_in ? stem_in_lds(L.IH, L.IW) : 0);
   L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;
+  // decoder: per input-tile pixel, its 2x-upsample taps (four lr offsets as
+  // u16 pairs, ly1, lx1), built while the prologue loads are in flight
+  L.uc = o;  o += mode == 2 ? 4 * L.P_in_pad : 0;
   L.stt = L.xt;
   L.total = o;
   return L;

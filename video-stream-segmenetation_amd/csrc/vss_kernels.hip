@@ -528,6 +528,29 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     }
     st_w.issue([&](int i) { return wsrc[i]; });
     VSS_STAMP(6);  // every load issued
+    // the upsample's tap records, one per input-tile pixel, while the loads
+    // are in flight: source coordinate max((o + 0.5) / 2 - 0.5, 0) in
+    // integers — o = 0 -> (0, 0); odd o -> ((o - 1) / 2, 0.25); even o > 0 ->
+    // (o / 2 - 1, 0.75), the same floats the float formula gives
+    static_assert(SR * SC * CL < 65536, "tap offsets are u16");
+    unsigned* uc = reinterpret_cast<unsigned*>(smem + L.uc);
+    for (int pix = tid; pix < P_IN_PAD; pix += 256) {
+      const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
+      uint4 rec = {0xFFFFFFFFu, 0u, 0u, 0u};  // outside the frame / padding: zeros
+      if (pix < P_IN && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo) {
+        const int y0 = yy > 0 ? (yy - 1) >> 1 : 0, y1 = y0 + (y0 < h - 1 ? 1 : 0);
+        const float ly1 = yy > 0 ? ((yy & 1) ? 0.25f : 0.75f) : 0.f;
+        const int x0 = xx > 0 ? (xx - 1) >> 1 : 0, x1 = x0 + (x0 < w - 1 ? 1 : 0);
+        const float lx1 = xx > 0 ? ((xx & 1) ? 0.25f : 0.75f) : 0.f;
+        const int r0 = min(max(y0 - sy0, 0), SR - 1), r1 = min(max(y1 - sy0, 0), SR - 1);
+        const int q0 = min(max(x0 - sx0, 0), SC - 1), q1 = min(max(x1 - sx0, 0), SC - 1);
+        rec.x = (unsigned)((r0 * SC + q0) * CL) | ((unsigned)((r0 * SC + q1) * CL) << 16);
+        rec.y = (unsigned)((r1 * SC + q0) * CL) | ((unsigned)((r1 * SC + q1) * CL) << 16);
+        rec.z = __float_as_uint(ly1);
+        rec.w = __float_as_uint(lx1);
+      }
+      reinterpret_cast<uint4*>(uc)[pix] = rec;
+    }
     if constexpr (NORM_IN) {
       // sum the slots (exact, any order) -> the src's scale/shift; the slots
       // are staged in xt, whose contents are committed only after this
@@ -572,22 +595,15 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       const int i = tid + 256 * k;
       if (i < P_IN_PAD * C4L) {
         const int pix = i / C4L, c4 = i % C4L;
-        const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
+        const uint4 rec = reinterpret_cast<const uint4*>(uc)[pix];
         f4 v = {0.f, 0.f, 0.f, 0.f};
-        if (pix < P_IN && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo) {
-          // source coordinate max((o + 0.5) / 2 - 0.5, 0) in integers: o = 0 -> (0, 0);
-          // odd o -> ((o - 1) / 2, 0.25); even o > 0 -> (o / 2 - 1, 0.75) — the
-          // same floats the float formula gives, without its converts
-          const int y0 = yy > 0 ? (yy - 1) >> 1 : 0, y1 = y0 + (y0 < h - 1 ? 1 : 0);
-          const float ly1 = yy > 0 ? ((yy & 1) ? 0.25f : 0.75f) : 0.f, ly0 = 1.f - ly1;
-          const int x0 = xx > 0 ? (xx - 1) >> 1 : 0, x1 = x0 + (x0 < w - 1 ? 1 : 0);
-          const float lx1 = xx > 0 ? ((xx & 1) ? 0.25f : 0.75f) : 0.f, lx0 = 1.f - lx1;
-          const int r0 = min(max(y0 - sy0, 0), SR - 1), r1 = min(max(y1 - sy0, 0), SR - 1);
-          const int q0 = min(max(x0 - sx0, 0), SC - 1), q1 = min(max(x1 - sx0, 0), SC - 1);
-          const f4 v00 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q0) * CL + 4 * c4);
-          const f4 v01 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q1) * CL + 4 * c4);
-          const f4 v10 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q0) * CL + 4 * c4);
-          const f4 v11 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q1) * CL + 4 * c4);
+        if (rec.x != 0xFFFFFFFFu) {
+          const float ly1 = __uint_as_float(rec.z), ly0 = 1.f - ly1;
+          const float lx1 = __uint_as_float(rec.w), lx0 = 1.f - lx1;
+          const f4 v00 = *reinterpret_cast<const f4*>(lr + (rec.x & 0xFFFFu) + 4 * c4);
+          const f4 v01 = *reinterpret_cast<const f4*>(lr + (rec.x >> 16) + 4 * c4);
+          const f4 v10 = *reinterpret_cast<const f4*>(lr + (rec.y & 0xFFFFu) + 4 * c4);
+          const f4 v11 = *reinterpret_cast<const f4*>(lr + (rec.y >> 16) + 4 * c4);
           v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
         }
         *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
