@@ -4,32 +4,43 @@ MI355X, one process per GPU.
 
 A step = one pass of the hot path over one batch: 8 synthetic 640x480 RGB
 frames already resident in HBM -> fused preprocess + network -> 8 float masks
-(144x256), then (N > 1) an RCCL all-gather of every rank's masks so each rank
-holds the whole 8N-frame batch in order.  Weak scaling:
-per-GPU work is fixed, global batch = 8N.
+(144x256), and (N > 1) the RCCL all-gather of every rank's masks inside the C
+ABI (vss_segment_gather_device: each rank's handle joined one clique with
+vss_comm_init_rank), so each rank holds the whole 8N-frame batch in order
+(SURVEY.md §8(e)).  Weak scaling: per-GPU work is fixed, global batch = 8N.
+Steps are issued round-robin on `--inflight` streams (default: the handle's
+queue depth, 4): consecutive batches take consecutive slots of the handle (own
+activations) and run concurrently — the serving engine's steady state, where
+the next batch's kernels fill the gaps of this one's launch chain.  K steps
+are timed between barriers + device synchronisation; value = frames / time.
 
-Also measured in the same run:
+Also measured in the same run (rank 0):
   * roofline: the dominant kernel's algorithmic bytes per launch / its mean
     duration from HIP events recorded by the kernel launches themselves
-    (hipExtLaunchKernelGGL on the stream the kernels run on) over a second pass
-    of K steps, against 8 TB/s;
+    (hipExtLaunchKernelGGL on the stream the kernels run on, one batch at a
+    time) against 8 TB/s; plus the whole step's algorithmic bytes at `value`;
+  * batch_sweep: 8 / 32 / 64 frames per step, one and `inflight` in flight;
   * mask max-abs error vs the CPU oracle on this run's frames;
-  * cpu_baseline: the oracle (C restatement, f32) on a bounded sample of the
-    same frames on this host's cores (rank 0, N=1 only);
-  * post: the GPU post-processing chain (EMA ->
-    opening -> joint bilateral -> refine -> u8 alpha) over the same batch as
-    consecutive frames of one stream: frames/s, its HBM roofline and parity
-    with the oracle (rank 0, outside the headline's timed region);
-  * host_path: the PCIe-inclusive rate of the host-buffer entry point
-    (vss_segment: host frames -> pinned staging -> H2D -> forward -> D2H),
-    never `value` (rank 0, outside the timed region).
+  * cpu_baseline: the oracle (C restatement, f32, frames x channels OpenMP) on
+    a bounded sample of the same frames on this host's cores (N = 1 only);
+  * post: the GPU post-processing chain over the same batch (outside the
+    headline's timed region);
+  * host_path: the PCIe-inclusive queued host entry point (vss_submit: host
+    frames -> pinned staging -> H2D -> forward -> D2H, `inflight` batches in
+    flight), from caller memory and zero-copy from the pinned staging, at
+    640x480 and 1920x1080 (never `value`);
+  * ts_path: the TypeScript host (Segmenter.segmentFrames, Node child
+    process) end to end — throughput and one-call latency.
 """
 from __future__ import annotations
 
 import argparse
+import collections
 import importlib.util
 import json
 import os
+import subprocess
+import shutil
 import sys
 import time
 
@@ -52,14 +63,30 @@ def _load_pkg():
     return mod
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(blob, frames, hm, wm, budget_s):
-    """Oracle (C, f32, OpenMP) on a bounded sample of the same frames."""
+    """Oracle (C, f32; frames x channels in nested OpenMP teams) on a bounded
+    sample of the same frames: every usable core of this process's share, and
+    4 threads (ORT-web's default intra-op cap)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py  # the checker / CPU baseline only
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    usable = len(os.sched_getaffinity(0))
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    # the GPU box sets OMP_NUM_THREADS to its CPU share (the affinity mask shows
+    # the whole machine there); without it, every core in the affinity mask
+    threads = min(usable, env_threads) if env_threads else usable
     res = {}
     for label, nt, budget in (("all", threads, budget_s), ("4", 4, budget_s / 2)):
-        oracle_py.forward(blob, frames[:1], hm, wm, mode=0, nthreads=nt)  # warm
+        oracle_py.forward(blob, frames, hm, wm, mode=0, nthreads=nt)  # warm
         done, t0 = 0, time.perf_counter()
         while True:
             oracle_py.forward(blob, frames, hm, wm, mode=0, nthreads=nt)
@@ -70,28 +97,76 @@ def cpu_baseline(blob, frames, hm, wm, budget_s):
         res[label] = (done / el, done, el)
     v, done, el = res["all"]
     return {"value": round(v, 2), "unit": "frames/s", "cores": threads, "kind": "port",
-            "value_4_threads": round(res["4"][0], 2),
-            "sample": f"{done} frames of the timed batch (640x480 -> 144x256, f32) in {el:.1f} s on "
-                      f"{threads} threads; 4 threads: {res['4'][1]} frames in {res['4'][2]:.1f} s"}
+            "value_4_threads": round(res["4"][0], 2), "scaling_4_to_all": round(v / res["4"][0], 2),
+            "nproc": usable, "omp_num_threads_env": env_threads or None, "cpu_model": cpu_model(),
+            "sample": f"{done} frames of the timed batch (640x480 -> 144x256, f32, the build's C restatement; the "
+                      f"reference's ORT-web path cannot run here) in {el:.1f} s on {threads} threads; 4 threads: "
+                      f"{res['4'][1]} frames in {res['4'][2]:.1f} s"}
 
 
-def host_leg(sess, frames, d_masks, B, steps):
-    """PCIe-inclusive rate of the host-buffer entry point (vss_segment, what the
+def host_leg(pkg, frames, B, fh, fw, inflight, iters, d_ref=None):
+    """PCIe-inclusive rate of the queued host entry point (vss_submit, what the
     N-API addon calls): host u8 frames -> pinned staging -> H2D -> forward ->
-    D2H into the caller's f32 masks, synchronous per call.  Never `value`."""
-    import numpy as np
-    n_iter = max(10, min(steps, 100))
-    for _ in range(3):
-        masks, _, _ = sess.segment_frames(frames)
-    t0 = time.perf_counter()
-    for _ in range(n_iter):
-        masks, _, _ = sess.segment_frames(frames)
-    el = time.perf_counter() - t0
-    same = bool(np.array_equal(masks, d_masks.cpu().numpy()))
-    return {"value": round(B * n_iter / el, 1), "unit": "frames/s", "ms_per_batch": round(el * 1e3 / n_iter, 4),
-            "iters": n_iter, "h2d_bytes_per_batch": int(frames.nbytes), "d2h_bytes_per_batch": int(masks.nbytes),
-            "masks_equal_device_path": same,
-            "entry": "vss_segment (host frames -> host masks, synchronous, PCIe-inclusive)"}
+    D2H into the caller's masks, `inflight` batches in flight.  Two forms:
+    'copy' (frames in the caller's memory, staged by the copy pool) and
+    'zero_copy' (the frames are already in the pinned staging buffer, as a
+    decoder writing there would leave them).  Never `value`."""
+    out = {}
+    with pkg.Session(max_batch=B, max_frame_h=fh, max_frame_w=fw, queue_depth=inflight) as s:
+        masks = np.empty((B, s.mask_h * s.mask_w), np.float32)
+        for _ in range(3):
+            s.segment_frames(frames)
+        # copy: caller memory
+        q = collections.deque()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            if len(q) == inflight:
+                s.wait(q.popleft())
+            q.append(s.submit(frames))
+        while q:
+            last = s.wait(q.popleft())[0]
+        el = time.perf_counter() - t0
+        same = bool(np.array_equal(last, d_ref)) if d_ref is not None else None
+        out["copy"] = {"value": round(B * iters / el, 1), "ms_per_batch": round(el * 1e3 / iters, 4),
+                       "masks_equal_device_path": same}
+        # zero-copy: each slot's pinned staging holds the frames
+        flat = frames.reshape(-1)
+        t0 = None
+        tick = collections.deque()
+        for it in range(iters + inflight):
+            if it == inflight:
+                t0 = time.perf_counter()
+            buf = s.staging_buffer()  # the next slot's buffer, once that slot is free
+            if it < inflight:
+                buf[:flat.size] = flat  # the synthetic "decoder" fills each slot once
+            tick.append(s.submit_raw(buf.ctypes.data, B, fh, fw, 3, fw * 3, masks))
+            if len(tick) > inflight:
+                s.wait(tick.popleft())
+        while tick:
+            s.wait(tick.popleft())
+        el = time.perf_counter() - t0
+        same = bool(np.array_equal(masks, d_ref)) if d_ref is not None else None
+        out["zero_copy"] = {"value": round(B * iters / el, 1), "ms_per_batch": round(el * 1e3 / iters, 4),
+                            "masks_equal_device_path": same}
+    out.update({"unit": "frames/s", "frame": f"{fw}x{fh}x3", "batch": B, "inflight": inflight, "iters": iters,
+                "h2d_bytes_per_batch": int(frames.nbytes), "d2h_bytes_per_batch": int(B * 144 * 256 * 4),
+                "entry": "vss_submit / vss_wait (host frames -> host masks, queued, PCIe-inclusive)"})
+    return out
+
+
+def ts_leg(B, fh, fw, iters, inflight):
+    """The TypeScript host end to end in a Node child process (tools/bench_ts.js)."""
+    node = shutil.which("node")
+    if not node:
+        return None
+    try:
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "bench_ts.js"), str(fh), str(fw), str(B), str(iters),
+                            str(inflight)], capture_output=True, text=True, timeout=240)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()[-400:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, steps, warmup, cpu_s):
@@ -171,6 +246,40 @@ def post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, st
             "composite": composite}
 
 
+def run_steps(sess, streams, n_steps, launch):
+    """Issue n_steps round-robin over the streams (launch(k, stream) per step)."""
+    for i in range(n_steps):
+        launch(i, streams[i % len(streams)])
+
+
+def sweep(pkg, torch, dev, fh, fw, dtype, inflight, steps):
+    """Frames/s at 8 / 32 / 64 frames per step, one batch and `inflight` batches in flight."""
+    import vss_amd.synthetic as syn
+    out = []
+    for B in (8, 32, 64):
+        frames = syn.make_batch(B, fh, fw, 3)
+        d = torch.from_numpy(frames).to(dev)
+        with pkg.Session(dtype=dtype, max_batch=B, max_frame_h=fh, max_frame_w=fw, queue_depth=inflight) as s:
+            masks = [torch.empty((B, s.mask_h * s.mask_w), dtype=torch.float32, device=dev) for _ in range(inflight)]
+            for S in sorted({1, inflight}):
+                streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
+
+                def go(i, st):
+                    s.segment_device(d.data_ptr(), B, fh, fw, 3, fw * 3, fh * fw * 3, masks[i % S].data_ptr(),
+                                     st.cuda_stream)
+
+                run_steps(s, streams, 10, go)
+                torch.cuda.synchronize(dev)
+                n = max(20, steps * 8 // B)
+                t0 = time.perf_counter()
+                run_steps(s, streams, n, go)
+                torch.cuda.synchronize(dev)
+                el = time.perf_counter() - t0
+                out.append({"batch": B, "inflight": S, "value": round(B * n / el, 1),
+                            "ms_per_step": round(el * 1e3 / n, 5)})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -180,133 +289,98 @@ def main():
     ap.add_argument("--frame", default="480x640")
     ap.add_argument("--model", default="144x256")
     ap.add_argument("--dtype", default="bf16x2", choices=["bf16x2", "f32"])
+    ap.add_argument("--inflight", type=int, default=4, help="batches in flight (streams = the handle's queue depth)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--branches", type=int, default=1, help="concurrent sub-batch chains inside the graph")
     ap.add_argument("--cpu-budget-s", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-post", action="store_true", help="skip the post-processing leg")
-    ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host-buffer leg")
-    ap.add_argument("--persistent", action="store_true",
-                    help="run the forward as ONE persistent k_forward launch (VSS_FORWARD=1) instead of "
-                         "one launch per layer")
+    ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host-buffer legs")
+    ap.add_argument("--no-ts", action="store_true", help="skip the TypeScript (Node) leg")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the batch sweep")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_traffic.json"),
                     help="per-kernel HBM traffic from tools/prof_summary.py (PMC passes)")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # VSS_BENCH_BACKEND=gloo: rehearse the N > 1 code path with ranks sharing
-    # fewer GPUs than ranks (plumbing check only; RCCL is the measured backend)
-    backend = os.environ.get("VSS_BENCH_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
-    gpu = local % ndev if backend != "nccl" else local
+    fh, fw = (int(v) for v in args.frame.split("x"))
+    hm, wm = (int(v) for v in args.model.split("x"))
+    B = args.batch
+
+    ts = None
+    if rank == 0 and world == 1 and not args.no_ts:
+        ts = ts_leg(B, fh, fw, max(100, min(args.steps, 400)), args.inflight)  # before this process touches the GPU
+
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
-        torch.cuda.set_device(gpu)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", gpu if world > 1 else 0)
+        # the process group carries only the clique id, barriers and the max-time
+        # reduction (CPU tensors); the masks go over the handle's own RCCL clique
+        dist.init_process_group("gloo")
+    ndev = torch.cuda.device_count()
+    gpu = local % max(1, ndev)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
 
     pkg = _load_pkg()
     import vss_amd.synthetic as syn
     import vss_amd.costmodel as cm
 
-    fh, fw = (int(v) for v in args.frame.split("x"))
-    hm, wm = (int(v) for v in args.model.split("x"))
-    B = args.batch
     frames = syn.make_batch(B, fh, fw, 3, start=rank * B)
-    if args.persistent:
-        os.environ["VSS_FORWARD"] = "1"  # read by vss_create
+    S = args.inflight
     sess = pkg.Session(model_h=hm, model_w=wm, dtype=args.dtype, device_id=dev.index, max_batch=B,
-                       max_frame_h=fh, max_frame_w=fw)
+                       max_frame_h=fh, max_frame_w=fw, queue_depth=S)
     if args.no_graph:
         sess.set_option(pkg.VSS_OPT_USE_GRAPH, 0)
-    sess.set_option(pkg.VSS_OPT_BRANCHES, args.branches)
+    if world > 1:
+        ids = [sess.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        sess.comm_init_rank(world, rank, ids[0])
     d_frames = torch.from_numpy(frames).to(dev)
-    # two mask buffers: the all-gather of step i (RCCL's own stream) overlaps the
-    # forward of step i+1; step i+2 waits for gather i before it rewrites buffer i%2
-    d_masks2 = [torch.empty((B, hm * wm), dtype=torch.float32, device=dev) for _ in range(2)]
-    d_masks = d_masks2[0]
-    gathered2 = [torch.empty((world * B, hm * wm), dtype=torch.float32, device=dev) for _ in range(2)] \
-        if world > 1 else None
-    pending = [None, None]
-    stream = torch.cuda.Stream(device=dev)
+    P = hm * wm
+    # one output buffer per stream: step i writes buffer i % S on stream i % S
+    outs = [torch.empty((world * B, P), dtype=torch.float32, device=dev) for _ in range(S)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
     rs, fs = fw * 3, fh * fw * 3
-    it = [0]
 
-    def step():
-        k = it[0] & 1
-        it[0] += 1
-        if pending[k] is not None:
-            pending[k].wait()  # the forward's stream waits for gather i-2 (reads this buffer)
-            pending[k] = None
-        sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_masks2[k].data_ptr(), stream.cuda_stream)
-        if gathered2 is not None:
-            pending[k] = dist.all_gather_into_tensor(gathered2[k], d_masks2[k], async_op=True)
-
-    def drain():
-        for k in range(2):
-            if pending[k] is not None:
-                pending[k].wait()
-                pending[k] = None
-
-    with torch.cuda.stream(stream):
-        for _ in range(args.warmup):
-            step()
-        drain()
-        torch.cuda.synchronize(dev)
+    def step(i, st):
         if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        drain()
-        torch.cuda.synchronize(dev)
-        el = time.perf_counter() - t0
-        if world > 1:
-            dist.barrier()
+            sess.segment_gather_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, outs[i % S].data_ptr(),
+                                       st.cuda_stream)
+        else:
+            sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, outs[i % S].data_ptr(), st.cuda_stream)
+
+    run_steps(sess, streams, args.warmup, step)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run_steps(sess, streams, args.steps, step)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    last = (args.steps - 1) % S
+    d_masks = outs[last][rank * B:(rank + 1) * B] if world > 1 else outs[last][:B]
     if world > 1:  # the gathered batch holds every rank's masks in frame order
-        last = (it[0] - 1) & 1
-        assert torch.equal(gathered2[last][rank * B:(rank + 1) * B], d_masks2[last])
-    d_masks = d_masks2[(it[0] - 1) & 1]
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
+        assert all(torch.equal(outs[last], o) for o in outs), "every step gathers the same masks"
+    t = torch.tensor([el], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el_max = float(t.item())
     value = world * B * args.steps / el_max
 
-    # ---- kernel timing pass (events recorded by the launches themselves) ----
-    persistent = sess.persistent
-
-    def profiled_pass():
-        sess.set_option(pkg.VSS_OPT_PROFILE, 1)
-        with torch.cuda.stream(stream):
-            for _ in range(args.steps):
-                sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, d_masks.data_ptr(),
-                                    stream.cuda_stream)
-        torch.cuda.synchronize(dev)
-        sess.set_option(pkg.VSS_OPT_PROFILE, 0)
-
-    fwd_ms = fwd_cnt = None
-    if persistent:
-        profiled_pass()
-        fwd_ms, fwd_cnt = sess.profile_read_forward()
-        faults = sess.forward_faults()
-        if faults:
-            raise RuntimeError(f"k_forward: {faults} dependency waits gave up")
-        sess.set_option(pkg.VSS_OPT_FORWARD, 0)  # per-layer breakdown from layer launches
-    profiled_pass()
+    # ---- kernel timing pass (events recorded by the launches, one batch at a time) ----
+    sess.set_option(pkg.VSS_OPT_PROFILE, 1)
+    prof_masks = torch.empty((B, P), dtype=torch.float32, device=dev)
+    for _ in range(args.steps):
+        sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, prof_masks.data_ptr(), streams[0].cuda_stream)
+    torch.cuda.synchronize(dev)
+    sess.set_option(pkg.VSS_OPT_PROFILE, 0)
     ms, cnt = sess.profile_read()
-    if persistent:
-        sess.set_option(pkg.VSS_OPT_FORWARD, 1)
 
     blob = open(sess.weights_path, "rb").read()
     sys.path.insert(0, os.path.join(PKG_DIR, "model"))
@@ -317,34 +391,28 @@ def main():
     per_layer = [{"layer": i, "kind": costs[i]["kind"], "kernel": names[i], "ms": round(m, 5),
                   "GBps": round(cm.launch_bytes(costs[i], B) / (m * 1e-3) / 1e9, 1) if m > 0 else None}
                  for i, m in enumerate(ms)]
-    if persistent:
-        # the dominant (only) kernel is the whole forward: every layer's
-        # compulsory HBM bytes (each activation written once, read once)
-        dom_name = sess.forward_kernel()
-        dom_label = f"persistent forward: {dom_name}"
-        dom_bytes = sum(cm.launch_bytes(c, B) for c in costs)
-        dom_ms, dom_cnt = fwd_ms, fwd_cnt
-    else:
-        dom = int(np.argmax(ms))
-        dom_name = names[dom]
-        dom_label = f"layer {dom} ({costs[dom]['kind']}): {dom_name}"
-        dom_bytes = cm.launch_bytes(costs[dom], B)
-        dom_ms, dom_cnt = ms[dom], cnt
-    achieved = dom_bytes / (dom_ms * 1e-3)
+    dom = int(np.argmax(ms))
+    dom_name = names[dom]
+    dom_bytes = cm.launch_bytes(costs[dom], B)
+    achieved = dom_bytes / (ms[dom] * 1e-3)
+    step_bytes = sum(cm.launch_bytes(c, B) for c in costs)  # every launch's algorithmic bytes, one batch
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json):
-        t = json.load(open(args.traffic_json)).get(dom_name)
-        if t and t.get("traffic_bytes"):
-            traffic = round(t["traffic_bytes"] / 1e6, 3)
+        tj = json.load(open(args.traffic_json)).get(dom_name)
+        if tj and tj.get("traffic_bytes"):
+            traffic = round(tj["traffic_bytes"] / 1e6, 3)
 
-    post = None
+    post = host = batch_sweep = None
     if rank == 0 and not args.no_post:
-        post = post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, args.steps,
+        post = post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, streams[0], args.steps,
                         args.warmup, 0.0 if args.no_cpu else 2.0)
-
-    host = None
-    if rank == 0 and not args.no_host:
-        host = host_leg(sess, frames, d_masks, B, args.steps)
+    if rank == 0 and world == 1 and not args.no_host:
+        ref = d_masks.cpu().numpy()
+        host = {"vga": host_leg(pkg, frames, B, fh, fw, S, max(50, min(args.steps, 400)), ref)}
+        big = syn.make_batch(B, 1080, 1920, 3)
+        host["1080p"] = host_leg(pkg, big, B, 1080, 1920, S, max(30, min(args.steps // 2, 200)))
+    if rank == 0 and world == 1 and not args.no_sweep:
+        batch_sweep = sweep(pkg, torch, dev, fh, fw, args.dtype, S, args.steps)
 
     out = None
     if rank == 0:
@@ -373,21 +441,22 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"{B} synthetic {fw}x{fh} RGB u8 frames per GPU per step (resident in HBM) -> "
-                            f"{wm}x{hm} f32 masks" + (", RCCL all-gather of masks (overlapped with the next step's forward)" if world > 1 else ""),
+                            f"{wm}x{hm} f32 masks, {S} steps in flight (one handle, {S} slots, {S} streams)"
+                            + (", RCCL all-gather of masks in the C ABI (vss_segment_gather_device)"
+                               if world > 1 else ""),
                 "global_batch": world * B,
                 "frame": f"{fw}x{fh}x3",
                 "model_res": f"{wm}x{hm}",
                 "pw_gemm": "v_mfma_f32_16x16x32_bf16, f32 activations split hi+lo" if args.dtype == "bf16x2"
                            else "v_mfma_f32_16x16x4_f32",
                 "graph": not args.no_graph,
-                "persistent_forward": persistent,
-                "branches": args.branches,
+                "inflight": S,
                 "parallelism": f"dp{world}",
             },
             "mask_max_abs_err": err,
             "roofline": {
                 "bound": "hbm",
-                "kernel": dom_label,
+                "kernel": f"layer {dom} ({costs[dom]['kind']}): {dom_name}",
                 "achieved": round(achieved / 1e9, 1),
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",
@@ -395,17 +464,19 @@ def main():
                 "traffic": traffic,
                 "traffic_unit": "MB/launch (rocprofv3 PMC: 2*FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
                 "alg_bytes_per_launch": dom_bytes,
-                "mean_kernel_ms": round(dom_ms, 5),
-                "events_count": dom_cnt,
+                "mean_kernel_ms": round(ms[dom], 5),
+                "events_count": cnt,
+                "step_alg_bytes": step_bytes,
+                "step_frac_at_value": round(step_bytes / B * value / world / HBM_PEAK, 4),
             },
             "kernels": per_layer,
-            "kernels_note": ("per-layer breakdown from the same plan run as one launch per layer "
-                             "(VSS_OPT_FORWARD=0); the headline runs the persistent forward")
-                            if persistent else "one launch per layer",
             "layer_launches_sum_ms": round(float(sum(ms)), 5),
+            "launches_per_forward": sum(1 for n in names if not n.startswith("(fused")),
+            "batch_sweep": batch_sweep,
             "cpu_baseline": cpu,
             "post": post,
             "host_path": host,
+            "ts_path": ts,
         }
         print(json.dumps(out), flush=True)
     sess.close()

@@ -14,8 +14,23 @@
  * _OrtGetLastError(code*, msg**) (client/public/ort-wasm-simd-threaded.mjs:50)
  * behind the rejecting `session.run` promise.
  *
- * Threading: one call in flight per handle (VSS_E_BUSY otherwise), which is the
- * reference's own usage (runModnetExclusive, client/src/core/main.ts:18-22).
+ * Threading / queueing: the reference serialises every session.run behind one
+ * promise chain (runModnetExclusive, client/src/core/main.ts:18-22), so one
+ * batch is ever in flight.  A handle here owns `queue_depth` slots — each its
+ * own activations, HIP stream, captured hipGraphs and pinned staging — and up
+ * to that many batches run at once: batch i+1's host->device copy overlaps
+ * batch i's forward and batch i-1's device->host copy (the steady-state
+ * decode -> infer loop of BASELINE config 5).  Callbacks fire, and tickets
+ * complete, in submission order; a queued call beyond the depth gets
+ * VSS_E_BUSY (vss_segment_async) or waits (the synchronous calls).  Calls may
+ * come from several host threads (submission is serialised inside).
+ *
+ * Multi-GPU: a handle created with n_gpus / device_ids owns
+ * one engine per GPU; the host-memory calls shard a batch contiguously over
+ * them and all-gather the masks over RCCL (ncclAllGather inside one
+ * ncclGroupStart/End, one communicator per device and slot).  Processes that
+ * each own one GPU (torchrun) join one RCCL clique instead through
+ * vss_comm_unique_id / vss_comm_init_rank and vss_segment_gather_device.
  */
 #ifndef VSS_H_
 #define VSS_H_
@@ -27,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSS_VERSION 10000 /* 1.0.0 */
+#define VSS_VERSION 20000 /* 2.0.0: queued slots, multi-GPU handles, RCCL */
 
 enum {
   VSS_OK = 0,
@@ -53,28 +68,19 @@ enum {
  * the canvas drawImage upscale of :177 defined as in vss_composite_device). */
 enum { VSS_OUT_MODEL = 0, VSS_OUT_FRAME = 1 };
 
-/* Options for vss_set_option. */
+/* Options for vss_set_option.  (Values 3-5 belonged to round-1 experiments —
+ * sub-batch graph branches and the persistent k_forward — measured slower and
+ * removed; DESIGN.md keeps the numbers.  Setting them fails with
+ * VSS_E_UNSUPPORTED.) */
 enum {
-  VSS_OPT_USE_GRAPH = 1, /* 1: replay a captured hipGraph per (shape, buffers) (default 1) */
+  VSS_OPT_USE_GRAPH = 1, /* 1: replay a captured hipGraph per (slot, shape, buffers) (default 1) */
   VSS_OPT_PROFILE = 2,   /* 1: time every kernel with HIP events (eager launches)         */
-  VSS_OPT_BRANCHES = 3,  /* 1..8: split a batch into that many sub-batches whose chains run
-                            concurrently on forked streams inside the graph (default 1;
-                            ignored while VSS_OPT_FORWARD is 1) */
-  VSS_OPT_FORWARD = 4,   /* 1: the whole forward as ONE persistent launch (k_forward: tasks =
-                            (layer, frame, tile) taken from ticket counters, per-frame
-                            dependency counters instead of kernel boundaries); 0: one launch
-                            per layer (default: measured faster).  Available when
-                            the handle was created with env VSS_FORWARD=1 (the planner then
-                            restricts tiles to the persistent forward's table and skips the
-                            autotuner).  Results are bitwise identical either way. */
-  VSS_OPT_FORWARD_FAULTS = 5, /* vss_get_option only: dependency waits of k_forward that gave up
-                                (bounded spins; 0 in a correct run).  Synchronises the device
-                                and clears the count. */
   VSS_OPT_KEEP_STEM = 6  /* 1: the stem fused into layer 1 also stores its activation, so
                             vss_read_layer(0) can report it (a debugging aid: 4.7 MB of HBM
                             writes per batch of 8 at 144x256 that no layer reads).  Default 0:
                             the forward writes only what a later layer or the caller reads;
-                            vss_read_layer(0) then fails with VSS_E_INVALID_ARG. */
+                            vss_read_layer(0) fails with VSS_E_INVALID_ARG unless the latest
+                            forward ran with the option set. */
 };
 
 typedef struct vss_handle vss_handle;
@@ -83,11 +89,18 @@ typedef struct vss_config {
   int model_h, model_w;    /* model input resolution; multiples of 16. Reference: 288x512
                               (MODEL_INPUT_SIZE, frameProcessorTest.ts:10); default 144x256 */
   int dtype;               /* VSS_DTYPE_* */
-  int device_id;           /* HIP device ordinal (one handle = one GPU) */
-  int max_batch;           /* frames per call */
+  int device_id;           /* HIP device ordinal when device_ids is NULL (one GPU) */
+  int max_batch;           /* frames per call (over all the handle's GPUs) */
   int max_frame_h, max_frame_w; /* host-staging capacity for vss_segment (channels <= 4) */
   const char* weights_path;     /* vss weights blob (model/make_weights.py) */
   int flags;                    /* VSS_CREATE_* */
+  /* one handle over n_gpus distinct GPUs device_ids[0..n_gpus-1]
+   * (the masks' consumer is device_ids[0]).  With device_ids != NULL the host
+   * calls always go through the RCCL path, n_gpus == 1 included. */
+  int n_gpus;
+  const int* device_ids;
+  int queue_depth;              /* batches in flight (slots per GPU); 0 = default 4, max 16 */
+  int staging_threads;          /* host threads for the pinned staging copies; 0 = default 4 */
 } vss_config;
 
 /* vss_config.flags */
@@ -100,12 +113,19 @@ typedef struct vss_info {
   int mask_h, mask_w;      /* (maskH, maskW) of the seam */
   int n_layers;
   int dtype;
-  size_t device_bytes;     /* HBM held by the handle */
+  size_t device_bytes;     /* HBM held by the handle (all its GPUs) */
+  int n_gpus;              /* GPUs of the handle */
+  int queue_depth;         /* slots (batches in flight) */
+  int rccl;                /* 1: the host calls all-gather the masks over RCCL */
 } vss_info;
 
 /* status callback for vss_segment_async: called on a runtime thread once the
- * masks are in masks_out (status = VSS_OK) or the call failed. */
+ * masks are in masks_out (status = VSS_OK) or the call failed; in submission
+ * order. */
 typedef void (*vss_callback)(void* user, int status);
+
+/* Submission ticket of a queued batch (vss_submit, vss_wait). */
+typedef uint64_t vss_ticket;
 
 /* Library version (VSS_VERSION). */
 int vss_version(void);
@@ -138,19 +158,58 @@ int vss_mask_to_frame_device(vss_handle* h, const float* d_masks, int n, int fra
 int vss_segment(vss_handle* h, const uint8_t* frames, int n, int height, int width, int channels,
                 size_t row_stride, float* masks_out, int out_mode);
 
-/* Same as vss_segment but returns at once; cb fires when masks_out is filled.
- * The caller keeps frames and masks_out alive until then (replaces the async
- * `await session.run`, frameProcessorTest.ts:91). */
+/* Same as vss_segment but queued: returns once the frames are staged (the
+ * caller may reuse `frames` then); cb fires when masks_out is filled, in
+ * submission order.  VSS_E_BUSY when queue_depth batches are already in
+ * flight.  The caller keeps masks_out alive until the callback (replaces the
+ * async `await session.run`, frameProcessorTest.ts:91). */
 int vss_segment_async(vss_handle* h, const uint8_t* frames, int n, int height, int width,
                       int channels, size_t row_stride, float* masks_out, int out_mode,
                       vss_callback cb, void* user);
 
-/* Device-resident variant: d_frames and d_masks are HBM pointers; the work is
- * enqueued on `stream` (a hipStream_t; NULL = the handle's stream) and not
- * waited for.  frame_stride = bytes between frames. */
+/* The queued call without a callback: *ticket identifies the batch for
+ * vss_wait / vss_query.  VSS_E_BUSY when the queue is full. */
+int vss_submit(vss_handle* h, const uint8_t* frames, int n, int height, int width, int channels,
+               size_t row_stride, float* masks_out, int out_mode, vss_ticket* ticket);
+
+/* vss_submit for frames that are not one contiguous buffer: frames[i] points
+ * at frame i (each height rows of row_stride bytes); each is copied straight
+ * into the pinned staging (no packing copy on the caller's side). */
+int vss_submit_list(vss_handle* h, const uint8_t* const* frames, int n, int height, int width, int channels,
+                    size_t row_stride, float* masks_out, int out_mode, vss_ticket* ticket);
+
+/* Block until batch `ticket` is done (its masks_out filled); returns that
+ * batch's status.  vss_query: 1 done, 0 still running, < 0 an error. */
+int vss_wait(vss_handle* h, vss_ticket ticket);
+int vss_query(vss_handle* h, vss_ticket ticket);
+
+/* Zero-copy staging: the pinned host buffer (capacity bytes) that the NEXT
+ * queued host call reads its frames from.  A decoder that writes its frames
+ * there and passes this pointer as `frames` saves the staging copy (frames
+ * must start at the buffer's first byte). */
+int vss_staging_buffer(vss_handle* h, uint8_t** frames, size_t* capacity);
+
+/* Device-resident variant: d_frames and d_masks are HBM pointers of the
+ * handle's first GPU; the work is enqueued on `stream` (a hipStream_t; NULL =
+ * the handle's stream) and not waited for.  frame_stride = bytes between
+ * frames.  Consecutive calls take consecutive slots, so calls on different
+ * streams run concurrently (each stream sees its own calls in order). */
 int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width,
                        int channels, size_t row_stride, size_t frame_stride, float* d_masks,
                        void* stream);
+
+/* ---- one GPU per process (torchrun): an RCCL clique over the processes ------
+ * Rank 0 calls vss_comm_unique_id (ids for every slot; *len bytes, at most
+ * cap), hands the bytes to every rank, and each rank calls vss_comm_init_rank
+ * on its own handle.  Then vss_segment_gather_device runs the rank's n frames
+ * and all-gathers every rank's masks into d_gathered [nranks * n][mask_h *
+ * mask_w] in rank order, on `stream`; every rank must make the same sequence
+ * of calls with the same n. */
+int vss_comm_unique_id(vss_handle* h, void* ids, size_t cap, size_t* len);
+int vss_comm_init_rank(vss_handle* h, int nranks, int rank, const void* ids, size_t len);
+int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width,
+                              int channels, size_t row_stride, size_t frame_stride, float* d_gathered,
+                              void* stream);
 
 /* Preprocessing alone (frameProcessorTest.ts:79-85): d_out = [n][3][mask_h][mask_w]
  * f32, the exact ORT input tensor. Enqueued on `stream`. */
@@ -163,15 +222,6 @@ int vss_synchronize(vss_handle* h);
 
 int vss_set_option(vss_handle* h, int option, int value);
 int vss_get_option(vss_handle* h, int option, int* value);
-
-/* Name of the persistent forward's kernel as rocprofv3 reports it, e.g.
- * "void vss::k_forward<1>(vss::FwdParams)"; VSS_E_UNSUPPORTED when the plan
- * has none.  Returns the string length. */
-int vss_forward_kernel(const vss_handle* h, char* buf, int cap);
-
-/* Mean k_forward duration (ms) over the VSS_OPT_PROFILE forwards that ran it
- * (HIP events recorded by the launch itself); resets the accumulator. */
-int vss_profile_read_forward(vss_handle* h, double* ms, int* count);
 
 /* Per-layer output shape (C, H, W) at the handle's model resolution. */
 int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww);
@@ -196,6 +246,10 @@ int vss_layer_tiles(const vss_handle* h, int layer, int* th, int* tw, int cap);
 /* Kernel times from VSS_OPT_PROFILE runs: per layer, the mean over `count`
  * forwards (ms).  Resets the accumulators. */
 int vss_profile_read(vss_handle* h, double* ms_per_layer, int cap, int* count);
+
+/* Bytes of LDS one k_block workgroup of this shape carves (block_lds in
+ * csrc/vss_kernels.h); no GPU needed.  tools/gen_registry.py mirrors it. */
+int vss_block_lds_bytes(int mode, int stride, int th, int tw, int cin, int cskip, int chid, int cout, int stem_in);
 
 /* ---- §8(f) row 1: the reference's mask post-processing, on the GPU ----------
  * processFrame's steps after the seam (frameProcessorTest.ts:115-169):

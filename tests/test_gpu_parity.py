@@ -142,13 +142,9 @@ def test_graph_vs_eager_and_profile(pkg, sess_bf, synthetic):
     sess_bf.set_option(pkg.VSS_OPT_PROFILE, 0)
     sess_bf.set_option(pkg.VSS_OPT_USE_GRAPH, 1)
     assert np.array_equal(a, b) and np.array_equal(a, c)
-    if sess_bf.persistent:  # one k_forward launch per forward
-        ms, cnt = sess_bf.profile_read_forward()
-        assert cnt == 1 and ms > 0
-    else:
-        ms, cnt = sess_bf.profile_read()
-        fused = ["fused" in sess_bf.layer_kernel(i) for i in range(len(ms))]
-        assert cnt == 1 and all((m == 0) if fu else (m > 0) for m, fu in zip(ms, fused)), (ms, fused)
+    ms, cnt = sess_bf.profile_read()
+    fused = ["fused" in sess_bf.layer_kernel(i) for i in range(len(ms))]
+    assert cnt == 1 and all((m == 0) if fu else (m > 0) for m, fu in zip(ms, fused)), (ms, fused)
 
 
 def test_device_path_row_stride(pkg, sess_bf, synthetic, torch_cuda):
@@ -168,21 +164,124 @@ def test_device_path_row_stride(pkg, sess_bf, synthetic, torch_cuda):
     assert np.array_equal(out.cpu().numpy(), ref)
 
 
-def test_async_and_busy(pkg, sess_bf, synthetic):
+def _hold_slots(pkg, torch, s, k, d_frames, out):
+    """Occupy k of the handle's slots with device calls queued behind a ~60 ms
+    GPU sleep on one stream: those slots stay in flight until it ends."""
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(100_000_000)
+    for _ in range(k):
+        s.segment_device(d_frames.data_ptr(), 2, 480, 640, 3, 640 * 3, 480 * 640 * 3, out.data_ptr(), st.cuda_stream)
+    return st
+
+
+def test_async_queue_order_and_busy(pkg, synthetic, torch_cuda):
+    """vss_segment_async is queued (SURVEY §8(b) threading; replaces the single
+    in-flight rule of runModnetExclusive, main.ts:18-22): a call finds a free
+    slot while fewer than queue_depth batches are in flight, gets VSS_E_BUSY
+    when all are, and callbacks fire in submission order with masks bitwise
+    those of the synchronous call."""
     import threading
-    f = _frames(synthetic, 2, start=400)
-    ref, _, _ = sess_bf.segment_frames(f)
-    done = threading.Event()
-    got = {}
+    torch = torch_cuda
+    batches = [_frames(synthetic, 2, start=400 + 10 * i) for i in range(3)]
+    with pkg.Session(dtype="bf16x2", max_batch=2, max_frame_h=480, max_frame_w=640, queue_depth=3) as s:
+        assert s.queue_depth == 3
+        refs = [s.segment_frames(b)[0] for b in batches]
+        d = torch.from_numpy(batches[0]).cuda()
+        scratch = torch.empty((2, 144 * 256), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        order, got, lock = [], {}, threading.Lock()
+        done = threading.Event()
 
-    def cb(masks, mw, mh, status):
-        got["m"], got["s"] = masks.copy(), status
-        done.set()
+        def cb_for(i):
+            def cb(masks, mw, mh, status):
+                with lock:
+                    order.append(i)
+                    got[i] = (masks.copy(), status)
+                    if len(order) == 3:
+                        done.set()
+            return cb
 
-    sess_bf.segment_frames_async(f, cb)
-    assert done.wait(30)
-    sess_bf.synchronize()
-    assert got["s"] == 0 and np.array_equal(got["m"], ref)
+        _hold_slots(pkg, torch, s, 1, d, scratch)  # one slot held by a sleeping stream
+        s.segment_frames_async(batches[0], cb_for(0))
+        s.segment_frames_async(batches[1], cb_for(1))
+        with pytest.raises(pkg.VssError) as e:  # three in flight: the queue is full
+            s.segment_frames_async(batches[2], cb_for(2))
+        assert e.value.code == pkg.VSS_E_BUSY
+        s.synchronize()
+        s.segment_frames_async(batches[2], cb_for(2))
+        assert done.wait(30)
+        s.synchronize()
+        assert order == [0, 1, 2], order
+        for i in range(3):
+            assert got[i][1] == 0 and np.array_equal(got[i][0], refs[i]), i
+
+
+def test_submit_wait_many_in_flight(pkg, synthetic, torch_cuda):
+    """vss_submit / vss_wait with 4 batches in flight (BASELINE config 5's
+    pipelined host path): every batch's masks bitwise equal the device path's;
+    with every slot held, vss_submit is VSS_E_BUSY and vss_query says 0."""
+    torch = torch_cuda
+    batches = [_frames(synthetic, 8, start=1000 + 8 * i) for i in range(8)]
+    with pkg.Session(dtype="bf16x2", max_batch=8, max_frame_h=480, max_frame_w=640, queue_depth=4) as s:
+        dev = torch.empty((8, 144 * 256), dtype=torch.float32, device="cuda")
+        refs = []
+        for b in batches:
+            d = torch.from_numpy(b).cuda()
+            s.segment_device(d.data_ptr(), 8, 480, 640, 3, 640 * 3, 480 * 640 * 3, dev.data_ptr(), 0)
+            s.synchronize()
+            refs.append(dev.cpu().numpy().copy())
+        for rep in range(2):
+            tickets = [s.submit(b) for b in batches[4 * rep:4 * rep + 4]]
+            outs = [s.wait(t)[0] for t in reversed(tickets)][::-1]  # waited out of order
+            for i in range(4):
+                assert np.array_equal(outs[i], refs[4 * rep + i]), (rep, i)
+        t = s.submit(batches[0])
+        s.wait(t)
+        d = torch.from_numpy(batches[0][:2]).cuda()
+        small = torch.empty((2, 144 * 256), dtype=torch.float32, device="cuda")
+        _hold_slots(pkg, torch, s, 4, d, small)
+        with pytest.raises(pkg.VssError) as e:
+            s.submit(batches[1])
+        assert e.value.code == pkg.VSS_E_BUSY
+        s.synchronize()
+        assert s.query(t)
+
+
+def test_zero_copy_staging(pkg, synthetic):
+    """A decoder writing straight into vss_staging_buffer: no staging copy, same masks."""
+    f = _frames(synthetic, 4, start=1100)
+    with pkg.Session(dtype="bf16x2", max_batch=4, max_frame_h=480, max_frame_w=640, queue_depth=2) as s:
+        ref, _, _ = s.segment_frames(f)
+        for it in range(4):  # every slot in turn
+            buf = s.staging_buffer()
+            assert buf.size >= f.nbytes
+            buf[:f.nbytes] = f.reshape(-1)
+            out = np.empty((4, 144 * 256), np.float32)
+            t = s.submit_raw(buf.ctypes.data, 4, 480, 640, 3, 640 * 3, out)
+            s.wait(t)
+            assert np.array_equal(out, ref), it
+
+
+def test_inflight_streams_bitwise(pkg, sess_bf, synthetic, torch_cuda):
+    """vss_segment_device on several streams at once: consecutive calls take
+    consecutive slots (own activations), run concurrently, and give bitwise
+    the masks of one call at a time."""
+    torch = torch_cuda
+    fs = [_frames(synthetic, 8, start=700 + 8 * i) for i in range(6)]
+    refs = [sess_bf.segment_frames(f)[0] for f in fs]
+    ds = [torch.from_numpy(f).cuda() for f in fs]
+    outs = [torch.zeros((8, 144 * 256), dtype=torch.float32, device="cuda") for _ in fs]
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i in range(6):
+            st = streams[i % 4]
+            sess_bf.segment_device(ds[i].data_ptr(), 8, 480, 640, 3, 640 * 3, 480 * 640 * 3, outs[i].data_ptr(),
+                                   st.cuda_stream)
+        torch.cuda.synchronize()
+        for i in range(6):
+            assert np.array_equal(outs[i].cpu().numpy(), refs[i]), (rep, i)
 
 
 def test_argument_errors(pkg, sess_bf, synthetic):
@@ -220,21 +319,6 @@ def test_results_independent_of_tiling(pkg, sess_bf, synthetic):
         assert np.array_equal(got, ref), (mb, at)
 
 
-def test_branches_bitwise(pkg, sess_bf, synthetic, torch_cuda):
-    torch = torch_cuda
-    f = _frames(synthetic, 8, start=700)
-    ref, _, _ = sess_bf.segment_frames(f)
-    d = torch.from_numpy(f).cuda()
-    out = torch.empty((8, 144 * 256), dtype=torch.float32, device="cuda")
-    for br in (2, 3, 8):
-        sess_bf.set_option(pkg.VSS_OPT_BRANCHES, br)
-        out.zero_()
-        sess_bf.segment_device(d.data_ptr(), 8, 480, 640, 3, 640 * 3, 480 * 640 * 3, out.data_ptr(), 0)
-        sess_bf.synchronize()
-        assert np.array_equal(out.cpu().numpy(), ref), br
-    sess_bf.set_option(pkg.VSS_OPT_BRANCHES, 1)
-
-
 def test_stem_fusion_bitwise(pkg, synthetic, torch_cuda):
     # the stem computed inside b1's prologue (STEM_IN, one launch fewer) gives
     # bitwise the activations and masks of the separate stem launch
@@ -269,6 +353,8 @@ def test_keep_stem_option(pkg, synthetic, torch_cuda):
             s.read_layer(0, 3)
         l1 = s.read_layer(1, 3)
         s.set_option(pkg.VSS_OPT_KEEP_STEM, 1)
+        with pytest.raises(pkg.VssError, match="VSS_OPT_KEEP_STEM"):  # set, but the forward ran without it
+            s.read_layer(0, 3)
         b, _, _ = s.segment_frames(f)
         stem = s.read_layer(0, 3)
         assert np.array_equal(a, b) and np.array_equal(l1, s.read_layer(1, 3))

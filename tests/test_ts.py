@@ -42,7 +42,7 @@ def test_node_module_loads_and_fails_loudly_without_gpu(addon_built):
                          timeout=60)
     assert out.returncode == 0, out.stderr
     lines = out.stdout.split()
-    assert lines[0] == "10000"
+    assert lines[0] == "20000"
     if not torch.cuda.is_available():
         assert lines[1:] == ["error", "-2"]
 
@@ -61,7 +61,7 @@ def test_node_segment_matches_oracle_and_python_host(addon_built, pkg, oracle, b
     assert out.returncode == 0, out.stderr
     info = json.loads(out.stdout.strip().splitlines()[-1])
     assert info == {"width": 256, "height": 144, "count": 3, "singleMatchesBatch": True,
-                    "oversizeRejected": True, "version": 10000, "frameDims": [640, 480, 3 * 480 * 640]}
+                    "oversizeRejected": True, "version": 20000, "frameDims": [640, 480, 3 * 480 * 640]}
     masks = np.fromfile(op, np.float32).reshape(3, -1)
     ref = oracle.forward(blob, frames, 144, 256, mode=0).reshape(3, -1)
     assert np.abs(masks - ref).max() <= 1e-3
@@ -71,6 +71,38 @@ def test_node_segment_matches_oracle_and_python_host(addon_built, pkg, oracle, b
     with pkg.Session(dtype=dtype, max_batch=3, max_frame_h=480, max_frame_w=640) as s:
         py, _, _ = s.segment_frames(frames)
     assert np.array_equal(masks, py)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ids", [None, "0"])
+def test_node_queue_resolves_in_call_order(addon_built, pkg, oracle, blob, synthetic, tmp_path, ids):
+    """Concurrent segmentFrames promises (more than queueDepth, so some wait in
+    the JS queue) resolve in call order with oracle-equal masks — the ordering
+    contract of runModnetExclusive (main.ts:18-22) with batches overlapping on
+    the GPU; deviceIds=[0] runs the same calls through the RCCL path.  Config 1
+    (a 144x256 frame: ratio-1 resize) goes through Node here."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = 3
+    for (h, w) in ((480, 640), (144, 256)):
+        frames = np.stack([synthetic.make_frame(800 + i, h, w, 3) for i in range(n)])
+        fp, op = tmp_path / f"q{h}.bin", tmp_path / f"q{h}"
+        frames.tofile(fp)
+        args = [NODE, os.path.join(ROOT, "tests", "node", "run_queue.js"), str(fp), str(n), str(h), str(w), "3",
+                str(op), "2"] + ([ids] if ids else [])
+        out = subprocess.run(args, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr
+        info = json.loads(out.stdout.strip().splitlines()[-1])
+        assert info["order"] == list(range(n + 2)) and info["empty"] == "rejected", info
+        assert info["queueDepth"] == 2 and info["nGpus"] == 1
+        ref = oracle.forward(blob, frames, 144, 256, mode=0).reshape(n, -1)
+        for i in range(n):
+            m = np.fromfile(f"{op}.{i}", np.float32)
+            assert np.abs(m - ref[i]).max() <= 1e-3, i
+        whole = np.fromfile(f"{op}.{n}", np.float32).reshape(n, -1)
+        rev = np.fromfile(f"{op}.{n + 1}", np.float32).reshape(n, -1)
+        assert np.abs(whole - ref).max() <= 1e-3 and np.array_equal(rev, whole[::-1])
 
 
 @pytest.mark.gpu

@@ -1,0 +1,53 @@
+// The TypeScript host timed end to end (SURVEY.md §8(d): segmentFrames call ->
+// promise resolve, including staging, H2D, the forward and D2H), the way the
+// reference times `Latency` (session.run, frameProcessorTest.ts:90-92) and
+// `Total Frame` (:180-185, shown at main.ts:96-105).  Run by bench.py as its
+// own child process:
+//   node bench_ts.js <height> <width> <batch> <iters> [queueDepth]
+// prints one JSON line: throughput with every call fired at once (the queue
+// keeps queueDepth batches in flight) and the latency of one call at a time.
+'use strict';
+const path = require('path');
+const seg = require(path.join(__dirname, '..', 'video-stream-segmenetation_amd', 'ts', 'segment.js'));
+
+function synthetic(n, h, w) {
+  const frames = [];
+  for (let i = 0; i < n; i++) {
+    const data = new Uint8Array(h * w * 3);
+    let s = 20251024 + i;
+    for (let k = 0; k < data.length; k++) {
+      s = (s * 1664525 + 1013904223) >>> 0;
+      data[k] = s >>> 24;
+    }
+    frames.push({ data: data, width: w, height: h, channels: 3 });
+  }
+  return frames;
+}
+
+async function main() {
+  const [h, w, b, it, depth] = process.argv.slice(2).map(Number);
+  const frames = synthetic(b, h, w);
+  const s = new seg.Segmenter({ maxBatch: b, maxFrameWidth: w, maxFrameHeight: h, queueDepth: depth || 0 });
+  for (let i = 0; i < 10; i++) await s.segmentFrames(frames);
+  // latency: one call at a time (the reference's serialised loop)
+  const lat = [];
+  for (let i = 0; i < Math.max(20, it / 5); i++) {
+    const t0 = process.hrtime.bigint();
+    await s.segmentFrames(frames);
+    lat.push(Number(process.hrtime.bigint() - t0) / 1e6);
+  }
+  lat.sort((a, c) => a - c);
+  // throughput: every call fired at once, resolved in order
+  const t0 = process.hrtime.bigint();
+  const ps = [];
+  for (let i = 0; i < it; i++) ps.push(s.segmentFrames(frames));
+  await Promise.all(ps);
+  const el = Number(process.hrtime.bigint() - t0) / 1e9;
+  console.log(JSON.stringify({ value: Math.round(b * it / el * 10) / 10, unit: 'frames/s',
+                               ms_per_batch: Math.round(el * 1e3 / it * 1e4) / 1e4, iters: it,
+                               latency_ms_p50: Math.round(lat[lat.length >> 1] * 1e4) / 1e4,
+                               latency_ms_min: Math.round(lat[0] * 1e4) / 1e4, queue_depth: s.queueDepth,
+                               entry: 'Segmenter.segmentFrames (TS -> N-API -> vss_submit_list / vss_wait)' }));
+  s.close();
+}
+main().catch((e) => { console.error(e); process.exit(1); });

@@ -10,16 +10,10 @@ consumer of it for XP / SP = 1 and its producer's KS.
 Tiles are every candidate that fits the kernel's limits (<= 16 accumulator
 tiles per wave, <= 160 KiB LDS); the host planner picks among them at run
 time for the handle's model resolution and batch.  The LDS formula mirrors
-block_lds() in csrc/vss_kernels.h.
+block_lds() in csrc/vss_kernels.h (tests/test_registry.py checks the two
+against each other through libvss's vss_block_lds_bytes).
 
-The persistent forward (k_forward, one launch per forward) dispatches a
-fixed subset of these shapes: per layer and per model resolution in
-MK_RESOLUTIONS, the tile the host planner's choose_tile() picks at batch
-MK_BATCH (mirrored below), restricted to <= MK_MAX_LDS so two workgroups fit
-a CU.  Those lines carry their dispatch id as the 10th field (-1 = not in
-the persistent forward) and are listed again in vss_mk.inc.
-
-    python tools/gen_registry.py [spec.json]   # writes csrc/vss_registry.inc and csrc/vss_mk.inc
+    python tools/gen_registry.py [spec.json]   # writes csrc/vss_registry*.inc
 """
 from __future__ import annotations
 
@@ -63,6 +57,7 @@ def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=False)
     f += r4(chid * (cin + 8) // 2) if mode == 0 else 0
     f += r4(cout * (chid + 8) // 2) + r4(9 * chid) + r4(chid) + (r4(chid) if mode == 0 else 0) + r4(cout)
     f += r4(2 * cin) if mode == 2 else 0
+    f += 4 * p_in_pad if mode == 2 else 0  # the decoder's upsample tap records (L.uc)
     # work: expand scratch / slabs / (decoder) the low-res src region; the
     # decoder's norm slots and stats scratch live in xt
     f += max(4 * p_in_pad * HID_STRIDE if mode == 0 else 1024, cs * p_out * (cout + 4),
@@ -114,62 +109,6 @@ def shapes(spec):
     return out
 
 
-MK_RESOLUTIONS = [(144, 256), (288, 512)]
-MK_BATCH = 8
-MK_MAX_LDS = 78 * 1024
-RES_DIV = {"/1": 1, "/2": 2, "/4": 4, "/8": 8, "/16": 16}
-KSPLIT_PIXELS = 256  # kDefaultKsplitPixels in csrc/vss_capi.hip
-KSPLIT_WEIGHT_BYTES = 40 * 1024  # kKsplitWeightBytes in csrc/vss_capi.hip
-
-
-def weight_image_bytes(l):
-    """Bytes of an unsplit expand layer's LDS weight image (block_lds regions w1..b2)."""
-    cin, chid, cout = l["cin"], l["chid"], l["cout"]
-    return 4 * (r4(chid * (cin + 8) // 2) + r4(cout * (chid + 8) // 2) + r4(9 * chid) + 2 * r4(chid) + r4(cout))
-
-
-def planned_shapes(spec, hm, wm):
-    """(name, shape key without tile, H, W) per block layer at model res hm x wm,
-    with the hidden split the host planner applies (plan() in vss_capi.hip)."""
-    layers = spec["layers"]
-    by = {l["name"]: l for l in layers}
-    ks = {}
-    out = []
-    for l in layers:
-        d = RES_DIV[l["res"]]
-        H, W = hm // d, wm // d
-        k = 1
-        if l["kind"] == "ir" and l["expand"] and (H * W <= KSPLIT_PIXELS or weight_image_bytes(l) > KSPLIT_WEIGHT_BYTES):
-            k = ks_max(l)
-        ks[l["name"]] = k
-        if l["kind"] == "ir":
-            mode = 0 if l["expand"] else 1
-            chid = l["chid"] if l["expand"] else l["cin"]
-            key = (mode, l["stride"], l["cin"], 0, chid // k, l["cout"],
-                   flags_of(False, l["residual"], ks[l["src"]], 1, k))
-            out.append((l["name"], key, H, W))
-        elif l["kind"] == "dec":
-            key = (2, 1, l["cin"], l["cskip"], l["cin"] + l["cskip"], l["cout"],
-                   flags_of(by[l["src"]]["kind"] == "dec", False, ks[l["src"]], ks[l["skip"]], 1))
-            out.append((l["name"], key, H, W))
-    return out
-
-
-def choose_tile(key, H, W, n, tiles):
-    """Mirror of choose_tile() in csrc/vss_capi.hip over the compiled tiles."""
-    mode, stride, cin, cskip, chid, cout, flags = key
-    best, best_score = None, -1
-    for th, tw in tiles:
-        lds, _ = block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout)
-        blocks = -(-H // th) * -(-W // tw) * n
-        score = ((1 << 40) if blocks >= 512 else (blocks << 20)) + th * tw * 1024 - lds // 1024
-        if blocks >= 512 and lds > 64 * 1024:
-            score -= 1 << 39
-        if score > best_score:
-            best, best_score = (th, tw), score
-    return best
-
-
 def main():
     spec = json.load(open(sys.argv[1] if len(sys.argv) > 1 else SPEC))
     entries = []
@@ -184,27 +123,11 @@ def main():
                 continue
             seen.add(key)
             entries.append((name, key, lds, nacc))
-    # the persistent forward's shapes
-    mk = {}
-    for hm, wm in MK_RESOLUTIONS:
-        for name, key, H, W in planned_shapes(spec, hm, wm):
-            mode, stride, cin, cskip, chid, cout, flags = key
-            tiles = [(th, tw) for (_, (m, s, th, tw, ci, ck, ch, co, fl), lds, _) in entries
-                     if (m, s, ci, ck, ch, co, fl) == key and lds <= MK_MAX_LDS]
-            if not tiles:
-                continue
-            th, tw = choose_tile(key, H, W, MK_BATCH, tiles)
-            full = (mode, stride, th, tw, cin, cskip, chid, cout, flags)
-            if full not in mk:
-                mk[full] = len(mk)
     head = f"// generated by tools/gen_registry.py from {os.path.basename(SPEC)} ({spec['name']}); do not edit"
     lines = [head]
     for name, key, lds, nacc in entries:
         args = ", ".join(str(v) for v in key)
-        lines.append(f"VSS_BLOCK({args}, {mk.get(key, -1)})  // {name}: {lds // 1024} KiB LDS, {nacc} acc")
-    mk_lines = [head, "// VSS_MK(id, mode, stride, TH, TW, cin, cskip, chid, cout, flags): k_forward's dispatch table"]
-    for key, i in sorted(mk.items(), key=lambda kv: kv[1]):
-        mk_lines.append(f"VSS_MK({i}, " + ", ".join(str(v) for v in key) + ")")
+        lines.append(f"VSS_BLOCK({args})  // {name}: {lds // 1024} KiB LDS, {nacc} acc")
     csrc = os.path.join(ROOT, "video-stream-segmenetation_amd", "csrc")
     open(os.path.join(csrc, "vss_registry.inc"), "w").write("\n".join(lines) + "\n")
     # the same lines dealt round-robin to the shard files the Makefile compiles in parallel
@@ -213,7 +136,6 @@ def main():
         open(os.path.join(csrc, f"vss_registry_{k}.inc"), "w").write("\n".join(part) + "\n")
     open(os.path.join(csrc, "vss_registry_shards.inc"), "w").write(
         "\n".join([head] + [f"VSS_SHARD_FN({k})" for k in range(SHARDS)]) + "\n")
-    open(os.path.join(csrc, "vss_mk.inc"), "w").write("\n".join(mk_lines) + "\n")
 
 
 if __name__ == "__main__":

@@ -13,6 +13,11 @@ TypeScript surface (segmentFrame/segmentFrames) is in ts/ over the same C ABI.
 Errors mirror ORT-web's rejecting `session.run`: every failing call raises
 VssError carrying the C code and vss_last_error().  There is no CPU fallback:
 if libvss.so is missing or no HIP device is present, creating a Session raises.
+
+A Session owns `queue_depth` slots: `submit(frames)` returns a ticket at once
+(the host -> device copy, forward and device -> host copy of consecutive
+batches overlap) and `wait(ticket)` returns the masks; `Session(device_ids=
+[...])` shards every batch over those GPUs and all-gathers the masks over RCCL.
 """
 from __future__ import annotations
 
@@ -33,8 +38,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "vss.h")
 VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_IO, VSS_E_UNSUPPORTED = (
     0, -1, -2, -3, -4, -5, -6, -7)
 DTYPES = {"f32": 0, "bf16x2": 1}
-VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_BRANCHES, VSS_OPT_FORWARD, VSS_OPT_FORWARD_FAULTS = 1, 2, 3, 4, 5
-VSS_OPT_KEEP_STEM = 6
+VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_KEEP_STEM = 1, 2, 6
 VSS_CREATE_NO_AUTOTUNE = 1
 VSS_OUT_MODEL, VSS_OUT_FRAME = 0, 1
 
@@ -48,12 +52,15 @@ class VssError(RuntimeError):
 class _Config(ctypes.Structure):
     _fields_ = [("model_h", ctypes.c_int), ("model_w", ctypes.c_int), ("dtype", ctypes.c_int),
                 ("device_id", ctypes.c_int), ("max_batch", ctypes.c_int), ("max_frame_h", ctypes.c_int),
-                ("max_frame_w", ctypes.c_int), ("weights_path", ctypes.c_char_p), ("flags", ctypes.c_int)]
+                ("max_frame_w", ctypes.c_int), ("weights_path", ctypes.c_char_p), ("flags", ctypes.c_int),
+                ("n_gpus", ctypes.c_int), ("device_ids", ctypes.POINTER(ctypes.c_int)), ("queue_depth", ctypes.c_int),
+                ("staging_threads", ctypes.c_int)]
 
 
 class _Info(ctypes.Structure):
     _fields_ = [("mask_h", ctypes.c_int), ("mask_w", ctypes.c_int), ("n_layers", ctypes.c_int),
-                ("dtype", ctypes.c_int), ("device_bytes", ctypes.c_size_t)]
+                ("dtype", ctypes.c_int), ("device_bytes", ctypes.c_size_t), ("n_gpus", ctypes.c_int),
+                ("queue_depth", ctypes.c_int), ("rccl", ctypes.c_int)]
 
 
 class PostConfig(ctypes.Structure):
@@ -82,9 +89,13 @@ _lock = threading.Lock()
 
 
 def build(force: bool = False) -> str:
-    """Compile libvss.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-s", "-C", os.path.join(HERE, "csrc")], check=True)
+    """Compile libvss.so for gfx950 in-tree (hipcc cross-compiles without a GPU).
+    Always runs make: its dependency tracking rebuilds exactly what changed, so
+    a library built from older sources is never reused."""
+    cmd = ["make", "-s", "-j", str(min(8, os.cpu_count() or 1)), "-C", os.path.join(HERE, "csrc")]
+    if force:
+        cmd.insert(2, "-B")
+    subprocess.run(cmd, check=True)
     return LIB_PATH
 
 
@@ -115,14 +126,20 @@ def lib() -> ctypes.CDLL:
                 "vss_get_info": ([P, ctypes.POINTER(_Info)], I),
                 "vss_segment": ([P, P, I, I, I, I, S, P, I], I),
                 "vss_segment_async": ([P, P, I, I, I, I, S, P, I, CALLBACK, P], I),
+                "vss_submit": ([P, P, I, I, I, I, S, P, I, ctypes.POINTER(ctypes.c_uint64)], I),
+                "vss_wait": ([P, ctypes.c_uint64], I),
+                "vss_query": ([P, ctypes.c_uint64], I),
+                "vss_staging_buffer": ([P, ctypes.POINTER(P), ctypes.POINTER(S)], I),
                 "vss_segment_device": ([P, P, I, I, I, I, S, S, P, P], I),
+                "vss_comm_unique_id": ([P, P, S, ctypes.POINTER(S)], I),
+                "vss_comm_init_rank": ([P, I, I, P, S], I),
+                "vss_segment_gather_device": ([P, P, I, I, I, I, S, S, P, P], I),
+                "vss_block_lds_bytes": ([I] * 9, I),
                 "vss_preprocess_device": ([P, P, I, I, I, I, S, S, P, P], I),
                 "vss_mask_to_frame_device": ([P, P, I, I, I, P, P], I),
                 "vss_synchronize": ([P], I),
                 "vss_set_option": ([P, I, I], I),
                 "vss_get_option": ([P, I, ctypes.POINTER(I)], I),
-                "vss_forward_kernel": ([P, ctypes.c_char_p, I], I),
-                "vss_profile_read_forward": ([P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I)], I),
                 "vss_layer_shape": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)], I),
                 "vss_read_layer": ([P, I, I, P], I),
                 "vss_profile_read": ([P, ctypes.POINTER(ctypes.c_double), I, ctypes.POINTER(I)], I),
@@ -172,12 +189,21 @@ class Session:
 
     def __init__(self, model_h: int = 144, model_w: int = 256, dtype: str = "bf16x2", device_id: int = 0,
                  max_batch: int = 8, max_frame_h: int = 1080, max_frame_w: int = 1920,
-                 weights_path: str | None = None, autotune: bool = True):
+                 weights_path: str | None = None, autotune: bool = True, device_ids=None, queue_depth: int = 0,
+                 staging_threads: int = 0):
+        """device_ids: one handle over these GPUs (batches sharded, masks all-gathered over
+        RCCL; a list of one GPU still takes the RCCL path); queue_depth: batches in flight."""
         if dtype not in DTYPES:
             raise VssError(VSS_E_INVALID_ARG, f"dtype must be one of {sorted(DTYPES)}")
         self.weights_path = ensure_weights(weights_path or DEFAULT_WEIGHTS)
+        ids = None
+        if device_ids is not None:
+            ids = (ctypes.c_int * max(1, len(device_ids)))(*[int(d) for d in device_ids])
         cfg = _Config(model_h, model_w, DTYPES[dtype], device_id, max_batch, max_frame_h, max_frame_w,
-                      self.weights_path.encode(), 0 if autotune else 1)
+                      self.weights_path.encode(), 0 if autotune else 1,
+                      len(device_ids) if device_ids is not None else 0,
+                      ctypes.cast(ids, ctypes.POINTER(ctypes.c_int)) if ids is not None else None,
+                      queue_depth, staging_threads)
         h = ctypes.c_void_p()
         _check(lib().vss_create(ctypes.byref(cfg), ctypes.byref(h)), None)
         self._h = h
@@ -185,8 +211,10 @@ class Session:
         _check(lib().vss_get_info(self._h, ctypes.byref(info)), self._h)
         self.mask_h, self.mask_w, self.n_layers = info.mask_h, info.mask_w, info.n_layers
         self.device_bytes = info.device_bytes
+        self.n_gpus, self.queue_depth, self.rccl = info.n_gpus, info.queue_depth, bool(info.rccl)
         self.dtype, self.max_batch = dtype, max_batch
         self._pending = []
+        self._tickets = {}
         self._posts = []
 
     # -- lifecycle --------------------------------------------------------
@@ -229,7 +257,9 @@ class Session:
         return masks[0], mw, mh
 
     def segment_frames_async(self, frames: np.ndarray, callback):
-        """Returns at once; callback(masks, maskW, maskH, status) fires when done."""
+        """Queued: returns once the frames are staged; callback(masks, maskW, maskH, status)
+        fires when done, in submission order.  Raises VssError(VSS_E_BUSY) when queue_depth
+        batches are in flight."""
         f = _as_frames(frames)
         n, hh, ww, c = f.shape
         out = np.empty((n, self.mask_h * self.mask_w), np.float32)
@@ -238,10 +268,70 @@ class Session:
             callback(_out, self.mask_w, self.mask_h, status)
 
         cb = CALLBACK(_done)
-        self._pending.append((cb, f, out))
+        self._pending.append((cb, out))
+        if len(self._pending) > 4 * max(1, self.queue_depth):
+            self._pending = self._pending[-2 * max(1, self.queue_depth):]  # callbacks long since fired
         _check(lib().vss_segment_async(self._h, f.ctypes.data, n, hh, ww, c, ww * c, out.ctypes.data,
                                        VSS_OUT_MODEL, cb, None), self._h)
         return out
+
+    def submit(self, frames: np.ndarray, output_size: str = "model") -> int:
+        """Queued host call: returns the batch's ticket once its frames are staged
+        (VssError(VSS_E_BUSY) when queue_depth batches are in flight); wait(ticket)
+        returns (masks, maskW, maskH)."""
+        f = _as_frames(frames)
+        n, hh, ww, c = f.shape
+        frame = output_size == "frame"
+        out = np.empty((n, hh * ww if frame else self.mask_h * self.mask_w), np.float32)
+        t = ctypes.c_uint64()
+        _check(lib().vss_submit(self._h, f.ctypes.data, n, hh, ww, c, ww * c, out.ctypes.data,
+                                VSS_OUT_FRAME if frame else VSS_OUT_MODEL, ctypes.byref(t)), self._h)
+        self._tickets[t.value] = (out, (ww, hh) if frame else (self.mask_w, self.mask_h))
+        return t.value
+
+    def wait(self, ticket: int):
+        """Block until batch `ticket` is done -> (masks, maskW, maskH)."""
+        _check(lib().vss_wait(self._h, ticket), self._h)
+        out, (mw, mh) = self._tickets.pop(ticket)
+        return out, mw, mh
+
+    def query(self, ticket: int) -> bool:
+        rc = lib().vss_query(self._h, ticket)
+        if rc < 0:
+            _check(rc, self._h)
+        return rc == 1
+
+    def staging_buffer(self) -> np.ndarray:
+        """The pinned buffer the NEXT queued host call reads its frames from (zero-copy
+        decode target), as a writable uint8 array of its capacity."""
+        p, cap = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(lib().vss_staging_buffer(self._h, ctypes.byref(p), ctypes.byref(cap)), self._h)
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(cap.value,))
+
+    def submit_raw(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int, out: np.ndarray) -> int:
+        """vss_submit on a raw host pointer (e.g. staging_buffer()); masks into `out`."""
+        t = ctypes.c_uint64()
+        _check(lib().vss_submit(self._h, frames_ptr, n, h, w, c, row_stride, out.ctypes.data, VSS_OUT_MODEL,
+                                ctypes.byref(t)), self._h)
+        self._tickets[t.value] = (out, (self.mask_w, self.mask_h))
+        return t.value
+
+    # -- one GPU per process: an RCCL clique over the processes ---------------
+    def comm_unique_id(self) -> bytes:
+        buf = ctypes.create_string_buffer(4096)
+        n = ctypes.c_size_t()
+        _check(lib().vss_comm_unique_id(self._h, buf, 4096, ctypes.byref(n)), self._h)
+        return buf.raw[:n.value]
+
+    def comm_init_rank(self, nranks: int, rank: int, ids: bytes):
+        buf = ctypes.create_string_buffer(ids, len(ids))
+        _check(lib().vss_comm_init_rank(self._h, nranks, rank, buf, len(ids)), self._h)
+
+    def segment_gather_device(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int,
+                              frame_stride: int, gathered_ptr: int, stream: int = 0):
+        """This rank's n frames -> every rank's masks [nranks * n][maskH * maskW] (RCCL all-gather)."""
+        _check(lib().vss_segment_gather_device(self._h, frames_ptr, n, h, w, c, row_stride, frame_stride,
+                                               gathered_ptr, stream or None), self._h)
 
     # -- device-resident path (bench, multi-GPU host) ----------------------
     def segment_device(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int, frame_stride: int,
@@ -271,27 +361,6 @@ class Session:
         v = ctypes.c_int()
         _check(lib().vss_get_option(self._h, option, ctypes.byref(v)), self._h)
         return v.value
-
-    @property
-    def persistent(self) -> bool:
-        """True when forwards run as ONE persistent k_forward launch."""
-        return bool(self.get_option(VSS_OPT_FORWARD))
-
-    def forward_faults(self) -> int:
-        """k_forward dependency waits that gave up since the last call (0 = healthy)."""
-        return self.get_option(VSS_OPT_FORWARD_FAULTS)
-
-    def forward_kernel(self) -> str | None:
-        """The persistent forward's kernel name as rocprofv3 reports it (None if unsupported)."""
-        buf = ctypes.create_string_buffer(128)
-        rc = lib().vss_forward_kernel(self._h, buf, 128)
-        return buf.value.decode() if rc > 0 else None
-
-    def profile_read_forward(self):
-        """(mean k_forward ms over profiled forwards, count)."""
-        ms, cnt = ctypes.c_double(), ctypes.c_int()
-        _check(lib().vss_profile_read_forward(self._h, ctypes.byref(ms), ctypes.byref(cnt)), self._h)
-        return ms.value, cnt.value
 
     # -- introspection -----------------------------------------------------
     def layer_shape(self, layer: int):
@@ -436,3 +505,8 @@ def composite_device(session: Session, frames_ptr: int, n: int, h: int, w: int, 
 
 def version() -> int:
     return lib().vss_version()
+
+
+def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=0) -> int:
+    """block_lds() of csrc/vss_kernels.h through the library (no GPU needed)."""
+    return lib().vss_block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in)

@@ -1,22 +1,36 @@
 // vss_capi.hip — the C ABI (include/vss.h) over the gfx950 kernels.
 //
-// One handle = one GPU + one private HIP stream, mirroring one ORT
-// InferenceSession (/root/reference/client/src/core/model.ts:12-29).  The
-// handle parses the weights blob's layer table once, plans per-layer tiles for
-// its model resolution, keeps every activation NHWC f32 in HBM for max_batch
-// frames, and replays one captured hipGraph per (shape, buffers) key.
+// One engine per GPU mirrors one ORT InferenceSession
+// (/root/reference/client/src/core/model.ts:12-29): it parses the weights
+// blob's layer table once, plans per-layer tiles for its model resolution and
+// uploads the per-layer LDS weight images.  Unlike the reference, which
+// serialises every session.run (client/src/core/main.ts:18-22), an engine owns
+// `queue_depth` slots — each its own NHWC f32 activations for max_batch
+// frames, decoder-norm accumulators, HIP stream, captured hipGraphs and
+// (allocated on first use) pinned staging — so consecutive batches run
+// concurrently: batch i+1's H2D overlaps batch i's forward (BASELINE config 5).
+//
+// A handle = engine 0 (device_ids[0], the masks' consumer) + peer engines for
+// the other GPUs.  Host calls shard a batch contiguously over the engines and
+// all-gather the masks over RCCL (one communicator per device and slot, so
+// concurrent slots never share one); one-GPU-per-process callers join a
+// clique with vss_comm_init_rank instead.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -37,6 +51,7 @@ constexpr uint32_t kMagic = 0x57535356u, kNone = 0xFFFFFFFFu;
 enum { K_STEM = 1, K_IR = 2, K_DEC = 3, K_HEAD = 4 };
 enum { F_EXPAND = 1, F_RESIDUAL = 2 };
 enum { O_W1, O_B1, O_WDW, O_BDW, O_W2, O_B2, O_GAMMA, O_BETA };
+constexpr int kDefaultQueueDepth = 4, kMaxQueueDepth = 16, kDefaultStagingThreads = 4;
 
 struct Rec {
   uint32_t kind, cin, chid, cout, stride, flags, src, skip, off[8];
@@ -47,18 +62,16 @@ struct LayerPlan {
   int C = 0, H = 0, W = 0;     // output shape
   int inH = 0, inW = 0;        // shape of rec.src's output (x)
   int mode = -1, stride = 1, chid = 0;
-  int TH = 0, TW = 0, tiles_x = 0, tiles_y = 0, grid_x = 0, grid_y = 0;
+  int TH = 0, TW = 0, tiles_x = 0, tiles_y = 0;
   int flags = 0;
   int ks = 1, xp = 1, sp = 1;  // hidden split of this layer, parts of its x / skip (block_flags)
-  size_t part_stride = 0;      // floats between the parts of act
+  size_t part_stride = 0;      // floats between the parts of an activation
   long wimg_stride = 0;        // floats between the slices' weight images
   size_t lds = 0;
   const BlockEntry* entry = nullptr;  // compiled shape (registry)
   bool fused = false;          // computed inside its only consumer's prologue (no launch of its own)
-  float* act = nullptr;        // [max_batch][H][W][C]
-  int acc_off = -1;            // DEC: offset of its [2][C] norm accumulator in a frame's row of d_acc
+  int acc_off = -1;            // DEC: offset of its [kAccSlots][2][C] norm accumulator in a frame's row
   const float* wimg = nullptr;  // LDS weight image (block_lds regions w1..b2)
-  int wimg_f4 = 0;
   const float *gamma = nullptr, *beta = nullptr;
   const float *stem_w = nullptr, *stem_b = nullptr, *head_w = nullptr;
   float head_b = 0.f;
@@ -66,86 +79,167 @@ struct LayerPlan {
 
 using GraphKey = std::tuple<const void*, const void*, int, int, int, int, size_t, size_t>;
 
+// One batch in flight on one GPU: everything a forward writes.
+struct Slot {
+  std::vector<float*> act;            // per layer: [ks][max_batch][H][W][C]
+  unsigned long long* acc = nullptr;  // decoder instance-norm accumulators [max_batch][acc_stride]
+  float* d_masks = nullptr;           // [max_batch][P]: host paths' masks (the all-gather's send buffer)
+  float* d_gather = nullptr;          // RCCL handles: [nranks * max_batch][P]
+  hipStream_t stream = nullptr;       // the slot's stream (queued host calls)
+  hipEvent_t done = nullptr;          // recorded after the slot's latest work
+  bool used = false;
+  int status = VSS_OK;                // of the slot's latest queued batch (set by its callback)
+  vss_ticket ticket = 0;              // latest ticket that ran in this slot
+  bool stem_stored = false;           // the latest forward stored the fused stem (VSS_OPT_KEEP_STEM)
+  std::map<GraphKey, hipGraphExec_t> graphs;
+  ncclComm_t comm = nullptr;          // this GPU's communicator of the slot (RCCL handles)
+  // host-path staging, allocated on the slot's first host call
+  uint8_t* d_frames = nullptr;
+  uint8_t* h_frames = nullptr;        // pinned
+  float* h_masks = nullptr;           // pinned [max_batch][P] (engine 0: the whole batch)
+  float* d_fmasks = nullptr;          // VSS_OUT_FRAME: [max_batch][frame] masks
+  float* h_fmasks = nullptr;
+};
+
 thread_local std::string g_tls_error;
+
+// Host threads for the pinned staging copies: a copy is cut into 1 MiB
+// pieces that the pool's threads and the caller take in turn (one core's
+// memcpy bandwidth, ~20 GB/s, would bound the host path below the PCIe rate).
+class CopyPool {
+ public:
+  explicit CopyPool(int threads) {
+    for (int i = 0; i < threads; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+  struct Job {
+    void* dst;
+    const void* src;
+    size_t len;
+  };
+  // Copies every job; returns when all bytes are in place and every worker
+  // has left this generation (so no worker ever touches a later one's pieces
+  // with a stale index).
+  void run(const std::vector<Job>& jobs) {
+    constexpr size_t kPiece = size_t(1) << 20;
+    std::vector<Job> pieces;
+    for (const Job& j : jobs)
+      for (size_t off = 0; off < j.len; off += kPiece)
+        pieces.push_back({static_cast<char*>(j.dst) + off, static_cast<const char*>(j.src) + off,
+                          std::min(kPiece, j.len - off)});
+    if (pieces.size() <= 1 || workers_.empty()) {
+      for (const Job& p : pieces) std::memcpy(p.dst, p.src, p.len);
+      return;
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    pieces_ = &pieces;
+    next_.store(0);
+    active_ = workers_.size();
+    ++gen_;
+    lk.unlock();
+    cv_.notify_all();
+    work(&pieces);
+    lk.lock();
+    done_cv_.wait(lk, [&] { return active_ == 0; });
+    pieces_ = nullptr;
+  }
+
+ private:
+  void work(const std::vector<Job>* ps) {
+    for (size_t i = next_.fetch_add(1); i < ps->size(); i = next_.fetch_add(1))
+      std::memcpy((*ps)[i].dst, (*ps)[i].src, (*ps)[i].len);
+  }
+  void loop() {
+    unsigned long seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      const std::vector<Job>* ps = pieces_;
+      lk.unlock();
+      work(ps);
+      lk.lock();
+      if (--active_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::vector<Job>* pieces_ = nullptr;
+  std::atomic<size_t> next_{0};
+  size_t active_ = 0;
+  unsigned long gen_ = 0;
+  bool stop_ = false;
+};
 
 }  // namespace
 
 constexpr long kDefaultKsplitPixels = 256;
 // expand layers whose unsplit LDS weight image exceeds this also split their
-// hidden channels (keeps every layer within the persistent forward's LDS
-// budget of two workgroups per CU; mirrors KSPLIT_WEIGHT_BYTES in
-// tools/gen_registry.py)
+// hidden channels (keeps every layer's LDS small enough for two workgroups per
+// CU; mirrors KSPLIT_WEIGHT_BYTES in tools/gen_registry.py)
 constexpr size_t kKsplitWeightBytes = 40 * 1024;
 
 struct vss_handle {
-  vss_config cfg{};
+  vss_config cfg{};            // this engine's config (max_batch = its share of the handle's)
   std::string weights_path;
   std::string err;
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;          // NULL-stream device calls, post / composite, autotune
+  hipStream_t capture_stream = nullptr;  // hipGraph capture only (never executes)
   std::vector<Rec> recs;
   std::vector<float> hdata;
   float eps = 1e-5f;
   std::vector<LayerPlan> L;
-  unsigned long long* d_acc = nullptr;  // decoder instance-norm accumulators [max_batch][acc_stride]
   int acc_stride = 0;
   std::vector<void*> dev_allocs;
+  std::vector<void*> host_allocs;
   size_t dev_bytes = 0;
-  uint8_t* d_frames = nullptr;
-  float* d_masks = nullptr;
-  size_t frame_cap = 0;
-  uint8_t* h_frames = nullptr;  // pinned staging
-  float* h_masks = nullptr;
-  float* d_fmasks = nullptr;  // VSS_OUT_FRAME: masks at frame resolution (allocated on first use)
-  float* h_fmasks = nullptr;
-  size_t fmask_cap = 0;       // floats
-  const float* out_src = nullptr;  // what the last staged call left for the host copy
-  size_t out_bytes = 0;
+  size_t frame_cap = 0;        // staging bytes per slot
+  std::vector<Slot> slots;
+  int last_slot = -1;          // slot of the latest forward (vss_read_layer)
 #ifdef VSS_TRACE
-  std::vector<unsigned long long*> trace;  // per layer, [grid][4] stamps
+  std::vector<unsigned long long*> trace;  // per layer, [grid][16] stamps
   std::vector<int> trace_wgs;              // workgroups of the layer's last launch
 #endif
   uint8_t* d_comp = nullptr;      // vss_segment_composite output, allocated on first use
   float* d_post_alpha = nullptr;  // vss_segment_post outputs [max_batch][P]
   uint8_t* d_post_u8 = nullptr;
-  std::atomic<int> busy{0};
   int use_graph = 1;
   int profile = 0;
-  static constexpr int kMaxBranches = 8;
-  int branches = 1;  // parallel sub-batch chains inside the captured graph
+  int fuse_stem = 1;              // env VSS_FUSE_STEM=0: launch the stem on its own
+  int keep_stem = 0;              // VSS_OPT_KEEP_STEM: the fused stem also stores its activation
   // expand layers with at most this many output pixels per frame split their
   // hidden channels over ks_max() workgroups (env VSS_KSPLIT_PIXELS overrides)
   long ksplit_pixels = kDefaultKsplitPixels;
-  hipStream_t branch_streams[kMaxBranches] = {};
-  hipEvent_t fork_ev = nullptr, join_ev[kMaxBranches] = {};
-  std::map<GraphKey, hipGraphExec_t> graphs;
   // profiling: ring of event pairs per layer
-  static constexpr int kSlots = 32;
-  std::vector<hipEvent_t> ev;  // [slot][layer][2]
-  std::vector<int> slot_pending;
+  static constexpr int kProfRing = 32;
+  std::vector<hipEvent_t> ev;  // [ring][layer][2]
+  std::vector<int> ring_pending;
   int prof_next = 0;
   std::vector<double> prof_sum;
   int prof_count = 0;
-  double fwd_prof_sum = 0.0;
-  int fwd_prof_count = 0;
   int last_n = 0;
-  // persistent forward (k_forward): the whole network in one launch
-  int want_forward = 0;          // env VSS_FORWARD=1 at create: plan for the persistent forward
-  bool fwd_ok = false;           // every layer of the plan has a k_forward case
-  int use_forward = 0;           // VSS_OPT_FORWARD
-  FwdLayer* d_fwd_layers = nullptr;
-  unsigned* d_fwd_ctl = nullptr;   // kFwdCtlWords (FwdParams::ctl)
-  unsigned* d_fwd_done = nullptr;  // [n_layers][max_batch]
-  int fwd_lds_floats = 0;
-  int fwd_grid = 0;
-  int fwd_order = 0;             // 0 layer-major, 1 diagonal (env VSS_FWD_ORDER=diag)
-  int fuse_stem = 1;             // env VSS_FUSE_STEM=0: launch the stem on its own
-  int keep_stem = 0;             // VSS_OPT_KEEP_STEM: the fused stem also stores its activation
-  std::map<int, std::pair<FwdTask*, int>> fwd_tasks;  // per batch size n
-  unsigned* fwd_dbg = nullptr;   // env VSS_FWD_DEBUG: host-mapped per-workgroup state
-  unsigned long long* fwd_trace = nullptr;  // env VSS_FWD_TRACE: per-task stamps of the last launch
-  size_t fwd_trace_cap = 0;                 // tasks
-  int fwd_trace_n = 0;                      // tasks of the last traced launch
+  // ---- the handle (engine 0 only) ----
+  std::vector<vss_handle*> peers;  // engines 1..R-1 (device_ids[1..])
+  int user_max_batch = 0;          // the handle's max_batch (all GPUs)
+  bool rccl = false;               // host calls all-gather over RCCL (device_ids given)
+  int nranks = 1, rank = 0;        // vss_comm_init_rank clique (one GPU per process)
+  bool clique = false;
+  std::mutex mu;                   // serialises submissions (slot choice, staging, enqueue)
+  std::mutex post_mu;              // the synchronous post / composite calls share scratch
+  vss_ticket next_ticket = 0;
+  static constexpr int kTicketRing = 64;
+  int ticket_slot[kTicketRing] = {};  // slot of each of the latest tickets
+  CopyPool* pool = nullptr;
 };
 
 namespace {
@@ -164,6 +258,13 @@ int fail(vss_handle* h, int code, const std::string& msg) {
                   std::string(#expr) + ": " + hipGetErrorString(e_));                     \
   } while (0)
 
+#define NCCL_TRY(h, expr)                                                                 \
+  do {                                                                                    \
+    ncclResult_t r_ = (expr);                                                             \
+    if (r_ != ncclSuccess)                                                                \
+      return fail((h), VSS_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));   \
+  } while (0)
+
 template <class T>
 int dalloc(vss_handle* h, T** p, size_t bytes) {
   void* q = nullptr;
@@ -172,6 +273,17 @@ int dalloc(vss_handle* h, T** p, size_t bytes) {
   if (e != hipSuccess) return fail(h, VSS_E_OOM, "hipMalloc(" + std::to_string(bytes) + ") failed");
   h->dev_allocs.push_back(q);
   h->dev_bytes += bytes;
+  *p = static_cast<T*>(q);
+  return VSS_OK;
+}
+
+template <class T>
+int halloc(vss_handle* h, T** p, size_t bytes) {
+  void* q = nullptr;
+  bytes = std::max<size_t>(bytes, 16);
+  if (hipHostMalloc(&q, bytes, hipHostMallocDefault) != hipSuccess)
+    return fail(h, VSS_E_OOM, "hipHostMalloc(" + std::to_string(bytes) + ") failed");
+  h->host_allocs.push_back(q);
   *p = static_cast<T*>(q);
   return VSS_OK;
 }
@@ -212,7 +324,7 @@ void set_tile(LayerPlan& l, const BlockEntry* e) {
 // Tile choice among the compiled shapes for this layer (csrc/vss_registry.inc):
 // the largest tile that still gives >= 2 workgroups per CU (256 CUs) at
 // max_batch, preferring <= 64 KiB of LDS; otherwise the most workgroups.
-int choose_tile(vss_handle* h, LayerPlan& l, int N, bool mk_only) {
+int choose_tile(vss_handle* h, LayerPlan& l, int N) {
   int count = 0;
   const BlockEntry* reg = block_registry(&count);
   const int cskip = l.mode == MODE_DEC ? (int)l.rec.chid : 0;
@@ -221,7 +333,7 @@ int choose_tile(vss_handle* h, LayerPlan& l, int N, bool mk_only) {
   for (int i = 0; i < count; ++i) {
     const BlockEntry& e = reg[i];
     if (e.mode != l.mode || e.stride != l.stride || e.cin != (int)l.rec.cin || e.cskip != cskip ||
-        e.chid != l.chid / l.ks || e.cout != l.C || e.flags != l.flags || (mk_only && e.mk < 0))
+        e.chid != l.chid / l.ks || e.cout != l.C || e.flags != l.flags)
       continue;
     const long blocks = (long)((l.H + e.TH - 1) / e.TH) * ((l.W + e.TW - 1) / e.TW) * N;
     const size_t lds = block_lds_bytes(l, e.TH, e.TW);
@@ -279,7 +391,7 @@ size_t weight_image_bytes(const LayerPlan& l) {
   return (size_t)(B.wimg_end - B.w1) * 4;
 }
 
-int plan_once(vss_handle* h, bool mk_only) {
+int plan(vss_handle* h) {
   const int Hm = h->cfg.model_h, Wm = h->cfg.model_w, N = h->cfg.max_batch;
   const int nl = (int)h->recs.size();
   h->L.assign(nl, LayerPlan{});
@@ -319,7 +431,10 @@ int plan_once(vss_handle* h, bool mk_only) {
       const LayerPlan& k = h->L[r.skip];
       if (r.skip >= (uint32_t)i) return bad("skip must precede layer");
       if ((int)r.cin != s.C || (int)r.chid != k.C) return bad("dec channels");
-      if (2 * s.H != k.H || 2 * s.W != k.W) return bad("dec src must be half the skip res");
+      // the decoder's 2x upsample taps (block_body's tap records) are exact for
+      // skip == 2 x src only (model_h / model_w multiples of 16 give that for
+      // the spec's four stride-2 levels); anything else is refused here
+      if (2 * s.H != k.H || 2 * s.W != k.W) return bad("dec skip must be exactly 2x its src");
       l.inH = s.H; l.inW = s.W;
       l.H = k.H; l.W = k.W;
       l.mode = MODE_DEC;
@@ -346,14 +461,14 @@ int plan_once(vss_handle* h, bool mk_only) {
     if (r.kind == K_DEC) l.sp = h->L[r.skip].ks;
     if (r.kind == K_IR) l.flags = block_flags(0, (r.flags & F_RESIDUAL) != 0, l.xp, 1, l.ks);
     // the stem fused into its only consumer, a stride-1 direct block (STEM_IN)
-    if (r.kind == K_IR && !mk_only && h->fuse_stem && l.mode == MODE_IR_DIRECT && l.stride == 1 &&
+    if (r.kind == K_IR && h->fuse_stem && l.mode == MODE_IR_DIRECT && l.stride == 1 &&
         h->L[r.src].rec.kind == K_STEM && consumers[r.src] == 1 && r.cin == 16) {
       l.flags |= block_flags(0, 0, 1, 1, 1, 1);
       h->L[r.src].fused = true;
     }
     if (r.kind == K_DEC) l.flags = block_flags(h->L[r.src].rec.kind == K_DEC, 0, l.xp, l.sp, 1);
     if (l.mode >= 0) {
-      int rc = choose_tile(h, l, N, mk_only);
+      int rc = choose_tile(h, l, N);
       if (rc) return rc;
     }
   }
@@ -361,20 +476,7 @@ int plan_once(vss_handle* h, bool mk_only) {
   return VSS_OK;
 }
 
-// Plan for the persistent forward when every layer has a k_forward case
-// (csrc/vss_mk.inc), else for per-layer launches.
-int plan(vss_handle* h) {
-  h->fwd_ok = h->want_forward != 0;
-  int rc = plan_once(h, h->fwd_ok);
-  if (rc == VSS_E_UNSUPPORTED && h->fwd_ok) {
-    h->fwd_ok = false;
-    rc = plan_once(h, false);
-  }
-  return rc;
-}
-
 int upload(vss_handle* h) {
-  const int N = h->cfg.max_batch;
   float* d_data = nullptr;
   int rc = dalloc(h, &d_data, h->hdata.size() * 4);
   if (rc) return rc;
@@ -430,32 +532,17 @@ int upload(vss_handle* h) {
   }
   float* d_img = nullptr;
   if ((rc = dalloc(h, &d_img, img.size() * 4))) return rc;
-  int acc_total = 0;
-  for (const LayerPlan& l : h->L)
-    if (l.rec.kind == K_DEC) acc_total += kAccSlots * 2 * l.C;
-  if ((rc = dalloc(h, &h->d_acc, (size_t)N * std::max(acc_total, 2) * 8))) return rc;
-  HIP_TRY(h, hipMemset(h->d_acc, 0, (size_t)N * std::max(acc_total, 2) * 8));
   if (!img.empty()) HIP_TRY(h, hipMemcpy(d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+  h->acc_stride = 0;
   for (size_t i = 0; i < h->L.size(); ++i) {
     LayerPlan& l = h->L[i];
     const Rec& r = l.rec;
-    l.part_stride = (size_t)N * l.H * l.W * l.C;
-    if ((rc = dalloc(h, &l.act, l.part_stride * l.ks * 4))) return rc;
-    HIP_TRY(h, hipMemset(l.act, 0, l.part_stride * l.ks * 4));
-#ifdef VSS_TRACE
-    if (h->trace.size() != h->L.size()) {
-      h->trace.assign(h->L.size(), nullptr);
-      h->trace_wgs.assign(h->L.size(), 0);
-    }
-    if ((rc = dalloc(h, &h->trace[i], (size_t)N * l.H * l.W * 16 * 8))) return rc;
-    HIP_TRY(h, hipMemset(h->trace[i], 0, (size_t)N * l.H * l.W * 16 * 8));
-#endif
+    l.part_stride = (size_t)h->cfg.max_batch * l.H * l.W * l.C;
     if (r.kind == K_STEM) {
       l.stem_w = dp(r.off[O_W1]);
       l.stem_b = dp(r.off[O_B1]);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
       l.wimg = d_img + img_off[i];
-      l.wimg_f4 = (int)(img_len[i] / 4);
       l.wimg_stride = (long)img_len[i];
       if (r.kind == K_DEC) {
         l.gamma = dp(r.off[O_GAMMA]);
@@ -468,11 +555,65 @@ int upload(vss_handle* h) {
       l.head_b = h->hdata[r.off[O_B2]];
     }
   }
+#ifdef VSS_TRACE
+  h->trace.assign(h->L.size(), nullptr);
+  h->trace_wgs.assign(h->L.size(), 0);
+  for (size_t i = 0; i < h->L.size(); ++i) {
+    const LayerPlan& l = h->L[i];
+    const size_t bytes = (size_t)h->cfg.max_batch * l.H * l.W * 16 * 8;
+    if ((rc = dalloc(h, &h->trace[i], bytes))) return rc;
+    HIP_TRY(h, hipMemset(h->trace[i], 0, bytes));
+  }
+#endif
   return VSS_OK;
 }
 
-int check_frames(vss_handle* h, int n, int fh, int fw, int fc, size_t rs, size_t fs) {
-  if (n < 1 || n > h->cfg.max_batch) return fail(h, VSS_E_INVALID_ARG, "n must be in [1, max_batch]");
+// A slot's device buffers (activations, norm accumulators, masks), stream and
+// completion event; the host staging comes on its first host call.
+int make_slot(vss_handle* h, Slot& s, int gather_ranks) {
+  const int N = h->cfg.max_batch;
+  const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
+  int rc;
+  s.act.assign(h->L.size(), nullptr);
+  for (size_t i = 0; i < h->L.size(); ++i) {
+    const LayerPlan& l = h->L[i];
+    if (l.rec.kind == K_HEAD) continue;  // the head writes the caller's masks
+    if ((rc = dalloc(h, &s.act[i], l.part_stride * l.ks * 4))) return rc;
+    HIP_TRY(h, hipMemset(s.act[i], 0, l.part_stride * l.ks * 4));
+  }
+  const size_t acc = (size_t)N * std::max(h->acc_stride, 2) * 8;
+  if ((rc = dalloc(h, &s.acc, acc))) return rc;
+  HIP_TRY(h, hipMemset(s.acc, 0, acc));
+  if ((rc = dalloc(h, &s.d_masks, (size_t)N * P * 4))) return rc;
+  if (gather_ranks > 0 && (rc = dalloc(h, &s.d_gather, (size_t)gather_ranks * N * P * 4))) return rc;
+  HIP_TRY(h, hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  HIP_TRY(h, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  return VSS_OK;
+}
+
+int ensure_staging(vss_handle* h, Slot& s) {
+  if (s.h_frames) return VSS_OK;
+  const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
+  int rc;
+  if ((rc = dalloc(h, &s.d_frames, h->frame_cap))) return rc;
+  if ((rc = halloc(h, &s.h_frames, h->frame_cap))) return rc;
+  // engine 0 receives the whole batch's masks (gathered from every GPU)
+  const size_t nm = (size_t)std::max(h->cfg.max_batch, h->user_max_batch);
+  if ((rc = halloc(h, &s.h_masks, nm * P * 4))) return rc;
+  return VSS_OK;
+}
+
+int ensure_frame_masks(vss_handle* h, Slot& s) {
+  if (s.h_fmasks) return VSS_OK;
+  const size_t cap = (size_t)std::max(h->cfg.max_batch, h->user_max_batch) * h->cfg.max_frame_h * h->cfg.max_frame_w;
+  int rc;
+  if ((rc = dalloc(h, &s.d_fmasks, cap * 4))) return rc;
+  if ((rc = halloc(h, &s.h_fmasks, cap * 4))) return rc;
+  return VSS_OK;
+}
+
+int check_frames(vss_handle* h, int n, int fh, int fw, int fc, size_t rs, size_t fs, int max_n) {
+  if (n < 1 || n > max_n) return fail(h, VSS_E_INVALID_ARG, "n must be in [1, max_batch]");
   if (fh < 1 || fw < 1) return fail(h, VSS_E_INVALID_ARG, "bad frame size");
   if (fc != 3 && fc != 4) return fail(h, VSS_E_INVALID_ARG, "channels must be 3 or 4");
   if (rs < (size_t)fw * fc) return fail(h, VSS_E_INVALID_ARG, "row_stride < width*channels");
@@ -480,36 +621,35 @@ int check_frames(vss_handle* h, int n, int fh, int fw, int fc, size_t rs, size_t
   return VSS_OK;
 }
 
-size_t frame_elems(const LayerPlan& l) { return (size_t)l.H * l.W * l.C; }
-
-// The stem's parameters for this call's frames (frames point at frame f0).
-StemParams stem_params(const vss_handle* h, const LayerPlan& l, const uint8_t* frames, size_t rs, size_t fs, int fh,
-                       int fw, int fc, int f0) {
+// The stem's parameters for this call's frames (frames point at frame 0 of the call).
+StemParams stem_params(const vss_handle* h, const Slot& s, int li, const uint8_t* frames, size_t rs, size_t fs,
+                       int fh, int fw, int fc) {
+  const LayerPlan& l = h->L[li];
   const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
   StemParams p{};
   p.frames = frames; p.row_stride = (long)rs; p.frame_stride = (long)fs;
   p.fh = fh; p.fw = fw; p.fc = fc; p.Hm = Hm; p.Wm = Wm;
   p.ry = (float)((double)fh / (double)Hm);
   p.rx = (float)((double)fw / (double)Wm);
-  p.w = l.stem_w; p.b = l.stem_b; p.y = l.act + (size_t)f0 * l.H * l.W * l.C;
+  p.w = l.stem_w; p.b = l.stem_b; p.y = s.act[li];
   p.Ho = l.H; p.Wo = l.W; p.cout = l.C;
-  p.acc_zero = h->d_acc + (size_t)f0 * h->acc_stride;
+  p.acc_zero = s.acc;
   p.acc_stride = h->acc_stride;
   return p;
 }
 
-// Kernel parameters of block layer l for frames [f0, f0 + n) of the batch.
-BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n, int f0 = 0) {
+// Kernel parameters of block layer li for the call's n frames.
+BlockParams block_params(const vss_handle* h, const Slot& s, int li, int n) {
+  const LayerPlan& l = h->L[li];
   const Rec& r = l.rec;
   const LayerPlan& src = h->L[r.src];
-  const size_t fa = (size_t)f0 * h->acc_stride;
   BlockParams p{};
   p.wimg = l.wimg;
   p.wimg_stride = l.wimg_stride;
   p.x_part_stride = (long)src.part_stride;
   p.y_part_stride = (long)l.part_stride;
-  p.x = src.act + f0 * frame_elems(src);
-  p.y = l.act + f0 * frame_elems(l);
+  p.x = s.act[r.src];
+  p.y = s.act[li];
   p.eps = h->eps;
   p.N = n; p.H = l.inH; p.W = l.inW; p.Ho = l.H; p.Wo = l.W;
   p.cin = (int)r.cin; p.cout = l.C; p.chid = l.chid; p.stride = l.stride;
@@ -520,14 +660,14 @@ BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n, int f0 
     p.residual = (r.flags & F_RESIDUAL) ? 1 : 0;
   } else {
     const LayerPlan& sk = h->L[r.skip];
-    p.skip = sk.act + f0 * frame_elems(sk);
+    p.skip = s.act[r.skip];
     p.skip_part_stride = (long)sk.part_stride;
     p.cskip = (int)r.chid;
     p.relu6_dw = 0;
-    p.out_acc = h->d_acc + fa + l.acc_off;
+    p.out_acc = s.acc + l.acc_off;
     p.norm_in = src.rec.kind == K_DEC ? 1 : 0;
     if (p.norm_in) {
-      p.in_acc = h->d_acc + fa + src.acc_off;
+      p.in_acc = s.acc + src.acc_off;
       p.in_gamma = src.gamma;
       p.in_beta = src.beta;
       p.in_hw = src.H * src.W;
@@ -536,181 +676,13 @@ BlockParams block_params(const vss_handle* h, const LayerPlan& l, int n, int f0 
   return p;
 }
 
-int n_tasks_per_frame(const LayerPlan& l, int Hm, int Wm) {
-  if (l.rec.kind == K_STEM) return ((l.W + kStemTW - 1) / kStemTW) * ((l.H + kStemTH - 1) / kStemTH);
-  if (l.rec.kind == K_HEAD) return ((Wm + kHeadTW - 1) / kHeadTW) * ((Hm + kHeadTH - 1) / kHeadTH);
-  return l.tiles_x * l.tiles_y * l.ks;
-}
-
-// The persistent forward's layer table (device), counters and launch shape.
-int setup_forward(vss_handle* h) {
-  if (!h->fwd_ok) return VSS_OK;
-  const int Hm = h->cfg.model_h, Wm = h->cfg.model_w, N = h->cfg.max_batch;
-  const int nl = (int)h->L.size();
-  std::vector<FwdLayer> fl(nl);
-  size_t lds = 0;
-  for (int i = 0; i < nl; ++i) {
-    const LayerPlan& l = h->L[i];
-    const Rec& r = l.rec;
-    FwdLayer& f = fl[i];
-    std::memset(&f, 0, sizeof(f));
-    f.dep[0] = f.dep[1] = -1;
-    f.ks = 1;
-    if (r.kind == K_STEM) {
-      f.kind = FWD_STEM;
-      f.tiles_x = (l.W + kStemTW - 1) / kStemTW;
-      f.tiles_y = (l.H + kStemTH - 1) / kStemTH;
-      StemParams& p = f.stem;
-      p.Hm = Hm; p.Wm = Wm;
-      p.w = l.stem_w; p.b = l.stem_b; p.y = l.act;
-      p.Ho = l.H; p.Wo = l.W; p.cout = l.C;
-      p.acc_zero = h->d_acc;
-      p.acc_stride = h->acc_stride;
-      lds = std::max(lds, (size_t)kStemLds * 4);
-    } else if (r.kind == K_IR || r.kind == K_DEC) {
-      f.kind = FWD_BLOCK;
-      f.mk = l.entry->mk;
-      f.tiles_x = l.tiles_x;
-      f.tiles_y = l.tiles_y;
-      f.ks = l.ks;
-      f.block = block_params(h, l, N);
-      f.dep[0] = (int)r.src;
-      if (r.kind == K_DEC) f.dep[1] = (int)r.skip;
-      lds = std::max(lds, l.lds);
-    } else {
-      const LayerPlan& src = h->L[r.src];
-      f.kind = FWD_HEAD;
-      f.tiles_x = (Wm + kHeadTW - 1) / kHeadTW;
-      f.tiles_y = (Hm + kHeadTH - 1) / kHeadTH;
-      HeadParams& p = f.head;
-      p.x = src.act;
-      p.in_acc = h->d_acc + src.acc_off;
-      p.acc_stride = h->acc_stride;
-      p.gamma = src.gamma; p.beta = src.beta; p.eps = h->eps;
-      p.w = l.head_w; p.b = l.head_b;
-      p.N = N; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
-      f.dep[0] = (int)r.src;
-      lds = std::max(lds, (size_t)kHeadLds * 4);
-    }
-    for (int k = 0; k < 2; ++k)
-      if (f.dep[k] >= 0) f.need[k] = n_tasks_per_frame(h->L[f.dep[k]], Hm, Wm);
-  }
-  h->fwd_lds_floats = (int)((lds + 15) / 16 * 4) + 16;  // + the control words
-  int rc = dalloc(h, &h->d_fwd_layers, sizeof(FwdLayer) * nl);
-  if (!rc) rc = dalloc(h, &h->d_fwd_ctl, kFwdCtlWords * sizeof(unsigned));
-  if (!rc) rc = dalloc(h, &h->d_fwd_done, sizeof(unsigned) * nl * N * kFwdLine);
-  if (rc) return rc;
-  HIP_TRY(h, hipMemcpy(h->d_fwd_layers, fl.data(), sizeof(FwdLayer) * nl, hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemset(h->d_fwd_ctl, 0, kFwdCtlWords * sizeof(unsigned)));
-  HIP_TRY(h, hipMemset(h->d_fwd_done, 0, sizeof(unsigned) * nl * N * kFwdLine));
-  const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
-  const FwdFn fn = forward_kernel(prec);
-  const int bytes = h->fwd_lds_floats * 4;
-  HIP_TRY(h, hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  int per_cu = 0;
-  HIP_TRY(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kThreads, bytes));
-  hipDeviceProp_t prop{};
-  HIP_TRY(h, hipGetDeviceProperties(&prop, h->device));
-  if (per_cu < 1) {  // cannot be resident: fall back to layer launches
-    h->fwd_ok = false;
-    return VSS_OK;
-  }
-  h->fwd_grid = per_cu * prop.multiProcessorCount / kFwdQueues * kFwdQueues;
-  if (h->fwd_grid < kFwdQueues) {
-    h->fwd_ok = false;
-    return VSS_OK;
-  }
-  if (const char* ev = std::getenv("VSS_FWD_ORDER")) h->fwd_order = std::strcmp(ev, "diag") == 0 ? 1 : 0;
-  h->use_forward = 1;
-  if (std::getenv("VSS_FWD_DEBUG")) {
-    HIP_TRY(h, hipHostMalloc((void**)&h->fwd_dbg, (size_t)h->fwd_grid * 4 * sizeof(unsigned), hipHostMallocCoherent));
-    std::memset(h->fwd_dbg, 0xFF, (size_t)h->fwd_grid * 4 * sizeof(unsigned));
-  }
-  return VSS_OK;
-}
-
-// Task list of a forward over n frames, in an order where every task's
-// dependencies come earlier (the ticket order is the only scheduling).
-//   layer-major: layer by layer, frame by frame within a layer, tiles in
-//                (slice, row, column) order;
-//   diagonal   : by layer + frame, so frame f runs layer L beside frame f+1's
-//                layer L-1.
-int forward_tasks(vss_handle* h, int n, FwdTask** out, int* count) {
-  auto it = h->fwd_tasks.find(n);
-  if (it == h->fwd_tasks.end()) {
-    const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
-    const int nl = (int)h->L.size();
-    std::vector<FwdTask> t;
-    auto emit = [&](int li, int f) {
-      const int k = n_tasks_per_frame(h->L[li], Hm, Wm);
-      for (int j = 0; j < k; ++j) t.push_back(FwdTask{li, f, j, 0});
-    };
-    const char* only = std::getenv("VSS_FWD_ONLY");  // debug: one layer's tasks, no waits
-    if (only) {
-      for (int f = 0; f < n; ++f) emit(std::atoi(only), f);
-    } else if (h->fwd_order == 1) {
-      for (int d = 0; d < nl + n - 1; ++d)
-        for (int f = std::max(0, d - nl + 1); f <= std::min(n - 1, d); ++f) emit(d - f, f);
-    } else {
-      for (int li = 0; li < nl; ++li)
-        for (int f = 0; f < n; ++f) emit(li, f);
-    }
-    FwdTask* d = nullptr;
-    int rc = dalloc(h, &d, t.size() * sizeof(FwdTask));
-    if (rc) return rc;
-    HIP_TRY(h, hipMemcpy(d, t.data(), t.size() * sizeof(FwdTask), hipMemcpyHostToDevice));
-    it = h->fwd_tasks.emplace(n, std::make_pair(d, (int)t.size())).first;
-  }
-  *out = it->second.first;
-  *count = it->second.second;
-  return VSS_OK;
-}
-
-// Enqueue the whole forward for frames [f0, f0 + n) on stream s (frames and
-// masks point at frame f0; no sync, no alloc: graph-capturable).
-int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs,
-                    size_t fs, float* masks, hipStream_t s, int prof_slot, int f0 = 0) {
+// Enqueue the whole forward of n frames on stream st with slot s's buffers
+// (no sync, no alloc: graph-capturable).
+int enqueue_forward(vss_handle* h, Slot& s, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs,
+                    size_t fs, float* masks, hipStream_t st, int prof_slot) {
   const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
   const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
   const int nl = (int)h->L.size();
-  if (h->use_forward && f0 == 0) {
-    FwdParams fp{};
-    int rc = forward_tasks(h, n, const_cast<FwdTask**>(&fp.tasks), &fp.ntasks);
-    if (rc) return rc;
-    fp.layers = h->d_fwd_layers;
-    fp.max_batch = h->cfg.max_batch;
-    fp.n_layers = nl;
-    fp.ctl = h->d_fwd_ctl;
-    fp.done = h->d_fwd_done;
-    fp.spin_limit = 20000000;  // 200 ms of s_memrealtime (100 MHz)
-    fp.lds_floats = h->fwd_lds_floats;
-    fp.frames = frames; fp.row_stride = (long)rs; fp.frame_stride = (long)fs;
-    fp.fh = fh; fp.fw = fw; fp.fc = fc;
-    fp.ry = (float)((double)fh / (double)Hm);
-    fp.rx = (float)((double)fw / (double)Wm);
-    fp.mask = masks;
-    fp.dbg = h->fwd_dbg;
-    fp.nowait = std::getenv("VSS_FWD_ONLY") ? 1 : 0;
-    if (std::getenv("VSS_FWD_TRACE")) {
-      if ((size_t)fp.ntasks > h->fwd_trace_cap) {
-        if ((rc = dalloc(h, &h->fwd_trace, (size_t)fp.ntasks * 4 * 8))) return rc;
-        h->fwd_trace_cap = (size_t)fp.ntasks;
-      }
-      fp.ttrace = h->fwd_trace;
-      h->fwd_trace_n = fp.ntasks;
-    }
-    // every queue needs a workgroup: round the grid to a multiple of kFwdQueues
-    const dim3 grid(std::min(h->fwd_grid, (fp.ntasks + kFwdQueues - 1) / kFwdQueues * kFwdQueues));
-    const size_t lds = (size_t)h->fwd_lds_floats * 4;
-    if (prof_slot >= 0)
-      hipExtLaunchKernelGGL(forward_kernel(prec), grid, dim3(kThreads), (uint32_t)lds, s,
-                            h->ev[(size_t)prof_slot * nl * 2], h->ev[(size_t)prof_slot * nl * 2 + 1], 0, fp);
-    else
-      hipLaunchKernelGGL(forward_kernel(prec), grid, dim3(kThreads), lds, s, fp);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("k_forward launch: ") + hipGetErrorString(e));
-    return VSS_OK;
-  }
   for (int i = 0; i < nl; ++i) {
     LayerPlan& l = h->L[i];
     const Rec& r = l.rec;
@@ -721,9 +693,9 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
     }
     auto go = [&](auto fn, dim3 grid, size_t lds, auto prm) {
       if (prof_slot >= 0)
-        hipExtLaunchKernelGGL(fn, grid, dim3(kThreads), (uint32_t)lds, s, e0, e1, 0, prm);
+        hipExtLaunchKernelGGL(fn, grid, dim3(kThreads), (uint32_t)lds, st, e0, e1, 0, prm);
       else
-        hipLaunchKernelGGL(fn, grid, dim3(kThreads), lds, s, prm);
+        hipLaunchKernelGGL(fn, grid, dim3(kThreads), lds, st, prm);
     };
     if (l.fused) {  // runs inside its consumer's launch
 #ifdef VSS_TRACE
@@ -732,16 +704,16 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
       continue;
     }
     if (r.kind == K_STEM) {
-      StemParams p = stem_params(h, l, frames, rs, fs, fh, fw, fc, f0);
+      StemParams p = stem_params(h, s, i, frames, rs, fs, fh, fw, fc);
 #ifdef VSS_TRACE
       p.trace = h->trace[i];
-      h->trace_wgs[i] = ((l.W + 31) / 32) * ((l.H + 7) / 8) * n;
+      h->trace_wgs[i] = ((l.W + kStemTW - 1) / kStemTW) * ((l.H + kStemTH - 1) / kStemTH) * n;
 #endif
       go(stem_kernel16(), dim3((l.W + kStemTW - 1) / kStemTW, (l.H + kStemTH - 1) / kStemTH, n), kStemLds * 4, p);
     } else if (r.kind == K_IR || r.kind == K_DEC) {
-      BlockParams p = block_params(h, l, n, f0);
+      BlockParams p = block_params(h, s, i, n);
       if (flags_stem_in(l.flags)) {
-        p.stem = stem_params(h, h->L[r.src], frames, rs, fs, fh, fw, fc, f0);
+        p.stem = stem_params(h, s, (int)r.src, frames, rs, fs, fh, fw, fc);
         if (!h->keep_stem) p.stem.y = nullptr;  // no layer reads it (vss_read_layer(0) only)
       }
 #ifdef VSS_TRACE
@@ -752,15 +724,15 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
     } else if (r.kind == K_HEAD) {
       const LayerPlan& src = h->L[r.src];
       HeadParams p{};
-      p.x = src.act + f0 * frame_elems(src);
-      p.in_acc = h->d_acc + (size_t)f0 * h->acc_stride + src.acc_off;
+      p.x = s.act[r.src];
+      p.in_acc = s.acc + src.acc_off;
       p.acc_stride = h->acc_stride;
       p.gamma = src.gamma; p.beta = src.beta; p.eps = h->eps;
       p.w = l.head_w; p.b = l.head_b; p.mask = masks;
       p.N = n; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
 #ifdef VSS_TRACE
       p.trace = h->trace[i];
-      h->trace_wgs[i] = ((Wm + 63) / 64) * ((Hm + 15) / 16) * n;
+      h->trace_wgs[i] = ((Wm + kHeadTW - 1) / kHeadTW) * ((Hm + kHeadTH - 1) / kHeadTH) * n;
 #endif
       go(head_kernel16(), dim3((Wm + kHeadTW - 1) / kHeadTW, (Hm + kHeadTH - 1) / kHeadTH, n), kHeadLds * 4, p);
     }
@@ -770,17 +742,8 @@ int enqueue_forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw,
   return VSS_OK;
 }
 
-int harvest_slot(vss_handle* h, int slot) {
+int harvest_ring(vss_handle* h, int slot) {
   const int nl = (int)h->L.size();
-  if (h->slot_pending[slot] == 2) {  // one k_forward launch
-    float ms = 0.f;
-    HIP_TRY(h, hipEventSynchronize(h->ev[(size_t)slot * nl * 2 + 1]));
-    HIP_TRY(h, hipEventElapsedTime(&ms, h->ev[(size_t)slot * nl * 2], h->ev[(size_t)slot * nl * 2 + 1]));
-    h->fwd_prof_sum += ms;
-    h->fwd_prof_count++;
-    h->slot_pending[slot] = 0;
-    return VSS_OK;
-  }
   for (int i = 0; i < nl; ++i) {
     float ms = 0.f;
     if (h->L[i].fused) continue;  // timed inside its consumer's launch
@@ -789,57 +752,44 @@ int harvest_slot(vss_handle* h, int slot) {
     h->prof_sum[i] += ms;
   }
   h->prof_count++;
-  h->slot_pending[slot] = 0;
+  h->ring_pending[slot] = 0;
   return VSS_OK;
 }
 
-int forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, size_t fs,
-            float* masks, hipStream_t s) {
+bool has_fused_stem(const vss_handle* h) {
+  for (const LayerPlan& l : h->L)
+    if (flags_stem_in(l.flags)) return true;
+  return false;
+}
+
+// The forward of n frames with slot `si`'s buffers, on stream st: a captured
+// hipGraph per (slot, frames, masks, shape) replayed, or eager launches.
+int forward(vss_handle* h, int si, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, size_t fs,
+            float* masks, hipStream_t st) {
+  Slot& s = h->slots[si];
   h->last_n = n;
+  h->last_slot = si;
+  s.stem_stored = !has_fused_stem(h) || h->keep_stem;
   if (h->profile) {
-    const int slot = h->prof_next;
-    h->prof_next = (h->prof_next + 1) % vss_handle::kSlots;
-    if (h->slot_pending[slot]) {
-      int rc = harvest_slot(h, slot);
+    const int ring = h->prof_next;
+    h->prof_next = (h->prof_next + 1) % vss_handle::kProfRing;
+    if (h->ring_pending[ring]) {
+      int rc = harvest_ring(h, ring);
       if (rc) return rc;
     }
-    int rc = enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, s, slot);
-    if (!rc) h->slot_pending[slot] = h->use_forward ? 2 : 1;
+    int rc = enqueue_forward(h, s, frames, n, fh, fw, fc, rs, fs, masks, st, ring);
+    if (!rc) h->ring_pending[ring] = 1;
     return rc;
   }
-  if (!h->use_graph) return enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, s, -1);
+  if (!h->use_graph) return enqueue_forward(h, s, frames, n, fh, fw, fc, rs, fs, masks, st, -1);
   GraphKey key{frames, masks, n, fh, fw, fc, rs, fs};
-  auto it = h->graphs.find(key);
-  if (it == h->graphs.end()) {
-    if (h->use_forward) {  // the task table is uploaded outside the capture
-      FwdTask* t = nullptr;
-      int cnt = 0;
-      int rc = forward_tasks(h, n, &t, &cnt);
-      if (rc) return rc;
-    }
+  auto it = s.graphs.find(key);
+  if (it == s.graphs.end()) {
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
-    HIP_TRY(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
-    // Independent sub-batches on forked streams: their kernels overlap, which
-    // fills the GPU while each chain waits on memory latency.
-    const int nb = h->use_forward ? 1 : std::max(1, std::min(h->branches, n));
-    int rc = VSS_OK;
-    if (nb == 1) {
-      rc = enqueue_forward(h, frames, n, fh, fw, fc, rs, fs, masks, h->stream, -1);
-    } else {
-      (void)hipEventRecord(h->fork_ev, h->stream);
-      const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
-      for (int b = 0; b < nb && !rc; ++b) {
-        const int f0 = (int)((long)n * b / nb), f1 = (int)((long)n * (b + 1) / nb);
-        hipStream_t bs = h->branch_streams[b];
-        (void)hipStreamWaitEvent(bs, h->fork_ev, 0);
-        rc = enqueue_forward(h, frames + (size_t)f0 * fs, f1 - f0, fh, fw, fc, rs, fs,
-                             masks + (size_t)f0 * Hm * Wm, bs, -1, f0);
-        (void)hipEventRecord(h->join_ev[b], bs);
-        (void)hipStreamWaitEvent(h->stream, h->join_ev[b], 0);
-      }
-    }
-    hipError_t e = hipStreamEndCapture(h->stream, &g);
+    HIP_TRY(h, hipStreamBeginCapture(h->capture_stream, hipStreamCaptureModeRelaxed));
+    int rc = enqueue_forward(h, s, frames, n, fh, fw, fc, rs, fs, masks, h->capture_stream, -1);
+    hipError_t e = hipStreamEndCapture(h->capture_stream, &g);
     if (rc) {
       if (g) (void)hipGraphDestroy(g);
       return rc;
@@ -848,26 +798,22 @@ int forward(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc,
     e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
-    if (h->graphs.size() >= 16) {  // bound the cache
-      (void)hipGraphExecDestroy(h->graphs.begin()->second);
-      h->graphs.erase(h->graphs.begin());
+    if (s.graphs.size() >= 16) {  // bound the cache
+      (void)hipGraphExecDestroy(s.graphs.begin()->second);
+      s.graphs.erase(s.graphs.begin());
     }
-    it = h->graphs.emplace(key, ge).first;
+    it = s.graphs.emplace(key, ge).first;
   }
-  HIP_TRY(h, hipGraphLaunch(it->second, s));
+  HIP_TRY(h, hipGraphLaunch(it->second, st));
   return VSS_OK;
 }
 
-struct Busy {
-  vss_handle* h;
-  bool ok;
-  explicit Busy(vss_handle* hh) : h(hh) {
-    int z = 0;
-    ok = h->busy.compare_exchange_strong(z, 1);
+void drop_graphs(vss_handle* h) {
+  for (Slot& s : h->slots) {
+    for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
+    s.graphs.clear();
   }
-  void release() { if (ok) { h->busy.store(0); ok = false; } }
-  ~Busy() { release(); }
-};
+}
 
 void enqueue_upmask(const vss_handle* h, const float* d_masks, int n, int fh, int fw, float* d_out, hipStream_t s) {
   UpmaskParams p{};
@@ -882,78 +828,219 @@ void enqueue_upmask(const vss_handle* h, const float* d_masks, int n, int fh, in
   launch_upmask(p, n, s);
 }
 
-int stage_in(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, float* masks_out,
-             int out_mode) {
-  if (!frames || !masks_out) return fail(h, VSS_E_INVALID_ARG, "null frames/masks_out");
-  if (out_mode != VSS_OUT_MODEL && out_mode != VSS_OUT_FRAME)
-    return fail(h, VSS_E_INVALID_ARG, "out_mode must be VSS_OUT_MODEL or VSS_OUT_FRAME");
-  int rc = check_frames(h, n, fh, fw, fc, rs, rs * (size_t)fh);
-  if (rc) return rc;
-  const size_t bytes = (size_t)n * fh * rs;
-  if (bytes > h->frame_cap)
-    return fail(h, VSS_E_INVALID_ARG, "frames exceed the handle's staging capacity (max_frame_h/w)");
-  if (out_mode == VSS_OUT_FRAME && !h->d_fmasks) {  // sized for max_batch frames of the largest size
-    const size_t cap = (size_t)h->cfg.max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w;
-    if ((rc = dalloc(h, &h->d_fmasks, cap * 4))) return rc;
-    HIP_TRY(h, hipHostMalloc((void**)&h->h_fmasks, cap * 4, hipHostMallocDefault));
-    h->fmask_cap = cap;
-  }
-  if (out_mode == VSS_OUT_FRAME && (size_t)n * fh * fw > h->fmask_cap)
-    return fail(h, VSS_E_INVALID_ARG, "frame-size masks exceed max_batch * max_frame_h * max_frame_w");
-  // staged in 1 MiB pieces, each piece's DMA queued as soon as it is in the
-  // pinned buffer, so the copy engine runs under the next piece's memcpy
-  // (the staging buffer is free: the previous call on this handle has
-  // finished — Busy — before this one starts)
-  constexpr size_t kStageChunk = size_t(1) << 20;
-  for (size_t off = 0; off < bytes; off += kStageChunk) {
-    const size_t len = std::min(kStageChunk, bytes - off);
-    std::memcpy(h->h_frames + off, frames + off, len);
-    HIP_TRY(h, hipMemcpyAsync(h->d_frames + off, h->h_frames + off, len, hipMemcpyHostToDevice, h->stream));
-  }
-  rc = forward(h, h->d_frames, n, fh, fw, fc, rs, rs * (size_t)fh, h->d_masks, h->stream);
-  if (rc) return rc;
-  if (out_mode == VSS_OUT_FRAME) {
-    enqueue_upmask(h, h->d_masks, n, fh, fw, h->d_fmasks, h->stream);
-    h->out_src = h->h_fmasks;
-    h->out_bytes = (size_t)n * fh * fw * 4;
-    HIP_TRY(h, hipMemcpyAsync(h->h_fmasks, h->d_fmasks, h->out_bytes, hipMemcpyDeviceToHost, h->stream));
-  } else {
-    h->out_src = h->h_masks;
-    h->out_bytes = (size_t)n * h->cfg.model_h * h->cfg.model_w * 4;
-    HIP_TRY(h, hipMemcpyAsync(h->h_masks, h->d_masks, h->out_bytes, hipMemcpyDeviceToHost, h->stream));
+// Every engine of the handle: engine 0 then the peers.
+std::vector<vss_handle*> engines(vss_handle* h) {
+  std::vector<vss_handle*> e{h};
+  e.insert(e.end(), h->peers.begin(), h->peers.end());
+  return e;
+}
+
+// Stream-order a slot's next user after its previous one (device side).
+int claim_slot(vss_handle* e, Slot& s, hipStream_t st) {
+  if (s.used) HIP_TRY(e, hipStreamWaitEvent(st, s.done, 0));
+  return VSS_OK;
+}
+
+int release_slot(vss_handle* e, Slot& s, hipStream_t st) {
+  HIP_TRY(e, hipEventRecord(s.done, st));
+  s.used = true;
+  return VSS_OK;
+}
+
+// Is slot k free on every GPU of the handle (its latest batch done)?
+int slot_free(vss_handle* h, int k, bool* free_) {
+  *free_ = true;
+  for (vss_handle* e : engines(h)) {
+    Slot& s = e->slots[k];
+    if (!s.used) continue;
+    HIP_TRY(e, hipSetDevice(e->device));
+    const hipError_t q = hipEventQuery(s.done);
+    if (q == hipErrorNotReady) {
+      *free_ = false;
+      return VSS_OK;
+    }
+    if (q != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
   }
   return VSS_OK;
 }
 
-struct AsyncCtx {
-  vss_handle* h;
+// The slot for the next ticket: the first free one from its round-robin slot
+// on; if every slot is in flight, VSS_E_BUSY — or, with wait_free, the
+// round-robin slot once it is done.
+int pick_slot(vss_handle* h, bool wait_free, int* out) {
+  const int S = (int)h->slots.size();
+  const int k0 = (int)(h->next_ticket % S);
+  for (int j = 0; j < S; ++j) {
+    bool fr = false;
+    if (int rc = slot_free(h, (k0 + j) % S, &fr)) return rc;
+    if (fr) {
+      *out = (k0 + j) % S;
+      return VSS_OK;
+    }
+  }
+  if (!wait_free) return fail(h, VSS_E_BUSY, "queue full: " + std::to_string(S) + " batches in flight");
+  for (vss_handle* e : engines(h)) {
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipEventSynchronize(e->slots[k0].done));
+  }
+  *out = k0;
+  return VSS_OK;
+}
+
+void note_ticket(vss_handle* h, int k) {
+  const vss_ticket t = h->next_ticket;
+  for (vss_handle* e : engines(h)) e->slots[k].ticket = t;
+  h->ticket_slot[t % vss_handle::kTicketRing] = k;
+  h->next_ticket = t + 1;
+}
+
+struct HostDone {
   float* out;
   const float* src;
   size_t bytes;
   vss_callback cb;
   void* user;
+  Slot* slot;
 };
 
-void async_done(void* p) {
-  AsyncCtx* c = static_cast<AsyncCtx*>(p);
-  std::memcpy(c->out, c->src, c->bytes);
-  c->h->busy.store(0);
+void host_done(void* p) {  // a HIP runtime thread, in stream order
+  HostDone* c = static_cast<HostDone*>(p);
+  if (c->out) std::memcpy(c->out, c->src, c->bytes);
+  c->slot->status = VSS_OK;
   if (c->cb) c->cb(c->user, VSS_OK);
   delete c;
+}
+
+// A queued host call: stage n host frames (each GPU its contiguous shard),
+// then on every GPU's slot stream H2D -> forward -> [RCCL all-gather] and on
+// engine 0's: [frame-size upsample] -> D2H -> the completion (host function,
+// after the previous batch's, so completions keep submission order).
+//   wait_free: block until the slot is free (else VSS_E_BUSY);
+//   sync: wait for the batch and copy the masks here (no host function).
+//   list: frame i at list[i] instead of frames + i * height * row_stride.
+int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list, int n, int fh, int fw, int fc,
+                size_t rs, float* masks_out, int out_mode, bool wait_free, bool sync, vss_callback cb, void* user,
+                vss_ticket* ticket) {
+  if ((!frames && !list) || !masks_out) return fail(h, VSS_E_INVALID_ARG, "null frames/masks_out");
+  if (list)
+    for (int i = 0; i < n; ++i)
+      if (!list[i]) return fail(h, VSS_E_INVALID_ARG, "null frame pointer in the list");
+  if (out_mode != VSS_OUT_MODEL && out_mode != VSS_OUT_FRAME)
+    return fail(h, VSS_E_INVALID_ARG, "out_mode must be VSS_OUT_MODEL or VSS_OUT_FRAME");
+  int rc = check_frames(h, n, fh, fw, fc, rs, rs * (size_t)fh, h->user_max_batch);
+  if (rc) return rc;
+  const std::vector<vss_handle*> E = engines(h);
+  const int R = (int)E.size();
+  const int m = (n + R - 1) / R;  // frames per GPU (the last GPUs may get fewer, or none)
+  const size_t fbytes = (size_t)fh * rs;
+  if ((size_t)m * fbytes > h->frame_cap)
+    return fail(h, VSS_E_INVALID_ARG, "frames exceed the handle's staging capacity (max_frame_h/w)");
+  if (out_mode == VSS_OUT_FRAME && (size_t)n * fh * fw > (size_t)h->user_max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w)
+    return fail(h, VSS_E_INVALID_ARG, "frame-size masks exceed max_batch * max_frame_h * max_frame_w");
+  const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
+  std::lock_guard<std::mutex> lk(h->mu);
+  const vss_ticket t = h->next_ticket;
+  // a free slot: its previous batch is done on every GPU, so its staging may be rewritten
+  int k = 0;
+  if ((rc = pick_slot(h, wait_free, &k))) return rc;
+  for (vss_handle* e : E) {
+    HIP_TRY(e, hipSetDevice(e->device));
+    if ((rc = ensure_staging(e, e->slots[k]))) return fail(h, rc, e->err);
+  }
+  Slot& s0 = h->slots[k];
+  if (out_mode == VSS_OUT_FRAME && (rc = ensure_frame_masks(h, s0))) return rc;
+  // stage every GPU's shard (zero-copy when the caller wrote into this slot's buffer)
+  std::vector<CopyPool::Job> jobs;
+  for (int r = 0; r < R; ++r) {
+    const int f0 = r * m, nr = std::max(0, std::min(n - f0, m));
+    uint8_t* dst = E[r]->slots[k].h_frames;
+    if (list) {
+      for (int i = 0; i < nr; ++i) jobs.push_back({dst + (size_t)i * fbytes, list[f0 + i], fbytes});
+    } else {
+      const uint8_t* src = frames + (size_t)f0 * fbytes;
+      if (nr > 0 && src != dst) jobs.push_back({dst, src, (size_t)nr * fbytes});
+    }
+  }
+  h->pool->run(jobs);
+  for (int r = 0; r < R; ++r) {
+    vss_handle* e = E[r];
+    Slot& s = e->slots[k];
+    const int f0 = r * m, nr = std::max(0, std::min(n - f0, m));
+    HIP_TRY(e, hipSetDevice(e->device));
+    if ((rc = claim_slot(e, s, s.stream))) return fail(h, rc, e->err);
+    if (nr > 0) {
+      HIP_TRY(e, hipMemcpyAsync(s.d_frames, s.h_frames, (size_t)nr * fbytes, hipMemcpyHostToDevice, s.stream));
+      if ((rc = forward(e, k, s.d_frames, nr, fh, fw, fc, rs, fbytes, s.d_masks, s.stream))) return fail(h, rc, e->err);
+    }
+  }
+  const float* res = s0.d_masks;
+  if (h->rccl) {
+    // one all-gather of f32 masks per GPU, m frames each (padding rows of the
+    // last shards are gathered and dropped): [rank][m][P] = frame order
+    NCCL_TRY(h, ncclGroupStart());
+    for (int r = 0; r < R; ++r) {
+      Slot& s = E[r]->slots[k];
+      const ncclResult_t nr_ = ncclAllGather(s.d_masks, s.d_gather, (size_t)m * P, ncclFloat32, s.comm, s.stream);
+      if (nr_ != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return fail(h, VSS_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr_));
+      }
+    }
+    NCCL_TRY(h, ncclGroupEnd());
+    res = s0.d_gather;
+  }
+  HIP_TRY(h, hipSetDevice(h->device));
+  const float* src = s0.h_masks;
+  size_t bytes = (size_t)n * P * 4;
+  if (out_mode == VSS_OUT_FRAME) {
+    enqueue_upmask(h, res, n, fh, fw, s0.d_fmasks, s0.stream);
+    HIP_TRY(h, hipGetLastError());
+    bytes = (size_t)n * fh * fw * 4;
+    HIP_TRY(h, hipMemcpyAsync(s0.h_fmasks, s0.d_fmasks, bytes, hipMemcpyDeviceToHost, s0.stream));
+    src = s0.h_fmasks;
+  } else {
+    HIP_TRY(h, hipMemcpyAsync(s0.h_masks, res, bytes, hipMemcpyDeviceToHost, s0.stream));
+  }
+  if (!sync) {
+    // completions in submission order: after the previous batch's
+    Slot& prev = h->slots[h->ticket_slot[(t + vss_handle::kTicketRing - 1) % vss_handle::kTicketRing]];
+    if (t > 0 && prev.used && &prev != &s0) HIP_TRY(h, hipStreamWaitEvent(s0.stream, prev.done, 0));
+    HostDone* c = new HostDone{masks_out, src, bytes, cb, user, &s0};
+    s0.status = 1;  // pending until the host function runs
+    const hipError_t e = hipLaunchHostFunc(s0.stream, host_done, c);
+    if (e != hipSuccess) {
+      delete c;
+      return fail(h, VSS_E_HIP, std::string("hipLaunchHostFunc: ") + hipGetErrorString(e));
+    }
+  }
+  for (vss_handle* e : E) {
+    HIP_TRY(e, hipSetDevice(e->device));
+    if ((rc = release_slot(e, e->slots[k], e->slots[k].stream))) return fail(h, rc, e->err);
+  }
+  note_ticket(h, k);
+  if (ticket) *ticket = t;
+  if (sync) {
+    HIP_TRY(h, hipSetDevice(h->device));
+    for (vss_handle* e : E) HIP_TRY(e, hipEventSynchronize(e->slots[k].done));
+    std::memcpy(masks_out, src, bytes);
+  }
+  return VSS_OK;
 }
 
 // Autotune: time every compiled tile of every block layer at max_batch on
 // this device and keep the fastest.  The kernels' arithmetic does not depend
 // on the tile (see block_lds), so this changes speed only, never results.
 int autotune(vss_handle* h) {
-  if (h->fwd_ok) return VSS_OK;  // the persistent forward's tiles are fixed (vss_mk.inc)
   const int N = h->cfg.max_batch;
   const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
+  Slot& s = h->slots[0];
+  if (int rc = ensure_staging(h, s)) return rc;  // the stem reads the staging buffer as frames
   hipEvent_t e0 = nullptr, e1 = nullptr;
   HIP_TRY(h, hipEventCreate(&e0));
   HIP_TRY(h, hipEventCreate(&e1));
   int rc = VSS_OK;
-  for (LayerPlan& l : h->L) {
+  for (size_t li = 0; li < h->L.size(); ++li) {
+    LayerPlan& l = h->L[li];
     if (l.mode < 0) continue;
     const std::vector<const BlockEntry*> cands = tile_candidates(l);
     if (cands.size() < 2) continue;
@@ -972,12 +1059,13 @@ int autotune(vss_handle* h) {
           usable[c] = 0;
           continue;
         }
-        BlockParams p = block_params(h, l, N);
-        if (flags_stem_in(l.flags))  // the staging buffer as frames: any bytes, valid memory
-          p.stem = stem_params(h, h->L[l.rec.src], h->d_frames, (size_t)h->cfg.max_frame_w * 3,
+        BlockParams p = block_params(h, s, (int)li, N);
+        if (flags_stem_in(l.flags)) {  // the staging buffer as frames: any bytes, valid memory
+          p.stem = stem_params(h, s, (int)l.rec.src, s.d_frames, (size_t)h->cfg.max_frame_w * 3,
                                (size_t)h->cfg.max_frame_w * 3 * h->cfg.max_frame_h, h->cfg.max_frame_h,
-                               h->cfg.max_frame_w, 3, 0);
-        if (flags_stem_in(l.flags)) p.stem.y = nullptr;  // timed as the forward runs it by default
+                               h->cfg.max_frame_w, 3);
+          p.stem.y = nullptr;  // timed as the forward runs it by default
+        }
         const dim3 grid(l.tiles_x, l.tiles_y, N * l.ks);
         for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(kThreads), l.lds, h->stream, p);
         (void)hipEventRecord(e0, h->stream);
@@ -1010,7 +1098,6 @@ int autotune(vss_handle* h) {
 // Pin layers to given compiled tiles (after the planner and the autotuner):
 // the tile-invariance tests run every compiled tile of every layer this way.
 int force_tiles(vss_handle* h, const char* spec) {
-  if (h->fwd_ok) return VSS_OK;  // the persistent forward's tiles are fixed (vss_mk.inc)
   const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
   const char* s = spec;
   while (*s) {
@@ -1033,6 +1120,83 @@ int force_tiles(vss_handle* h, const char* spec) {
   return VSS_OK;
 }
 
+void destroy_engine(vss_handle* h);
+
+// One engine on one GPU: weights, plan, slots (gather_ranks > 0: each slot
+// holds a gather buffer for that many GPUs' masks).
+int create_engine(const vss_config* cfg, int device, int max_batch, int user_max_batch, int depth, int gather_ranks,
+                  vss_handle** out) {
+  vss_handle* h = new vss_handle();
+  *out = h;
+  h->cfg = *cfg;
+  h->cfg.max_batch = max_batch;
+  h->cfg.device_id = device;
+  h->cfg.device_ids = nullptr;
+  h->weights_path = cfg->weights_path;
+  h->cfg.weights_path = nullptr;
+  h->device = device;
+  h->user_max_batch = user_max_batch;
+  if (hipSetDevice(h->device) != hipSuccess) return fail(h, VSS_E_HIP, "hipSetDevice failed");
+  if (const char* ev = std::getenv("VSS_KSPLIT_PIXELS")) h->ksplit_pixels = std::atol(ev);
+  if (const char* ev = std::getenv("VSS_FUSE_STEM")) h->fuse_stem = std::atoi(ev) != 0;
+  int rc = load_weights(h);
+  if (!rc) rc = plan(h);
+  if (!rc) rc = upload(h);
+  if (rc) return rc;
+  HIP_TRY(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  HIP_TRY(h, hipStreamCreateWithFlags(&h->capture_stream, hipStreamNonBlocking));
+  h->frame_cap = (size_t)max_batch * cfg->max_frame_h * cfg->max_frame_w * 4;
+  h->slots.resize(depth);
+  for (Slot& s : h->slots)
+    if ((rc = make_slot(h, s, gather_ranks))) return rc;
+  const size_t P = (size_t)cfg->model_h * cfg->model_w;
+  if ((rc = dalloc(h, &h->d_post_alpha, (size_t)max_batch * P * 4))) return rc;
+  if ((rc = dalloc(h, &h->d_post_u8, (size_t)max_batch * P))) return rc;
+  for (const LayerPlan& l : h->L)
+    if (l.entry)
+      for (BlockFn fn : l.entry->fn)
+        HIP_TRY(h, hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l.lds));
+  const int nl = (int)h->L.size();
+  h->ev.resize((size_t)vss_handle::kProfRing * nl * 2);
+  for (auto& e : h->ev) HIP_TRY(h, hipEventCreate(&e));
+  h->ring_pending.assign(vss_handle::kProfRing, 0);
+  h->prof_sum.assign(nl, 0.0);
+  if (!(cfg->flags & VSS_CREATE_NO_AUTOTUNE) && (rc = autotune(h))) return rc;
+  if (const char* ev = std::getenv("VSS_TILE"))  // tests / scans: "layer:THxTW[,layer:THxTW...]"
+    if ((rc = force_tiles(h, ev))) return rc;
+  return VSS_OK;
+}
+
+void destroy_engine(vss_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  for (Slot& s : h->slots) {
+    for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
+    if (s.comm) (void)ncclCommDestroy(s.comm);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
+  for (auto e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (void* p : h->dev_allocs) (void)hipFree(p);
+  for (void* p : h->host_allocs) (void)hipHostFree(p);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->capture_stream) (void)hipStreamDestroy(h->capture_stream);
+  delete h->pool;
+  delete h;
+}
+
+int wait_slot(vss_handle* h, int k) {
+  for (vss_handle* e : engines(h)) {
+    Slot& s = e->slots[k];
+    if (!s.used) continue;
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipEventSynchronize(s.done));
+  }
+  return VSS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1051,83 +1215,84 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
   if (cfg->max_batch < 1 || cfg->max_frame_h < 1 || cfg->max_frame_w < 1)
     return fail(nullptr, VSS_E_INVALID_ARG, "max_batch/max_frame_h/max_frame_w must be >= 1");
   if (!cfg->weights_path) return fail(nullptr, VSS_E_INVALID_ARG, "weights_path is required");
+  if (cfg->queue_depth < 0 || cfg->queue_depth > kMaxQueueDepth)
+    return fail(nullptr, VSS_E_INVALID_ARG, "queue_depth must be 0 (default) .. " + std::to_string(kMaxQueueDepth));
+  if (cfg->staging_threads < 0 || cfg->staging_threads > 64)
+    return fail(nullptr, VSS_E_INVALID_ARG, "staging_threads must be 0 (default) .. 64");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(nullptr, VSS_E_HIP, "no HIP device available");
-  if (cfg->device_id < 0 || cfg->device_id >= ndev) return fail(nullptr, VSS_E_INVALID_ARG, "bad device_id");
-  vss_handle* h = new vss_handle();
-  h->cfg = *cfg;
-  h->weights_path = cfg->weights_path;
-  h->cfg.weights_path = nullptr;
-  h->device = cfg->device_id;
-  auto bail = [&](int rc) {
-    g_tls_error = h->err;
-    vss_destroy(h);
+  std::vector<int> devs;
+  if (cfg->device_ids) {
+    if (cfg->n_gpus < 1) return fail(nullptr, VSS_E_INVALID_ARG, "n_gpus must be >= 1 with device_ids");
+    for (int r = 0; r < cfg->n_gpus; ++r) {
+      const int d = cfg->device_ids[r];
+      if (d < 0 || d >= ndev)
+        return fail(nullptr, VSS_E_INVALID_ARG, "device_ids[" + std::to_string(r) + "] = " + std::to_string(d) +
+                                                    " is not a HIP device (0.." + std::to_string(ndev - 1) + ")");
+      if (std::find(devs.begin(), devs.end(), d) != devs.end())
+        return fail(nullptr, VSS_E_INVALID_ARG, "device_ids lists GPU " + std::to_string(d) + " twice");
+      devs.push_back(d);
+    }
+  } else {
+    if (cfg->n_gpus > 1) return fail(nullptr, VSS_E_INVALID_ARG, "n_gpus > 1 needs device_ids");
+    if (cfg->device_id < 0 || cfg->device_id >= ndev) return fail(nullptr, VSS_E_INVALID_ARG, "bad device_id");
+    devs.push_back(cfg->device_id);
+  }
+  const int R = (int)devs.size();
+  if (cfg->max_batch < R) return fail(nullptr, VSS_E_INVALID_ARG, "max_batch must be >= n_gpus");
+  const int depth = cfg->queue_depth ? cfg->queue_depth : kDefaultQueueDepth;
+  const int per = (cfg->max_batch + R - 1) / R;  // frames per GPU
+  const bool rccl = cfg->device_ids != nullptr;
+  vss_handle* h = nullptr;
+  auto bail = [&](vss_handle* bad, int rc) {
+    g_tls_error = bad && !bad->err.empty() ? bad->err : g_tls_error;
+    if (h) {
+      for (vss_handle* p : h->peers) destroy_engine(p);
+      h->peers.clear();
+      if (bad && bad != h) destroy_engine(bad);
+      destroy_engine(h);
+    } else if (bad) {
+      destroy_engine(bad);
+    }
     return rc;
   };
-  if (hipSetDevice(h->device) != hipSuccess) return bail(fail(h, VSS_E_HIP, "hipSetDevice failed"));
-  if (const char* ev = std::getenv("VSS_KSPLIT_PIXELS")) h->ksplit_pixels = std::atol(ev);
-  if (const char* ev = std::getenv("VSS_FORWARD")) h->want_forward = std::atoi(ev) != 0;
-  if (const char* ev = std::getenv("VSS_FUSE_STEM")) h->fuse_stem = std::atoi(ev) != 0;
-  int rc = load_weights(h);
-  if (!rc) rc = plan(h);
-  if (!rc) rc = upload(h);
-  if (rc) return bail(rc);
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
-    return bail(fail(h, VSS_E_HIP, "hipStreamCreate failed"));
-  for (int b = 0; b < vss_handle::kMaxBranches; ++b)
-    if (hipStreamCreateWithFlags(&h->branch_streams[b], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->join_ev[b], hipEventDisableTiming) != hipSuccess)
-      return bail(fail(h, VSS_E_HIP, "branch stream/event create failed"));
-  if (hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming) != hipSuccess)
-    return bail(fail(h, VSS_E_HIP, "hipEventCreate failed"));
-  h->frame_cap = (size_t)cfg->max_batch * cfg->max_frame_h * cfg->max_frame_w * 4;
-  if ((rc = dalloc(h, &h->d_frames, h->frame_cap))) return bail(rc);
-  if ((rc = dalloc(h, &h->d_masks, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w * 4))) return bail(rc);
-  if ((rc = dalloc(h, &h->d_post_alpha, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w * 4))) return bail(rc);
-  if ((rc = dalloc(h, &h->d_post_u8, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w))) return bail(rc);
-  if (hipHostMalloc((void**)&h->h_frames, h->frame_cap, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void**)&h->h_masks, (size_t)cfg->max_batch * cfg->model_h * cfg->model_w * 4,
-                    hipHostMallocDefault) != hipSuccess)
-    return bail(fail(h, VSS_E_OOM, "hipHostMalloc staging failed"));
-  for (const LayerPlan& l : h->L)
-    if (l.entry)
-      for (BlockFn fn : l.entry->fn)
-        if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l.lds) != hipSuccess)
-          return bail(fail(h, VSS_E_HIP, "hipFuncSetAttribute(max dynamic LDS) failed"));
-  const int nl = (int)h->L.size();
-  h->ev.resize((size_t)vss_handle::kSlots * nl * 2);
-  for (auto& e : h->ev)
-    if (hipEventCreate(&e) != hipSuccess) return bail(fail(h, VSS_E_HIP, "hipEventCreate failed"));
-  h->slot_pending.assign(vss_handle::kSlots, 0);
-  h->prof_sum.assign(nl, 0.0);
-  if ((rc = setup_forward(h))) return bail(rc);
-  if (!(cfg->flags & VSS_CREATE_NO_AUTOTUNE) && (rc = autotune(h))) return bail(rc);
-  if (const char* ev = std::getenv("VSS_TILE"))  // tests / scans: "layer:THxTW[,layer:THxTW...]"
-    if ((rc = force_tiles(h, ev))) return bail(rc);
+  int rc = create_engine(cfg, devs[0], per, cfg->max_batch, depth, rccl ? R : 0, &h);
+  if (rc) {
+    vss_handle* bad = h;
+    h = nullptr;
+    return bail(bad, rc);
+  }
+  h->rccl = rccl;
+  for (int r = 1; r < R; ++r) {
+    vss_handle* p = nullptr;
+    rc = create_engine(cfg, devs[r], per, per, depth, R, &p);
+    if (rc) return bail(p, rc);
+    h->peers.push_back(p);
+  }
+  if (rccl) {
+    // one communicator per slot over the handle's GPUs (concurrent slots never share one)
+    for (int k = 0; k < depth; ++k) {
+      std::vector<ncclComm_t> comms(R, nullptr);
+      const ncclResult_t nr = ncclCommInitAll(comms.data(), R, devs.data());
+      if (nr != ncclSuccess)
+        return bail(nullptr, fail(nullptr, VSS_E_RCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(nr)));
+      std::vector<vss_handle*> E = engines(h);
+      for (int r = 0; r < R; ++r) E[r]->slots[k].comm = comms[r];
+    }
+  }
+  const int threads = cfg->staging_threads ? cfg->staging_threads : kDefaultStagingThreads;
+  h->pool = new CopyPool(threads - 1);  // the submitting thread copies too
+  (void)hipSetDevice(h->device);
   *out = h;
   return VSS_OK;
 }
 
 void vss_destroy(vss_handle* h) {
   if (!h) return;
-  (void)hipSetDevice(h->device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
-  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
-  for (auto e : h->ev)
-    if (e) (void)hipEventDestroy(e);
-  for (int b = 0; b < vss_handle::kMaxBranches; ++b) {
-    if (h->branch_streams[b]) (void)hipStreamDestroy(h->branch_streams[b]);
-    if (h->join_ev[b]) (void)hipEventDestroy(h->join_ev[b]);
-  }
-  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
-  for (void* p : h->dev_allocs) (void)hipFree(p);
-  if (h->h_frames) (void)hipHostFree(h->h_frames);
-  if (h->h_masks) (void)hipHostFree(h->h_masks);
-  if (h->h_fmasks) (void)hipHostFree(h->h_fmasks);
-  if (h->fwd_dbg) (void)hipHostFree(h->fwd_dbg);
-  if (h->stream) (void)hipStreamDestroy(h->stream);
-  delete h;
+  for (vss_handle* p : h->peers) destroy_engine(p);
+  h->peers.clear();
+  destroy_engine(h);
 }
 
 int vss_get_info(const vss_handle* h, vss_info* info) {
@@ -1137,37 +1302,90 @@ int vss_get_info(const vss_handle* h, vss_info* info) {
   info->n_layers = (int)h->L.size();
   info->dtype = h->cfg.dtype;
   info->device_bytes = h->dev_bytes;
+  for (const vss_handle* p : h->peers) info->device_bytes += p->dev_bytes;
+  info->n_gpus = 1 + (int)h->peers.size();
+  info->queue_depth = (int)h->slots.size();
+  info->rccl = h->rccl ? 1 : 0;
   return VSS_OK;
 }
 
 int vss_segment(vss_handle* h, const uint8_t* frames, int n, int height, int width, int channels,
                 size_t row_stride, float* masks_out, int out_mode) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
-  Busy b(h);
-  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
-  HIP_TRY(h, hipSetDevice(h->device));
-  int rc = stage_in(h, frames, n, height, width, channels, row_stride, masks_out, out_mode);
-  if (rc) return rc;
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
-  std::memcpy(masks_out, h->out_src, h->out_bytes);
-  return VSS_OK;
+  return submit_host(h, frames, nullptr, n, height, width, channels, row_stride, masks_out, out_mode, true, true,
+                     nullptr, nullptr, nullptr);
 }
 
 int vss_segment_async(vss_handle* h, const uint8_t* frames, int n, int height, int width, int channels,
                       size_t row_stride, float* masks_out, int out_mode, vss_callback cb, void* user) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
-  Busy b(h);
-  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
-  HIP_TRY(h, hipSetDevice(h->device));
-  int rc = stage_in(h, frames, n, height, width, channels, row_stride, masks_out, out_mode);
-  if (rc) return rc;
-  AsyncCtx* c = new AsyncCtx{h, masks_out, h->out_src, h->out_bytes, cb, user};
-  hipError_t e = hipLaunchHostFunc(h->stream, async_done, c);
-  if (e != hipSuccess) {
-    delete c;
-    return fail(h, VSS_E_HIP, std::string("hipLaunchHostFunc: ") + hipGetErrorString(e));
+  return submit_host(h, frames, nullptr, n, height, width, channels, row_stride, masks_out, out_mode, false, false, cb,
+                     user, nullptr);
+}
+
+int vss_submit(vss_handle* h, const uint8_t* frames, int n, int height, int width, int channels, size_t row_stride,
+               float* masks_out, int out_mode, vss_ticket* ticket) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (!ticket) return fail(h, VSS_E_INVALID_ARG, "null ticket");
+  return submit_host(h, frames, nullptr, n, height, width, channels, row_stride, masks_out, out_mode, false, false,
+                     nullptr, nullptr, ticket);
+}
+
+int vss_submit_list(vss_handle* h, const uint8_t* const* frames, int n, int height, int width, int channels,
+                    size_t row_stride, float* masks_out, int out_mode, vss_ticket* ticket) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (!ticket || !frames) return fail(h, VSS_E_INVALID_ARG, "null ticket/frames");
+  return submit_host(h, nullptr, frames, n, height, width, channels, row_stride, masks_out, out_mode, false, false,
+                     nullptr, nullptr, ticket);
+}
+
+int vss_wait(vss_handle* h, vss_ticket ticket) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  int k;
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (ticket >= h->next_ticket) return fail(h, VSS_E_INVALID_ARG, "unknown ticket");
+    if (h->next_ticket - ticket > (vss_ticket)vss_handle::kTicketRing) return VSS_OK;  // long done: its
+    // slot was taken again by a later batch, which is only picked once its slot is free
+    k = h->ticket_slot[ticket % vss_handle::kTicketRing];
+    if (h->slots[k].ticket != ticket) return VSS_OK;  // reused likewise
   }
-  b.ok = false;  // released by async_done
+  int rc = wait_slot(h, k);
+  if (rc) return rc;
+  const int st = h->slots[k].status;
+  return st > 0 ? VSS_OK : st;
+}
+
+int vss_query(vss_handle* h, vss_ticket ticket) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (ticket >= h->next_ticket) return fail(h, VSS_E_INVALID_ARG, "unknown ticket");
+  if (h->next_ticket - ticket > (vss_ticket)vss_handle::kTicketRing) return 1;
+  const int k = h->ticket_slot[ticket % vss_handle::kTicketRing];
+  if (h->slots[k].ticket != ticket) return 1;
+  for (vss_handle* e : engines(h)) {
+    Slot& s = e->slots[k];
+    HIP_TRY(e, hipSetDevice(e->device));
+    const hipError_t q = hipEventQuery(s.done);
+    if (q == hipErrorNotReady) return 0;
+    if (q != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+  }
+  return 1;
+}
+
+int vss_staging_buffer(vss_handle* h, uint8_t** frames, size_t* capacity) {
+  if (!h || !frames) return fail(h, VSS_E_INVALID_ARG, "null handle/frames");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!h->peers.empty())
+    return fail(h, VSS_E_UNSUPPORTED, "zero-copy staging is per GPU: a multi-GPU handle stages its shards itself");
+  // the round-robin slot, once free: the next call picks it (the first free
+  // slot from there on) unless another thread's call comes first
+  const int k = (int)(h->next_ticket % h->slots.size());
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (int rc = ensure_staging(h, h->slots[k])) return rc;
+  if (h->slots[k].used) HIP_TRY(h, hipEventSynchronize(h->slots[k].done));
+  *frames = h->slots[k].h_frames;
+  if (capacity) *capacity = h->frame_cap;
   return VSS_OK;
 }
 
@@ -1175,20 +1393,84 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
                        size_t row_stride, size_t frame_stride, float* d_masks, void* stream) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (!d_frames || !d_masks) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
-  Busy b(h);
-  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
-  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride);
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride, h->cfg.max_batch);
   if (rc) return rc;
+  std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(h, hipSetDevice(h->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
-  return forward(h, d_frames, n, height, width, channels, row_stride, frame_stride, d_masks, s);
+  // round-robin slots, ordered on the device (no host wait): consecutive
+  // calls on different streams run concurrently
+  const int k = (int)(h->next_ticket % h->slots.size());
+  Slot& sl = h->slots[k];
+  if ((rc = claim_slot(h, sl, s))) return rc;
+  if ((rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, d_masks, s))) return rc;
+  if ((rc = release_slot(h, sl, s))) return rc;
+  sl.status = VSS_OK;
+  note_ticket(h, k);
+  return VSS_OK;
+}
+
+int vss_comm_unique_id(vss_handle* h, void* ids, size_t cap, size_t* len) {
+  if (!h || !ids) return fail(h, VSS_E_INVALID_ARG, "null handle/ids");
+  const size_t need = h->slots.size() * sizeof(ncclUniqueId);
+  if (len) *len = need;
+  if (cap < need) return fail(h, VSS_E_INVALID_ARG, "ids buffer needs " + std::to_string(need) + " bytes");
+  for (size_t k = 0; k < h->slots.size(); ++k)
+    NCCL_TRY(h, ncclGetUniqueId(reinterpret_cast<ncclUniqueId*>(static_cast<char*>(ids) + k * sizeof(ncclUniqueId))));
+  return VSS_OK;
+}
+
+int vss_comm_init_rank(vss_handle* h, int nranks, int rank, const void* ids, size_t len) {
+  if (!h || !ids) return fail(h, VSS_E_INVALID_ARG, "null handle/ids");
+  if (!h->peers.empty() || h->rccl)
+    return fail(h, VSS_E_UNSUPPORTED, "a handle over several GPUs has its own communicators");
+  if (h->clique) return fail(h, VSS_E_INVALID_ARG, "the handle already joined a clique");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(h, VSS_E_INVALID_ARG, "bad nranks/rank");
+  if (len != h->slots.size() * sizeof(ncclUniqueId))
+    return fail(h, VSS_E_INVALID_ARG, "ids must be the " + std::to_string(h->slots.size() * sizeof(ncclUniqueId)) +
+                                          " bytes of vss_comm_unique_id (same queue_depth on every rank)");
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipDeviceSynchronize());
+  for (size_t k = 0; k < h->slots.size(); ++k) {
+    ncclUniqueId id;
+    std::memcpy(&id, static_cast<const char*>(ids) + k * sizeof(ncclUniqueId), sizeof(id));
+    NCCL_TRY(h, ncclCommInitRank(&h->slots[k].comm, nranks, id, rank));
+  }
+  h->nranks = nranks;
+  h->rank = rank;
+  h->clique = true;
+  return VSS_OK;
+}
+
+int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width, int channels,
+                              size_t row_stride, size_t frame_stride, float* d_gathered, void* stream) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (!h->clique) return fail(h, VSS_E_INVALID_ARG, "vss_comm_init_rank first");
+  if (!d_frames || !d_gathered) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride, h->cfg.max_batch);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(h, hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  // round-robin, so every rank uses the same slot's communicator for the same call
+  const int k = (int)(h->next_ticket % h->slots.size());
+  Slot& sl = h->slots[k];
+  if ((rc = claim_slot(h, sl, s))) return rc;
+  if ((rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, sl.d_masks, s))) return rc;
+  const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
+  NCCL_TRY(h, ncclAllGather(sl.d_masks, d_gathered, (size_t)n * P, ncclFloat32, sl.comm, s));
+  if ((rc = release_slot(h, sl, s))) return rc;
+  sl.status = VSS_OK;
+  note_ticket(h, k);
+  return VSS_OK;
 }
 
 int vss_mask_to_frame_device(vss_handle* h, const float* d_masks, int n, int frame_h, int frame_w, float* d_out,
                              void* stream) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (!d_masks || !d_out) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
-  if (n < 1 || n > h->cfg.max_batch || frame_h < 1 || frame_w < 1)
+  if (n < 1 || n > h->user_max_batch || frame_h < 1 || frame_w < 1)
     return fail(h, VSS_E_INVALID_ARG, "n must be 1..max_batch and the frame size positive");
   HIP_TRY(h, hipSetDevice(h->device));
   enqueue_upmask(h, d_masks, n, frame_h, frame_w, d_out, stream ? static_cast<hipStream_t>(stream) : h->stream);
@@ -1200,7 +1482,7 @@ int vss_preprocess_device(vss_handle* h, const uint8_t* d_frames, int n, int hei
                           size_t row_stride, size_t frame_stride, float* d_out, void* stream) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (!d_frames || !d_out) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
-  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride);
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride, h->user_max_batch);
   if (rc) return rc;
   HIP_TRY(h, hipSetDevice(h->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
@@ -1219,42 +1501,35 @@ int vss_preprocess_device(vss_handle* h, const uint8_t* d_frames, int n, int hei
 
 int vss_synchronize(vss_handle* h) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  for (vss_handle* e : engines(h)) {
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    for (Slot& s : e->slots) {
+      HIP_TRY(e, hipStreamSynchronize(s.stream));
+      if (s.used) HIP_TRY(e, hipEventSynchronize(s.done));
+    }
+  }
   HIP_TRY(h, hipSetDevice(h->device));
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
   return VSS_OK;
 }
 
 int vss_set_option(vss_handle* h, int option, int value) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
-  if (option == VSS_OPT_FORWARD) {
-    if (value && !h->fwd_ok)
-      return fail(h, VSS_E_UNSUPPORTED, "this plan has no persistent forward (a layer shape outside vss_mk.inc)");
-    if ((value ? 1 : 0) != h->use_forward) {
-      for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
-      h->graphs.clear();
+  if (option == 3 || option == 4 || option == 5)
+    return fail(h, VSS_E_UNSUPPORTED, "option removed (round-1 experiment measured slower; DESIGN.md)");
+  if (option != VSS_OPT_KEEP_STEM && option != VSS_OPT_USE_GRAPH && option != VSS_OPT_PROFILE)
+    return fail(h, VSS_E_INVALID_ARG, "unknown option");
+  std::lock_guard<std::mutex> lk(h->mu);
+  for (vss_handle* e : engines(h)) {
+    if (option == VSS_OPT_KEEP_STEM) {
+      if ((value ? 1 : 0) != e->keep_stem) drop_graphs(e);  // the captured graphs hold the stem pointer
+      e->keep_stem = value ? 1 : 0;
+    } else if (option == VSS_OPT_USE_GRAPH) {
+      e->use_graph = value ? 1 : 0;
+    } else {
+      e->profile = value ? 1 : 0;
     }
-    h->use_forward = value ? 1 : 0;
-    return VSS_OK;
   }
-  if (option == VSS_OPT_KEEP_STEM) {
-    if ((value ? 1 : 0) != h->keep_stem) {  // the captured graphs hold the stem pointer
-      for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
-      h->graphs.clear();
-    }
-    h->keep_stem = value ? 1 : 0;
-    return VSS_OK;
-  }
-  if (option == VSS_OPT_USE_GRAPH) h->use_graph = value ? 1 : 0;
-  else if (option == VSS_OPT_PROFILE) h->profile = value ? 1 : 0;
-  else if (option == VSS_OPT_BRANCHES) {
-    if (value < 1 || value > vss_handle::kMaxBranches) return fail(h, VSS_E_INVALID_ARG, "branches must be 1..8");
-    if (value != h->branches) {
-      for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
-      h->graphs.clear();
-    }
-    h->branches = value;
-  }
-  else return fail(h, VSS_E_INVALID_ARG, "unknown option");
   return VSS_OK;
 }
 
@@ -1264,68 +1539,9 @@ int vss_get_option(vss_handle* h, int option, int* value) {
   switch (option) {
     case VSS_OPT_USE_GRAPH: *value = h->use_graph; return VSS_OK;
     case VSS_OPT_PROFILE: *value = h->profile; return VSS_OK;
-    case VSS_OPT_BRANCHES: *value = h->branches; return VSS_OK;
-    case VSS_OPT_FORWARD: *value = h->use_forward; return VSS_OK;
     case VSS_OPT_KEEP_STEM: *value = h->keep_stem; return VSS_OK;
-    case VSS_OPT_FORWARD_FAULTS: {
-      *value = 0;
-      if (!h->d_fwd_ctl) return VSS_OK;
-      HIP_TRY(h, hipSetDevice(h->device));
-      HIP_TRY(h, hipDeviceSynchronize());
-      unsigned w = 0;
-      unsigned* fw = h->d_fwd_ctl + kFwdQueues * kFwdLine + 1;
-      HIP_TRY(h, hipMemcpy(&w, fw, sizeof(w), hipMemcpyDeviceToHost));
-      HIP_TRY(h, hipMemset(fw, 0, sizeof(unsigned)));
-      *value = (int)w;
-      return VSS_OK;
-    }
     default: return fail(h, VSS_E_INVALID_ARG, "unknown option");
   }
-}
-
-int vss_forward_kernel(const vss_handle* h, char* buf, int cap) {
-  if (!h || !buf || cap < 1) return VSS_E_INVALID_ARG;
-  if (!h->fwd_ok) return VSS_E_UNSUPPORTED;
-  char tmp[96];
-  std::snprintf(tmp, sizeof(tmp), "void vss::k_forward<%d>(vss::FwdParams)",
-                h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2);
-  std::snprintf(buf, (size_t)cap, "%s", tmp);
-  return (int)std::strlen(tmp);
-}
-
-int vss_profile_read_forward(vss_handle* h, double* ms, int* count) {
-  if (!h || !ms) return fail(h, VSS_E_INVALID_ARG, "null handle/ms");
-  HIP_TRY(h, hipSetDevice(h->device));
-  for (int s = 0; s < vss_handle::kSlots; ++s)
-    if (h->slot_pending[s]) {
-      int rc = harvest_slot(h, s);
-      if (rc) return rc;
-    }
-  *ms = h->fwd_prof_count ? h->fwd_prof_sum / h->fwd_prof_count : 0.0;
-  if (count) *count = h->fwd_prof_count;
-  h->fwd_prof_sum = 0.0;
-  h->fwd_prof_count = 0;
-  return VSS_OK;
-}
-
-// Debug (not in vss.h): per-task stamps of the last VSS_FWD_TRACE launch, [n][4]
-// {taken, deps met, body done, workgroup}; returns the task count.
-int vss_fwd_trace_read(vss_handle* h, unsigned long long* out, int cap) {
-  if (!h || !out || !h->fwd_trace) return VSS_E_INVALID_ARG;
-  HIP_TRY(h, hipDeviceSynchronize());
-  const int n = std::min(cap, h->fwd_trace_n);
-  HIP_TRY(h, hipMemcpy(out, h->fwd_trace, (size_t)n * 4 * 8, hipMemcpyDeviceToHost));
-  return n;
-}
-
-// Debug (not in vss.h): the k_forward per-workgroup state words (VSS_FWD_DEBUG),
-// read WITHOUT synchronising, so a stuck launch can be inspected.
-int vss_fwd_debug(const vss_handle* h, unsigned* out, int cap, int* grid) {
-  if (!h || !out || !h->fwd_dbg) return VSS_E_INVALID_ARG;
-  const int n = std::min(cap, h->fwd_grid * 4);
-  for (int i = 0; i < n; ++i) out[i] = __atomic_load_n(h->fwd_dbg + i, __ATOMIC_RELAXED);
-  if (grid) *grid = h->fwd_grid;
-  return n;
 }
 
 int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww) {
@@ -1375,19 +1591,20 @@ int vss_read_layer(vss_handle* h, int layer, int n, float* host_out) {
     return fail(h, VSS_E_INVALID_ARG, "bad layer/n/out");
   const LayerPlan& l = h->L[layer];
   if (l.rec.kind == K_HEAD) return fail(h, VSS_E_INVALID_ARG, "the head's output is the mask buffer");
-  if (l.rec.kind == K_STEM && !h->keep_stem)
-    for (const LayerPlan& c : h->L)
-      if (flags_stem_in(c.flags))
-        return fail(h, VSS_E_INVALID_ARG,
-                    "the stem is fused into layer 1 and not stored: set VSS_OPT_KEEP_STEM before the forward");
+  if (h->last_slot < 0) return fail(h, VSS_E_INVALID_ARG, "no forward has run on this handle");
+  const Slot& s = h->slots[h->last_slot];
+  if (l.rec.kind == K_STEM && !s.stem_stored)
+    return fail(h, VSS_E_INVALID_ARG,
+                "the stem is fused into layer 1 and the latest forward did not store it: set VSS_OPT_KEEP_STEM "
+                "before the forward");
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipDeviceSynchronize());
   const size_t cnt = (size_t)n * l.H * l.W * l.C;
-  HIP_TRY(h, hipMemcpy(host_out, l.act, cnt * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(h, hipMemcpy(host_out, s.act[layer], cnt * 4, hipMemcpyDeviceToHost));
   if (l.ks > 1) {  // a split layer's value = its parts summed in part order, as its consumers do
     std::vector<float> part(cnt);
     for (int q = 1; q < l.ks; ++q) {
-      HIP_TRY(h, hipMemcpy(part.data(), l.act + q * l.part_stride, cnt * 4, hipMemcpyDeviceToHost));
+      HIP_TRY(h, hipMemcpy(part.data(), s.act[layer] + q * l.part_stride, cnt * 4, hipMemcpyDeviceToHost));
       for (size_t k = 0; k < cnt; ++k) host_out[k] += part[k];
     }
   }
@@ -1399,9 +1616,9 @@ int vss_profile_read(vss_handle* h, double* ms_per_layer, int cap, int* count) {
   const int nl = (int)h->L.size();
   if (!ms_per_layer || cap < nl) return fail(h, VSS_E_INVALID_ARG, "cap < n_layers");
   HIP_TRY(h, hipSetDevice(h->device));
-  for (int s = 0; s < vss_handle::kSlots; ++s)
-    if (h->slot_pending[s]) {
-      int rc = harvest_slot(h, s);
+  for (int s = 0; s < vss_handle::kProfRing; ++s)
+    if (h->ring_pending[s]) {
+      int rc = harvest_ring(h, s);
       if (rc) return rc;
     }
   for (int i = 0; i < nl; ++i) ms_per_layer[i] = h->prof_count ? h->prof_sum[i] / h->prof_count : 0.0;
@@ -1524,6 +1741,31 @@ int post_enqueue(vss_post_state* st, const uint8_t* d_frames, int n, int fh, int
   return VSS_OK;
 }
 
+// The seam for the synchronous post / composite host calls on engine 0:
+// stage the frames into the next slot, H2D and forward on the handle's stream
+// (after that slot's previous batch); returns the slot.
+int seam_on_stream(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, int* slot) {
+  if (!frames) return fail(h, VSS_E_INVALID_ARG, "null frames");
+  int rc = check_frames(h, n, fh, fw, fc, rs, rs * (size_t)fh, h->cfg.max_batch);
+  if (rc) return rc;
+  const size_t fbytes = (size_t)fh * rs;
+  if ((size_t)n * fbytes > h->frame_cap)
+    return fail(h, VSS_E_INVALID_ARG, "frames exceed the handle's staging capacity (max_frame_h/w)");
+  HIP_TRY(h, hipSetDevice(h->device));
+  int k = 0;
+  if ((rc = pick_slot(h, true, &k))) return rc;  // free: its staging is rewritten below
+  Slot& s = h->slots[k];
+  if ((rc = ensure_staging(h, s))) return rc;
+  if (frames != s.h_frames) h->pool->run({{s.h_frames, frames, (size_t)n * fbytes}});
+  if ((rc = claim_slot(h, s, h->stream))) return rc;
+  HIP_TRY(h, hipMemcpyAsync(s.d_frames, s.h_frames, (size_t)n * fbytes, hipMemcpyHostToDevice, h->stream));
+  if ((rc = forward(h, k, s.d_frames, n, fh, fw, fc, rs, fbytes, s.d_masks, h->stream))) return rc;
+  s.status = VSS_OK;
+  note_ticket(h, k);
+  *slot = k;
+  return VSS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1548,14 +1790,15 @@ int vss_post_create(vss_handle* h, const vss_post_config* cfg, vss_post_state** 
   if (cfg) st->cfg = *cfg;
   else vss_post_config_default(&st->cfg);
   const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
+  const size_t nb = (size_t)std::max(h->cfg.max_batch, h->user_max_batch);
   auto bail = [&](int rc) {
     vss_post_destroy(st);
     return rc;
   };
   HIP_TRY(h, hipSetDevice(h->device));
   if (hipMalloc(&st->state, P * 4) != hipSuccess || hipMalloc(&st->valid, 16) != hipSuccess ||
-      hipMalloc(&st->ema, P * 4 * h->cfg.max_batch) != hipSuccess || hipMalloc(&st->state2, P * 4) != hipSuccess ||
-      hipMalloc(&st->d_faces, sizeof(FaceFrame) * h->cfg.max_batch) != hipSuccess ||
+      hipMalloc(&st->ema, P * 4 * nb) != hipSuccess || hipMalloc(&st->state2, P * 4) != hipSuccess ||
+      hipMalloc(&st->d_faces, sizeof(FaceFrame) * nb) != hipSuccess ||
       hipMalloc(&st->rtab, (size_t)kRangeTab * 8) != hipSuccess)
     return bail(fail(h, VSS_E_OOM, "post: hipMalloc failed"));
   if (hipMemset(st->valid, 0, 16) != hipSuccess || hipMemset(st->state, 0, P * 4) != hipSuccess)
@@ -1570,7 +1813,7 @@ void vss_post_destroy(vss_post_state* st) {
   if (!st) return;
   if (st->h) {
     (void)hipSetDevice(st->h->device);
-    (void)hipStreamSynchronize(st->h->stream);
+    (void)hipDeviceSynchronize();
   }
   if (st->state) (void)hipFree(st->state);
   if (st->valid) (void)hipFree(st->valid);
@@ -1584,7 +1827,7 @@ void vss_post_destroy(vss_post_state* st) {
 int vss_post_reset(vss_post_state* st) {
   if (!st) return VSS_E_INVALID_ARG;
   HIP_TRY(st->h, hipSetDevice(st->h->device));
-  HIP_TRY(st->h, hipStreamSynchronize(st->h->stream));
+  HIP_TRY(st->h, hipDeviceSynchronize());
   HIP_TRY(st->h, hipMemset(st->valid, 0, sizeof(int)));
   st->faces_n = 0;
   st->faces = nullptr;
@@ -1595,9 +1838,11 @@ static_assert(sizeof(FaceFrame) == sizeof(vss_face_frame), "FaceFrame mirrors vs
 
 int vss_post_set_faces(vss_post_state* st, const vss_face_frame* faces, int n) {
   if (!st) return VSS_E_INVALID_ARG;
-  if (!faces || n < 1 || n > st->h->cfg.max_batch) return post_fail(st, VSS_E_INVALID_ARG, "faces: 1..max_batch frames");
+  if (!faces || n < 1 || n > std::max(st->h->cfg.max_batch, st->h->user_max_batch))
+    return post_fail(st, VSS_E_INVALID_ARG, "faces: 1..max_batch frames");
   HIP_TRY(st->h, hipSetDevice(st->h->device));
   HIP_TRY(st->h, hipMemcpyAsync(st->d_faces, faces, sizeof(FaceFrame) * n, hipMemcpyHostToDevice, st->h->stream));
+  HIP_TRY(st->h, hipStreamSynchronize(st->h->stream));  // consumers may run on any stream
   st->faces = st->d_faces;
   st->faces_n = n;
   return VSS_OK;
@@ -1605,7 +1850,7 @@ int vss_post_set_faces(vss_post_state* st, const vss_face_frame* faces, int n) {
 
 int vss_post_set_faces_device(vss_post_state* st, const vss_face_frame* d_faces, int n) {
   if (!st) return VSS_E_INVALID_ARG;
-  if (!d_faces || n < 1 || n > st->h->cfg.max_batch)
+  if (!d_faces || n < 1 || n > std::max(st->h->cfg.max_batch, st->h->user_max_batch))
     return post_fail(st, VSS_E_INVALID_ARG, "faces: a device array of 1..max_batch frames");
   st->faces = reinterpret_cast<const FaceFrame*>(d_faces);
   st->faces_n = n;
@@ -1616,7 +1861,7 @@ int vss_post_set_config(vss_post_state* st, const vss_post_config* cfg) {
   if (!st || !cfg) return VSS_E_INVALID_ARG;
   if (cfg->sigma_spatial <= 0 || cfg->sigma_range <= 0) return post_fail(st, VSS_E_INVALID_ARG, "sigmas must be > 0");
   HIP_TRY(st->h, hipSetDevice(st->h->device));
-  HIP_TRY(st->h, hipStreamSynchronize(st->h->stream));
+  HIP_TRY(st->h, hipDeviceSynchronize());
   st->cfg = *cfg;
   return post_tables(st);
 }
@@ -1627,7 +1872,8 @@ int vss_postprocess_device(vss_post_state* st, const uint8_t* d_frames, int n, i
   if (!st) return fail(nullptr, VSS_E_INVALID_ARG, "null post state");
   vss_handle* h = st->h;
   if (!d_masks || (!d_frames && st->cfg.use_bilateral)) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
-  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride);
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride,
+                        std::max(h->cfg.max_batch, h->user_max_batch));
   if (rc) return rc;
   HIP_TRY(h, hipSetDevice(h->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
@@ -1639,21 +1885,22 @@ int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, i
                      int channels, size_t row_stride, float* alpha_out, uint8_t* alpha_u8_out) {
   if (!h || !st || st->h != h) return fail(h, VSS_E_INVALID_ARG, "handle / post state mismatch");
   if (!alpha_out && !alpha_u8_out) return fail(h, VSS_E_INVALID_ARG, "no output requested");
-  Busy b(h);
-  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
-  HIP_TRY(h, hipSetDevice(h->device));
-  const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
-  int rc = stage_in(h, frames, n, height, width, channels, row_stride, h->h_masks, VSS_OUT_MODEL);
+  std::lock_guard<std::mutex> pl(h->post_mu);
+  std::lock_guard<std::mutex> lk(h->mu);
+  int k = 0;
+  int rc = seam_on_stream(h, frames, n, height, width, channels, row_stride, &k);
   if (rc) return rc;
-  // outputs: alpha into d_masks' tail is not allowed (masks are the input): use the post scratch
+  Slot& s = h->slots[k];
+  const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
   float* d_alpha = alpha_out ? h->d_post_alpha : nullptr;
   uint8_t* d_u8 = alpha_u8_out ? h->d_post_u8 : nullptr;
-  rc = post_enqueue(st, h->d_frames, n, height, width, channels, row_stride, row_stride * (size_t)height,
-                    h->d_masks, d_alpha, d_u8, h->stream);
+  rc = post_enqueue(st, s.d_frames, n, height, width, channels, row_stride, row_stride * (size_t)height, s.d_masks,
+                    d_alpha, d_u8, h->stream);
   if (rc) return rc;
   if (alpha_out) HIP_TRY(h, hipMemcpyAsync(alpha_out, d_alpha, (size_t)n * P * 4, hipMemcpyDeviceToHost, h->stream));
   if (alpha_u8_out)
     HIP_TRY(h, hipMemcpyAsync(alpha_u8_out, d_u8, (size_t)n * P, hipMemcpyDeviceToHost, h->stream));
+  if ((rc = release_slot(h, s, h->stream))) return rc;
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   return VSS_OK;
 }
@@ -1665,7 +1912,7 @@ int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, i
 // (s_memrealtime ticks, 100 MHz).  Returns the workgroup count.
 extern "C" int vss_trace_read(vss_handle* h, int layer, unsigned long long* out, int cap) {
   if (!h || layer < 0 || layer >= (int)h->L.size() || !out) return VSS_E_INVALID_ARG;
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  HIP_TRY(h, hipDeviceSynchronize());
   const int wgs = std::min(h->trace_wgs[layer], cap);
   HIP_TRY(h, hipMemcpy(out, h->trace[layer], (size_t)wgs * 16 * 8, hipMemcpyDeviceToHost));
   return wgs;
@@ -1704,7 +1951,8 @@ int vss_composite_device(vss_handle* h, const uint8_t* d_frames, int n, int heig
                          size_t out_row_stride, size_t out_frame_stride, void* stream) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (!d_frames || !d_alpha_u8 || !d_out_rgba) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
-  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride);
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride,
+                        std::max(h->cfg.max_batch, h->user_max_batch));
   if (rc) return rc;
   if (out_row_stride < (size_t)width * 4 || out_row_stride % 4 || out_frame_stride < out_row_stride * height ||
       (reinterpret_cast<uintptr_t>(d_out_rgba) & 3))
@@ -1719,28 +1967,38 @@ int vss_segment_composite(vss_handle* h, vss_post_state* st, const uint8_t* fram
                           int channels, size_t row_stride, uint8_t* out_rgba) {
   if (!h || !st || st->h != h) return fail(h, VSS_E_INVALID_ARG, "handle / post state mismatch");
   if (!out_rgba) return fail(h, VSS_E_INVALID_ARG, "null output");
-  Busy b(h);
-  if (!b.ok) return fail(h, VSS_E_BUSY, "a call is already in flight on this handle");
+  std::lock_guard<std::mutex> pl(h->post_mu);
+  std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(h, hipSetDevice(h->device));
+  const size_t cap = (size_t)h->cfg.max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w * 4;
   if (!h->d_comp) {
-    const size_t cap = (size_t)h->cfg.max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w * 4;
     int rc = dalloc(h, &h->d_comp, cap);
     if (rc) return rc;
   }
-  int rc = stage_in(h, frames, n, height, width, channels, row_stride, h->h_masks, VSS_OUT_MODEL);
-  if (rc) return rc;
   const size_t fs = row_stride * (size_t)height, ors = (size_t)width * 4, ofs = ors * height;
-  if ((size_t)n * ofs > (size_t)h->cfg.max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w * 4)
+  if ((size_t)n * ofs > cap)
     return fail(h, VSS_E_INVALID_ARG, "RGBA output exceeds the handle's capacity (max_batch, max_frame_h/w)");
-  rc = post_enqueue(st, h->d_frames, n, height, width, channels, row_stride, fs, h->d_masks, nullptr, h->d_post_u8,
+  int k = 0;
+  int rc = seam_on_stream(h, frames, n, height, width, channels, row_stride, &k);
+  if (rc) return rc;
+  Slot& s = h->slots[k];
+  rc = post_enqueue(st, s.d_frames, n, height, width, channels, row_stride, fs, s.d_masks, nullptr, h->d_post_u8,
                     h->stream);
   if (rc) return rc;
-  rc = composite_enqueue(h, h->d_frames, n, height, width, channels, row_stride, fs, h->d_post_u8, h->d_comp, ors,
+  rc = composite_enqueue(h, s.d_frames, n, height, width, channels, row_stride, fs, h->d_post_u8, h->d_comp, ors,
                          ofs, h->stream);
   if (rc) return rc;
   HIP_TRY(h, hipMemcpyAsync(out_rgba, h->d_comp, (size_t)n * ofs, hipMemcpyDeviceToHost, h->stream));
+  if ((rc = release_slot(h, s, h->stream))) return rc;
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   return VSS_OK;
 }
 
 }  // extern "C"
+
+// Introspection for the registry generator's LDS mirror (tests/test_registry.py):
+// the bytes of LDS block_lds() carves for one k_block shape.
+extern "C" int vss_block_lds_bytes(int mode, int stride, int th, int tw, int cin, int cskip, int chid, int cout,
+                                   int stem_in) {
+  return block_lds(mode, stride, th, tw, cin, cskip, chid, cout, stem_in).total * 4;
+}

@@ -212,9 +212,9 @@ struct BlockParams {
 using BlockFn = void (*)(BlockParams);
 
 // One compiled k_block shape (tools/gen_registry.py -> vss_registry.inc).
-// flags: block_flags().  mk: its case in k_forward's dispatch (vss_mk.inc), -1 = none.
+// flags: block_flags().
 struct BlockEntry {
-  int mode, stride, TH, TW, cin, cskip, chid, cout, flags, mk;
+  int mode, stride, TH, TW, cin, cskip, chid, cout, flags;
   BlockFn fn[2];  // [PREC_F32, PREC_BF16X2]
 };
 const BlockEntry* block_registry(int* count);
@@ -241,56 +241,6 @@ constexpr int kStemTH = 8, kStemTW = 32, kStemIH = 2 * kStemTH + 1, kStemIWP = 2
 constexpr int kStemLds = r4(3 * kStemIH * kStemIWP) + 27 * 16 + 16;
 constexpr int kHeadTH = 16, kHeadTW = 64, kHeadZR = 10, kHeadZC = 34, kHeadZCP = 35;
 constexpr int kHeadLds = kAccSlots * 2 * 16 * 2 + r4(kHeadZR * kHeadZCP) + 3 * 16;
-
-// ---- persistent forward (k_forward): the whole network in ONE launch ------
-// Tasks = (layer, frame, tile) in a host-built topological order; workgroups
-// take them from one ticket counter and, before running one, wait for the
-// per-frame completion counters of the layers it reads.  Activations are
-// handed over write-through (sc1 stores, sc1 loads: Guideline 16 R1), so no
-// fence; one lane per workgroup signals each finished task.
-enum FwdKind : int { FWD_STEM = 1, FWD_BLOCK = 2, FWD_HEAD = 3 };
-
-struct FwdLayer {
-  int kind;              // FwdKind
-  int mk;                // FWD_BLOCK: case in vss_mk.inc
-  int tiles_x, tiles_y, ks;
-  int dep[2];            // layers this one reads (-1 = none): waits for their counters
-  int need[2];           // tasks per frame of dep[k]
-  StemParams stem;
-  BlockParams block;
-  HeadParams head;
-};
-
-struct FwdTask { int layer, frame, tile, pad; };
-
-constexpr int kFwdQueues = 8;   // ticket counters (dequeue throughput: one word serves ~88/us)
-constexpr int kFwdLine = 32;    // words per counter line (128 B)
-constexpr int kFwdCtlWords = (kFwdQueues + 1) * kFwdLine;
-
-struct FwdParams {
-  const FwdLayer* layers;
-  const FwdTask* tasks;
-  int ntasks, max_batch, n_layers;
-  unsigned* ctl;         // kFwdCtlWords: ticket of queue q at [q * kFwdLine], exited workgroups at
-                         // [kFwdQueues * kFwdLine], fault at [kFwdQueues * kFwdLine + 1] (sticky; host clears)
-  unsigned* done;        // [n_layers][max_batch] finished tasks per (layer, frame), one counter per
-                         // 128-B line (kFwdLine words apart): pollers and signals spread over lines
-  long long spin_limit;  // s_memrealtime ticks (100 MHz) a dependency wait may take
-  int lds_floats;        // dynamic LDS of the launch; the last 16 floats are the control words
-  // this call's frames (the stem's StemParams fields) and mask buffer (the head's)
-  const uint8_t* frames;
-  long row_stride, frame_stride;
-  int fh, fw, fc;
-  float ry, rx;
-  float* mask;
-  unsigned long long* ttrace;  // optional (env VSS_FWD_TRACE): per task {taken, deps met, body done, wg}
-                               // s_memrealtime stamps (100 MHz), for tools/fwd_trace.py
-  int nowait;            // debug (env VSS_FWD_ONLY): the task list is one layer, run without waits
-  unsigned* dbg;         // optional (env VSS_FWD_DEBUG): per workgroup {ticket, state, layer, frame},
-                         // host-mapped so a stuck launch can be inspected while it runs
-};
-using FwdFn = void (*)(FwdParams);
-FwdFn forward_kernel(int prec);
 
 // Instance-norm scale/shift of one channel from the exact fixed-point totals.
 __host__ __device__ inline void norm_affine(unsigned long long s_fx, unsigned long long q_fx, int hw, float eps,

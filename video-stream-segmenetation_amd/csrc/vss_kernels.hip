@@ -1029,215 +1029,26 @@ __global__ __launch_bounds__(256) void k_head(HeadParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// Persistent forward: the whole network in one launch (FwdParams, vss_kernels.h).
-// A dependency wait polls ONE word from ONE lane (relaxed agent loads = sc1,
-// with s_sleep) and gives up after spin_limit ticks, setting the sticky fault
-// word (the host reports it; no wave ever spins forever).
-__device__ __forceinline__ void fwd_wait(unsigned* w, unsigned need, unsigned* fault, long long limit) {
-  if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) return;
-  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    // ~0.5 us between polls: hundreds of waiting workgroups polling the same
-    // few counters otherwise load the memory system every task depends on
-    __builtin_amdgcn_s_sleep(16);
-    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) return;
-    if (__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > limit) {
-      __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-  }
-}
-
-// One task of the persistent forward, each shape its own (non-inlined)
-// function so every body keeps the register allocation of its layer launch
-// instead of sharing one allocation with every other shape.  Arguments of a
-// device function live in VGPRs, so the wave-uniform ones are re-established
-// with readfirstlane (buffer descriptors from divergent bases would be
-// waterfalled).
-
-// The layer table and task list never change during a launch: read them
-// through the constant address space (scalar loads into SGPRs, like kernel
-// arguments) and copy the parameters into registers once per task, instead
-// of re-loading them from global memory after every store.
-template <class T>
-using const_as = const __attribute__((address_space(4))) T;
-template <class T>
-__device__ __forceinline__ const_as<T>* as_const(const T* p) {
-  return (const_as<T>*)(unsigned long long)uniform_ptr(p);
-}
-template <class T>
-__device__ __forceinline__ T load_const(const T* p) {  // dword by dword: scalar loads
-  static_assert(sizeof(T) % 4 == 0, "dword-sized parameter blocks");
-  T out;
-  const_as<unsigned>* src = (const_as<unsigned>*)(unsigned long long)uniform_ptr(p);
-  unsigned* dst = reinterpret_cast<unsigned*>(&out);
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = src[i];
-  return out;
-}
-
-template <int M, int S, int TH, int TW, int CI, int CK, int CH, int CO, int FL, int PREC>
-__device__ __noinline__ void fwd_block(const BlockParams* p, int bx, int by, int bz) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const BlockParams pu = load_const(p);
-  block_body<M, S, TH, TW, CI, CK, CH, CO, FL, PREC, true>(pu, __builtin_amdgcn_readfirstlane(bx),
-                                                          __builtin_amdgcn_readfirstlane(by),
-                                                          __builtin_amdgcn_readfirstlane(bz), smem);
-}
-
-__device__ __noinline__ void fwd_stem(const FwdLayer* L, const uint8_t* frames, long rs, long fs, int fh, int fw,
-                                     int fc, float ry, float rx, int bx, int by, int f) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  StemParams sp = load_const(&L->stem);  // + this call's frames
-  sp.frames = static_cast<const uint8_t*>(uniform_ptr(frames));
-  sp.row_stride = (long)uniform_ptr(reinterpret_cast<const void*>(rs));
-  sp.frame_stride = (long)uniform_ptr(reinterpret_cast<const void*>(fs));
-  sp.fh = __builtin_amdgcn_readfirstlane(fh);
-  sp.fw = __builtin_amdgcn_readfirstlane(fw);
-  sp.fc = __builtin_amdgcn_readfirstlane(fc);
-  sp.ry = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ry)));
-  sp.rx = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rx)));
-  stem_body<16, true>(sp, __builtin_amdgcn_readfirstlane(bx), __builtin_amdgcn_readfirstlane(by),
-                      __builtin_amdgcn_readfirstlane(f), smem);
-}
-
-__device__ __noinline__ void fwd_head(const FwdLayer* L, float* mask, int bx, int by, int f) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  HeadParams hp = load_const(&L->head);  // + this call's mask buffer
-  hp.mask = static_cast<float*>(const_cast<void*>(uniform_ptr(mask)));
-  head_body<16, true>(hp, __builtin_amdgcn_readfirstlane(bx), __builtin_amdgcn_readfirstlane(by),
-                      __builtin_amdgcn_readfirstlane(f), smem);
-}
-
-template <int PREC>
-__global__ __launch_bounds__(256, 2) void k_forward(FwdParams fp) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  int* slot = reinterpret_cast<int*>(smem + fp.lds_floats - 16);  // [2]: this / next ticket
-  const int tid = threadIdx.x;
-  // tickets: kFwdQueues counters, each on its own 128-B line; workgroup b
-  // serves queue b % kFwdQueues, which holds the tasks t = k * kFwdQueues + q
-  // in order (the host's order is topological, so every queue is too)
-  const int q = (int)blockIdx.x & (kFwdQueues - 1);
-  unsigned* fault = fp.ctl + kFwdQueues * kFwdLine + 1;
-  unsigned* dbg = fp.dbg ? fp.dbg + blockIdx.x * 4 : nullptr;
-  auto trace = [&](int k, unsigned v) {
-    if (dbg && tid == 0) __hip_atomic_store(dbg + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  };
-  trace(1, 1);
-  const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
-  const int ntasks = fp.ntasks;
-  auto take = [&]() {  // lane 0 only
-    int t = (int)__hip_atomic_fetch_add(fp.ctl + q * kFwdLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) *
-                kFwdQueues + q;
-    // a launch past its deadline stops taking work (and says so): whatever
-    // went wrong, every workgroup drains
-    if (t < ntasks && (long long)__builtin_amdgcn_s_memrealtime() - t_start > 10 * fp.spin_limit) {
-      __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      t = ntasks;
-    }
-    return t < ntasks ? t : ntasks;
-  };
-  if (tid == 0) slot[0] = take();
-  for (int it = 0;; ++it) {
-    __syncthreads();
-    const int t = __builtin_amdgcn_readfirstlane(slot[it & 1]);
-    if (t >= ntasks) break;
-    const_as<FwdTask>& tk = as_const(fp.tasks)[t];
-    const int li = __builtin_amdgcn_readfirstlane(tk.layer);
-    const int f = __builtin_amdgcn_readfirstlane(tk.frame);
-    const int tile = __builtin_amdgcn_readfirstlane(tk.tile);
-    const_as<FwdLayer>& L = as_const(fp.layers)[li];
-    unsigned long long* tt = fp.ttrace ? fp.ttrace + 4L * t : nullptr;
-    if (tt && tid == 0) {
-      tt[0] = __builtin_amdgcn_s_memrealtime();
-      tt[3] = blockIdx.x | ((unsigned long long)li << 16) | ((unsigned long long)f << 24);
-    }
-    trace(0, (unsigned)t);
-    trace(2, (unsigned)li);
-    trace(3, (unsigned)f);
-    trace(1, 2);
-    if (tid == 0) {
-      const int tn = take();  // the next ticket: its round trip overlaps this task's wait and body
-      if (!fp.nowait)
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-          if (L.dep[k] >= 0) fwd_wait(fp.done + (L.dep[k] * fp.max_batch + f) * kFwdLine, (unsigned)L.need[k], fault, fp.spin_limit);
-      slot[(it + 1) & 1] = tn;  // read after the next loop-top barrier
-    }
-    __syncthreads();  // the other waves load only after the polling lane matched
-    if (tt && tid == 0) tt[1] = __builtin_amdgcn_s_memrealtime();
-    trace(1, 3);
-    const int txy = L.tiles_x * L.tiles_y;
-    const int ks = tile / txy, rem = tile - ks * txy;
-    const int by = rem / L.tiles_x, bx = rem - by * L.tiles_x;
-    if (L.kind == FWD_STEM) {
-      fwd_stem(fp.layers + li, fp.frames, fp.row_stride, fp.frame_stride, fp.fh, fp.fw, fp.fc, fp.ry, fp.rx, bx, by, f);
-    } else if (L.kind == FWD_HEAD) {
-      fwd_head(fp.layers + li, fp.mask, bx, by, f);
-    } else {
-      const int bz = f * L.ks + ks;
-      switch (L.mk) {
-#define VSS_MK(ID, M, S, TH, TW, CI, CK, CH, CO, FL)                      \
-  case ID:                                                               \
-    fwd_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC>(&fp.layers[li].block, bx, by, bz); \
-    break;
-#include "vss_mk.inc"
-#undef VSS_MK
-        default:
-          break;
-      }
-    }
-    trace(1, 4);
-    if (tt && tid == 0) tt[2] = __builtin_amdgcn_s_memrealtime();
-    // every storing wave drains its write-through stores (and norm atomics),
-    // then ONE lane signals the task done
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(fp.done + (li * fp.max_batch + f) * kFwdLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    trace(1, 5);
-  }
-  trace(1, 6);
-  // the last workgroup out re-arms the counters for the next launch (stream
-  // order puts it before that launch; the fault word stays for the host)
-  if (tid == 0) {
-    unsigned* exits = fp.ctl + kFwdQueues * kFwdLine;
-    const unsigned e = __hip_atomic_fetch_add(exits, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (e == gridDim.x - 1) {
-      for (int i = 0; i < fp.n_layers * fp.max_batch; ++i)
-        __hip_atomic_store(fp.done + i * kFwdLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int k = 0; k < kFwdQueues; ++k)
-        __hip_atomic_store(fp.ctl + k * kFwdLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Host-visible launch table (used by vss_capi.hip): one entry per compiled
 // block shape, generated from the layer table by tools/gen_registry.py and
 // dealt to kRegistryShards files (vss_registry_<k>.inc) so that the shapes
 // compile in parallel: this file is compiled once per shard with
-// -DVSS_SHARD=<k>; shard 0 also holds k_forward, the stem, head and
-// preprocessing kernels and the concatenated table.
+// -DVSS_SHARD=<k>; shard 0 also holds the stem, head and preprocessing
+// kernels and the concatenated table.
 #ifndef VSS_SHARD
 #define VSS_SHARD 0
 #endif
-#define VSS_BLOCK(M, S, TH, TW, CI, CK, CH, CO, FL, MK)                                \
-  {M, S, TH, TW, CI, CK, CH, CO, FL, MK,                                              \
+#define VSS_BLOCK(M, S, TH, TW, CI, CK, CH, CO, FL)                                    \
+  {M, S, TH, TW, CI, CK, CH, CO, FL,                                                  \
    {k_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC_F32>,                              \
     k_block<M, S, TH, TW, CI, CK, CH, CO, FL, PREC_BF16X2>}},
 #define VSS_STR2(x) #x
 #define VSS_STR(x) VSS_STR2(x)
 #define VSS_CAT2(a, b) a##b
 #define VSS_CAT(a, b) VSS_CAT2(a, b)
-#ifndef VSS_ONLY_FORWARD  // (quick compile of k_forward alone for resource checks)
 static const BlockEntry kShardBlocks[] = {
 #include VSS_STR(VSS_CAT(vss_registry_, VSS_SHARD).inc)
 };
-#else
-static const BlockEntry kShardBlocks[] = {{0}};
-#endif
 #undef VSS_BLOCK
 
 const BlockEntry* VSS_CAT(registry_shard_, VSS_SHARD)(int* count) {
@@ -1269,7 +1080,6 @@ const BlockEntry* block_registry(int* count) {
 void (*stem_kernel16())(StemParams) { return k_stem<16>; }
 void (*head_kernel16())(HeadParams) { return k_head<16>; }
 void (*prep_kernel())(PrepParams) { return k_prep; }
-FwdFn forward_kernel(int prec) { return prec == PREC_F32 ? k_forward<PREC_F32> : k_forward<PREC_BF16X2>; }
 #endif
 
 }  // namespace vss

@@ -5,12 +5,17 @@
 // _OrtCreateSession/_OrtRun/_OrtGetLastError exports behind
 // InferenceSession.run).  Exports:
 //   version() -> number
-//   create(opts) -> handle            (opts: modelH, modelW, dtype, deviceId, maxBatch,
-//                                       maxFrameH, maxFrameW, weightsPath, autotune)
-//   info(handle) -> {maskW, maskH, nLayers, deviceBytes}
-//   segment(handle, frames: Uint8Array|Uint8ClampedArray, n, height, width, channels, rowStride, outMode?)
+//   create(opts) -> handle            (opts: modelH, modelW, dtype, deviceId, deviceIds, maxBatch,
+//                                       maxFrameH, maxFrameW, weightsPath, autotune, queueDepth,
+//                                       stagingThreads)
+//   info(handle) -> {maskW, maskH, nLayers, deviceBytes, nGpus, queueDepth, rccl}
+//   segment(handle, frames: Uint8Array | Uint8Array[], n, height, width, channels, rowStride, outMode?)
 //       -> Promise<Float32Array>      (n * maskH * maskW masks, or n * height * width with
-//                                      outMode 1 = VSS_OUT_FRAME; rejects with Error(vss_last_error))
+//                                      outMode 1 = VSS_OUT_FRAME; rejects with Error(vss_last_error)).
+//       Queued (vss_submit / vss_submit_list on the calling thread, vss_wait on a libuv
+//       worker): returns once the frames are staged, up to queueDepth batches in flight
+//       (beyond that it rejects with code -4 = VSS_E_BUSY; segment.ts keeps within it).
+//       An array of frames is copied frame by frame into the pinned staging (no packing).
 //   destroy(handle)
 //   postCreate(handle, config?) -> post     (config keys as the reference's `config`:
 //                                             EMA, NOISE_CUTOFF, HIGH_THRESHOLD, GAMMA,
@@ -36,7 +41,7 @@
 //       -> Promise<{affine: number[6] | null, box: number[4] | null, videoW, videoH}[]>
 //       (the postSetFaces form, one entry per frame)
 //   faceReset(tracker), faceDestroy(tracker)
-// segment runs vss_segment on a libuv worker thread (napi_create_async_work),
+// segment waits for its batch on a libuv worker thread (napi_create_async_work),
 // so the event loop is not blocked — as `await session.run` does not block.
 #include <node_api.h>
 
@@ -159,6 +164,7 @@ napi_value Create(napi_env env, napi_callback_info info) {
   cfg.model_h = 144; cfg.model_w = 256; cfg.dtype = VSS_DTYPE_BF16X2; cfg.device_id = 0;
   cfg.max_batch = 8; cfg.max_frame_h = 1080; cfg.max_frame_w = 1920;
   std::string weights, dtype;
+  std::vector<int> device_ids;
   int autotune = 1;
   if (argc >= 1) {
     get_int_prop(env, argv[0], "modelH", &cfg.model_h);
@@ -168,7 +174,32 @@ napi_value Create(napi_env env, napi_callback_info info) {
     get_int_prop(env, argv[0], "maxFrameH", &cfg.max_frame_h);
     get_int_prop(env, argv[0], "maxFrameW", &cfg.max_frame_w);
     get_int_prop(env, argv[0], "autotune", &autotune);
+    get_int_prop(env, argv[0], "queueDepth", &cfg.queue_depth);
+    get_int_prop(env, argv[0], "stagingThreads", &cfg.staging_threads);
     get_str_prop(env, argv[0], "weightsPath", &weights);
+    bool has = false;
+    if (napi_has_named_property(env, argv[0], "deviceIds", &has) == napi_ok && has) {
+      napi_value arr;
+      napi_get_named_property(env, argv[0], "deviceIds", &arr);
+      bool is_arr = false;
+      napi_is_array(env, arr, &is_arr);
+      if (is_arr) {
+        uint32_t len = 0;
+        napi_get_array_length(env, arr, &len);
+        for (uint32_t i = 0; i < len; ++i) {
+          napi_value v;
+          int d = -1;
+          napi_get_element(env, arr, i, &v);
+          if (napi_get_value_int32(env, v, &d) != napi_ok) {
+            napi_throw_type_error(env, nullptr, "deviceIds must be an array of GPU ordinals");
+            return nullptr;
+          }
+          device_ids.push_back(d);
+        }
+        cfg.n_gpus = (int)device_ids.size();
+        cfg.device_ids = device_ids.data();
+      }
+    }
     if (get_str_prop(env, argv[0], "dtype", &dtype)) {
       if (dtype == "f32") cfg.dtype = VSS_DTYPE_F32;
       else if (dtype == "bf16x2") cfg.dtype = VSS_DTYPE_BF16X2;
@@ -216,6 +247,12 @@ napi_value Info(napi_env env, napi_callback_info info) {
   napi_set_named_property(env, o, "nLayers", v);
   napi_create_double(env, (double)inf.device_bytes, &v);
   napi_set_named_property(env, o, "deviceBytes", v);
+  napi_create_int32(env, inf.n_gpus, &v);
+  napi_set_named_property(env, o, "nGpus", v);
+  napi_create_int32(env, inf.queue_depth, &v);
+  napi_set_named_property(env, o, "queueDepth", v);
+  napi_get_boolean(env, inf.rccl != 0, &v);
+  napi_set_named_property(env, o, "rccl", v);
   return o;
 }
 
@@ -382,6 +419,147 @@ napi_value PostDestroy(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+// ---- queued segment: submit on the JS thread, wait on a libuv worker -------
+struct QueuedWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  napi_ref out_ref = nullptr;
+  vss_handle* h = nullptr;
+  vss_ticket ticket = 0;
+  size_t out_count = 0;
+  int rc = 0;
+  std::string err;
+};
+
+void QueuedExecute(napi_env, void* data) {  // libuv worker thread: no JS calls here
+  QueuedWork* w = static_cast<QueuedWork*>(data);
+  w->rc = vss_wait(w->h, w->ticket);
+  if (w->rc != VSS_OK) w->err = vss_last_error(w->h);
+}
+
+napi_value make_error(napi_env env, const std::string& what, int rc, const std::string& err) {
+  napi_value msg, code, e;
+  const std::string m = what + " failed (" + std::to_string(rc) + "): " + err;
+  napi_create_string_utf8(env, m.c_str(), m.size(), &msg);
+  napi_create_string_utf8(env, std::to_string(rc).c_str(), NAPI_AUTO_LENGTH, &code);
+  napi_create_error(env, code, msg, &e);
+  return e;
+}
+
+void QueuedComplete(napi_env env, napi_status, void* data) {
+  QueuedWork* w = static_cast<QueuedWork*>(data);
+  if (w->rc == VSS_OK) {
+    napi_value ab = nullptr, arr;
+    napi_get_reference_value(env, w->out_ref, &ab);
+    napi_create_typedarray(env, napi_float32_array, w->out_count, ab, 0, &arr);
+    napi_resolve_deferred(env, w->deferred, arr);
+  } else {
+    napi_reject_deferred(env, w->deferred, make_error(env, "vss_wait", w->rc, w->err));
+  }
+  napi_delete_reference(env, w->out_ref);
+  napi_delete_async_work(env, w->work);
+  delete w;
+}
+
+bool u8_view(napi_env env, napi_value v, const uint8_t** data, size_t* len) {
+  bool is_ta = false;
+  napi_is_typedarray(env, v, &is_ta);
+  if (!is_ta) return false;
+  napi_typedarray_type tt;
+  void* d = nullptr;
+  napi_value buf;
+  size_t off = 0;
+  if (napi_get_typedarray_info(env, v, &tt, len, &d, &buf, &off) != napi_ok) return false;
+  if (tt != napi_uint8_array && tt != napi_uint8_clamped_array) return false;
+  *data = static_cast<const uint8_t*>(d);
+  return true;
+}
+
+// segment(handle, frames | frames[], n, height, width, channels, rowStride, outMode?)
+napi_value Segment(napi_env env, napi_callback_info info) {
+  size_t argc = 8;
+  napi_value argv[8];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  if (argc < 7) {
+    napi_throw_type_error(env, nullptr, "segment(handle, frames, n, height, width, channels, rowStride, outMode?)");
+    return nullptr;
+  }
+  Handle* hd = get_handle(env, argv[0]);
+  if (!hd) return nullptr;
+  int n = 0, height = 0, width = 0, channels = 0, rs = 0, out_mode = VSS_OUT_MODEL;
+  napi_get_value_int32(env, argv[2], &n);
+  napi_get_value_int32(env, argv[3], &height);
+  napi_get_value_int32(env, argv[4], &width);
+  napi_get_value_int32(env, argv[5], &channels);
+  napi_get_value_int32(env, argv[6], &rs);
+  if (argc >= 8) napi_get_value_int32(env, argv[7], &out_mode);
+  if (n < 1 || height < 1 || width < 1 || rs < 1) {
+    napi_throw_range_error(env, nullptr, "segment: n, height, width and rowStride must be >= 1");
+    return nullptr;
+  }
+  const size_t fbytes = (size_t)height * (size_t)rs;
+  bool is_arr = false;
+  napi_is_array(env, argv[1], &is_arr);
+  const uint8_t* contiguous = nullptr;
+  std::vector<const uint8_t*> list;
+  if (is_arr) {
+    uint32_t len = 0;
+    napi_get_array_length(env, argv[1], &len);
+    if (len != (uint32_t)n) {
+      napi_throw_range_error(env, nullptr, "segment: the frame list must hold n frames");
+      return nullptr;
+    }
+    for (uint32_t i = 0; i < len; ++i) {
+      napi_value v;
+      napi_get_element(env, argv[1], i, &v);
+      const uint8_t* d = nullptr;
+      size_t l = 0;
+      if (!u8_view(env, v, &d, &l)) {
+        napi_throw_type_error(env, nullptr, "frames must be Uint8Array or Uint8ClampedArray");
+        return nullptr;
+      }
+      if (l < fbytes) {
+        napi_throw_range_error(env, nullptr, "a frame buffer is smaller than height * rowStride");
+        return nullptr;
+      }
+      list.push_back(d);
+    }
+  } else {
+    size_t l = 0;
+    if (!u8_view(env, argv[1], &contiguous, &l)) {
+      napi_throw_type_error(env, nullptr, "frames must be a Uint8Array or Uint8ClampedArray");
+      return nullptr;
+    }
+    if (l < (size_t)n * fbytes) {
+      napi_throw_range_error(env, nullptr, "frames buffer smaller than n * height * rowStride");
+      return nullptr;
+    }
+  }
+  QueuedWork* w = new QueuedWork();
+  w->h = hd->h;
+  w->out_count = out_mode == VSS_OUT_FRAME ? (size_t)n * height * width : (size_t)n * hd->mask_h * hd->mask_w;
+  napi_value ab, promise;
+  void* out = nullptr;
+  NAPI_OK(env, napi_create_arraybuffer(env, w->out_count * 4, &out, &ab));
+  NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
+  // staged here: the frames may be reused by the caller as soon as this returns
+  const int rc = is_arr ? vss_submit_list(hd->h, list.data(), n, height, width, channels, (size_t)rs,
+                                          static_cast<float*>(out), out_mode, &w->ticket)
+                        : vss_submit(hd->h, contiguous, n, height, width, channels, (size_t)rs,
+                                     static_cast<float*>(out), out_mode, &w->ticket);
+  if (rc != VSS_OK) {
+    napi_reject_deferred(env, w->deferred, make_error(env, "vss_submit", rc, vss_last_error(hd->h)));
+    delete w;
+    return promise;
+  }
+  napi_create_reference(env, ab, 1, &w->out_ref);  // masks_out stays alive until the batch is done
+  napi_value name;
+  napi_create_string_utf8(env, "vss_wait", NAPI_AUTO_LENGTH, &name);
+  NAPI_OK(env, napi_create_async_work(env, nullptr, name, QueuedExecute, QueuedComplete, w, &w->work));
+  NAPI_OK(env, napi_queue_async_work(env, w->work));
+  return promise;
+}
+
 struct SegmentWork {
   napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
@@ -404,11 +582,9 @@ void SegmentExecute(napi_env, void* data) {  // libuv worker thread: no JS calls
   if (w->composite)
     w->rc = vss_segment_composite(w->h, w->post, w->frames, w->n, w->height, w->width, w->channels, w->row_stride,
                                   w->out_u8);
-  else if (w->post)
+  else
     w->rc = vss_segment_post(w->h, w->post, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out,
                              w->out_u8);
-  else
-    w->rc = vss_segment(w->h, w->frames, w->n, w->height, w->width, w->channels, w->row_stride, w->out, w->out_mode);
   if (w->rc != VSS_OK) w->err = vss_last_error(w->h);
 }
 
@@ -437,8 +613,7 @@ void SegmentComplete(napi_env env, napi_status, void* data) {
     }
   } else {
     napi_value msg, code, e;
-    const std::string m = std::string(w->composite ? "vss_segment_composite"
-                                                   : (w->post ? "vss_segment_post" : "vss_segment")) + " failed (" +
+    const std::string m = std::string(w->composite ? "vss_segment_composite" : "vss_segment_post") + " failed (" +
                           std::to_string(w->rc) + "): " + w->err;
     napi_create_string_utf8(env, m.c_str(), m.size(), &msg);
     napi_create_string_utf8(env, std::to_string(w->rc).c_str(), NAPI_AUTO_LENGTH, &code);
@@ -452,7 +627,7 @@ void SegmentComplete(napi_env env, napi_status, void* data) {
   delete w;
 }
 
-// segment(handle, frames, ...) and segmentPost(handle, post, frames, ...)
+// segmentPost(handle, post, frames, ...) and segmentComposite(handle, post, frames, ...)
 napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post, bool composite = false) {
   size_t argc = 9;
   napi_value all[9];
@@ -533,7 +708,6 @@ napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post, bo
   return promise;
 }
 
-napi_value Segment(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, false); }
 napi_value SegmentPost(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, true); }
 napi_value SegmentComposite(napi_env env, napi_callback_info info) { return SegmentImpl(env, info, true, true); }
 
