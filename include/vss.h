@@ -75,12 +75,19 @@ enum { VSS_OUT_MODEL = 0, VSS_OUT_FRAME = 1 };
 enum {
   VSS_OPT_USE_GRAPH = 1, /* 1: replay a captured hipGraph per (slot, shape, buffers) (default 1) */
   VSS_OPT_PROFILE = 2,   /* 1: time every kernel with HIP events (eager launches)         */
-  VSS_OPT_KEEP_STEM = 6  /* 1: the stem fused into layer 1 also stores its activation, so
+  VSS_OPT_KEEP_STEM = 6, /* 1: the stem fused into layer 1 also stores its activation, so
                             vss_read_layer(0) can report it (a debugging aid: 4.7 MB of HBM
                             writes per batch of 8 at 144x256 that no layer reads).  Default 0:
                             the forward writes only what a later layer or the caller reads;
                             vss_read_layer(0) fails with VSS_E_INVALID_ARG unless the latest
                             forward ran with the option set. */
+  VSS_OPT_ROW_FETCH = 7  /* 1 (default): the queued host calls move only the frame rows the
+                            tfjs-legacy resize reads (frameProcessorTest.ts:80) across PCIe —
+                            staged host-side and fetched by a kernel from pinned memory — when
+                            that skips 60 % of the rows or more (four fifths at 720p and 1080p
+                            for 144 model rows; at 640x480 half, where one DMA of the whole
+                            frames is faster); 0: whole frames by DMA.  Masks are identical
+                            either way. */
 };
 
 typedef struct vss_handle vss_handle;

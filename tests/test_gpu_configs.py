@@ -90,3 +90,25 @@ def test_unsupported_model_resolution_refused(pkg, torch_cuda):
     with pytest.raises(pkg.VssError) as e:
         pkg.Session(model_h=144, model_w=250)
     assert e.value.code == pkg.VSS_E_INVALID_ARG
+
+
+@pytest.mark.parametrize("h,w,c", [(480, 640, 3), (1080, 1920, 3), (721, 1283, 4), (300, 200, 3), (144, 256, 3)])
+def test_row_fetch_bitwise(pkg, synthetic, torch_cuda, h, w, c):
+    """VSS_OPT_ROW_FETCH: the queued host path moving only the rows the resize
+    reads (pinned -> HBM by k_fetch_rows) gives bitwise the masks of whole
+    frames by DMA and of the device path — 16-B and byte-granular rows, RGBA,
+    and sizes where no row can be skipped (the DMA path then)."""
+    torch = torch_cuda
+    f = _frames(synthetic, 3, h, w, c, start=900)
+    with pkg.Session(dtype="bf16x2", max_batch=3, max_frame_h=h, max_frame_w=w, queue_depth=2) as s:
+        d = torch.from_numpy(f).cuda()
+        dev = torch.empty((3, 144 * 256), dtype=torch.float32, device="cuda")
+        s.segment_device(d.data_ptr(), 3, h, w, c, w * c, h * w * c, dev.data_ptr(), 0)
+        s.synchronize()
+        ref = dev.cpu().numpy()
+        assert s.get_option(pkg.VSS_OPT_ROW_FETCH) == 1
+        a = s.wait(s.submit(f))[0]
+        b, _, _ = s.segment_frames(f)
+        s.set_option(pkg.VSS_OPT_ROW_FETCH, 0)
+        c_, _, _ = s.segment_frames(f)
+        assert np.array_equal(a, ref) and np.array_equal(b, ref) and np.array_equal(c_, ref)

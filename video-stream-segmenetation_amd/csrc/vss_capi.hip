@@ -79,6 +79,15 @@ struct LayerPlan {
 
 using GraphKey = std::tuple<const void*, const void*, int, int, int, int, size_t, size_t>;
 
+// The rows of an fh-row frame that the tfjs-legacy resize to the model's rows
+// reads (prep_tap's y0 / y1, the same float arithmetic), for the queued host
+// path's row staging (vss_stage.hip).
+struct RowPlan {
+  std::vector<int> rows;                    // sorted, distinct
+  std::vector<std::pair<int, int>> runs;    // [first, last + 1) runs of consecutive rows
+  int* d_rows = nullptr;                    // device copy of rows
+};
+
 // One batch in flight on one GPU: everything a forward writes.
 struct Slot {
   std::vector<float*> act;            // per layer: [ks][max_batch][H][W][C]
@@ -206,6 +215,8 @@ struct vss_handle {
   size_t frame_cap = 0;        // staging bytes per slot
   std::vector<Slot> slots;
   int last_slot = -1;          // slot of the latest forward (vss_read_layer)
+  std::map<int, RowPlan> row_plans;  // by frame height
+  int row_fetch = 1;           // VSS_OPT_ROW_FETCH
 #ifdef VSS_TRACE
   std::vector<unsigned long long*> trace;  // per layer, [grid][16] stamps
   std::vector<int> trace_wgs;              // workgroups of the layer's last launch
@@ -612,6 +623,38 @@ int ensure_frame_masks(vss_handle* h, Slot& s) {
   return VSS_OK;
 }
 
+// prep_tap's rows, computed exactly as the kernel computes them (f32, no contraction).
+#pragma clang fp contract(off)
+int row_plan(vss_handle* h, int fh, const RowPlan** out) {
+  auto it = h->row_plans.find(fh);
+  if (it == h->row_plans.end()) {
+    const int Hm = h->cfg.model_h;
+    const float ry = (float)((double)fh / (double)Hm);
+    std::vector<char> need(fh, 0);
+    for (int y = 0; y < Hm; ++y) {
+      const float fy = (float)y * ry;
+      const int y0 = (int)std::floor(std::max(fy, 0.f));
+      const int y1 = std::min(fh - 1, (int)std::ceil(fy));
+      need[std::min(y0, fh - 1)] = 1;
+      need[y1] = 1;
+    }
+    RowPlan rp;
+    for (int r = 0; r < fh; ++r)
+      if (need[r]) {
+        rp.rows.push_back(r);
+        if (!rp.runs.empty() && rp.runs.back().second == r) rp.runs.back().second = r + 1;
+        else rp.runs.push_back({r, r + 1});
+      }
+    int rc = dalloc(h, &rp.d_rows, rp.rows.size() * sizeof(int));
+    if (rc) return rc;
+    HIP_TRY(h, hipMemcpy(rp.d_rows, rp.rows.data(), rp.rows.size() * sizeof(int), hipMemcpyHostToDevice));
+    it = h->row_plans.emplace(fh, std::move(rp)).first;
+  }
+  *out = &it->second;
+  return VSS_OK;
+}
+#pragma clang fp contract(on)
+
 int check_frames(vss_handle* h, int n, int fh, int fw, int fc, size_t rs, size_t fs, int max_n) {
   if (n < 1 || n > max_n) return fail(h, VSS_E_INVALID_ARG, "n must be in [1, max_batch]");
   if (fh < 1 || fw < 1) return fail(h, VSS_E_INVALID_ARG, "bad frame size");
@@ -949,16 +992,34 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   }
   Slot& s0 = h->slots[k];
   if (out_mode == VSS_OUT_FRAME && (rc = ensure_frame_masks(h, s0))) return rc;
+  // only the rows the resize reads cross PCIe when that skips 60 % of them or
+  // more (measured: 1080p, 20 % of the rows, 8.7k -> 23-29k frames/s; at
+  // 640x480, 50 %, the kernel's reads of pinned memory lost to one DMA of the
+  // whole frames, 38-46k -> 31-39k)
+  std::vector<const RowPlan*> plans(R, nullptr);
+  for (int r = 0; r < R; ++r) {
+    HIP_TRY(E[r], hipSetDevice(E[r]->device));
+    if ((rc = row_plan(E[r], fh, &plans[r]))) return fail(h, rc, E[r]->err);
+    if (!h->row_fetch || plans[r]->rows.size() * 5 > (size_t)fh * 2) plans[r] = nullptr;
+  }
   // stage every GPU's shard (zero-copy when the caller wrote into this slot's buffer)
   std::vector<CopyPool::Job> jobs;
   for (int r = 0; r < R; ++r) {
     const int f0 = r * m, nr = std::max(0, std::min(n - f0, m));
     uint8_t* dst = E[r]->slots[k].h_frames;
-    if (list) {
-      for (int i = 0; i < nr; ++i) jobs.push_back({dst + (size_t)i * fbytes, list[f0 + i], fbytes});
-    } else {
-      const uint8_t* src = frames + (size_t)f0 * fbytes;
-      if (nr > 0 && src != dst) jobs.push_back({dst, src, (size_t)nr * fbytes});
+    for (int i = 0; i < nr; ++i) {
+      const uint8_t* src = list ? list[f0 + i] : frames + (size_t)(f0 + i) * fbytes;
+      uint8_t* d = dst + (size_t)i * fbytes;
+      if (src == d) continue;
+      if (plans[r]) {
+        for (const auto& run : plans[r]->runs)
+          jobs.push_back({d + (size_t)run.first * rs, src + (size_t)run.first * rs, (size_t)(run.second - run.first) * rs});
+      } else if (list) {
+        jobs.push_back({d, src, fbytes});
+      } else {  // contiguous: the shard in one job
+        jobs.push_back({d, src, (size_t)(nr - i) * fbytes});
+        break;
+      }
     }
   }
   h->pool->run(jobs);
@@ -969,7 +1030,20 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
     HIP_TRY(e, hipSetDevice(e->device));
     if ((rc = claim_slot(e, s, s.stream))) return fail(h, rc, e->err);
     if (nr > 0) {
-      HIP_TRY(e, hipMemcpyAsync(s.d_frames, s.h_frames, (size_t)nr * fbytes, hipMemcpyHostToDevice, s.stream));
+      if (plans[r]) {
+        FetchRowsParams fp{};
+        fp.src = s.h_frames;
+        fp.dst = s.d_frames;
+        fp.rows = plans[r]->d_rows;
+        fp.row_stride = (long)rs;
+        fp.frame_stride = (long)fbytes;
+        fp.row_bytes = fw * fc;
+        fp.vec16 = (rs % 16 == 0 && fbytes % 16 == 0 && (fw * fc) % 16 == 0) ? 1 : 0;
+        launch_fetch_rows(fp, (int)plans[r]->rows.size(), nr, s.stream);
+        HIP_TRY(e, hipGetLastError());
+      } else {
+        HIP_TRY(e, hipMemcpyAsync(s.d_frames, s.h_frames, (size_t)nr * fbytes, hipMemcpyHostToDevice, s.stream));
+      }
       if ((rc = forward(e, k, s.d_frames, nr, fh, fw, fc, rs, fbytes, s.d_masks, s.stream))) return fail(h, rc, e->err);
     }
   }
@@ -1517,7 +1591,8 @@ int vss_set_option(vss_handle* h, int option, int value) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (option == 3 || option == 4 || option == 5)
     return fail(h, VSS_E_UNSUPPORTED, "option removed (round-1 experiment measured slower; DESIGN.md)");
-  if (option != VSS_OPT_KEEP_STEM && option != VSS_OPT_USE_GRAPH && option != VSS_OPT_PROFILE)
+  if (option != VSS_OPT_KEEP_STEM && option != VSS_OPT_USE_GRAPH && option != VSS_OPT_PROFILE &&
+      option != VSS_OPT_ROW_FETCH)
     return fail(h, VSS_E_INVALID_ARG, "unknown option");
   std::lock_guard<std::mutex> lk(h->mu);
   for (vss_handle* e : engines(h)) {
@@ -1526,6 +1601,8 @@ int vss_set_option(vss_handle* h, int option, int value) {
       e->keep_stem = value ? 1 : 0;
     } else if (option == VSS_OPT_USE_GRAPH) {
       e->use_graph = value ? 1 : 0;
+    } else if (option == VSS_OPT_ROW_FETCH) {
+      e->row_fetch = value ? 1 : 0;
     } else {
       e->profile = value ? 1 : 0;
     }
@@ -1540,6 +1617,7 @@ int vss_get_option(vss_handle* h, int option, int* value) {
     case VSS_OPT_USE_GRAPH: *value = h->use_graph; return VSS_OK;
     case VSS_OPT_PROFILE: *value = h->profile; return VSS_OK;
     case VSS_OPT_KEEP_STEM: *value = h->keep_stem; return VSS_OK;
+    case VSS_OPT_ROW_FETCH: *value = h->row_fetch; return VSS_OK;
     default: return fail(h, VSS_E_INVALID_ARG, "unknown option");
   }
 }

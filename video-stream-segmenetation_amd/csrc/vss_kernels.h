@@ -340,6 +340,18 @@ struct UpmaskParams {
 };
 void launch_upmask(const UpmaskParams& p, int n, hipStream_t s);
 
+// Queued host path: only the frame rows the resize reads, pinned host -> HBM
+// (vss_stage.hip).  rows: device list of the row indices; src / dst = frame 0.
+struct FetchRowsParams {
+  const uint8_t* src;    // pinned host staging (device-accessible)
+  uint8_t* dst;          // the slot's HBM frame buffer (same layout)
+  const int* rows;       // [nrows] rows to move
+  long row_stride, frame_stride;
+  int row_bytes;         // width * channels
+  int vec16;             // 1: every row start and row_bytes are multiples of 16 B
+};
+void launch_fetch_rows(const FetchRowsParams& p, int nrows, int nframes, hipStream_t s);
+
 void launch_post_ema(const PostEmaParams& p, hipStream_t s);
 void launch_post_filter(const PostFilterParams& p, int n, hipStream_t s);
 
