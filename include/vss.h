@@ -190,11 +190,17 @@ int vss_submit_list(vss_handle* h, const uint8_t* const* frames, int n, int heig
 int vss_wait(vss_handle* h, vss_ticket ticket);
 int vss_query(vss_handle* h, vss_ticket ticket);
 
-/* Zero-copy staging: the pinned host buffer (capacity bytes) that the NEXT
- * queued host call reads its frames from.  A decoder that writes its frames
- * there and passes this pointer as `frames` saves the staging copy (frames
- * must start at the buffer's first byte). */
-int vss_staging_buffer(vss_handle* h, uint8_t** frames, size_t* capacity);
+/* Zero-copy staging (the decode -> infer loop of BASELINE config 5): reserve
+ * a free slot (waits for one) and get its pinned host buffer (capacity
+ * bytes); decode the frames straight into it (frame i at i * height *
+ * row_stride) and queue them with vss_submit_staged — no staging copy.  The
+ * lease holds the slot until then (vss_staging_release gives it back
+ * unused); other calls skip leased slots.  cb may be NULL (then vss_wait on
+ * *ticket). */
+int vss_staging_acquire(vss_handle* h, int* slot, uint8_t** frames, size_t* capacity);
+int vss_staging_release(vss_handle* h, int slot);
+int vss_submit_staged(vss_handle* h, int slot, int n, int height, int width, int channels, size_t row_stride,
+                      float* masks_out, int out_mode, vss_callback cb, void* user, vss_ticket* ticket);
 
 /* Device-resident variant: d_frames and d_masks are HBM pointers of the
  * handle's first GPU; the work is enqueued on `stream` (a hipStream_t; NULL =

@@ -31,8 +31,20 @@ async function main() {
     const m = res[i].masks;
     fs.writeFileSync(outPrefix + '.' + i, Buffer.from(m.buffer, m.byteOffset, m.byteLength));
   }
+  // zero-copy leases (single-GPU handles): frames decoded into pinned staging
+  let leaseEqual = null;
+  if (!ids) {
+    const whole = res[N].masks;
+    const lease = s.acquireFrames();
+    for (let i = 0; i < N; i++) lease.data.set(frames[i].data, i * bytes);
+    const other = s.segmentFrames(frames);  // runs on another slot meanwhile
+    const r = await s.segmentLease(lease, N, W, H, C);
+    await other;
+    leaseEqual = r.count === N && r.masks.every((v, i) => v === whole[i]);
+    s.releaseFrames(s.acquireFrames());  // a lease given back unused
+  }
   console.log(JSON.stringify({ order: order, calls: calls.length, empty: res[calls.length],
-                               queueDepth: s.queueDepth, nGpus: s.nGpus }));
+                               queueDepth: s.queueDepth, nGpus: s.nGpus, leaseEqual: leaseEqual }));
   s.close();
 }
 main().catch((e) => { console.error(e); process.exit(1); });

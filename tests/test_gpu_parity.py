@@ -248,19 +248,33 @@ def test_submit_wait_many_in_flight(pkg, synthetic, torch_cuda):
         assert s.query(t)
 
 
-def test_zero_copy_staging(pkg, synthetic):
-    """A decoder writing straight into vss_staging_buffer: no staging copy, same masks."""
+def test_zero_copy_staging_leases(pkg, synthetic):
+    """A decoder writing straight into a leased slot's pinned staging
+    (vss_staging_acquire / vss_submit_staged): no staging copy, same masks; a
+    leased slot is skipped by other calls, and releasing it returns it."""
     f = _frames(synthetic, 4, start=1100)
+    g = _frames(synthetic, 4, start=1200)
     with pkg.Session(dtype="bf16x2", max_batch=4, max_frame_h=480, max_frame_w=640, queue_depth=2) as s:
         ref, _, _ = s.segment_frames(f)
-        for it in range(4):  # every slot in turn
-            buf = s.staging_buffer()
+        ref_g, _, _ = s.segment_frames(g)
+        for it in range(4):
+            slot, buf = s.staging_acquire()
             assert buf.size >= f.nbytes
             buf[:f.nbytes] = f.reshape(-1)
-            out = np.empty((4, 144 * 256), np.float32)
-            t = s.submit_raw(buf.ctypes.data, 4, 480, 640, 3, 640 * 3, out)
-            s.wait(t)
-            assert np.array_equal(out, ref), it
+            mid, _, _ = s.segment_frames(g)  # other calls run meanwhile, on the other slot
+            assert np.array_equal(mid, ref_g)
+            assert np.array_equal(s.wait(s.submit_staged(slot, 4, 480, 640, 3))[0], ref), it
+        a, _ = s.staging_acquire()
+        b, _ = s.staging_acquire()
+        assert a != b
+        with pytest.raises(pkg.VssError) as e:  # both slots leased
+            s.submit(f)
+        assert e.value.code == pkg.VSS_E_BUSY
+        s.staging_release(a)
+        s.staging_release(b)
+        with pytest.raises(pkg.VssError):
+            s.staging_release(b)
+        assert np.array_equal(s.segment_frames(f)[0], ref)
 
 
 def test_inflight_streams_bitwise(pkg, sess_bf, synthetic, torch_cuda):

@@ -96,6 +96,7 @@ def test_node_queue_resolves_in_call_order(addon_built, pkg, oracle, blob, synth
         info = json.loads(out.stdout.strip().splitlines()[-1])
         assert info["order"] == list(range(n + 2)) and info["empty"] == "rejected", info
         assert info["queueDepth"] == 2 and info["nGpus"] == 1
+        assert info["leaseEqual"] is (None if ids else True)
         ref = oracle.forward(blob, frames, 144, 256, mode=0).reshape(n, -1)
         for i in range(n):
             m = np.fromfile(f"{op}.{i}", np.float32)

@@ -129,7 +129,10 @@ def lib() -> ctypes.CDLL:
                 "vss_submit": ([P, P, I, I, I, I, S, P, I, ctypes.POINTER(ctypes.c_uint64)], I),
                 "vss_wait": ([P, ctypes.c_uint64], I),
                 "vss_query": ([P, ctypes.c_uint64], I),
-                "vss_staging_buffer": ([P, ctypes.POINTER(P), ctypes.POINTER(S)], I),
+                "vss_staging_acquire": ([P, ctypes.POINTER(I), ctypes.POINTER(P), ctypes.POINTER(S)], I),
+                "vss_staging_release": ([P, I], I),
+                "vss_submit_staged": ([P, I, I, I, I, I, S, P, I, CALLBACK, P, ctypes.POINTER(ctypes.c_uint64)], I),
+                "vss_submit_list": ([P, ctypes.POINTER(P), I, I, I, I, S, P, I, ctypes.POINTER(ctypes.c_uint64)], I),
                 "vss_segment_device": ([P, P, I, I, I, I, S, S, P, P], I),
                 "vss_comm_unique_id": ([P, P, S, ctypes.POINTER(S)], I),
                 "vss_comm_init_rank": ([P, I, I, P, S], I),
@@ -301,18 +304,25 @@ class Session:
             _check(rc, self._h)
         return rc == 1
 
-    def staging_buffer(self) -> np.ndarray:
-        """The pinned buffer the NEXT queued host call reads its frames from (zero-copy
-        decode target), as a writable uint8 array of its capacity."""
-        p, cap = ctypes.c_void_p(), ctypes.c_size_t()
-        _check(lib().vss_staging_buffer(self._h, ctypes.byref(p), ctypes.byref(cap)), self._h)
-        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(cap.value,))
+    def staging_acquire(self):
+        """Zero-copy input (the decode -> infer loop): reserve a free slot and return
+        (slot, its pinned staging buffer as a writable uint8 array); decode frames into
+        it, then submit_staged(slot, ...)."""
+        k, p, cap = ctypes.c_int(), ctypes.c_void_p(), ctypes.c_size_t()
+        _check(lib().vss_staging_acquire(self._h, ctypes.byref(k), ctypes.byref(p), ctypes.byref(cap)), self._h)
+        return k.value, np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(cap.value,))
 
-    def submit_raw(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int, out: np.ndarray) -> int:
-        """vss_submit on a raw host pointer (e.g. staging_buffer()); masks into `out`."""
+    def staging_release(self, slot: int):
+        _check(lib().vss_staging_release(self._h, slot), self._h)
+
+    def submit_staged(self, slot: int, n: int, h: int, w: int, c: int, out: np.ndarray | None = None,
+                      row_stride: int = 0) -> int:
+        """Queue the n frames written into `slot`'s staging buffer; wait(ticket) -> masks."""
+        if out is None:
+            out = np.empty((n, self.mask_h * self.mask_w), np.float32)
         t = ctypes.c_uint64()
-        _check(lib().vss_submit(self._h, frames_ptr, n, h, w, c, row_stride, out.ctypes.data, VSS_OUT_MODEL,
-                                ctypes.byref(t)), self._h)
+        _check(lib().vss_submit_staged(self._h, slot, n, h, w, c, row_stride or w * c, out.ctypes.data,
+                                       VSS_OUT_MODEL, CALLBACK(), None, ctypes.byref(t)), self._h)
         self._tickets[t.value] = (out, (self.mask_w, self.mask_h))
         return t.value
 

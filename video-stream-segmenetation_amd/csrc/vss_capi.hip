@@ -51,7 +51,7 @@ constexpr uint32_t kMagic = 0x57535356u, kNone = 0xFFFFFFFFu;
 enum { K_STEM = 1, K_IR = 2, K_DEC = 3, K_HEAD = 4 };
 enum { F_EXPAND = 1, F_RESIDUAL = 2 };
 enum { O_W1, O_B1, O_WDW, O_BDW, O_W2, O_B2, O_GAMMA, O_BETA };
-constexpr int kDefaultQueueDepth = 4, kMaxQueueDepth = 16, kDefaultStagingThreads = 4;
+constexpr int kDefaultQueueDepth = 4, kMaxQueueDepth = 16, kDefaultStagingThreads = 8;
 
 struct Rec {
   uint32_t kind, cin, chid, cout, stride, flags, src, skip, off[8];
@@ -97,6 +97,7 @@ struct Slot {
   hipStream_t stream = nullptr;       // the slot's stream (queued host calls)
   hipEvent_t done = nullptr;          // recorded after the slot's latest work
   bool used = false;
+  bool leased = false;                // reserved by vss_staging_acquire for its holder's next call
   int status = VSS_OK;                // of the slot's latest queued batch (set by its callback)
   vss_ticket ticket = 0;              // latest ticket that ran in this slot
   bool stem_stored = false;           // the latest forward stored the fused stem (VSS_OPT_KEEP_STEM)
@@ -112,9 +113,14 @@ struct Slot {
 
 thread_local std::string g_tls_error;
 
-// Host threads for the pinned staging copies: a copy is cut into 1 MiB
-// pieces that the pool's threads and the caller take in turn (one core's
-// memcpy bandwidth, ~20 GB/s, would bound the host path below the PCIe rate).
+// Host threads for the pinned staging copies: a copy is cut into 256 KiB
+// pieces that the pool's threads and the caller take in turn.  Measured on the
+// MI355X box's host (tools/micro/pinned_copy.cpp, 7.4 MB into pinned memory):
+// one thread 39 GB/s, two to four 58-61 GB/s when the copy runs alone; inside
+// the queued pipeline (DMA engines reading the other slots' staging at the
+// same time) 8 threads sustained ~29 GB/s against ~25 GB/s for 4 (spinning
+// idle workers measured slower still).  The zero-copy lease
+// (vss_staging_acquire) avoids the copy altogether.
 class CopyPool {
  public:
   explicit CopyPool(int threads) {
@@ -137,7 +143,7 @@ class CopyPool {
   // has left this generation (so no worker ever touches a later one's pieces
   // with a stale index).
   void run(const std::vector<Job>& jobs) {
-    constexpr size_t kPiece = size_t(1) << 20;
+    constexpr size_t kPiece = size_t(256) << 10;
     std::vector<Job> pieces;
     for (const Job& j : jobs)
       for (size_t off = 0; off < j.len; off += kPiece)
@@ -598,7 +604,10 @@ int make_slot(vss_handle* h, Slot& s, int gather_ranks) {
   if ((rc = dalloc(h, &s.d_masks, (size_t)N * P * 4))) return rc;
   if (gather_ranks > 0 && (rc = dalloc(h, &s.d_gather, (size_t)gather_ranks * N * P * 4))) return rc;
   HIP_TRY(h, hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-  HIP_TRY(h, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  // host waits on it sleep instead of spinning: several waiting threads (the
+  // N-API addon's libuv workers, vss_wait callers) would otherwise take the
+  // cores the staging copies run on
+  HIP_TRY(h, hipEventCreateWithFlags(&s.done, hipEventDisableTiming | hipEventBlockingSync));
   return VSS_OK;
 }
 
@@ -890,9 +899,10 @@ int release_slot(vss_handle* e, Slot& s, hipStream_t st) {
   return VSS_OK;
 }
 
-// Is slot k free on every GPU of the handle (its latest batch done)?
+// Is slot k free on every GPU of the handle (its latest batch done, no lease)?
 int slot_free(vss_handle* h, int k, bool* free_) {
-  *free_ = true;
+  *free_ = !h->slots[k].leased;
+  if (!*free_) return VSS_OK;
   for (vss_handle* e : engines(h)) {
     Slot& s = e->slots[k];
     if (!s.used) continue;
@@ -922,11 +932,14 @@ int pick_slot(vss_handle* h, bool wait_free, int* out) {
     }
   }
   if (!wait_free) return fail(h, VSS_E_BUSY, "queue full: " + std::to_string(S) + " batches in flight");
+  int k = k0;
+  for (int j = 0; j < S && h->slots[k].leased; ++j) k = (k0 + j + 1) % S;
+  if (h->slots[k].leased) return fail(h, VSS_E_BUSY, "every slot is leased (vss_staging_acquire)");
   for (vss_handle* e : engines(h)) {
     HIP_TRY(e, hipSetDevice(e->device));
-    HIP_TRY(e, hipEventSynchronize(e->slots[k0].done));
+    HIP_TRY(e, hipEventSynchronize(e->slots[k].done));
   }
-  *out = k0;
+  *out = k;
   return VSS_OK;
 }
 
@@ -961,9 +974,10 @@ void host_done(void* p) {  // a HIP runtime thread, in stream order
 //   wait_free: block until the slot is free (else VSS_E_BUSY);
 //   sync: wait for the batch and copy the masks here (no host function).
 //   list: frame i at list[i] instead of frames + i * height * row_stride.
+//   lease: the slot a vss_staging_acquire reserved (-1: pick a free one).
 int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list, int n, int fh, int fw, int fc,
                 size_t rs, float* masks_out, int out_mode, bool wait_free, bool sync, vss_callback cb, void* user,
-                vss_ticket* ticket) {
+                vss_ticket* ticket, int lease = -1) {
   if ((!frames && !list) || !masks_out) return fail(h, VSS_E_INVALID_ARG, "null frames/masks_out");
   if (list)
     for (int i = 0; i < n; ++i)
@@ -984,8 +998,14 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   std::lock_guard<std::mutex> lk(h->mu);
   const vss_ticket t = h->next_ticket;
   // a free slot: its previous batch is done on every GPU, so its staging may be rewritten
-  int k = 0;
-  if ((rc = pick_slot(h, wait_free, &k))) return rc;
+  int k = lease;
+  if (lease >= 0) {
+    if (lease >= (int)h->slots.size() || !h->slots[lease].leased)
+      return fail(h, VSS_E_INVALID_ARG, "not a leased slot (vss_staging_acquire)");
+    h->slots[lease].leased = false;  // its batch runs now
+  } else if ((rc = pick_slot(h, wait_free, &k))) {
+    return rc;
+  }
   for (vss_handle* e : E) {
     HIP_TRY(e, hipSetDevice(e->device));
     if ((rc = ensure_staging(e, e->slots[k]))) return fail(h, rc, e->err);
@@ -1447,20 +1467,38 @@ int vss_query(vss_handle* h, vss_ticket ticket) {
   return 1;
 }
 
-int vss_staging_buffer(vss_handle* h, uint8_t** frames, size_t* capacity) {
-  if (!h || !frames) return fail(h, VSS_E_INVALID_ARG, "null handle/frames");
+int vss_staging_acquire(vss_handle* h, int* slot, uint8_t** frames, size_t* capacity) {
+  if (!h || !slot || !frames) return fail(h, VSS_E_INVALID_ARG, "null handle/slot/frames");
   std::lock_guard<std::mutex> lk(h->mu);
   if (!h->peers.empty())
     return fail(h, VSS_E_UNSUPPORTED, "zero-copy staging is per GPU: a multi-GPU handle stages its shards itself");
-  // the round-robin slot, once free: the next call picks it (the first free
-  // slot from there on) unless another thread's call comes first
-  const int k = (int)(h->next_ticket % h->slots.size());
+  int k = 0;
+  int rc = pick_slot(h, true, &k);  // a free slot (waits for one)
+  if (rc) return rc;
   HIP_TRY(h, hipSetDevice(h->device));
-  if (int rc = ensure_staging(h, h->slots[k])) return rc;
-  if (h->slots[k].used) HIP_TRY(h, hipEventSynchronize(h->slots[k].done));
+  if ((rc = ensure_staging(h, h->slots[k]))) return rc;
+  h->slots[k].leased = true;
+  *slot = k;
   *frames = h->slots[k].h_frames;
   if (capacity) *capacity = h->frame_cap;
   return VSS_OK;
+}
+
+int vss_staging_release(vss_handle* h, int slot) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (slot < 0 || slot >= (int)h->slots.size() || !h->slots[slot].leased)
+    return fail(h, VSS_E_INVALID_ARG, "not a leased slot");
+  h->slots[slot].leased = false;
+  return VSS_OK;
+}
+
+int vss_submit_staged(vss_handle* h, int slot, int n, int height, int width, int channels, size_t row_stride,
+                      float* masks_out, int out_mode, vss_callback cb, void* user, vss_ticket* ticket) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (slot < 0 || slot >= (int)h->slots.size()) return fail(h, VSS_E_INVALID_ARG, "bad slot");
+  return submit_host(h, h->slots[slot].h_frames, nullptr, n, height, width, channels, row_stride, masks_out, out_mode,
+                     false, false, cb, user, ticket, slot);
 }
 
 int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width, int channels,

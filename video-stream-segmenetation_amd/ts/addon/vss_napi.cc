@@ -16,6 +16,11 @@
 //       worker): returns once the frames are staged, up to queueDepth batches in flight
 //       (beyond that it rejects with code -4 = VSS_E_BUSY; segment.ts keeps within it).
 //       An array of frames is copied frame by frame into the pinned staging (no packing).
+//   stagingAcquire(handle) -> {slot, data: Uint8Array}   zero-copy input: a free slot's pinned
+//       staging buffer (valid until the handle is destroyed; waits for a free slot)
+//   segmentStaged(handle, slot, n, height, width, channels, rowStride, outMode?) -> Promise<Float32Array>
+//       queue the frames decoded into that slot's buffer (no staging copy)
+//   stagingRelease(handle, slot)      give a lease back unused
 //   destroy(handle)
 //   postCreate(handle, config?) -> post     (config keys as the reference's `config`:
 //                                             EMA, NOISE_CUTOFF, HIGH_THRESHOLD, GAMMA,
@@ -47,6 +52,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -461,6 +467,29 @@ void QueuedComplete(napi_env env, napi_status, void* data) {
   delete w;
 }
 
+// The masks' ArrayBuffer: malloc'd (not zero-filled: Node 12's
+// napi_create_arraybuffer spent ~0.19 ms clearing 1.2 MB on the JS thread per
+// call) and handed to V8 as external memory, freed by its finalizer; V8's GC
+// is told about the bytes so it collects results at the usual pace.
+void free_masks(napi_env env, void* data, void* hint) {
+  std::free(data);
+  int64_t adj = 0;
+  napi_adjust_external_memory(env, -(int64_t)(uintptr_t)hint, &adj);
+}
+
+bool masks_buffer(napi_env env, size_t bytes, void** data, napi_value* ab) {
+  void* p = std::malloc(std::max<size_t>(bytes, 16));
+  if (!p) return false;
+  if (napi_create_external_arraybuffer(env, p, bytes, free_masks, (void*)(uintptr_t)bytes, ab) != napi_ok) {
+    std::free(p);
+    return false;
+  }
+  int64_t adj = 0;
+  napi_adjust_external_memory(env, (int64_t)bytes, &adj);
+  *data = p;
+  return true;
+}
+
 bool u8_view(napi_env env, napi_value v, const uint8_t** data, size_t* len) {
   bool is_ta = false;
   napi_is_typedarray(env, v, &is_ta);
@@ -540,7 +569,11 @@ napi_value Segment(napi_env env, napi_callback_info info) {
   w->out_count = out_mode == VSS_OUT_FRAME ? (size_t)n * height * width : (size_t)n * hd->mask_h * hd->mask_w;
   napi_value ab, promise;
   void* out = nullptr;
-  NAPI_OK(env, napi_create_arraybuffer(env, w->out_count * 4, &out, &ab));
+  if (!masks_buffer(env, w->out_count * 4, &out, &ab)) {
+    delete w;
+    napi_throw_error(env, nullptr, "out of host memory for the masks");
+    return nullptr;
+  }
   NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
   // staged here: the frames may be reused by the caller as soon as this returns
   const int rc = is_arr ? vss_submit_list(hd->h, list.data(), n, height, width, channels, (size_t)rs,
@@ -553,6 +586,94 @@ napi_value Segment(napi_env env, napi_callback_info info) {
     return promise;
   }
   napi_create_reference(env, ab, 1, &w->out_ref);  // masks_out stays alive until the batch is done
+  napi_value name;
+  napi_create_string_utf8(env, "vss_wait", NAPI_AUTO_LENGTH, &name);
+  NAPI_OK(env, napi_create_async_work(env, nullptr, name, QueuedExecute, QueuedComplete, w, &w->work));
+  NAPI_OK(env, napi_queue_async_work(env, w->work));
+  return promise;
+}
+
+void noop_finalize(napi_env, void*, void*) {}  // the pinned staging belongs to the handle
+
+napi_value StagingAcquire(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Handle* hd = get_handle(env, argv[0]);
+  if (!hd) return nullptr;
+  int slot = -1;
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  const int rc = vss_staging_acquire(hd->h, &slot, &p, &cap);
+  if (rc != VSS_OK) {
+    napi_throw(env, make_error(env, "vss_staging_acquire", rc, vss_last_error(hd->h)));
+    return nullptr;
+  }
+  napi_value ab, arr, o, v;
+  NAPI_OK(env, napi_create_external_arraybuffer(env, p, cap, noop_finalize, nullptr, &ab));
+  NAPI_OK(env, napi_create_typedarray(env, napi_uint8_array, cap, ab, 0, &arr));
+  NAPI_OK(env, napi_create_object(env, &o));
+  napi_create_int32(env, slot, &v);
+  napi_set_named_property(env, o, "slot", v);
+  napi_set_named_property(env, o, "data", arr);
+  return o;
+}
+
+napi_value StagingRelease(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Handle* hd = get_handle(env, argv[0]);
+  if (!hd) return nullptr;
+  int slot = -1;
+  napi_get_value_int32(env, argv[1], &slot);
+  const int rc = vss_staging_release(hd->h, slot);
+  if (rc != VSS_OK) napi_throw(env, make_error(env, "vss_staging_release", rc, vss_last_error(hd->h)));
+  return nullptr;
+}
+
+// segmentStaged(handle, slot, n, height, width, channels, rowStride, outMode?)
+napi_value SegmentStaged(napi_env env, napi_callback_info info) {
+  size_t argc = 8;
+  napi_value argv[8];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  if (argc < 7) {
+    napi_throw_type_error(env, nullptr, "segmentStaged(handle, slot, n, height, width, channels, rowStride, outMode?)");
+    return nullptr;
+  }
+  Handle* hd = get_handle(env, argv[0]);
+  if (!hd) return nullptr;
+  int slot = -1, n = 0, height = 0, width = 0, channels = 0, rs = 0, out_mode = VSS_OUT_MODEL;
+  napi_get_value_int32(env, argv[1], &slot);
+  napi_get_value_int32(env, argv[2], &n);
+  napi_get_value_int32(env, argv[3], &height);
+  napi_get_value_int32(env, argv[4], &width);
+  napi_get_value_int32(env, argv[5], &channels);
+  napi_get_value_int32(env, argv[6], &rs);
+  if (argc >= 8) napi_get_value_int32(env, argv[7], &out_mode);
+  if (n < 1 || height < 1 || width < 1 || rs < 1) {
+    napi_throw_range_error(env, nullptr, "segmentStaged: n, height, width and rowStride must be >= 1");
+    return nullptr;
+  }
+  QueuedWork* w = new QueuedWork();
+  w->h = hd->h;
+  w->out_count = out_mode == VSS_OUT_FRAME ? (size_t)n * height * width : (size_t)n * hd->mask_h * hd->mask_w;
+  napi_value ab, promise;
+  void* out = nullptr;
+  if (!masks_buffer(env, w->out_count * 4, &out, &ab)) {
+    delete w;
+    napi_throw_error(env, nullptr, "out of host memory for the masks");
+    return nullptr;
+  }
+  NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
+  const int rc = vss_submit_staged(hd->h, slot, n, height, width, channels, (size_t)rs, static_cast<float*>(out),
+                                   out_mode, nullptr, nullptr, &w->ticket);
+  if (rc != VSS_OK) {
+    napi_reject_deferred(env, w->deferred, make_error(env, "vss_submit_staged", rc, vss_last_error(hd->h)));
+    delete w;
+    return promise;
+  }
+  napi_create_reference(env, ab, 1, &w->out_ref);
   napi_value name;
   napi_create_string_utf8(env, "vss_wait", NAPI_AUTO_LENGTH, &name);
   NAPI_OK(env, napi_create_async_work(env, nullptr, name, QueuedExecute, QueuedComplete, w, &w->work));
@@ -1192,6 +1313,9 @@ napi_value Init(napi_env env, napi_value exports) {
       {"create", nullptr, Create, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"info", nullptr, Info, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"segment", nullptr, Segment, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"stagingAcquire", nullptr, StagingAcquire, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"stagingRelease", nullptr, StagingRelease, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"segmentStaged", nullptr, SegmentStaged, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"destroy", nullptr, Destroy, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"postCreate", nullptr, PostCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"postSetConfig", nullptr, PostSetConfig, nullptr, nullptr, nullptr, napi_default, nullptr},
