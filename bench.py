@@ -392,8 +392,10 @@ def main():
     recs, _, _ = mw.parse_blob(blob)
     costs = cm.layer_costs(recs, hm, wm, fh, fw, 3, pw_weight_bytes=2 if args.dtype == "bf16x2" else 4)
     names = [sess.layer_kernel(i) for i in range(len(ms))]
+    occ = [sess.layer_occupancy(i) for i in range(len(ms))]
     per_layer = [{"layer": i, "kind": costs[i]["kind"], "kernel": names[i], "ms": round(m, 5),
-                  "GBps": round(cm.launch_bytes(costs[i], B) / (m * 1e-3) / 1e9, 1) if m > 0 else None}
+                  "GBps": round(cm.launch_bytes(costs[i], B) / (m * 1e-3) / 1e9, 1) if m > 0 else None,
+                  "wg_per_cu": occ[i][0] or None, "lds_bytes": occ[i][1] or None}
                  for i, m in enumerate(ms)]
     dom = int(np.argmax(ms))
     dom_name = names[dom]

@@ -256,6 +256,12 @@ int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap);
  * do not depend on the tile (bitwise). */
 int vss_layer_tiles(const vss_handle* h, int layer, int* th, int* tw, int cap);
 
+/* Workgroups of `layer`'s kernel that fit one CU at once (registers, from
+ * hipOccupancyMaxActiveBlocksPerMultiprocessor, and the layer's dynamic LDS in
+ * gfx950's 2 KiB allocation granules) and its LDS bytes per workgroup; 0 for
+ * the fused stem and the head. */
+int vss_layer_occupancy(const vss_handle* h, int layer, int* wg_per_cu, int* lds_bytes);
+
 /* Kernel times from VSS_OPT_PROFILE runs: per layer, the mean over `count`
  * forwards (ms).  Resets the accumulators. */
 int vss_profile_read(vss_handle* h, double* ms_per_layer, int cap, int* count);

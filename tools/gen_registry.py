@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SPEC = os.path.join(ROOT, "video-stream-segmenetation_amd", "model", "spec.json")
 CANDIDATES = [(8, 16), (6, 16), (4, 16), (3, 16), (8, 8), (6, 8), (4, 8), (2, 16), (2, 8), (1, 16)]
 MAX_ACC, MAX_LDS = 16, 160 * 1024
-HID_STRIDE = 20  # kHidStride in csrc/vss_kernels.h
+HID_STRIDE = 20  # hid_stride() in csrc/vss_kernels.h
 SHARDS = 6  # compile units for the block shapes (csrc/Makefile: VSS_SHARDS)
 
 

@@ -148,6 +148,7 @@ def lib() -> ctypes.CDLL:
                 "vss_profile_read": ([P, ctypes.POINTER(ctypes.c_double), I, ctypes.POINTER(I)], I),
                 "vss_layer_kernel": ([P, I, ctypes.c_char_p, I], I),
                 "vss_layer_tiles": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I), I], I),
+                "vss_layer_occupancy": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I)], I),
                 "vss_post_config_default": ([ctypes.POINTER(PostConfig)], None),
                 "vss_post_create": ([P, ctypes.POINTER(PostConfig), ctypes.POINTER(P)], I),
                 "vss_post_destroy": ([P], None),
@@ -385,6 +386,12 @@ class Session:
         if n < 0:
             _check(n, self._h)
         return [(th[k], tw[k]) for k in range(n)]
+
+    def layer_occupancy(self, layer: int):
+        """(workgroups per CU, LDS bytes per workgroup) of `layer`'s kernel."""
+        w, b = ctypes.c_int(), ctypes.c_int()
+        _check(lib().vss_layer_occupancy(self._h, layer, ctypes.byref(w), ctypes.byref(b)), self._h)
+        return w.value, b.value
 
     def layer_kernel(self, layer: int) -> str:
         """The kernel running `layer`, named as rocprofv3 reports it."""

@@ -1668,6 +1668,21 @@ int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww) {
   return VSS_OK;
 }
 
+int vss_layer_occupancy(const vss_handle* h, int layer, int* wg_per_cu, int* lds_bytes) {
+  if (!h || layer < 0 || layer >= (int)h->L.size() || !wg_per_cu) return VSS_E_INVALID_ARG;
+  const LayerPlan& l = h->L[layer];
+  *wg_per_cu = 0;
+  if (lds_bytes) *lds_bytes = (int)l.lds;
+  if (!l.entry) return VSS_OK;
+  const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
+  HIP_TRY(const_cast<vss_handle*>(h), hipSetDevice(h->device));
+  HIP_TRY(const_cast<vss_handle*>(h),
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(wg_per_cu, (const void*)l.entry->fn[pi], kThreads, l.lds));
+  // the API assumes a finer LDS granule than gfx950 allocates (kLdsGranule)
+  *wg_per_cu = std::min(*wg_per_cu, lds_wg_per_cu((int)l.lds));
+  return VSS_OK;
+}
+
 int vss_layer_tiles(const vss_handle* h, int layer, int* th, int* tw, int cap) {
   if (!h || layer < 0 || layer >= (int)h->L.size() || cap < 0 || (cap > 0 && (!th || !tw))) return VSS_E_INVALID_ARG;
   const LayerPlan& l = h->L[layer];

@@ -42,10 +42,39 @@ __host__ __device__ constexpr int flags_sp(int f) { return ((f >> 4) & 3) + 1; }
 __host__ __device__ constexpr int flags_ks(int f) { return ((f >> 6) & 3) + 1; }
 
 constexpr int kThreads = 256;       // 4 wave64 per workgroup
+// gfx950 allocates LDS to workgroups in 2 KiB granules, 80 per CU (measured:
+// tools/micro/lds_resident.cpp; hipOccupancyMaxActiveBlocksPerMultiprocessor
+// assumes a finer granule and reports 3 per CU up to 54,613 B where only
+// 53,248 B fit three)
+constexpr int kLdsGranule = 2048, kLdsGranulesPerCu = 80;
+__host__ __device__ constexpr int lds_wg_per_cu(int bytes) {
+  return kLdsGranulesPerCu / ((bytes + kLdsGranule - 1) / kLdsGranule);
+}
 constexpr int kMaxAcc = 16;         // 16x16 project accumulators per wave
-constexpr int kHidStride = 20;      // floats per pixel of an expand wave's hidden chunk in LDS: 16
-                                    // channels + 4 pad, so the 16 lanes of one 16-B LDS access
-                                    // (lane = pixel) hit 16 distinct bank quads (stride 16: 4-way)
+// LDS layout of the input tile and the expand waves' hidden chunks.  Measured
+// (round 2, tools/lds_model.py + tools/micro/lds_taps.cpp + tools/ab_pinned.sh):
+// gfx950's ds_read_b128 serves lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}
+// (and +32), so a 16-pixel block read with a pixel stride of 5 or 13 bank quads
+// (the padding below) is 2-way conflicted.  A layout that is conflict-free for
+// every depthwise tap (VSS_PERM=1: lanes {0-3,12-15} take pixels 0-7, lanes
+// {4-11} pixels 8-15; VSS_XS_PAD=8 and VSS_HS1=24: 2 mod 4 quads per pixel)
+// has 4.5x fewer conflict cycles (model; SQ_LDS_BANK_CONFLICT agreed within
+// 5 %) and makes the tap reads alone 1.6x faster, but its extra LDS costs
+// occupancy (LDS is allocated in 2 KiB granules, 80 per CU — d3's 6x16 tile
+// went from 3 to 2 workgroups per CU at 53,952 B) and the whole layers
+// measured equal or slower except d2 (-5 %): the default stays the tight one.
+#ifndef VSS_PERM
+#define VSS_PERM 0
+#endif
+#ifndef VSS_XS_PAD
+#define VSS_XS_PAD 4
+#endif
+#ifndef VSS_HS1
+#define VSS_HS1 20
+#endif
+__host__ __device__ constexpr int block_pix(int r) { return VSS_PERM ? (r < 4 ? r : (r < 12 ? r + 4 : r - 8)) : r; }
+// floats per pixel of an expand wave's hidden chunk in LDS (16 channels + pad)
+__host__ __device__ constexpr int hid_stride(int stride) { return stride == 2 ? 20 : VSS_HS1; }
 constexpr int kAccSlots = 16;       // instance-norm accumulator slots per frame and layer
                                     // (spreads the producers' atomics over 16x the cache lines)
 
@@ -76,7 +105,7 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   L.P_in_pad = (L.P_in + 15) & ~15;
   L.P_out = TH * TW;
   L.CX = mode == 2 /*MODE_DEC*/ ? cin + cskip : cin;
-  L.XS = L.CX + 4;
+  L.XS = L.CX + VSS_XS_PAD;
   L.LD1 = cin + 8;   // bf16 elements per W1 row in LDS (16-B aligned rows)
   L.LD2 = chid + 8;  // bf16 elements per W2 row
   L.SR = (TH + 1) / 2 + 3;
@@ -115,7 +144,7 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   // both points (before the input tile is committed / after the main loop).
   L.work = o;
   L.lr = o;
-  o += cmax(cmax(cmax(mode == 0 ? 4 * L.P_in_pad * kHidStride : 1024, L.CS * L.slab_stride),
+  o += cmax(cmax(cmax(mode == 0 ? 4 * L.P_in_pad * hid_stride(stride) : 1024, L.CS * L.slab_stride),
                  mode == 2 ? r4(L.SR * L.SC * cin) : 0),
             stem_in ? stem_in_lds(L.IH, L.IW) : 0);
   L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;

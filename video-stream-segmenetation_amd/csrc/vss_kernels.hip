@@ -736,7 +736,8 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   const int pw = wave % PW, cw = wave / PW;
 
   if constexpr (MODE == MODE_IR_EXPAND) {
-    float* hid = work + wave * P_IN_PAD * kHidStride;
+    constexpr int HSD = hid_stride(STRIDE);
+    float* hid = work + wave * P_IN_PAD * HSD;
     constexpr int NK = CIN / 16;
     for (int ck = wave; ck < NCHUNK; ck += 4) {
       const int c0 = ck << 4;
@@ -753,7 +754,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         for (int s = 0; s < NK; ++s) d = mma16_op<PREC>(d, aw[s], *reinterpret_cast<const f4*>(xt + pix * XS + 16 * s + 4 * g));
         const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
         const bool valid = pix < P_IN && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
-        *reinterpret_cast<f4*>(hid + pix * kHidStride + 4 * g) = valid ? relu6v(d + bias) : f4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(hid + pix * HSD + 4 * g) = valid ? relu6v(d + bias) : f4{0.f, 0.f, 0.f, 0.f};
       }
       wave_sync();
       // dw 3x3 computed straight into the project MFMA's B layout: lane (r, g)
@@ -768,7 +769,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         for (int cb = 0; cb < NCB; ++cb) a2[cb] = lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g);
 #pragma unroll
         for (int pb = 0; pb < NPB; ++pb) {
-          const int pix = pb * 16 + r;
+          const int pix = pb * 16 + block_pix(r);
           const int ly = pix / TW, lx = pix % TW;
           f4 a = bb;
 #pragma unroll
@@ -776,7 +777,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
               const int sp = (STRIDE * ly + ky) * IW + (STRIDE * lx + kx);
-              a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(hid + sp * kHidStride + 4 * g) + a;
+              a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(hid + sp * HSD + 4 * g) + a;
             }
           const f4 b = to_operand<PREC>(relu6v(a));
 #pragma unroll
@@ -802,7 +803,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       for (int cb = 0; cb < NCB; ++cb) a2[cb] = lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g);
 #pragma unroll
       for (int i = 0; i < NPBW; ++i) {
-        const int pix = (pw + i * PW) * 16 + r;
+        const int pix = (pw + i * PW) * 16 + block_pix(r);
         const int ly = pix / TW, lx = pix % TW;
         f4 a = bb;
 #pragma unroll
@@ -828,7 +829,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
         const int pb = pw + i * PW;
-        *reinterpret_cast<f4*>(slab + (pb * 16 + r) * RS + cb * 16 + 4 * g) = acc[i * NCB + cb];
+        *reinterpret_cast<f4*>(slab + (pb * 16 + block_pix(r)) * RS + cb * 16 + 4 * g) = acc[i * NCB + cb];
       }
   }
   __syncthreads();
