@@ -11,8 +11,8 @@
  * (frameProcessorTest.ts:91, :406, :478).  A vso_session parses an ONNX
  * ModelProto with its own protobuf reader, infers every shape for the
  * session's input shape, folds the shape arithmetic, and runs the graph as a
- * fixed list of HIP kernels (dense convolutions as implicit GEMMs on
- * v_mfma_f32_16x16x4_f32, depthwise convolutions direct, activations and
+ * fixed list of HIP kernels (dense convolutions as implicit GEMMs on MFMA —
+ * f32, or bf16 / f16 operands by option — depthwise convolutions direct, activations and
  * residual adds fused into the convolution epilogues), replayed from a
  * hipGraph.  Tensors are float32 NCHW.
  *
@@ -56,12 +56,31 @@ enum {
 
 typedef struct vso_session vso_session;
 
+/* Session options (the part of ORT's SessionOptions this runtime has).
+ * conv_precision: operands of the dense k x k convolutions (k_conv_tile,
+ * vso_conv.hip) — VSO_PRECISION_F32: exact f32 products
+ * (v_mfma_f32_16x16x4_f32), the default; _BF16 / _F16: activations and weights
+ * rounded to bfloat16 / float16 (nearest even) on
+ * v_mfma_f32_16x16x32_{bf16,f16}, f32 accumulation.  _F16 keeps every
+ * float16-typed weight of a q4f16 export exact. */
+enum { VSO_PRECISION_F32 = 0, VSO_PRECISION_BF16 = 1, VSO_PRECISION_F16 = 2 };
+typedef struct vso_options {
+  int conv_precision;
+  int reserved[7];
+} vso_options;
+
+void vso_options_default(vso_options* o);
+
 /* Replaces InferenceSession.create(url) (model.ts:14) / _OrtCreateSession(modelPtr,
  * len, opts) (ort-wasm-simd-threaded.mjs:51): model = the ONNX file's bytes.
  * input_dims/input_ndim: the shape of input 0 when the model leaves dims
  * symbolic (NULL/0 = the model's own static shape).  device_id: HIP ordinal. */
 int vso_create(const void* model, size_t bytes, const int64_t* input_dims, int input_ndim, int device_id,
                vso_session** out);
+
+/* vso_create with options (NULL = vso_options_default): InferenceSession.create(url, options). */
+int vso_create_ex(const void* model, size_t bytes, const int64_t* input_dims, int input_ndim, int device_id,
+                  const vso_options* opts, vso_session** out);
 
 /* Replaces InferenceSession.release / _OrtReleaseSession (:51). */
 void vso_destroy(vso_session* s);
@@ -92,6 +111,8 @@ int vso_run_device(vso_session* s, const float* const* d_inputs, float* const* d
  * kernel name as rocprofv3 reports it (returns the string length). */
 int vso_launch_count(const vso_session* s);
 int vso_launch_name(const vso_session* s, int k, char* buf, int cap);
+/* Convolutions planned on the LDS-tiled MFMA kernel (k_conv_tile). */
+int vso_tile_conv_count(const vso_session* s);
 
 #ifdef __cplusplus
 }

@@ -371,14 +371,23 @@ def conv2d(x, w, b, attrs):
     wo = (wd + pl + pr - d[1] * (kw - 1) - 1) // s[1] + 1
     out = np.zeros((n, m, ho, wo), np.float64)
     mg = m // g
-    for gi in range(g):
-        xs = xp[:, gi * cg:(gi + 1) * cg]
-        ws = w[gi * mg:(gi + 1) * mg]
+    if g == c and g == m:  # depthwise: every channel at once, tap by tap
         for ky in range(kh):
             for kx in range(kw):
                 y0, x0 = ky * d[0], kx * d[1]
-                patch = xs[:, :, y0:y0 + s[0] * (ho - 1) + 1:s[0], x0:x0 + s[1] * (wo - 1) + 1:s[1]]
-                out[:, gi * mg:(gi + 1) * mg] += np.einsum("nchw,mc->nmhw", patch, ws[:, :, ky, kx])
+                patch = xp[:, :, y0:y0 + s[0] * (ho - 1) + 1:s[0], x0:x0 + s[1] * (wo - 1) + 1:s[1]]
+                out += patch * w[None, :, 0, ky, kx, None, None]
+    else:
+        for gi in range(g):
+            xs = xp[:, gi * cg:(gi + 1) * cg]
+            ws = w[gi * mg:(gi + 1) * mg]
+            for ky in range(kh):
+                for kx in range(kw):
+                    y0, x0 = ky * d[0], kx * d[1]
+                    patch = xs[:, :, y0:y0 + s[0] * (ho - 1) + 1:s[0], x0:x0 + s[1] * (wo - 1) + 1:s[1]]
+                    # float64 BLAS product over the group's input channels
+                    out[:, gi * mg:(gi + 1) * mg] += np.tensordot(ws[:, :, ky, kx], patch, axes=([1], [1])).transpose(
+                        1, 0, 2, 3)
     if b is not None:
         out += b.astype(np.float64)[None, :, None, None]
     return out.astype(np.float32)
@@ -518,9 +527,31 @@ def _dequant_nbits(bq, scales, zp, attrs):
     return w.astype(np.float16) if np.asarray(scales).dtype == np.float16 else w
 
 
-def run(model: Model, feeds: dict, want=None) -> dict:
+def round_operand(a, mode):
+    """float32 values rounded to bfloat16 / float16 (nearest even), as float32."""
+    a = np.ascontiguousarray(a, np.float32)
+    if mode == "bf16":
+        u = a.view(np.uint32).astype(np.uint64)
+        u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+        return u.astype(np.uint32).view(np.float32)
+    with np.errstate(over="ignore"):
+        return a.astype(np.float16).astype(np.float32)
+
+
+def tiled_conv(w, attrs):
+    """The convolutions the GPU runs on k_conv_tile with 16-bit operands
+    (conv_tile_shape in video-stream-segmenetation_amd/csrc/vso_conv.hip):
+    ungrouped, undilated, square 1/3/5 at stride 1 or 3 at stride 2."""
+    k, s, d = w.shape[2], attrs.get("strides", [1, 1]), attrs.get("dilations", [1, 1])
+    return (attrs.get("group", 1) == 1 and d[0] == 1 and d[1] == 1 and w.shape[2] == w.shape[3] and s[0] == s[1]
+            and ((s[0] == 1 and k in (1, 3, 5)) or (s[0] == 2 and k == 3)))
+
+
+def run(model: Model, feeds: dict, want=None, conv_operands=None) -> dict:
     """Evaluate the graph on numpy feeds; returns {output name: array} (or
-    every value named in `want`)."""
+    every value named in `want`).  conv_operands "bf16" / "f16": the inputs
+    and weights of the convolutions tiled_conv() names are rounded to that
+    type first (vso_options.conv_precision), the products still in f64."""
     env = dict(model.inits)
     env.update({k: np.asarray(v) for k, v in feeds.items()})
     env[""] = None
@@ -528,7 +559,10 @@ def run(model: Model, feeds: dict, want=None) -> dict:
         op, a, ins = nd["op"], nd["attrs"], [env.get(i) for i in nd["inputs"]]
         x = ins[0] if ins else None
         if op == "Conv":
-            y = conv2d(x, ins[1], ins[2] if len(ins) > 2 else None, a)
+            w = ins[1]
+            if conv_operands and tiled_conv(w, a):
+                x, w = round_operand(x, conv_operands), round_operand(w, conv_operands)
+            y = conv2d(x, w, ins[2] if len(ins) > 2 else None, a)
         elif op == "Relu":
             y = np.maximum(x, 0).astype(x.dtype)
         elif op == "LeakyRelu":

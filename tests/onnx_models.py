@@ -235,6 +235,153 @@ def q4f16_like(h=64, w=96):
     return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])], opset=21)
 
 
+def modnet(h=288, w=512, hr=32, q4f16=False, seed=7):
+    """The public MODNet topology (Ke et al., "MODNet: Real-Time Trimap-Free
+    Portrait Matting via Objective Decomposition", AAAI 2022; the authors'
+    src/models/modnet.py) at inference, the graph an ONNX export of the
+    reference's model_q4f16.onnx holds (model.ts:12-29, run at 288x512 by
+    frameProcessorTest.ts:91), with seeded weights (the real ones are absent):
+      backbone  MobileNetV2 1.0 (stem 3x3 s2 32, inverted residuals
+                t,c,n,s = 1,16,1,1 / 6,24,2,2 / 6,32,3,2 / 6,64,4,2 / 6,96,3,1 /
+                6,160,3,2 / 6,320,1,1, 1x1 320 -> 1280; ReLU6 as Clip; BN folded
+                into the conv as the exporter does); enc2x 16ch, enc4x 24ch,
+                enc32x 1280ch
+      LR        SE block on enc32x (GAP -> MatMul 1280x320 -> Relu -> MatMul
+                320x1280 -> Sigmoid -> Mul), x2 bilinear -> Conv-IBNorm-Relu 5x5
+                1280 -> 96, x2 -> 5x5 96 -> 32 (lr8x)
+      HR        img/2, img/4 (bilinear); 1x1 16 -> hr on enc2x, 3x3 s2 (hr+3) ->
+                hr; 1x1 24 -> hr on enc4x, 3x3 2hr -> 2hr; lr8x x2; 3x3 (3hr+3)
+                -> 2hr -> 2hr -> hr; x2; 3x3 2hr -> 2hr -> hr -> hr -> hr (hr2x)
+      fusion    lr8x x2 -> 5x5 32 -> hr; x2; 3x3 2hr -> hr; x2; 3x3 (hr+3) ->
+                hr/2; 1x1 hr/2 -> 1; Sigmoid (the matte)
+    IBNorm = Slice -> BatchNormalization (first half) / InstanceNormalization
+    (second half, affine=False) -> Concat.  q4f16=True gives the export's form:
+    float16 weights, the input Cast to FLOAT16 and the matte back to FLOAT, the
+    SE's two MatMuls as com.microsoft MatMulNBits (4-bit, block 32)."""
+    b = Builder(seed)
+    rng = b.rng
+    x = "input"
+    dt = np.float16 if q4f16 else np.float32
+
+    def cst(v):
+        return b.const(np.array(v, dt))
+
+    def wt(*shape, scale=None):
+        n = b.w(*shape, scale=scale)
+        b.inits[n] = b.inits[n].astype(dt)
+        return n
+
+    def conv(t, cin, cout, k, stride=1, group=1):
+        ins = [t, wt(cout, cin // group, k, k), wt(cout, scale=0.1)]
+        return b.op("Conv", ins, kernel_shape=[k, k], strides=[stride, stride], pads=[k // 2] * 4, group=group)
+
+    def relu6(t):
+        return b.op("Clip", [t, cst(0), cst(6)])
+
+    def ir(t, cin, cout, stride, e):
+        hd = cin * e
+        u = relu6(conv(t, cin, hd, 1)) if e != 1 else t
+        u = relu6(conv(u, hd, hd, 3, stride=stride, group=hd))
+        o = conv(u, hd, cout, 1)
+        return b.op("Add", [o, t]) if stride == 1 and cin == cout else o
+
+    def ibn_relu(t, cin, cout, k, stride=1):
+        c = conv(t, cin, cout, k, stride)
+        nb = cout // 2
+        lo = b.op("Slice", [c, b.const(np.array([0], np.int64)), b.const(np.array([nb], np.int64)),
+                            b.const(np.array([1], np.int64))])
+        hi = b.op("Slice", [c, b.const(np.array([nb], np.int64)), b.const(np.array([cout], np.int64)),
+                            b.const(np.array([1], np.int64))])
+        bn = b.op("BatchNormalization", [lo, b.const((rng.random(nb) + 0.5).astype(dt)),
+                                         b.const((rng.standard_normal(nb) * 0.1).astype(dt)),
+                                         b.const((rng.standard_normal(nb) * 0.1).astype(dt)),
+                                         b.const((rng.random(nb) + 0.5).astype(dt))], epsilon=1e-5)
+        inn = b.op("InstanceNormalization", [hi, b.const(np.ones(cout - nb, dt)), b.const(np.zeros(cout - nb, dt))],
+                   epsilon=1e-5)
+        return b.op("Relu", [b.op("Concat", [bn, inn], axis=1)])
+
+    def resize(t, s):
+        return b.op("Resize", [t, "", b.const(np.array([1, 1, s, s], np.float32))], mode="linear",
+                    coordinate_transformation_mode="pytorch_half_pixel")
+
+    def matmul(t, K, N):
+        if not q4f16:
+            return b.op("MatMul", [t, b.w(K, N, scale=(2.0 / K) ** 0.5)])
+        bs = 32
+        kb = -(-K // bs)
+        n = b.name("q")
+        b.inits[n] = rng.integers(0, 256, (N, kb, bs // 2), dtype=np.uint8)
+        sc = b.const((rng.random(N * kb) * (0.4 / K ** 0.5) + 0.01 / K ** 0.5).astype(np.float16))
+        zp = b.const(np.full((N * (-(-kb // 2)),), 0x88, np.uint8))
+        return b.op("MatMulNBits", [t, n, sc, zp], domain="com.microsoft", K=K, N=N, bits=4, block_size=bs)
+
+    img = b.op("Cast", [x], to=R.DT_FLOAT16) if q4f16 else x
+    # MobileNetV2 backbone
+    t = relu6(conv(img, 3, 32, 3, stride=2))
+    cin, enc = 32, {}
+    for i, (e, c, n, s) in enumerate(((1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2), (6, 96, 3, 1),
+                                      (6, 160, 3, 2), (6, 320, 1, 1))):
+        for j in range(n):
+            t = ir(t, cin, c, s if j == 0 else 1, e)
+            cin = c
+        enc[i] = t
+    enc2x, enc4x = enc[0], enc[1]
+    enc32x = relu6(conv(t, 320, 1280, 1))
+    # LR branch
+    gp = b.op("Flatten", [b.op("GlobalAveragePool", [enc32x])])
+    f = b.op("Relu", [matmul(gp, 1280, 320)])
+    f = b.op("Sigmoid", [matmul(f, 320, 1280)])
+    f = b.op("Reshape", [f, b.const(np.array([1, 1280, 1, 1], np.int64))])
+    lr = b.op("Mul", [enc32x, f])
+    lr16x = ibn_relu(resize(lr, 2), 1280, 96, 5)
+    lr8x = ibn_relu(resize(lr16x, 2), 96, 32, 5)
+    # HR branch
+    img2x, img4x = resize(img, 0.5), resize(img, 0.25)
+    e2 = ibn_relu(enc2x, 16, hr, 1)
+    hr4x = ibn_relu(b.op("Concat", [img2x, e2], axis=1), hr + 3, hr, 3, stride=2)
+    e4 = ibn_relu(enc4x, 24, hr, 1)
+    hr4x = ibn_relu(b.op("Concat", [hr4x, e4], axis=1), 2 * hr, 2 * hr, 3)
+    lr4x = resize(lr8x, 2)
+    u = ibn_relu(b.op("Concat", [hr4x, lr4x, img4x], axis=1), 3 * hr + 3, 2 * hr, 3)
+    u = ibn_relu(u, 2 * hr, 2 * hr, 3)
+    hr4x = ibn_relu(u, 2 * hr, hr, 3)
+    u = b.op("Concat", [resize(hr4x, 2), e2], axis=1)
+    u = ibn_relu(u, 2 * hr, 2 * hr, 3)
+    u = ibn_relu(u, 2 * hr, hr, 3)
+    u = ibn_relu(u, hr, hr, 3)
+    hr2x = ibn_relu(u, hr, hr, 3)
+    # fusion branch
+    l4 = ibn_relu(resize(lr8x, 2), 32, hr, 5)
+    f2x = ibn_relu(b.op("Concat", [resize(l4, 2), hr2x], axis=1), 2 * hr, hr, 3)
+    fu = ibn_relu(b.op("Concat", [resize(f2x, 2), img], axis=1), hr + 3, hr // 2, 3)
+    m = b.op("Sigmoid", [conv(fu, hr // 2, 1, 1)])
+    if q4f16:
+        m = b.op("Cast", [m], to=R.DT_FLOAT)
+    return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])], opset=21 if q4f16 else 13)
+
+
+def conv_tiles():
+    """Every k_conv_tile form (vso_conv.hip) on odd-sized batch-2 inputs, each
+    convolution reading a graph input so 16-bit operand rounding is the
+    oracle's exactly: 1x1, 3x3 (M 16 / 70: one and two channel tiles), 5x5,
+    3x3 stride 2, channel counts off the 32-channel chunk (40), a K split over
+    workgroups (x2: 200 channels at 9x16, 5x5) with a residual Add and Relu in
+    the reduction's epilogue, and Clip / Sigmoid epilogues."""
+    b = Builder(8)
+    x, x2 = "x", "x2"
+    c1 = b.op("Relu", [b.conv(x, 40, 24, 1)])
+    c3 = b.conv(x, 40, 16, 3)
+    c3b = b.op("Clip", [b.conv(x, 40, 70, 3), b.const(np.array(-0.5, np.float32)), b.const(np.array(0.5, np.float32))])
+    c5 = b.op("Sigmoid", [b.conv(x, 40, 32, 5)])
+    s2 = b.conv(x, 40, 24, 3, stride=2)
+    k1 = b.conv(x2, 200, 48, 5)
+    k2 = b.conv(x2, 200, 48, 3)
+    ks = b.op("Relu", [b.op("Add", [k1, k2])])
+    return b.model([(x, [2, 40, 37, 70]), (x2, [2, 200, 9, 16])],
+                   [(c1, [2, 24, 37, 70]), (c3, [2, 16, 37, 70]), (c3b, [2, 70, 37, 70]), (c5, [2, 32, 37, 70]),
+                    (s2, [2, 24, 19, 35]), (ks, [2, 48, 9, 16])])
+
+
 def face_detector_like(S=256, A=896, score_bias=3.0, seed=5):
     """A stand-in with the I/O of the reference's face detector
     (MediaPipeFaceDetector.onnx: image [1,3,S,S] -> box_coords [1,A,16],

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--modnet", default="256x256")
+    ap.add_argument("--full", default="288x512", help="the MODNet topology (onnx_models.modnet) at this size")
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--only-modnet", action="store_true")
     args = ap.parse_args()
     import torch
     import bench
@@ -34,13 +37,20 @@ def main():
     import onnx_models as M
 
     mh, mw = (int(v) for v in args.modnet.split("x"))
+    fh, fw = (int(v) for v in args.full.split("x"))
     cases = []
-    for key in ("mediapipe_face_detector", "mediapipe_face_landmarks"):
-        model, feeds, _, _ = M.load_golden(os.path.join(ROOT, "tests", "golden", key + ".npz"))
-        cases.append((key, model, None))
-    cases.append((f"modnet_like_{mh}x{mw}", M.modnet_like(), (1, 3, mh, mw)))
-    for name, model, shape in cases:
-        with ort.InferenceSession(model, input_shape=shape) as s:
+    if not args.only_modnet:
+        for key in ("mediapipe_face_detector", "mediapipe_face_landmarks"):
+            model, feeds, _, _ = M.load_golden(os.path.join(ROOT, "tests", "golden", key + ".npz"))
+            cases.append((key, model, None))
+        cases.append((f"modnet_like_{mh}x{mw}", M.modnet_like(), (1, 3, mh, mw)))
+    for q in (False, True):
+        for prec in ("f32", "f16" if q else "bf16"):
+            cases.append((f"modnet{'_q4f16' if q else ''}_{fh}x{fw}_b{args.batch}_{prec}", M.modnet(fh, fw, q4f16=q),
+                          (args.batch, 3, fh, fw), prec))
+    cases = [c if len(c) == 4 else c + ("f32",) for c in cases]
+    for name, model, shape, prec in cases:
+        with ort.InferenceSession(model, input_shape=shape, precision=prec) as s:
             din = [torch.rand(sh, dtype=torch.float32, device="cuda") for sh in s.input_shapes]
             dout = [torch.empty(sh, dtype=torch.float32, device="cuda") for sh in s.output_shapes]
             st = torch.cuda.Stream()
@@ -55,9 +65,13 @@ def main():
             e1.record(st)
             st.synchronize()
             ms = e0.elapsed_time(e1) / args.iters
+            frames = s.input_shapes[0][0]
             print(json.dumps({"model": name, "input": [list(x) for x in s.input_shapes], "ms_per_run": round(ms, 4),
-                              "runs_per_s": round(1000.0 / ms, 1), "launches": len(s.launches())}), flush=True)
-    face_stage(args, torch, ort, M)
+                              "runs_per_s": round(1000.0 / ms, 1), "ms_per_frame": round(ms / frames, 4),
+                              "launches": len(s.launches()),
+                              "tile_convs": s.tile_convs()}), flush=True)
+    if not args.only_modnet:
+        face_stage(args, torch, ort, M)
 
 
 def face_stage(args, torch, ort, M):

@@ -1,0 +1,290 @@
+// vso_conv.hip — the dense k x k convolutions of the ONNX sessions
+// (include/vso.h) as LDS-tiled implicit GEMMs on gfx950 MFMA.
+//
+// MODNet (the reference's model_q4f16.onnx, model.ts:12-29, run at 288x512 by
+// frameProcessorTest.ts:91) spends ~90 % of its 8.7 GMAC per frame in dense
+// 3x3 / 5x5 convolutions with 16-99 input and 16-96 output channels at
+// 72x128 .. 288x512 pixels.  k_conv_tile computes one
+// TH x TW output tile x BM output channels per workgroup:
+//
+//   * the input tile of 32 channels at a time (its halo included) is staged
+//     from the f32 NCHW tensor into LDS as [pixel][32 channels] in the MFMA
+//     operand type T, every element once per chunk (the im2col gather of all
+//     KS*KS taps then reads LDS), the next chunk's global loads in flight
+//     during the current chunk's MFMAs;
+//   * each wave owns TH*TW/64 blocks of 16 consecutive output pixels of one
+//     row and all BM output channels; per tap it reads one 16-byte B fragment
+//     per block from LDS (8 channels of one pixel) and the A fragments (8
+//     channels of one output channel's tap weights, packed at create as
+//     [tap][Mp][Cp] in T) from global memory / L2;
+//   * T = float: v_mfma_f32_16x16x4_f32, exact f32 products (8 MFMAs per 32
+//     channels); T = bf16 / f16: v_mfma_f32_16x16x32_{bf16,f16} (one MFMA per
+//     32 channels, 16x the rate), operands rounded to nearest-even, f32
+//     accumulation;
+//   * bias, residual and activation fused into the epilogue (vso_device.h);
+//     when the grid would be too small to fill 256 CUs the channel chunks are
+//     split over workgroups (ksplit) and k_conv_reduce adds the partial sums
+//     in a fixed order (deterministic) and applies the epilogue.
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+
+#include "vso_device.h"
+#include "vso_kernels.h"
+
+namespace vso {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+constexpr int CK = 32;  // input channels per staged chunk
+
+template <int PREC> struct Elem;
+template <> struct Elem<PREC_F32> { using T = float; };
+template <> struct Elem<PREC_BF16> { using T = __bf16; };
+template <> struct Elem<PREC_F16> { using T = _Float16; };
+
+// 16 bytes of the LDS pixel row: 4 f32 or 8 16-bit channels
+template <int PREC> __device__ __forceinline__ uint4 pack_quad(const float* v);
+template <> __device__ __forceinline__ uint4 pack_quad<PREC_F32>(const float* v) {
+  return uint4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+}
+template <> __device__ __forceinline__ uint4 pack_quad<PREC_BF16>(const float* v) {
+  bf8 b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b[e] = (__bf16)v[e];
+  return __builtin_bit_cast(uint4, b);
+}
+template <> __device__ __forceinline__ uint4 pack_quad<PREC_F16>(const float* v) {
+  h8 b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b[e] = (_Float16)v[e];
+  return __builtin_bit_cast(uint4, b);
+}
+
+// acc += A (16 out channels x 32 in channels) * B (32 in channels x 16 pixels).
+// a / b: this lane's fragments — 16-bit: one quad (channels 8g .. 8g+7);
+// f32: two quads (channels 4g .. 4g+3 and 16+4g .. 16+4g+3), MFMA s taking
+// element s (the same channel on both sides: the sum over all 32 channels).
+template <int PREC> __device__ __forceinline__ f4 mma32(const uint4* a, const uint4* b, f4 acc);
+template <> __device__ __forceinline__ f4 mma32<PREC_F32>(const uint4* a, const uint4* b, f4 acc) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[h].x), __uint_as_float(b[h].x), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[h].y), __uint_as_float(b[h].y), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[h].z), __uint_as_float(b[h].z), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[h].w), __uint_as_float(b[h].w), acc, 0, 0, 0);
+  }
+  return acc;
+}
+template <> __device__ __forceinline__ f4 mma32<PREC_BF16>(const uint4* a, const uint4* b, f4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a[0]), __builtin_bit_cast(bf8, b[0]), acc,
+                                                  0, 0, 0);
+}
+template <> __device__ __forceinline__ f4 mma32<PREC_F16>(const uint4* a, const uint4* b, f4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a[0]), __builtin_bit_cast(h8, b[0]), acc, 0,
+                                                 0, 0);
+}
+
+template <int PREC, int KS, int S, int TH, int TW, int BM>
+__global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
+  using T = typename Elem<PREC>::T;
+  constexpr int NQ = CK * (int)sizeof(T) / 16;     // quads of one pixel's chunk: 8 (f32) / 4
+  constexpr int QS = NQ + 1;                       // LDS pixel stride in quads (odd)
+  constexpr int CG = 16 / (int)sizeof(T);          // channels per quad
+  constexpr int NF = PREC == PREC_F32 ? 2 : 1;     // fragment quads per lane
+  constexpr int IH = (TH - 1) * S + KS, IW = (TW - 1) * S + KS, NPIX = IH * IW;
+  constexpr int ITEMS = NPIX * NQ;                 // quads staged per chunk
+  constexpr int PER = (ITEMS + 255) / 256;
+  constexpr int NB = TH * TW / 16, PBW = NB / 4;   // 16-pixel blocks per tile / per wave
+  constexpr int MI = BM / 16;
+  static_assert(NB % 4 == 0 && TW % 16 == 0, "tile");
+  __shared__ uint4 xs[NPIX * QS];
+
+  const ConvParams& c = p.c;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int t = blockIdx.x;
+  const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * TW;
+  const int m0 = blockIdx.y * BM;
+  const int n = blockIdx.z / p.ksplit, kz = blockIdx.z % p.ksplit;
+  const int nch = p.Cp / CK;
+  const int cbeg = kz * p.cps, cend = min(nch, cbeg + p.cps);
+  const int iy0 = oy0 * S - c.pt, ix0 = ox0 * S - c.pl;
+  const float* xn = c.x + (long)n * c.C * c.H * c.W;
+  const long plane = (long)c.H * c.W;
+
+  float st[PER][CG];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + 256 * u;
+      const int q = idx / NPIX, pix = idx - q * NPIX;
+      const int iy = pix / IW, ix = pix - (pix / IW) * IW;
+      const int gy = iy0 + iy, gx = ix0 + ix;
+      const bool in = idx < ITEMS && gy >= 0 && gy < c.H && gx >= 0 && gx < c.W;
+      const int cb = ch * CK + q * CG;
+      const float* src = xn + (long)cb * plane + (long)gy * c.W + gx;
+#pragma unroll
+      for (int e = 0; e < CG; ++e) st[u][e] = (in && cb + e < c.C) ? src[e * plane] : 0.f;
+    }
+  };
+  f4 acc[MI][PBW];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < PBW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // this wave's blocks: LDS pixel of lane r at tap (0, 0)
+  int bpix[PBW];
+#pragma unroll
+  for (int j = 0; j < PBW; ++j) {
+    const int b = wave * PBW + j;
+    const int ty = b / (TW / 16), tx = (b % (TW / 16)) * 16 + r;
+    bpix[j] = ty * S * IW + tx * S;
+  }
+  const uint4* wq = static_cast<const uint4*>(p.wp);  // [tap][Mp][Cp] in quads of T
+  const int cq = p.Cp / CG;                            // quads per weight row
+
+  if (cbeg < cend) load(cbeg);
+  for (int ch = cbeg; ch < cend; ++ch) {
+    __syncthreads();  // the previous chunk's fragment reads are done
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + 256 * u;
+      if (idx < ITEMS) {
+        const int q = idx / NPIX, pix = idx - q * NPIX;
+        xs[pix * QS + q] = pack_quad<PREC>(st[u]);
+      }
+    }
+    __syncthreads();
+    if (ch + 1 < cend) load(ch + 1);  // in flight during this chunk's MFMAs
+    const int wc = ch * (CK / CG);    // this chunk's first quad in a weight row
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky) {
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {
+        const int tap = ky * KS + kx;
+        uint4 a[MI][NF];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const uint4* row = wq + ((long)tap * p.Mp + m0 + 16 * i + r) * cq + wc;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) a[i][f] = row[g + 4 * f];
+        }
+#pragma unroll
+        for (int j = 0; j < PBW; ++j) {
+          uint4 b[NF];
+          const uint4* px = xs + (bpix[j] + ky * IW + kx) * QS;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) b[f] = px[g + 4 * f];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) acc[i][j] = mma32<PREC>(a[i], b, acc[i][j]);
+        }
+      }
+    }
+  }
+
+  // acc[i][j][v] = out channel m0 + 16 i + 4 g + v, pixel r of block j
+  const int P = c.Ho * c.Wo;
+#pragma unroll
+  for (int j = 0; j < PBW; ++j) {
+    const int b = wave * PBW + j;
+    const int oy = oy0 + b / (TW / 16), ox = ox0 + (b % (TW / 16)) * 16 + r;
+    if (oy >= c.Ho || ox >= c.Wo) continue;
+    const int pix = oy * c.Wo + ox;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int ch = m0 + 16 * i + 4 * g + v;
+        if (ch >= c.M) continue;
+        if (p.ksplit > 1) {
+          p.part[(((long)kz * c.N + n) * c.M + ch) * P + pix] = acc[i][j][v];
+        } else {
+          const long o = ((long)n * c.M + ch) * P + pix;
+          c.y[o] = epilogue(c.ep, acc[i][j][v], ch, o, n, pix);
+        }
+      }
+  }
+}
+
+// y = epilogue(sum over the ksplit partial sums, in split order)
+__global__ __launch_bounds__(256) void k_conv_reduce(ConvTileParams p) {
+  const ConvParams& c = p.c;
+  const int P = c.Ho * c.Wo;
+  const long total = (long)c.N * c.M * P;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    float s = p.part[o];
+    for (int k = 1; k < p.ksplit; ++k) s += p.part[(long)k * total + o];
+    const int pix = (int)(o % P);
+    const long nc = o / P;
+    c.y[o] = epilogue(c.ep, s, (int)(nc % c.M), o, (int)(nc / c.M), pix);
+  }
+}
+
+// ---- instantiations and dispatch --------------------------------------------
+// (KS, S, TH, TW): stride 1: 1x1, 3x3, 5x5 on 8x32 or 16x16 tiles; stride 2: 3x3 on 2x32
+#define VSO_TILE_SHAPES(X, PR, BMV) \
+  X(PR, 1, 1, 8, 32, BMV) X(PR, 1, 1, 16, 16, BMV) X(PR, 3, 1, 8, 32, BMV) X(PR, 3, 1, 16, 16, BMV) \
+  X(PR, 5, 1, 8, 32, BMV) X(PR, 5, 1, 16, 16, BMV) X(PR, 3, 2, 2, 32, BMV)
+#define VSO_TILE_ALL(X) \
+  VSO_TILE_SHAPES(X, 0, 32) VSO_TILE_SHAPES(X, 0, 64) VSO_TILE_SHAPES(X, 1, 32) VSO_TILE_SHAPES(X, 1, 64) \
+  VSO_TILE_SHAPES(X, 2, 32) VSO_TILE_SHAPES(X, 2, 64)
+
+bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
+  if (prec < PREC_F32 || prec > PREC_F16) return false;
+  if (c.G != 1 || c.kh != c.kw || c.dh != 1 || c.dw != 1 || c.sh != c.sw || c.pre.w) return false;
+  const int ks = c.kh, s = c.sh;
+  if (!((s == 1 && (ks == 1 || ks == 3 || ks == 5)) || (s == 2 && ks == 3))) return false;
+  ConvTileShape t{};
+  t.prec = prec;
+  t.ks = ks;
+  t.s = s;
+  if (s == 2) { t.th = 2; t.tw = 32; }
+  else if (c.Wo >= 32) { t.th = 8; t.tw = 32; }
+  else { t.th = 16; t.tw = 16; }
+  t.bm = c.M <= 32 ? 32 : 64;
+  t.tiles_x = (c.Wo + t.tw - 1) / t.tw;
+  t.tiles = t.tiles_x * ((c.Ho + t.th - 1) / t.th);
+  t.Mp = (c.M + t.bm - 1) / t.bm * t.bm;
+  t.Cp = (c.C + CK - 1) / CK * CK;
+  const int nch = t.Cp / CK;
+  const long base = (long)t.tiles * (t.Mp / t.bm) * c.N;
+  t.ksplit = 1;
+  if (base < 256 && nch > 1) {
+    int k = (int)std::min<long>(nch, (512 + base - 1) / base);
+    t.cps = (nch + k - 1) / k;
+    t.ksplit = (nch + t.cps - 1) / t.cps;
+  }
+  if (t.ksplit == 1) t.cps = nch;
+  *sh = t;
+  return true;
+}
+
+const char* conv_tile_name(const ConvTileShape& t) {
+  static thread_local char buf[128];
+  std::snprintf(buf, sizeof buf, "void vso::k_conv_tile<%d, %d, %d, %d, %d, %d>(vso::ConvTileParams)", t.prec, t.ks,
+                t.s, t.th, t.tw, t.bm);
+  return buf;
+}
+
+void launch_conv_tile(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s) {
+  const dim3 grid((unsigned)t.tiles, (unsigned)(t.Mp / t.bm), (unsigned)(p.c.N * t.ksplit));
+#define VSO_TILE_CASE(PR, KSV, SV, THV, TWV, BMV)                                                              \
+  if (t.prec == PR && t.ks == KSV && t.s == SV && t.th == THV && t.tw == TWV && t.bm == BMV) {                 \
+    hipLaunchKernelGGL((k_conv_tile<PR, KSV, SV, THV, TWV, BMV>), grid, dim3(256), 0, s, p);                   \
+  } else
+  VSO_TILE_ALL(VSO_TILE_CASE) { std::fprintf(stderr, "vso: no k_conv_tile instance for %s\n", conv_tile_name(t)); }
+#undef VSO_TILE_CASE
+}
+
+void launch_conv_reduce(const ConvTileParams& p, hipStream_t s) {
+  const long total = (long)p.c.N * p.c.M * p.c.Ho * p.c.Wo;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_conv_reduce, dim3(blocks), dim3(256), 0, s, p);
+}
+
+}  // namespace vso

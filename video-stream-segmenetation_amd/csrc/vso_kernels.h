@@ -50,6 +50,24 @@ struct ConvParams {
   DwPre pre;       // k_conv_dwpw only (x is then the depthwise input)
 };
 
+// Operand precision of the dense convolutions (vso_conv.hip; vso_options.conv_precision)
+enum ConvPrec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_F16 = 2 };
+
+// k_conv_tile's plan: tile shape, padding of the packed weights, K split
+struct ConvTileShape {
+  int prec, ks, s, th, tw, bm;
+  int tiles_x, tiles;  // pixel tiles per tile row / per image
+  int Mp, Cp;          // output channels padded to bm, input channels to 32
+  int ksplit, cps;     // workgroups splitting the 32-channel chunks, chunks per split
+};
+
+struct ConvTileParams {
+  ConvParams c;        // geometry, x, y, epilogue
+  const void* wp;      // weights packed [kh*kw][Mp][Cp] in the operand type
+  int Mp, Cp, tiles_x, ksplit, cps;
+  float* part;         // ksplit > 1: partial sums [ksplit][N][M][Ho*Wo]
+};
+
 constexpr int kDwPwMaxC = 256;  // channels a fused depthwise -> 1x1 pair may have
 
 enum BinOp : int { BIN_ADD = 0, BIN_SUB = 1, BIN_MUL = 2, BIN_DIV = 3, BIN_PRELU = 4 };
@@ -139,6 +157,11 @@ struct GemmParams {  // y[b][m][n] = alpha * sum_k A[b][m][k] B[b][k][n] + beta 
 };
 
 const char* conv_kernel_name(const ConvParams& p);
+// false: not a k_conv_tile convolution (grouped, dilated, other kernel sizes)
+bool conv_tile_shape(const ConvParams& p, int prec, ConvTileShape* sh);
+const char* conv_tile_name(const ConvTileShape& t);
+void launch_conv_tile(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s);
+void launch_conv_reduce(const ConvTileParams& p, hipStream_t s);
 void launch_conv(const ConvParams& p, hipStream_t s, const char** name);
 void launch_binary(const BinParams& p, hipStream_t s);
 void launch_unary(const UnaryParams& p, hipStream_t s);

@@ -149,6 +149,23 @@ float half_to_float(uint16_t h) {
 
 // f -> the nearest float16 value (ties to even), as a float: what a Cast to
 // FLOAT16 or a float16-typed result holds (the GPU's __float2half_rn).
+// f -> bfloat16 bits, round to nearest even (NaN stays NaN)
+uint16_t float_to_bf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// f -> float16 bits, round to nearest even (the GPU's __float2half_rn)
+uint16_t float_to_half_bits(float f) {
+  const _Float16 h = (_Float16)f;
+  uint16_t b;
+  std::memcpy(&b, &h, 2);
+  return b;
+}
+
 float round_half(float f) {
   const float a = std::fabs(f);
   if (!(a < INFINITY)) return f;  // inf / nan
@@ -434,6 +451,8 @@ struct Launch {
 
 struct vso_session {
   int device = 0;
+  int conv_precision = 0;  // ConvPrec
+  int tile_convs = 0;      // convolutions planned on k_conv_tile
   hipStream_t stream = nullptr;
   std::string err;
   std::vector<std::string> in_names, out_names;
@@ -980,7 +999,49 @@ struct Planner {
       p.x = pre->second.first;
       p.pre = pre->second.second;
     }
+    ConvTileShape ts{};
+    const double macs = (double)p.N * p.M * p.Ho * p.Wo * p.Cg * p.kh * p.kw;
+    if (!p.pre.w && conv_tile_shape(p, s->conv_precision, &ts) &&
+        (s->conv_precision != PREC_F32 || macs >= kTileMinMacs))
+      return plan_conv_tile(p, ts, wf);
     add(conv_kernel_name(p), [p](hipStream_t st) { launch_conv(p, st, nullptr); });
+    return true;
+  }
+
+  // A dense convolution on k_conv_tile (vso_conv.hip): weights (BatchNorm
+  // folded) packed [tap][Mp][Cp] in the operand type, zero padded; a
+  // partial-sum buffer when the channel chunks are split over workgroups.
+  static constexpr double kTileMinMacs = 8e6;  // f32: smaller convs keep k_conv_small / k_conv_gemm
+  bool plan_conv_tile(const ConvParams& p, const ConvTileShape& ts, const std::vector<float>& wf) {
+    const int taps = p.kh * p.kw;
+    const size_t n = (size_t)taps * ts.Mp * ts.Cp;
+    ConvTileParams tp{};
+    tp.c = p;
+    tp.Mp = ts.Mp; tp.Cp = ts.Cp; tp.tiles_x = ts.tiles_x; tp.ksplit = ts.ksplit; tp.cps = ts.cps;
+    auto src = [&](size_t tap, int m, int c) { return wf[((size_t)m * p.C + c) * taps + tap]; };
+    void* d = nullptr;
+    if (ts.prec == PREC_F32) {
+      std::vector<float> w(n, 0.f);
+      for (int tap = 0; tap < taps; ++tap)
+        for (int m = 0; m < p.M; ++m)
+          for (int c = 0; c < p.C; ++c) w[((size_t)tap * ts.Mp + m) * ts.Cp + c] = src(tap, m, c);
+      if (!dalloc(&d, n * 4) || hipMemcpy(d, w.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return fail("conv weight upload failed");
+    } else {
+      std::vector<uint16_t> w(n, 0);
+      for (int tap = 0; tap < taps; ++tap)
+        for (int m = 0; m < p.M; ++m)
+          for (int c = 0; c < p.C; ++c)
+            w[((size_t)tap * ts.Mp + m) * ts.Cp + c] =
+                ts.prec == PREC_BF16 ? float_to_bf16(src(tap, m, c)) : float_to_half_bits(src(tap, m, c));
+      if (!dalloc(&d, n * 2) || hipMemcpy(d, w.data(), n * 2, hipMemcpyHostToDevice) != hipSuccess)
+        return fail("conv weight upload failed");
+    }
+    tp.wp = d;
+    if (ts.ksplit > 1 && !dalloc(&tp.part, (size_t)ts.ksplit * p.N * p.M * p.Ho * p.Wo * 4)) return false;
+    add(conv_tile_name(ts), [tp, ts](hipStream_t st) { launch_conv_tile(tp, ts, st); });
+    if (ts.ksplit > 1) add("vso::k_conv_reduce(vso::ConvTileParams)", [tp](hipStream_t st) { launch_conv_reduce(tp, st); });
+    s->tile_convs++;
     return true;
   }
 
@@ -1647,9 +1708,25 @@ struct Busy {
 
 extern "C" {
 
+void vso_options_default(vso_options* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof *o);
+  o->conv_precision = VSO_PRECISION_F32;
+}
+
 int vso_create(const void* model, size_t bytes, const int64_t* input_dims, int input_ndim, int device_id,
                vso_session** out) {
+  return vso_create_ex(model, bytes, input_dims, input_ndim, device_id, nullptr, out);
+}
+
+int vso_create_ex(const void* model, size_t bytes, const int64_t* input_dims, int input_ndim, int device_id,
+                  const vso_options* opts, vso_session** out) {
   if (!model || !bytes || !out) return fail_s(nullptr, VSO_E_INVALID_ARG, "null model/out");
+  vso_options o;
+  vso_options_default(&o);
+  if (opts) o = *opts;
+  if (o.conv_precision < VSO_PRECISION_F32 || o.conv_precision > VSO_PRECISION_F16)
+    return fail_s(nullptr, VSO_E_INVALID_ARG, "conv_precision must be VSO_PRECISION_F32, _BF16 or _F16");
   *out = nullptr;
   Graph g;
   std::string err;
@@ -1665,6 +1742,7 @@ int vso_create(const void* model, size_t bytes, const int64_t* input_dims, int i
   }
   vso_session* s = new vso_session();
   s->device = device_id;
+  s->conv_precision = o.conv_precision;
   if (hipSetDevice(device_id) != hipSuccess) {
     delete s;
     return fail_s(nullptr, VSO_E_HIP, "hipSetDevice failed");
@@ -1766,6 +1844,8 @@ int vso_run_device(vso_session* s, const float* const* d_inputs, float* const* d
 }
 
 int vso_launch_count(const vso_session* s) { return s ? (int)s->launches.size() : VSO_E_INVALID_ARG; }
+
+int vso_tile_conv_count(const vso_session* s) { return s ? s->tile_convs : VSO_E_INVALID_ARG; }
 
 int vso_launch_name(const vso_session* s, int k, char* buf, int cap) {
   if (!s || k < 0 || k >= (int)s->launches.size() || !buf || cap < 1) return VSO_E_INVALID_ARG;

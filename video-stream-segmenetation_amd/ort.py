@@ -21,6 +21,11 @@ import numpy as np
 from . import lib as _vss_lib
 
 VSO_OK, VSO_E_INVALID_ARG, VSO_E_HIP, VSO_E_PARSE, VSO_E_UNSUPPORTED, VSO_E_OOM = 0, -1, -2, -3, -4, -5
+PRECISIONS = {"f32": 0, "bf16": 1, "f16": 2}  # vso_options.conv_precision
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("conv_precision", ctypes.c_int), ("reserved", ctypes.c_int * 7)]
 
 _bound = False
 
@@ -39,6 +44,9 @@ def lib():
         I64P = ctypes.POINTER(ctypes.c_int64)
         sig = {
             "vso_create": ([P, S, I64P, I, I, ctypes.POINTER(P)], I),
+            "vso_create_ex": ([P, S, I64P, I, I, ctypes.POINTER(Options), ctypes.POINTER(P)], I),
+            "vso_options_default": ([ctypes.POINTER(Options)], None),
+            "vso_tile_conv_count": ([P], I),
             "vso_destroy": ([P], None),
             "vso_last_error": ([P], ctypes.c_char_p),
             "vso_io_count": ([P, ctypes.POINTER(I), ctypes.POINTER(I)], I),
@@ -67,9 +75,10 @@ def _check(rc, handle=None):
 
 
 class InferenceSession:
-    """One ONNX model on one GPU with a fixed input shape."""
+    """One ONNX model on one GPU with a fixed input shape.  precision: the
+    dense convolutions' operands ("f32" exact, "bf16", "f16"; vso_options)."""
 
-    def __init__(self, model, input_shape=None, device_id: int = 0):
+    def __init__(self, model, input_shape=None, device_id: int = 0, precision: str = "f32"):
         if isinstance(model, (bytes, bytearray)):
             data = bytes(model)
         else:
@@ -81,8 +90,14 @@ class InferenceSession:
         if input_shape is not None:
             nd = len(input_shape)
             dims = (ctypes.c_int64 * nd)(*input_shape)
+        if precision not in PRECISIONS:
+            raise VsoError(VSO_E_INVALID_ARG, f"precision must be one of {sorted(PRECISIONS)}")
+        opts = Options()
+        lib().vso_options_default(ctypes.byref(opts))
+        opts.conv_precision = PRECISIONS[precision]
+        self.precision = precision
         h = ctypes.c_void_p()
-        _check(lib().vso_create(data, len(data), dims, nd, device_id, ctypes.byref(h)), None)
+        _check(lib().vso_create_ex(data, len(data), dims, nd, device_id, ctypes.byref(opts), ctypes.byref(h)), None)
         self._h = h
         ni, no = ctypes.c_int(), ctypes.c_int()
         _check(lib().vso_io_count(self._h, ctypes.byref(ni), ctypes.byref(no)), self._h)
@@ -128,6 +143,10 @@ class InferenceSession:
         """Kernel names of one run, in launch order (as rocprofv3 names them)."""
         n = _check(lib().vso_launch_count(self._h), self._h)
         return [self._name(lib().vso_launch_name, k) for k in range(n)]
+
+    def tile_convs(self) -> int:
+        """Convolutions planned on the LDS-tiled MFMA kernel (k_conv_tile)."""
+        return _check(lib().vso_tile_conv_count(self._h), self._h)
 
     def close(self):
         if getattr(self, "_h", None):
