@@ -43,6 +43,7 @@ __device__ __forceinline__ float epilogue(const Epilogue& e, float v, int ch, lo
       }
     }
   }
+  if (e.act_c_end && ch >= e.act_c_end) return v;
   return act_apply(v, e.act, e.a0, e.a1, e.slope, ch, e.slope_stride);
 }
 

@@ -26,6 +26,7 @@ struct Epilogue {
   // value added is its 2x2 stride-2 max (a MaxPool, fused, then that Pad)
   int res_mode, res_c, res_h, res_w;
   int out_c, out_hw, out_w;  // the output's M, Ho*Wo, Wo (res_mode != 0)
+  int act_c_end;             // > 0: the activation applies to channels < act_c_end only (an IBNorm's BN half)
 };
 
 // A depthwise convolution fused in front of a 1x1 one (k_conv_dwpw): `x` is
@@ -124,6 +125,25 @@ struct RowParams {  // per-row reductions over `inner` contiguous elements (rows
   float eps;
 };
 
+// InstanceNormalization of N*C planes of `inner` elements, plane (n, c) at
+// x + (n * ctot + c0 + c) * inner (c0 / ctot: an IBNorm's InstanceNorm half
+// of a convolution's output, normalised in place), in two parallel passes:
+// k_norm_stats writes each `chunk`-element piece's (mean, M2, count), then
+// k_norm_apply merges a plane's pieces in order (Chan et al.) and normalises
+// its piece, with an optional Relu.
+struct NormParams {
+  const float* x;
+  float* y;  // addressed as x (may be x)
+  int N, C, c0, ctot;
+  long inner;
+  const float* scale;  // [C]
+  const float* shift;
+  float eps;
+  int act;             // ACT_NONE or ACT_RELU
+  float* stats;        // [N*C][chunks][3]
+  int chunks, chunk;
+};
+
 struct AffineParams {  // y = x * scale[c] + shift[c] over NC(HW)
   const float* x;
   float* y;
@@ -168,10 +188,14 @@ void launch_unary(const UnaryParams& p, hipStream_t s);
 void launch_copy(const CopyParams& p, hipStream_t s);
 void launch_pool(const PoolParams& p, hipStream_t s);
 void launch_gap(const RowParams& p, hipStream_t s);
-void launch_inorm(const RowParams& p, hipStream_t s);
+void launch_norm_stats(const NormParams& p, hipStream_t s);
+void launch_norm_apply(const NormParams& p, hipStream_t s);
+constexpr int kNormChunk = 4096;  // elements per k_norm_stats / k_norm_apply workgroup
 void launch_softmax(const RowParams& p, hipStream_t s);
 void launch_affine(const AffineParams& p, hipStream_t s);
 void launch_resize(const ResizeParams& p, hipStream_t s);
 void launch_gemm(const GemmParams& p, hipStream_t s);
+bool gemm_vec(const GemmParams& p);
+const char* gemm_kernel_name(const GemmParams& p);
 
 }  // namespace vso

@@ -533,22 +533,58 @@ __global__ __launch_bounds__(256) void k_gap(RowParams p) {
   if (threadIdx.x == 0) p.y[blockIdx.x] = s / (float)p.inner;
 }
 
-__global__ __launch_bounds__(256) void k_inorm(RowParams p) {
+__global__ __launch_bounds__(256) void k_norm_stats(NormParams p) {
   __shared__ float sh[4];
-  const float* x = p.x + (long)blockIdx.x * p.inner;
-  float* y = p.y + (long)blockIdx.x * p.inner;
+  constexpr int PER = kNormChunk / 256;
+  const int row = blockIdx.y, n = row / p.C, c = row - n * p.C;
+  const float* x = p.x + ((long)n * p.ctot + p.c0 + c) * p.inner;
+  const long beg = (long)blockIdx.x * p.chunk;
+  const int cnt = (int)min((long)p.chunk, p.inner - beg);
+  float v[PER];
   float s = 0.f;
-  for (long i = threadIdx.x; i < p.inner; i += 256) s += x[i];
-  const float mean = block_sum(s, sh) / (float)p.inner;
-  float q = 0.f;
-  for (long i = threadIdx.x; i < p.inner; i += 256) {
-    const float d = x[i] - mean;
-    q += d * d;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    v[i] = e < cnt ? x[beg + e] : 0.f;
+    s += v[i];
   }
-  const float var = block_sum(q, sh) / (float)p.inner;
-  const int c = (int)(blockIdx.x % p.C);
-  const float sc = p.scale[c] / sqrtf(var + p.eps), sf = p.shift[c];
-  for (long i = threadIdx.x; i < p.inner; i += 256) y[i] = (x[i] - mean) * sc + sf;
+  const float mean = block_sum(s, sh) / (float)cnt;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const float d = v[i] - mean;
+    if ((int)threadIdx.x + 256 * i < cnt) q += d * d;
+  }
+  q = block_sum(q, sh);
+  if (threadIdx.x == 0) {
+    float* st = p.stats + ((long)row * p.chunks + blockIdx.x) * 3;
+    st[0] = mean;
+    st[1] = q;
+    st[2] = (float)cnt;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_norm_apply(NormParams p) {
+  const int row = blockIdx.y, n = row / p.C, c = row - n * p.C;
+  const long off = ((long)n * p.ctot + p.c0 + c) * p.inner;
+  // the plane's statistics: its pieces merged in piece order (every thread alike)
+  const float* st = p.stats + (long)row * p.chunks * 3;
+  float mean = st[0], m2 = st[1], cnt = st[2];
+  for (int k = 1; k < p.chunks; ++k) {
+    const float mb = st[3 * k], m2b = st[3 * k + 1], nb = st[3 * k + 2];
+    const float nab = cnt + nb, d = mb - mean;
+    mean += d * (nb / nab);
+    m2 += m2b + d * d * (cnt * nb / nab);
+    cnt = nab;
+  }
+  const float sc = p.scale[c] / sqrtf(m2 / cnt + p.eps), sf = p.shift[c];
+  const long beg = (long)blockIdx.x * p.chunk;
+  const long end = min(beg + p.chunk, p.inner);
+  for (long i = beg + threadIdx.x; i < end; i += 256) {
+    float y = (p.x[off + i] - mean) * sc + sf;
+    if (p.act == ACT_RELU) y = fmaxf(y, 0.f);
+    p.y[off + i] = y;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_softmax(RowParams p) {
@@ -613,21 +649,89 @@ __global__ __launch_bounds__(256) void k_resize(ResizeParams p) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_gemm(GemmParams p) {
-  const long total = (long)p.batch * p.M * p.N;
-  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
-    const int nn = (int)(o % p.N);
-    const long t = o / p.N;
-    const int m = (int)(t % p.M);
-    const int b = (int)(t / p.M);
-    const float* a = p.a + b * p.sab + m * p.sam;
-    const float* bb = p.b + b * p.sbb + nn * p.sbn;
-    float acc = 0.f;
-    for (int k = 0; k < p.K; ++k) acc = __builtin_fmaf(a[k * p.sak], bb[k * p.sbk], acc);
-    float v = p.alpha * acc;
-    if (p.c) v += p.beta * p.c[m * p.scm + nn * p.scn];
-    p.y[o] = act_apply(v, p.ep.act, p.ep.a0, p.ep.a1, p.ep.slope, nn, p.ep.slope_stride);
+// y[b][m][n] = act(alpha * sum_k A[b][m][k] B[b][k][n] + beta * c[m][n]) on
+// v_mfma_f32_16x16x4_f32: one workgroup per 16 x 16 output tile, its four
+// waves each taking a quarter of K (partial tiles summed through LDS in wave
+// order: deterministic).  VEC (A rows and B columns contiguous in k — Gemm
+// transB, MatMul with a constant B stored transposed, MatMulNBits' [N][K]
+// weights — K % 4 == 0, 16-byte aligned): lane (r, g) loads float4
+// A[m0 + r][k + 4g ..] and B[k + 4g ..][n0 + r] and issues 4 MFMAs, element e
+// of both in MFMA e (every k once per 16); 8 such loads in flight per lane.
+// Otherwise one element per lane per MFMA.  The SE blocks' [1, 1280] x
+// [1280, 320] layers ran 214 us on the old one-thread-per-output kernel.
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_gemm(GemmParams p, int tiles_m, int tiles_n) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int tile = blockIdx.x;
+  const int bt = tile / (tiles_m * tiles_n), rem = tile - bt * tiles_m * tiles_n;
+  const int m0 = (rem / tiles_n) * 16, n0 = (rem % tiles_n) * 16;
+  const int m = m0 + r, nn = n0 + r;
+  const bool m_ok = m < p.M, n_ok = nn < p.N;
+  const float* a = p.a + bt * p.sab + (long)(m_ok ? m : 0) * p.sam;
+  const float* b = p.b + bt * p.sbb + (long)(n_ok ? nn : 0) * p.sbn;
+  const int kq = VEC ? ((p.K + 63) / 64) * 16 : ((p.K + 15) / 16) * 4;  // this wave's quarter of K
+  const int kbeg = wave * kq, kend = min(p.K, kbeg + kq);
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  if (VEC) {
+    constexpr int U = 8;
+    for (int k0 = kbeg; k0 < kend; k0 += 16 * U) {
+      f4 av[U], bv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + 16 * u + 4 * g;
+        const bool in = k < kend;
+        av[u] = (in && m_ok) ? *reinterpret_cast<const f4*>(a + k) : f4{0.f, 0.f, 0.f, 0.f};
+        bv[u] = (in && n_ok) ? *reinterpret_cast<const f4*>(b + k) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + 16 * u >= kend) break;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][e], bv[u][e], acc, 0, 0, 0);
+      }
+    }
+  } else {
+    constexpr int U = 8;
+    for (int k0 = kbeg; k0 < kend; k0 += 4 * U) {
+      float av[U], bv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + 4 * u + g;
+        const bool in = k < kend;
+        av[u] = (in && m_ok) ? a[(long)k * p.sak] : 0.f;
+        bv[u] = (in && n_ok) ? b[(long)k * p.sbk] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + 4 * u >= kend) break;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+      }
+    }
   }
+  __shared__ f4 part[4][64];
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0) return;
+  acc = part[0][lane];
+#pragma unroll
+  for (int w2 = 1; w2 < 4; ++w2) acc += part[w2][lane];
+  // acc[v] = D[row m0 + 4g + v][column n0 + r]
+  if (!n_ok) return;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int mm = m0 + 4 * g + v;
+    if (mm >= p.M) continue;
+    float y = p.alpha * acc[v];
+    if (p.c) y += p.beta * p.c[mm * p.scm + nn * p.scn];
+    p.y[((long)bt * p.M + mm) * p.N + nn] = act_apply(y, p.ep.act, p.ep.a0, p.ep.a1, p.ep.slope, nn, p.ep.slope_stride);
+  }
+}
+
+bool gemm_vec(const GemmParams& p) {
+  const auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  return p.sak == 1 && p.sbk == 1 && p.K % 4 == 0 && p.sam % 4 == 0 && p.sbn % 4 == 0 && p.sab % 4 == 0 &&
+         p.sbb % 4 == 0 && al(p.a) && al(p.b);
 }
 
 void launch_binary(const BinParams& p, hipStream_t s) {
@@ -645,8 +749,11 @@ void launch_pool(const PoolParams& p, hipStream_t s) {
 void launch_gap(const RowParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_gap, dim3((unsigned)p.rows), dim3(256), 0, s, p);
 }
-void launch_inorm(const RowParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_inorm, dim3((unsigned)p.rows), dim3(256), 0, s, p);
+void launch_norm_stats(const NormParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_norm_stats, dim3((unsigned)p.chunks, (unsigned)(p.N * p.C)), dim3(256), 0, s, p);
+}
+void launch_norm_apply(const NormParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_norm_apply, dim3((unsigned)p.chunks, (unsigned)(p.N * p.C)), dim3(256), 0, s, p);
 }
 void launch_softmax(const RowParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_softmax, dim3((unsigned)p.rows), dim3(256), 0, s, p);
@@ -658,7 +765,15 @@ void launch_resize(const ResizeParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_resize, dim3(grid_for((long)p.N * p.C * p.Ho * p.Wo)), dim3(256), 0, s, p);
 }
 void launch_gemm(const GemmParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_gemm, dim3(grid_for((long)p.batch * p.M * p.N)), dim3(256), 0, s, p);
+  const int tm = (p.M + 15) / 16, tn = (p.N + 15) / 16;
+  const dim3 grid((unsigned)(tm * tn * p.batch));
+  if (gemm_vec(p)) hipLaunchKernelGGL(k_gemm<true>, grid, dim3(256), 0, s, p, tm, tn);
+  else hipLaunchKernelGGL(k_gemm<false>, grid, dim3(256), 0, s, p, tm, tn);
+}
+
+const char* gemm_kernel_name(const GemmParams& p) {
+  return gemm_vec(p) ? "void vso::k_gemm<true>(vso::GemmParams, int, int)"
+                     : "void vso::k_gemm<false>(vso::GemmParams, int, int)";
 }
 
 }  // namespace vso

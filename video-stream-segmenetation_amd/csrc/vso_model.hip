@@ -922,6 +922,26 @@ struct Planner {
     size_t last = ni;
     Epilogue ep{};
     int c1 = sole_consumer(out, last);
+    const auto ib = ibn.find(ni);
+    if (ib != ibn.end()) {  // an IBNorm: BN folded into channels < nb, Relu there; the InstanceNorm after the launch
+      const IbnFuse& f = ib->second;
+      const Node& bn = g.nodes[f.bn];
+      Value *sc = val(bn.in[1]), *bb = val(bn.in[2]), *mu = val(bn.in[3]), *vr = val(bn.in[4]);
+      const double eps = bn.af("epsilon", 1e-5f);
+      const int64_t per = (int64_t)p.Cg * p.kh * p.kw;
+      for (int m = 0; m < f.nb; ++m) {
+        const double a = sc->c.f[m] / std::sqrt((double)vr->c.f[m] + eps);
+        for (int64_t k = 0; k < per; ++k) wf[m * per + k] = (float)(wf[m * per + k] * a);
+        bias[m] = (float)((bias[m] - mu->c.f[m]) * a + bb->c.f[m]);
+      }
+      has_bias = true;
+      if (f.relu >= 0) {
+        ep.act = ACT_RELU;
+        ep.act_c_end = f.nb;
+      }
+      out = f.out;
+      c1 = -1;
+    }
     if (c1 >= 0 && g.nodes[c1].op == "BatchNormalization") {
       const Node& bn = g.nodes[c1];
       Value *sc = val(bn.in[1]), *bb = val(bn.in[2]), *mu = val(bn.in[3]), *vr = val(bn.in[4]);
@@ -988,7 +1008,7 @@ struct Planner {
     p.x = dptr(*x);
     if (!set_runtime(out, oshape)) return false;
     p.y = dptr(vals[out]);
-    if (p.G == p.C && p.G == p.M && !ep.res && p.C <= kDwPwMaxC && feeds_pointwise(out, last, p.M)) {
+    if (p.G == p.C && p.G == p.M && !ep.res && ib == ibn.end() && p.C <= kDwPwMaxC && feeds_pointwise(out, last, p.M)) {
       pending_dw[out] = {p.x, DwPre{p.w, p.H, p.W, p.kh, p.kw, p.sh, p.sw, p.dh, p.dw, p.pt, p.pl, ep}};
       return true;  // no launch: its 1x1 consumer computes it (k_conv_dwpw)
     }
@@ -1002,9 +1022,17 @@ struct Planner {
     ConvTileShape ts{};
     const double macs = (double)p.N * p.M * p.Ho * p.Wo * p.Cg * p.kh * p.kw;
     if (!p.pre.w && conv_tile_shape(p, s->conv_precision, &ts) &&
-        (s->conv_precision != PREC_F32 || macs >= kTileMinMacs))
-      return plan_conv_tile(p, ts, wf);
-    add(conv_kernel_name(p), [p](hipStream_t st) { launch_conv(p, st, nullptr); });
+        (s->conv_precision != PREC_F32 || macs >= kTileMinMacs)) {
+      if (!plan_conv_tile(p, ts, wf)) return false;
+    } else {
+      add(conv_kernel_name(p), [p](hipStream_t st) { launch_conv(p, st, nullptr); });
+    }
+    if (ib != ibn.end()) {
+      const IbnFuse& f = ib->second;
+      const Node& inn = g.nodes[f.inorm];
+      return plan_norm(p.y, p.y, p.N, p.M - f.nb, f.nb, p.M, (int64_t)p.Ho * p.Wo, inn, val(inn.in[1]),
+                       val(inn.in[2]), f.relu >= 0 ? ACT_RELU : ACT_NONE);
+    }
     return true;
   }
 
@@ -1239,19 +1267,12 @@ struct Planner {
     }
     if (op == "InstanceNormalization") {
       if (!in[1]->is_const || !in[2]->is_const) return fail("InstanceNormalization: constant scale/B only");
-      RowParams p{};
-      p.x = dptr(*x);
-      p.rows = xs[0] * xs[1];
-      p.inner = 1;
-      for (size_t d = 2; d < xs.size(); ++d) p.inner *= xs[d];
-      p.C = (int)xs[1];
-      p.eps = nd.af("epsilon", 1e-5f);
-      p.scale = upload(in[1]->c);
-      p.shift = upload(in[2]->c);
+      if (xs.size() < 3) return fail("InstanceNormalization: rank >= 3 only");
+      int64_t inner = 1;
+      for (size_t d = 2; d < xs.size(); ++d) inner *= xs[d];
       if (!set_runtime(nd.out[0], xs)) return false;
-      p.y = dptr(vals[nd.out[0]]);
-      add("vso::k_inorm(vso::RowParams)", [p](hipStream_t st) { launch_inorm(p, st); });
-      return true;
+      return plan_norm(dptr(*x), dptr(vals[nd.out[0]]), (int)xs[0], (int)xs[1], 0, (int)xs[1], inner, nd, in[1], in[2],
+                       ACT_NONE);
     }
     if (op == "BatchNormalization") {
       for (int k = 1; k <= 4; ++k)
@@ -1492,11 +1513,20 @@ struct Planner {
         os.push_back(p.N);
       }
       p.a = operand(*a);
-      p.b = operand(*b);
+      if (op == "MatMul" && b->is_const && p.sbb == 0) {
+        // a constant B stored transposed ([N][K]): k contiguous for k_gemm<true>
+        std::vector<float> bt((size_t)p.K * p.N);
+        for (int k = 0; k < p.K; ++k)
+          for (int n2 = 0; n2 < p.N; ++n2) bt[(size_t)n2 * p.K + k] = b->c.f[(size_t)k * p.N + n2];
+        p.b = upload_vec(bt);
+        p.sbk = 1; p.sbn = p.K;
+      } else {
+        p.b = operand(*b);
+      }
       if (!p.a || !p.b) return false;
       if (!set_runtime(nd.out[0], os)) return false;
       p.y = dptr(vals[nd.out[0]]);
-      add("vso::k_gemm(vso::GemmParams)", [p](hipStream_t st) { launch_gemm(p, st); });
+      add(gemm_kernel_name(p), [p](hipStream_t st) { launch_gemm(p, st); });
       return true;
     }
     if (op == "MatMulNBits") return plan_matmul_nbits(nd, in);
@@ -1554,7 +1584,7 @@ struct Planner {
     os.push_back(N);
     if (!set_runtime(nd.out[0], os)) return false;
     p.y = dptr(vals[nd.out[0]]);
-    add("vso::k_gemm(vso::GemmParams)", [p](hipStream_t st) { launch_gemm(p, st); });
+    add(gemm_kernel_name(p), [p](hipStream_t st) { launch_gemm(p, st); });
     return true;
   }
 
@@ -1563,6 +1593,103 @@ struct Planner {
       for (const std::string& o : g.nodes[k].out)
         if (o == name) return (int)k;
     return -1;
+  }
+
+  // InstanceNormalization (node `nd`, constant scale / B) of planes c0 .. c0+C-1
+  // of an [N][ctot][inner] tensor, as k_norm_stats + k_norm_apply
+  bool plan_norm(const float* x, float* y, int N, int C, int c0, int ctot, int64_t inner, const Node& nd, Value* sc,
+                 Value* sh, int act) {
+    if (sc->c.numel() != C || sh->c.numel() != C) return fail("InstanceNormalization '" + nd.name + "': scale/B size");
+    NormParams p{};
+    p.x = x; p.y = y;
+    p.N = N; p.C = C; p.c0 = c0; p.ctot = ctot;
+    p.inner = inner;
+    p.scale = upload(sc->c);
+    p.shift = upload(sh->c);
+    p.eps = nd.af("epsilon", 1e-5f);
+    p.act = act;
+    p.chunk = kNormChunk;
+    p.chunks = (int)((inner + kNormChunk - 1) / kNormChunk);
+    if (!p.scale || !p.shift || !dalloc(&p.stats, (size_t)N * C * std::max(p.chunks, 1) * 3 * 4)) return false;
+    if (inner == 0 || N * C == 0) return true;
+    add("vso::k_norm_stats(vso::NormParams)", [p](hipStream_t st) { launch_norm_stats(p, st); });
+    add("vso::k_norm_apply(vso::NormParams)", [p](hipStream_t st) { launch_norm_apply(p, st); });
+    return true;
+  }
+
+  // MODNet's IBNorm (Conv2dIBNormRelu; the authors' src/models/modnet.py):
+  //   c = Conv(x); Concat(BN(Slice(c, 0:nb)), InstanceNorm(Slice(c, nb:M)), axis 1) [-> Relu]
+  // with every intermediate used once.  The conv writes the concatenation
+  // directly: the BatchNorm folded into its first nb output channels' weights,
+  // the Relu applied to those channels in its epilogue; the InstanceNorm then
+  // normalises channels nb .. M-1 in place (+ Relu).  Seven launches -> three.
+  struct IbnFuse {
+    int nb;
+    size_t bn, inorm, concat;
+    int relu;  // node index or -1
+    std::string out;
+  };
+  std::map<size_t, IbnFuse> ibn;  // conv node -> its IBNorm
+
+  bool slice_range(const Node& nd, int64_t C, int64_t* b, int64_t* e) {
+    if (nd.op != "Slice" || nd.in.size() < 3) return false;
+    auto cint = [&](size_t k, std::vector<int64_t>* out) {
+      if (k >= nd.in.size() || nd.in[k].empty()) return false;
+      Value* v = val(nd.in[k]);
+      if (!v || !v->is_const || !v->c.is_int) return false;
+      *out = v->c.i;
+      return true;
+    };
+    std::vector<int64_t> st, en, ax{0}, sp{1};
+    if (!cint(1, &st) || !cint(2, &en) || st.size() != 1 || en.size() != 1) return false;
+    if (nd.in.size() > 3 && !nd.in[3].empty() && !cint(3, &ax)) return false;
+    if (nd.in.size() > 4 && !nd.in[4].empty() && !cint(4, &sp)) return false;
+    if (ax.size() != 1 || ax[0] != 1 || sp.size() != 1 || sp[0] != 1) return false;
+    *b = std::clamp<int64_t>(st[0] < 0 ? st[0] + C : st[0], 0, C);
+    *e = std::clamp<int64_t>(en[0] < 0 ? en[0] + C : en[0], 0, C);
+    return true;
+  }
+
+  void find_ibnorm() {
+    for (size_t k = 0; k < g.nodes.size(); ++k) {
+      const Node& cat = g.nodes[k];
+      if (cat.op != "Concat" || cat.in.size() != 2 || cat.ai("axis", 0) != 1) continue;
+      const int pbn = producer(cat.in[0]), pin = producer(cat.in[1]);
+      if (pbn < 0 || pin < 0 || g.nodes[pbn].op != "BatchNormalization" || g.nodes[pin].op != "InstanceNormalization")
+        continue;
+      if (sole_consumer(cat.in[0], (size_t)pbn) != (int)k || sole_consumer(cat.in[1], (size_t)pin) != (int)k) continue;
+      const Node &bn = g.nodes[pbn], &inn = g.nodes[pin];
+      bool consts = bn.in.size() == 5 && inn.in.size() == 3;
+      for (size_t q = 1; consts && q < bn.in.size(); ++q) consts = val(bn.in[q]) && val(bn.in[q])->is_const;
+      for (size_t q = 1; consts && q < inn.in.size(); ++q) consts = val(inn.in[q]) && val(inn.in[q])->is_const;
+      if (!consts) continue;
+      const int sa = producer(bn.in[0]), sb = producer(inn.in[0]);
+      if (sa < 0 || sb < 0 || sole_consumer(bn.in[0], (size_t)sa) != pbn || sole_consumer(inn.in[0], (size_t)sb) != pin)
+        continue;
+      const Node &la = g.nodes[sa], &lb = g.nodes[sb];
+      if (la.op != "Slice" || lb.op != "Slice" || la.in[0] != lb.in[0]) continue;
+      const std::string& c = la.in[0];
+      const int pc = producer(c);
+      if (pc < 0 || g.nodes[pc].op != "Conv" || consumers[c] != 2) continue;
+      bool is_out = false;
+      for (const IO& o : g.outputs) is_out = is_out || o.name == c;
+      Value* wv = val(g.nodes[pc].in[1]);
+      if (is_out || !wv || !wv->is_const || wv->c.dims.size() != 4) continue;
+      const int64_t M = wv->c.dims[0];
+      int64_t b0, e0, b1, e1;
+      if (!slice_range(la, M, &b0, &e0) || !slice_range(lb, M, &b1, &e1)) continue;
+      if (b0 != 0 || e0 != b1 || e1 != M || e0 <= 0 || e0 >= M) continue;
+      if (val(bn.in[1])->c.numel() != e0 || val(inn.in[1])->c.numel() != M - e0) continue;
+      IbnFuse f{(int)e0, (size_t)pbn, (size_t)pin, k, -1, cat.out[0]};
+      const int r = sole_consumer(cat.out[0], k);
+      if (r >= 0 && g.nodes[r].op == "Relu") {
+        f.relu = r;
+        f.out = g.nodes[r].out[0];
+      }
+      for (size_t q : {(size_t)sa, (size_t)sb, (size_t)pbn, (size_t)pin, k}) done.insert(q);
+      if (f.relu >= 0) done.insert((size_t)f.relu);
+      ibn[(size_t)pc] = f;
+    }
   }
 
   // MaxPool(2x2, stride 2, unpadded, floor) -> [Pad: zeros appended on the
@@ -1641,6 +1768,7 @@ struct Planner {
       s->in_bufs.push_back(vals[g.inputs[k].name].buf);
     }
     find_residual_fusions();
+    find_ibnorm();
     for (size_t k = 0; k < g.nodes.size(); ++k) {
       if (done.count(k)) continue;
       if (!plan_node(k)) return false;
