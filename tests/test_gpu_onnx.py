@@ -78,7 +78,8 @@ def test_reference_mediapipe_models(ort, key):
 def test_conv_tile_forms(ort, precision):
     """k_conv_tile against the oracle with the same operand rounding
     (onnx_ref.run(conv_operands=...)): every convolution reads a graph input,
-    so the only difference left is f32 (GPU) vs f64 (oracle) accumulation."""
+    so the only difference left is f32 (GPU) vs f64 (oracle) accumulation.
+    Run twice: the split-K arrival counters reset themselves (bitwise equal)."""
     data = M.conv_tiles()
     rng = np.random.default_rng(5)
     feeds = {"x": rng.standard_normal((2, 40, 37, 70)).astype(np.float32),
@@ -86,10 +87,15 @@ def test_conv_tile_forms(ort, precision):
     want = R.run(R.load(data), feeds, conv_operands=None if precision == "f32" else precision)
     with ort.InferenceSession(data, precision=precision) as s:
         got = s.run(feeds)
+        again = s.run(feeds)
+        for k in got:
+            assert np.array_equal(got[k], again[k])
         names = s.launches()
         print(precision, s.tile_convs(), "tiled:", [n for n in names if "conv" in n])
         assert s.tile_convs() == (6 if precision == "f32" else 7)  # f32: the 1x1 (< 8 MMAC) stays on k_conv_small
-        assert any("k_conv_reduce" in n for n in names)
+        # x2 (9x16, batch 2) runs on 4x16 tiles with its 7 chunks split over 7
+        # workgroups (the last to arrive adds the partials): conv_tile_shape
+        assert any("k_conv_tile" in n and ", 4, 16, 64>" in n for n in names)
     _check(got, want, f"conv_tiles {precision}")
 
 

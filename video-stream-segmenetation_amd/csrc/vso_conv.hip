@@ -22,9 +22,18 @@
 //     32 channels, 16x the rate), operands rounded to nearest-even, f32
 //     accumulation;
 //   * bias, residual and activation fused into the epilogue (vso_device.h);
-//     when the grid would be too small to fill 256 CUs the channel chunks are
-//     split over workgroups (ksplit) and k_conv_reduce adds the partial sums
-//     in a fixed order (deterministic) and applies the epilogue.
+//   * the tile (8x32 .. 2x32 / 16x16 .. 4x16 pixels) is the largest that
+//     still gives ~4 workgroups per CU: at batch 1 MODNet's layers are small
+//     (36864 pixels x 64 channels), and a workgroup's global-load latency is
+//     only hidden by other workgroups on the same CU;
+//   * when even the smallest tile leaves the chip half empty the 32-channel
+//     chunks are split over ksplit workgroups: each writes its partial sums,
+//     and the last of them to arrive (a per-output-block arrival counter)
+//     adds all ksplit partials in split order — deterministic — and applies
+//     the epilogue, so no reduction launch is needed.
+//
+// Compiled once per operand precision (-DVSO_CONV_PREC=0/1/2: the template
+// instances) and once with -DVSO_CONV_DISPATCH (planning and dispatch).
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
@@ -88,6 +97,7 @@ template <> __device__ __forceinline__ f4 mma32<PREC_F16>(const uint4* a, const 
                                                  0, 0);
 }
 
+#ifdef VSO_CONV_PREC
 template <int PREC, int KS, int S, int TH, int TW, int BM>
 __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   using T = typename Elem<PREC>::T;
@@ -100,7 +110,7 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   constexpr int PER = (ITEMS + 255) / 256;
   constexpr int NB = TH * TW / 16, PBW = NB / 4;   // 16-pixel blocks per tile / per wave
   constexpr int MI = BM / 16;
-  static_assert(NB % 4 == 0 && TW % 16 == 0, "tile");
+  static_assert(NB % 4 == 0 && TW % 16 == 0, "tile: a multiple of 64 pixels, rows of 16");
   __shared__ uint4 xs[NPIX * QS];
 
   const ConvParams& c = p.c;
@@ -189,6 +199,50 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
 
   // acc[i][j][v] = out channel m0 + 16 i + 4 g + v, pixel r of block j
   const int P = c.Ho * c.Wo;
+  if (p.ksplit > 1) {
+    // the partial tile in accumulator order: [output block][split][i, j][thread] as
+    // f4, stored write-through (8-byte agent-scope stores: sc1) so the last
+    // workgroup to arrive — on any XCD — reads them from memory with sc1 loads
+    // (MI355X_MICROARCH.md, hand-off table row 1: no fences)
+    const long blk = ((long)n * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    uint64_t* part = reinterpret_cast<uint64_t*>(p.part) + (blk * p.ksplit + kz) * (MI * PBW * 256 * 2);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < PBW; ++j) {
+        const uint64_t lo = (uint64_t)__float_as_uint(acc[i][j][0]) | ((uint64_t)__float_as_uint(acc[i][j][1]) << 32);
+        const uint64_t hi = (uint64_t)__float_as_uint(acc[i][j][2]) | ((uint64_t)__float_as_uint(acc[i][j][3]) << 32);
+        uint64_t* q = part + ((i * PBW + j) * 256 + tid) * 2;
+        __hip_atomic_store(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int last;
+    __syncthreads();
+    if (tid == 0) {
+      int* cnt = p.counters + blk;
+      const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == p.ksplit - 1;
+      if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next run
+    }
+    __syncthreads();
+    if (!last) return;
+    const uint64_t* base = reinterpret_cast<const uint64_t*>(p.part) + blk * p.ksplit * (MI * PBW * 256 * 2);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < PBW; ++j) {
+        f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < p.ksplit; ++k) {  // split order: deterministic
+          const uint64_t* q = base + ((k * MI * PBW + i * PBW + j) * 256 + tid) * 2;
+          const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sum += f4{__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)),
+                    __uint_as_float((uint32_t)hi), __uint_as_float((uint32_t)(hi >> 32))};
+        }
+        acc[i][j] = sum;
+      }
+  }
 #pragma unroll
   for (int j = 0; j < PBW; ++j) {
     const int b = wave * PBW + j;
@@ -201,39 +255,41 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
       for (int v = 0; v < 4; ++v) {
         const int ch = m0 + 16 * i + 4 * g + v;
         if (ch >= c.M) continue;
-        if (p.ksplit > 1) {
-          p.part[(((long)kz * c.N + n) * c.M + ch) * P + pix] = acc[i][j][v];
-        } else {
-          const long o = ((long)n * c.M + ch) * P + pix;
-          c.y[o] = epilogue(c.ep, acc[i][j][v], ch, o, n, pix);
-        }
+        const long o = ((long)n * c.M + ch) * P + pix;
+        c.y[o] = epilogue(c.ep, acc[i][j][v], ch, o, n, pix);
       }
   }
 }
+#endif
 
-// y = epilogue(sum over the ksplit partial sums, in split order)
-__global__ __launch_bounds__(256) void k_conv_reduce(ConvTileParams p) {
-  const ConvParams& c = p.c;
-  const int P = c.Ho * c.Wo;
-  const long total = (long)c.N * c.M * P;
-  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
-    float s = p.part[o];
-    for (int k = 1; k < p.ksplit; ++k) s += p.part[(long)k * total + o];
-    const int pix = (int)(o % P);
-    const long nc = o / P;
-    c.y[o] = epilogue(c.ep, s, (int)(nc % c.M), o, (int)(nc / c.M), pix);
-  }
-}
-
-// ---- instantiations and dispatch --------------------------------------------
-// (KS, S, TH, TW): stride 1: 1x1, 3x3, 5x5 on 8x32 or 16x16 tiles; stride 2: 3x3 on 2x32
+// ---- instantiations (one precision per compile unit) and dispatch ---------------
+// (KS, S, TH, TW): stride 1 (1x1, 3x3, 5x5) on 8x32, 4x32, 2x32, 16x16, 4x16 tiles;
+// stride 2 (3x3) on 2x32, 4x16
+#define VSO_TILE_SHAPES_S1(X, PR, K, BMV) \
+  X(PR, K, 1, 8, 32, BMV) X(PR, K, 1, 4, 32, BMV) X(PR, K, 1, 2, 32, BMV) X(PR, K, 1, 16, 16, BMV) X(PR, K, 1, 4, 16, BMV)
 #define VSO_TILE_SHAPES(X, PR, BMV) \
-  X(PR, 1, 1, 8, 32, BMV) X(PR, 1, 1, 16, 16, BMV) X(PR, 3, 1, 8, 32, BMV) X(PR, 3, 1, 16, 16, BMV) \
-  X(PR, 5, 1, 8, 32, BMV) X(PR, 5, 1, 16, 16, BMV) X(PR, 3, 2, 2, 32, BMV)
-#define VSO_TILE_ALL(X) \
-  VSO_TILE_SHAPES(X, 0, 32) VSO_TILE_SHAPES(X, 0, 64) VSO_TILE_SHAPES(X, 1, 32) VSO_TILE_SHAPES(X, 1, 64) \
-  VSO_TILE_SHAPES(X, 2, 32) VSO_TILE_SHAPES(X, 2, 64)
+  VSO_TILE_SHAPES_S1(X, PR, 1, BMV) VSO_TILE_SHAPES_S1(X, PR, 3, BMV) VSO_TILE_SHAPES_S1(X, PR, 5, BMV) \
+  X(PR, 3, 2, 2, 32, BMV) X(PR, 3, 2, 4, 16, BMV)
 
+template <int PREC>
+void launch_conv_tile_prec(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s);
+
+#ifdef VSO_CONV_PREC
+template <>
+void launch_conv_tile_prec<VSO_CONV_PREC>(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s) {
+  const dim3 grid((unsigned)t.tiles, (unsigned)(t.Mp / t.bm), (unsigned)(p.c.N * t.ksplit));
+#define VSO_TILE_CASE(PR, KSV, SV, THV, TWV, BMV)                                              \
+  if (t.ks == KSV && t.s == SV && t.th == THV && t.tw == TWV && t.bm == BMV) {                  \
+    hipLaunchKernelGGL((k_conv_tile<PR, KSV, SV, THV, TWV, BMV>), grid, dim3(256), 0, s, p);   \
+  } else
+  VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 32) VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 64) {
+    std::fprintf(stderr, "vso: no k_conv_tile instance for %s\n", conv_tile_name(t));
+  }
+#undef VSO_TILE_CASE
+}
+#endif
+
+#ifdef VSO_CONV_DISPATCH
 bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   if (prec < PREC_F32 || prec > PREC_F16) return false;
   if (c.G != 1 || c.kh != c.kw || c.dh != 1 || c.dw != 1 || c.sh != c.sw || c.pre.w) return false;
@@ -243,48 +299,53 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   t.prec = prec;
   t.ks = ks;
   t.s = s;
-  if (s == 2) { t.th = 2; t.tw = 32; }
-  else if (c.Wo >= 32) { t.th = 8; t.tw = 32; }
-  else { t.th = 16; t.tw = 16; }
   t.bm = c.M <= 32 ? 32 : 64;
-  t.tiles_x = (c.Wo + t.tw - 1) / t.tw;
-  t.tiles = t.tiles_x * ((c.Ho + t.th - 1) / t.th);
   t.Mp = (c.M + t.bm - 1) / t.bm * t.bm;
   t.Cp = (c.C + CK - 1) / CK * CK;
+  // candidate tiles, largest first: the first giving >= kWant workgroups wins,
+  // else the smallest
+  static const int s1w[][2] = {{8, 32}, {4, 32}, {2, 32}}, s1n[][2] = {{16, 16}, {4, 16}};
+  static const int s2w[][2] = {{2, 32}}, s2n[][2] = {{4, 16}};
+  const int(*cand)[2];
+  int nc;
+  if (s == 1) { cand = c.Wo >= 32 ? s1w : s1n; nc = c.Wo >= 32 ? 3 : 2; }
+  else { cand = c.Wo >= 32 ? s2w : s2n; nc = 1; }
+  constexpr long kWant = 1024;  // ~4 workgroups per CU
+  long wgs = 0;
+  for (int k = 0; k < nc; ++k) {
+    t.th = cand[k][0];
+    t.tw = cand[k][1];
+    t.tiles_x = (c.Wo + t.tw - 1) / t.tw;
+    t.tiles = t.tiles_x * ((c.Ho + t.th - 1) / t.th);
+    wgs = (long)t.tiles * (t.Mp / t.bm) * c.N;
+    if (wgs >= kWant) break;
+  }
   const int nch = t.Cp / CK;
-  const long base = (long)t.tiles * (t.Mp / t.bm) * c.N;
   t.ksplit = 1;
-  if (base < 256 && nch > 1) {
-    int k = (int)std::min<long>(nch, (512 + base - 1) / base);
+  t.cps = nch;
+  if (wgs < kWant / 2 && nch > 1) {
+    const int k = (int)std::min<long>(nch, (kWant + wgs - 1) / wgs);
     t.cps = (nch + k - 1) / k;
     t.ksplit = (nch + t.cps - 1) / t.cps;
   }
-  if (t.ksplit == 1) t.cps = nch;
   *sh = t;
   return true;
 }
 
+void launch_conv_tile(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s) {
+  if (t.prec == PREC_F32) launch_conv_tile_prec<PREC_F32>(p, t, s);
+  else if (t.prec == PREC_BF16) launch_conv_tile_prec<PREC_BF16>(p, t, s);
+  else launch_conv_tile_prec<PREC_F16>(p, t, s);
+}
+#endif
+
+#ifdef VSO_CONV_DISPATCH
 const char* conv_tile_name(const ConvTileShape& t) {
   static thread_local char buf[128];
   std::snprintf(buf, sizeof buf, "void vso::k_conv_tile<%d, %d, %d, %d, %d, %d>(vso::ConvTileParams)", t.prec, t.ks,
                 t.s, t.th, t.tw, t.bm);
   return buf;
 }
-
-void launch_conv_tile(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s) {
-  const dim3 grid((unsigned)t.tiles, (unsigned)(t.Mp / t.bm), (unsigned)(p.c.N * t.ksplit));
-#define VSO_TILE_CASE(PR, KSV, SV, THV, TWV, BMV)                                                              \
-  if (t.prec == PR && t.ks == KSV && t.s == SV && t.th == THV && t.tw == TWV && t.bm == BMV) {                 \
-    hipLaunchKernelGGL((k_conv_tile<PR, KSV, SV, THV, TWV, BMV>), grid, dim3(256), 0, s, p);                   \
-  } else
-  VSO_TILE_ALL(VSO_TILE_CASE) { std::fprintf(stderr, "vso: no k_conv_tile instance for %s\n", conv_tile_name(t)); }
-#undef VSO_TILE_CASE
-}
-
-void launch_conv_reduce(const ConvTileParams& p, hipStream_t s) {
-  const long total = (long)p.c.N * p.c.M * p.c.Ho * p.c.Wo;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(k_conv_reduce, dim3(blocks), dim3(256), 0, s, p);
-}
+#endif
 
 }  // namespace vso

@@ -66,7 +66,8 @@ struct ConvTileParams {
   ConvParams c;        // geometry, x, y, epilogue
   const void* wp;      // weights packed [kh*kw][Mp][Cp] in the operand type
   int Mp, Cp, tiles_x, ksplit, cps;
-  float* part;         // ksplit > 1: partial sums [ksplit][N][M][Ho*Wo]
+  float* part;         // ksplit > 1: partial tiles [output block][ksplit][bm/16][th*tw/64][256 threads] as f4
+  int* counters;       // ksplit > 1: arrivals per output block [N][M tiles][tiles], zero between runs
 };
 
 constexpr int kDwPwMaxC = 256;  // channels a fused depthwise -> 1x1 pair may have
@@ -181,7 +182,7 @@ const char* conv_kernel_name(const ConvParams& p);
 bool conv_tile_shape(const ConvParams& p, int prec, ConvTileShape* sh);
 const char* conv_tile_name(const ConvTileShape& t);
 void launch_conv_tile(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s);
-void launch_conv_reduce(const ConvTileParams& p, hipStream_t s);
+
 void launch_conv(const ConvParams& p, hipStream_t s, const char** name);
 void launch_binary(const BinParams& p, hipStream_t s);
 void launch_unary(const UnaryParams& p, hipStream_t s);

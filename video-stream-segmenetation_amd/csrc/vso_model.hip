@@ -1066,9 +1066,15 @@ struct Planner {
         return fail("conv weight upload failed");
     }
     tp.wp = d;
-    if (ts.ksplit > 1 && !dalloc(&tp.part, (size_t)ts.ksplit * p.N * p.M * p.Ho * p.Wo * 4)) return false;
+    if (ts.ksplit > 1) {
+      const size_t blocks = (size_t)p.N * (ts.Mp / ts.bm) * ts.tiles;
+      // partial tiles in accumulator order: per output block and split, 256 threads x bm/16 x th*tw/64 f4
+      const size_t per = (size_t)256 * (ts.bm / 16) * (ts.th * ts.tw / 64) * 16;
+      if (!dalloc(&tp.part, blocks * ts.ksplit * per) || !dalloc(&tp.counters, blocks * 4))
+        return false;
+      if (hipMemset(tp.counters, 0, blocks * 4) != hipSuccess) return fail("hipMemset failed");
+    }
     add(conv_tile_name(ts), [tp, ts](hipStream_t st) { launch_conv_tile(tp, ts, st); });
-    if (ts.ksplit > 1) add("vso::k_conv_reduce(vso::ConvTileParams)", [tp](hipStream_t st) { launch_conv_reduce(tp, st); });
     s->tile_convs++;
     return true;
   }
