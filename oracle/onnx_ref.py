@@ -541,10 +541,10 @@ def round_operand(a, mode):
 def tiled_conv(w, attrs):
     """The convolutions the GPU runs on k_conv_tile with 16-bit operands
     (conv_tile_shape in video-stream-segmenetation_amd/csrc/vso_conv.hip):
-    ungrouped, undilated, square 1/3/5 at stride 1 or 3 at stride 2."""
+    ungrouped, undilated, square 3/5 at stride 1 or 3 at stride 2."""
     k, s, d = w.shape[2], attrs.get("strides", [1, 1]), attrs.get("dilations", [1, 1])
     return (attrs.get("group", 1) == 1 and d[0] == 1 and d[1] == 1 and w.shape[2] == w.shape[3] and s[0] == s[1]
-            and ((s[0] == 1 and k in (1, 3, 5)) or (s[0] == 2 and k == 3)))
+            and ((s[0] == 1 and k in (3, 5)) or (s[0] == 2 and k == 3)))
 
 
 def run(model: Model, feeds: dict, want=None, conv_operands=None) -> dict:

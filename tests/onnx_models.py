@@ -363,7 +363,7 @@ def modnet(h=288, w=512, hr=32, q4f16=False, seed=7):
 def conv_tiles():
     """Every k_conv_tile form (vso_conv.hip) on odd-sized batch-2 inputs, each
     convolution reading a graph input so 16-bit operand rounding is the
-    oracle's exactly: 1x1, 3x3 (M 16 / 70: one and two channel tiles), 5x5,
+    oracle's exactly: a 1x1 (k_conv_small), 3x3 (M 16 / 70: one and two channel tiles), 5x5,
     3x3 stride 2, channel counts off the 32-channel chunk (40), a K split over
     workgroups (x2: 200 channels at 9x16, 5x5) with a residual Add and Relu in
     the reduction's epilogue, and Clip / Sigmoid epilogues."""

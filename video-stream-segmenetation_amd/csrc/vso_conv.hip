@@ -111,7 +111,15 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   constexpr int NB = TH * TW / 16, PBW = NB / 4;   // 16-pixel blocks per tile / per wave
   constexpr int MI = BM / 16;
   static_assert(NB % 4 == 0 && TW % 16 == 0, "tile: a multiple of 64 pixels, rows of 16");
+  // 16-bit operands, k <= 3: the chunk's weights of all taps staged in LDS too
+  // ([tap][BM rows][NQ quads + 1]), loaded once per workgroup instead of once
+  // per wave and tap from L2 (whose latency the per-tap MFMAs cannot cover)
+  constexpr bool WL = PREC != PREC_F32 && KS <= 3;
+  constexpr int QW = NQ + 1;
+  constexpr int WITEMS = KS * KS * BM * NQ;
+  constexpr int PERW = WL ? (WITEMS + 255) / 256 : 1;
   __shared__ uint4 xs[NPIX * QS];
+  __shared__ uint4 wsm[WL ? KS * KS * BM * QW : 1];
 
   const ConvParams& c = p.c;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -141,6 +149,19 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
       for (int e = 0; e < CG; ++e) st[u][e] = (in && cb + e < c.C) ? src[e * plane] : 0.f;
     }
   };
+  const uint4* wq = static_cast<const uint4*>(p.wp);  // [tap][Mp][Cp] in quads of T
+  const int cq = p.Cp / CG;                            // quads per weight row
+  uint4 stw[PERW];
+  auto load_w = [&](int ch) {
+    if (!WL) return;
+#pragma unroll
+    for (int u = 0; u < PERW; ++u) {
+      const int idx = tid + 256 * u;
+      const int tap = idx / (BM * NQ), rem = idx - tap * (BM * NQ);
+      const int m = rem / NQ, q = rem - (rem / NQ) * NQ;
+      if (idx < WITEMS) stw[u] = wq[((long)tap * p.Mp + m0 + m) * cq + ch * NQ + q];
+    }
+  };
   f4 acc[MI][PBW];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -155,10 +176,10 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
     const int ty = b / (TW / 16), tx = (b % (TW / 16)) * 16 + r;
     bpix[j] = ty * S * IW + tx * S;
   }
-  const uint4* wq = static_cast<const uint4*>(p.wp);  // [tap][Mp][Cp] in quads of T
-  const int cq = p.Cp / CG;                            // quads per weight row
-
-  if (cbeg < cend) load(cbeg);
+  if (cbeg < cend) {
+    load(cbeg);
+    load_w(cbeg);
+  }
   for (int ch = cbeg; ch < cend; ++ch) {
     __syncthreads();  // the previous chunk's fragment reads are done
 #pragma unroll
@@ -169,8 +190,20 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
         xs[pix * QS + q] = pack_quad<PREC>(st[u]);
       }
     }
+    if (WL) {
+#pragma unroll
+      for (int u = 0; u < PERW; ++u) {
+        const int idx = tid + 256 * u;
+        const int tap = idx / (BM * NQ), rem = idx - tap * (BM * NQ);
+        const int m = rem / NQ, q = rem - (rem / NQ) * NQ;
+        if (idx < WITEMS) wsm[(tap * BM + m) * QW + q] = stw[u];
+      }
+    }
     __syncthreads();
-    if (ch + 1 < cend) load(ch + 1);  // in flight during this chunk's MFMAs
+    if (ch + 1 < cend) {  // in flight during this chunk's MFMAs
+      load(ch + 1);
+      load_w(ch + 1);
+    }
     const int wc = ch * (CK / CG);    // this chunk's first quad in a weight row
 #pragma unroll
     for (int ky = 0; ky < KS; ++ky) {
@@ -180,9 +213,13 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
         uint4 a[MI][NF];
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
-          const uint4* row = wq + ((long)tap * p.Mp + m0 + 16 * i + r) * cq + wc;
+          if (WL) {
+            a[i][0] = wsm[(tap * BM + 16 * i + r) * QW + g];
+          } else {
+            const uint4* row = wq + ((long)tap * p.Mp + m0 + 16 * i + r) * cq + wc;
 #pragma unroll
-          for (int f = 0; f < NF; ++f) a[i][f] = row[g + 4 * f];
+            for (int f = 0; f < NF; ++f) a[i][f] = row[g + 4 * f];
+          }
         }
 #pragma unroll
         for (int j = 0; j < PBW; ++j) {
@@ -233,12 +270,21 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
 #pragma unroll
       for (int j = 0; j < PBW; ++j) {
         f4 sum = f4{0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < p.ksplit; ++k) {  // split order: deterministic
-          const uint64_t* q = base + ((k * MI * PBW + i * PBW + j) * 256 + tid) * 2;
-          const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          sum += f4{__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)),
-                    __uint_as_float((uint32_t)hi), __uint_as_float((uint32_t)(hi >> 32))};
+        for (int k0 = 0; k0 < p.ksplit; k0 += 8) {  // 8 splits' loads in flight, summed in split order
+          uint64_t lo[8], hi[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if (k0 + u < p.ksplit) {
+              const uint64_t* q = base + (((k0 + u) * MI * PBW + i * PBW + j) * 256 + tid) * 2;
+              lo[u] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              hi[u] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (k0 + u < p.ksplit)
+              sum += f4{__uint_as_float((uint32_t)lo[u]), __uint_as_float((uint32_t)(lo[u] >> 32)),
+                        __uint_as_float((uint32_t)hi[u]), __uint_as_float((uint32_t)(hi[u] >> 32))};
         }
         acc[i][j] = sum;
       }
@@ -263,12 +309,12 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
 #endif
 
 // ---- instantiations (one precision per compile unit) and dispatch ---------------
-// (KS, S, TH, TW): stride 1 (1x1, 3x3, 5x5) on 8x32, 4x32, 2x32, 16x16, 4x16 tiles;
+// (KS, S, TH, TW): stride 1 (3x3, 5x5) on 8x32, 4x32, 2x32, 16x16, 4x16 tiles;
 // stride 2 (3x3) on 2x32, 4x16
 #define VSO_TILE_SHAPES_S1(X, PR, K, BMV) \
   X(PR, K, 1, 8, 32, BMV) X(PR, K, 1, 4, 32, BMV) X(PR, K, 1, 2, 32, BMV) X(PR, K, 1, 16, 16, BMV) X(PR, K, 1, 4, 16, BMV)
 #define VSO_TILE_SHAPES(X, PR, BMV) \
-  VSO_TILE_SHAPES_S1(X, PR, 1, BMV) VSO_TILE_SHAPES_S1(X, PR, 3, BMV) VSO_TILE_SHAPES_S1(X, PR, 5, BMV) \
+  VSO_TILE_SHAPES_S1(X, PR, 3, BMV) VSO_TILE_SHAPES_S1(X, PR, 5, BMV) \
   X(PR, 3, 2, 2, 32, BMV) X(PR, 3, 2, 4, 16, BMV)
 
 template <int PREC>
@@ -295,6 +341,10 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   if (c.G != 1 || c.kh != c.kw || c.dh != 1 || c.dw != 1 || c.sh != c.sw || c.pre.w) return false;
   const int ks = c.kh, s = c.sh;
   if (!((s == 1 && (ks == 1 || ks == 3 || ks == 5)) || (s == 2 && ks == 3))) return false;
+  // 1x1: a plain GEMM with K = C, faster on k_conv_small's LDS-free 16x16
+  // wave tiles in f32 than here in any precision (measured: MODNet's 1x1
+  // layers 240 us per frame there, 630 here in f32 and 16-bit alike)
+  if (ks == 1) return false;
   ConvTileShape t{};
   t.prec = prec;
   t.ks = ks;
