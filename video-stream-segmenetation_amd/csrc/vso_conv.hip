@@ -112,10 +112,10 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   constexpr int MI = BM / 16;
   static_assert(NB % 4 == 0 && TW % 16 == 0, "tile: a multiple of 64 pixels, rows of 16");
   // 16-bit operands, k <= 3: the chunk's weights of all taps staged in LDS too
-  // ([tap][BM rows][NQ quads + 1]), loaded once per workgroup instead of once
+  // ([tap][BM rows][NQ quads]), loaded once per workgroup instead of once
   // per wave and tap from L2 (whose latency the per-tap MFMAs cannot cover)
   constexpr bool WL = PREC != PREC_F32 && KS <= 3;
-  constexpr int QW = NQ + 1;
+  constexpr int QW = NQ;
   constexpr int WITEMS = KS * KS * BM * NQ;
   constexpr int PERW = WL ? (WITEMS + 255) / 256 : 1;
   __shared__ uint4 xs[NPIX * QS];
@@ -152,16 +152,15 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   const uint4* wq = static_cast<const uint4*>(p.wp);  // [tap][Mp][Cp] in quads of T
   const int cq = p.Cp / CG;                            // quads per weight row
   uint4 stw[PERW];
-  auto load_w = [&](int ch) {
-    if (!WL) return;
-#pragma unroll
-    for (int u = 0; u < PERW; ++u) {
-      const int idx = tid + 256 * u;
-      const int tap = idx / (BM * NQ), rem = idx - tap * (BM * NQ);
-      const int m = rem / NQ, q = rem - (rem / NQ) * NQ;
-      if (idx < WITEMS) stw[u] = wq[((long)tap * p.Mp + m0 + m) * cq + ch * NQ + q];
-    }
-  };
+#define VSO_LOAD_W(CH)                                                                   \
+  if (WL) {                                                                              \
+    _Pragma("unroll") for (int u = 0; u < PERW; ++u) {                                   \
+      const int idx = tid + 256 * u;                                                     \
+      const int tap = idx / (BM * NQ), rem = idx - tap * (BM * NQ);                      \
+      const int m = rem / NQ, q = rem - (rem / NQ) * NQ;                                 \
+      stw[u] = idx < WITEMS ? wq[((long)tap * p.Mp + m0 + m) * cq + (CH) * NQ + q] : uint4{0, 0, 0, 0}; \
+    }                                                                                    \
+  }
   f4 acc[MI][PBW];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -178,7 +177,7 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   }
   if (cbeg < cend) {
     load(cbeg);
-    load_w(cbeg);
+    VSO_LOAD_W(cbeg)
   }
   for (int ch = cbeg; ch < cend; ++ch) {
     __syncthreads();  // the previous chunk's fragment reads are done
@@ -202,7 +201,7 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
     __syncthreads();
     if (ch + 1 < cend) {  // in flight during this chunk's MFMAs
       load(ch + 1);
-      load_w(ch + 1);
+      VSO_LOAD_W(ch + 1)
     }
     const int wc = ch * (CK / CG);    // this chunk's first quad in a weight row
 #pragma unroll
@@ -306,6 +305,7 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
       }
   }
 }
+#undef VSO_LOAD_W
 #endif
 
 // ---- instantiations (one precision per compile unit) and dispatch ---------------
