@@ -331,7 +331,7 @@ def modnet(h=288, w=512, hr=32, q4f16=False, seed=7):
     gp = b.op("Flatten", [b.op("GlobalAveragePool", [enc32x])])
     f = b.op("Relu", [matmul(gp, 1280, 320)])
     f = b.op("Sigmoid", [matmul(f, 320, 1280)])
-    f = b.op("Reshape", [f, b.const(np.array([1, 1280, 1, 1], np.int64))])
+    f = b.op("Reshape", [f, b.const(np.array([-1, 1280, 1, 1], np.int64))])
     lr = b.op("Mul", [enc32x, f])
     lr16x = ibn_relu(resize(lr, 2), 1280, 96, 5)
     lr8x = ibn_relu(resize(lr16x, 2), 96, 32, 5)

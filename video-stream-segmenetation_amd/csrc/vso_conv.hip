@@ -124,10 +124,16 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   const ConvParams& c = p.c;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int t = blockIdx.x;
+  // 1-D grid, split index fastest: workgroups b and b + 8 share an XCD
+  // (round-robin dispatch), so with ksplit a multiple of 8 each XCD's L2 holds
+  // the weights of its own splits only (MODNet's 5x5 1280 -> 96 layer: 6 MB
+  // of bf16 weights, re-read per pixel tile, no longer from HBM)
+  const int L = blockIdx.x;
+  const int kz = L % p.ksplit;
+  const int rest = L / p.ksplit;
+  const int t = rest % p.tiles, mt = (rest / p.tiles) % p.mtiles, n = rest / (p.tiles * p.mtiles);
   const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * TW;
-  const int m0 = blockIdx.y * BM;
-  const int n = blockIdx.z / p.ksplit, kz = blockIdx.z % p.ksplit;
+  const int m0 = mt * BM;
   const int nch = p.Cp / CK;
   const int cbeg = kz * p.cps, cend = min(nch, cbeg + p.cps);
   const int iy0 = oy0 * S - c.pt, ix0 = ox0 * S - c.pl;
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
     // f4, stored write-through (8-byte agent-scope stores: sc1) so the last
     // workgroup to arrive — on any XCD — reads them from memory with sc1 loads
     // (MI355X_MICROARCH.md, hand-off table row 1: no fences)
-    const long blk = ((long)n * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const long blk = ((long)n * p.mtiles + mt) * p.tiles + t;
     uint64_t* part = reinterpret_cast<uint64_t*>(p.part) + (blk * p.ksplit + kz) * (MI * PBW * 256 * 2);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -323,7 +329,7 @@ void launch_conv_tile_prec(const ConvTileParams& p, const ConvTileShape& t, hipS
 #ifdef VSO_CONV_PREC
 template <>
 void launch_conv_tile_prec<VSO_CONV_PREC>(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s) {
-  const dim3 grid((unsigned)t.tiles, (unsigned)(t.Mp / t.bm), (unsigned)(p.c.N * t.ksplit));
+  const dim3 grid((unsigned)((long)t.tiles * (t.Mp / t.bm) * p.c.N * t.ksplit));
 #define VSO_TILE_CASE(PR, KSV, SV, THV, TWV, BMV)                                              \
   if (t.ks == KSV && t.s == SV && t.th == THV && t.tw == TWV && t.bm == BMV) {                  \
     hipLaunchKernelGGL((k_conv_tile<PR, KSV, SV, THV, TWV, BMV>), grid, dim3(256), 0, s, p);   \
@@ -374,7 +380,8 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   t.ksplit = 1;
   t.cps = nch;
   if (wgs < kWant / 2 && nch > 1) {
-    const int k = (int)std::min<long>(nch, (kWant + wgs - 1) / wgs);
+    int k = (int)std::min<long>(nch, (kWant + wgs - 1) / wgs);
+    if (k > 8) k = k / 8 * 8;  // a multiple of 8: one XCD per split residue (the grid order above)
     t.cps = (nch + k - 1) / k;
     t.ksplit = (nch + t.cps - 1) / t.cps;
   }

@@ -65,7 +65,7 @@ struct ConvTileShape {
 struct ConvTileParams {
   ConvParams c;        // geometry, x, y, epilogue
   const void* wp;      // weights packed [kh*kw][Mp][Cp] in the operand type
-  int Mp, Cp, tiles_x, ksplit, cps;
+  int Mp, Cp, tiles_x, tiles, mtiles, ksplit, cps;
   float* part;         // ksplit > 1: partial tiles [output block][ksplit][bm/16][th*tw/64][256 threads] as f4
   int* counters;       // ksplit > 1: arrivals per output block [N][M tiles][tiles], zero between runs
 };
@@ -106,6 +106,14 @@ struct CopyParams {
   int start[kMaxDims], step[kMaxDims], lim[kMaxDims];
   long dst_base, src_base;
   float fill;
+};
+
+// dst[dst_base + r * dst_row + i] = src[src_base + r * src_row + i], i < inner,
+// r < rows: a Concat / Split / Slice of whole trailing dimensions
+struct RowCopyParams {
+  const float* src;
+  float* dst;
+  long inner, rows, src_row, dst_row, src_base, dst_base;
 };
 
 struct PoolParams {
@@ -187,6 +195,8 @@ void launch_conv(const ConvParams& p, hipStream_t s, const char** name);
 void launch_binary(const BinParams& p, hipStream_t s);
 void launch_unary(const UnaryParams& p, hipStream_t s);
 void launch_copy(const CopyParams& p, hipStream_t s);
+void launch_copy_rows(const RowCopyParams& p, hipStream_t s);
+const char* row_copy_name(const RowCopyParams& p);
 void launch_pool(const PoolParams& p, hipStream_t s);
 void launch_gap(const RowParams& p, hipStream_t s);
 void launch_norm_stats(const NormParams& p, hipStream_t s);

@@ -474,6 +474,45 @@ __global__ __launch_bounds__(256) void k_copy(CopyParams p) {
   else copy_body<long>(p);
 }
 
+// grid (ceil(inner / (256 * 4 * U)), rows); VEC: 16-byte moves (every offset a multiple of 4)
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_copy_rows(RowCopyParams p) {
+  constexpr int U = 4;
+  const float* src = p.src + p.src_base + (long)blockIdx.y * p.src_row;
+  float* dst = p.dst + p.dst_base + (long)blockIdx.y * p.dst_row;
+  if (VEC) {
+    const long n4 = p.inner >> 2;
+    const long i0 = (long)blockIdx.x * 256 * U + threadIdx.x;
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + 256 * u < n4) v[u] = reinterpret_cast<const f4*>(src)[i0 + 256 * u];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + 256 * u < n4) reinterpret_cast<f4*>(dst)[i0 + 256 * u] = v[u];
+  } else {
+    const long i0 = (long)blockIdx.x * 256 * U * 4 + threadIdx.x;
+    for (int u = 0; u < U * 4; ++u)
+      if (i0 + 256 * u < p.inner) dst[i0 + 256 * u] = src[i0 + 256 * u];
+  }
+}
+
+static bool rows_vec(const RowCopyParams& p) {
+  const auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  return p.inner % 4 == 0 && p.src_row % 4 == 0 && p.dst_row % 4 == 0 && p.src_base % 4 == 0 &&
+         p.dst_base % 4 == 0 && al(p.src) && al(p.dst);
+}
+
+void launch_copy_rows(const RowCopyParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)((p.inner + 4096 - 1) / 4096), (unsigned)p.rows);
+  if (rows_vec(p)) hipLaunchKernelGGL(k_copy_rows<true>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(k_copy_rows<false>, grid, dim3(256), 0, s, p);
+}
+
+const char* row_copy_name(const RowCopyParams& p) {
+  return rows_vec(p) ? "void vso::k_copy_rows<true>(vso::RowCopyParams)" : "void vso::k_copy_rows<false>(vso::RowCopyParams)";
+}
+
 template <typename I>
 __device__ __forceinline__ void pool_body(const PoolParams& p, I total) {
   for (I o = (I)blockIdx.x * 256 + (I)threadIdx.x; o < total; o += (I)gridDim.x * 256) {

@@ -1046,6 +1046,7 @@ struct Planner {
     ConvTileParams tp{};
     tp.c = p;
     tp.Mp = ts.Mp; tp.Cp = ts.Cp; tp.tiles_x = ts.tiles_x; tp.ksplit = ts.ksplit; tp.cps = ts.cps;
+    tp.tiles = ts.tiles; tp.mtiles = ts.Mp / ts.bm;
     auto src = [&](size_t tap, int m, int c) { return wf[((size_t)m * p.C + c) * taps + tap]; };
     void* d = nullptr;
     if (ts.prec == PREC_F32) {
@@ -1161,6 +1162,35 @@ struct Planner {
     p.dst = dst;
     p.fill = fill;
     if (p.n == 0) return true;
+    // a block copy (Concat / Split / Slice of whole trailing dims, no fill):
+    // rows of one contiguous run in both tensors -> k_copy_rows (16-byte moves)
+    bool block = src_perm.empty();
+    for (size_t d = 0; block && d < rk; ++d)
+      block = src_step[d] == 1 && src_start[d] >= 0 && src_start[d] + iter[d] <= src_shape[d];
+    if (block) {
+      int d = (int)rk - 1;
+      int64_t inner = 1;
+      while (d >= 0 && iter[d] == src_shape[d] && iter[d] == dst_shape[d]) inner *= iter[d--];
+      if (d >= 0) inner *= iter[d--];
+      bool one_outer = true;  // at most one outer dimension left (dim 0)
+      for (int k = 0; k <= d && k < (int)rk; ++k)
+        if (k > 0 && iter[k] != 1) one_outer = false;
+      if (one_outer && d <= 0) {
+        RowCopyParams q{};
+        q.src = src;
+        q.dst = dst;
+        q.inner = inner;
+        q.rows = d == 0 ? iter[0] : 1;
+        q.src_row = d == 0 ? sst[0] : 0;
+        q.dst_row = d == 0 ? dst_st[0] : 0;
+        int64_t sb = 0;
+        for (size_t k = 0; k < rk; ++k) sb += src_start[k] * sst[k];
+        q.src_base = sb;
+        q.dst_base = base;
+        add(row_copy_name(q), [q](hipStream_t st) { launch_copy_rows(q, st); });
+        return true;
+      }
+    }
     add("vso::k_copy(vso::CopyParams)", [p](hipStream_t st) { launch_copy(p, st); });
     return true;
   }
