@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--full", default="288x512", help="the MODNet topology (onnx_models.modnet) at this size")
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--only-modnet", action="store_true")
+    ap.add_argument("--cases", default="", help="comma-separated substrings: run only the cases whose name has one")
     args = ap.parse_args()
     import torch
     import bench
@@ -49,6 +50,9 @@ def main():
             cases.append((f"modnet{'_q4f16' if q else ''}_{fh}x{fw}_b{args.batch}_{prec}", M.modnet(fh, fw, q4f16=q),
                           (args.batch, 3, fh, fw), prec))
     cases = [c if len(c) == 4 else c + ("f32",) for c in cases]
+    if args.cases:
+        keys = args.cases.split(",")
+        cases = [c for c in cases if any(k in c[0] for k in keys)]
     for name, model, shape, prec in cases:
         with ort.InferenceSession(model, input_shape=shape, precision=prec) as s:
             din = [torch.rand(sh, dtype=torch.float32, device="cuda") for sh in s.input_shapes]

@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
+    command = sys.argv[3] if len(sys.argv) > 3 else f"bash tools/prof_run.sh {tag} ..."
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
@@ -64,10 +65,11 @@ def main():
                 traffic[name]["mfma_util"] = mf["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8.0 * 256 * 4)
     json.dump(traffic, open(os.path.join(out, f"{tag}_traffic.json"), "w"), indent=1)
     log = open(os.path.join(src, "trace.log")).read().strip().splitlines()
-    bench_line = next((l for l in reversed(log) if l.startswith("{")), "")
+    bench_lines = [l for l in log if l.startswith("{")]
+    bench_line = "\n".join(bench_lines[-4:]) if "prof_onnx" in command else (bench_lines[-1] if bench_lines else "")
     with open(os.path.join(out, f"{tag}_summary.md"), "w") as fh:
         fh.write(f"# rocprofv3 summary `{tag}`\n\n")
-        fh.write("Command: `bash tools/prof_run.sh " + tag + " ...` (kernel trace + stats pass; separate FETCH_SIZE "
+        fh.write("Command: `" + command + "` (kernel trace + stats pass; separate FETCH_SIZE "
                  "and WRITE_SIZE PMC passes).  HBM bytes = 2 x FETCH_SIZE KiB + WRITE_SIZE KiB (gfx950 "
                  "correction); memory-side counters include Infinity-Cache hits.\n\n")
         fh.write("| kernel | calls | mean us | HBM read MB/launch | HBM write MB/launch | GB/s (PMC) | MFMA util | "
