@@ -1,7 +1,7 @@
 // Driver for tests/test_ts.py: run an ONNX model through the TypeScript host's
 // onnxruntime-web surface (segment.js InferenceSession / Tensor) and write the
 // outputs back.
-//   node run_onnx.js <model.onnx> <inputs.bin> <out prefix> [<unsupported.onnx>]
+//   node run_onnx.js <model.onnx> <inputs.bin> <out prefix> [<unsupported.onnx> [<precision>]]
 // inputs.bin holds every input's float32 data, in the session's input order;
 // output k is written to <out prefix>_<k>.bin.
 'use strict';
@@ -10,10 +10,10 @@ const path = require('path');
 const ort = require(path.join(__dirname, '..', '..', 'video-stream-segmenetation_amd', 'ts', 'segment.js'));
 
 async function main() {
-  const [modelPath, inputsPath, outPrefix, badModel] = process.argv.slice(2);
+  const [modelPath, inputsPath, outPrefix, badModel, precision] = process.argv.slice(2);
   // from bytes, as a bundler-fetched ArrayBuffer would arrive
   const session = await ort.InferenceSession.create(new Uint8Array(fs.readFileSync(modelPath)),
-                                                    { executionProviders: ['wasm'] });
+                                                    { executionProviders: ['wasm'], precision: precision || 'f32' });
   const raw = fs.readFileSync(inputsPath);
   const all = new Float32Array(raw.buffer.slice(raw.byteOffset, raw.byteOffset + raw.byteLength));
   const feeds = {};

@@ -165,11 +165,14 @@ ort.InferenceSession.create(new Uint8Array([8, 1, 18, 4, 110, 111, 112, 101]), {
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("key", ["modnet_like", "mediapipe_face_detector"])
-def test_node_onnx_session_matches_oracle_and_python_host(addon_built, pkg, tmp_path, key):
+@pytest.mark.parametrize("key,precision", [("modnet_like", "f32"), ("mediapipe_face_detector", "f32"),
+                                           ("conv_tiles", "f16")])
+def test_node_onnx_session_matches_oracle_and_python_host(addon_built, pkg, tmp_path, key, precision):
     """InferenceSession.create/run from TypeScript == the ONNX oracle (within
-    the 1e-4 relative bar of tests/test_gpu_onnx.py) and == the Python host's
-    session bit for bit; concurrent runs serialise, bad feeds reject."""
+    the 1e-4 relative bar of tests/test_gpu_onnx.py; with { precision: 'f16' }
+    the oracle rounds the tiled convolutions' operands the same way) and ==
+    the Python host's session bit for bit; concurrent runs serialise, bad
+    feeds reject."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -179,6 +182,12 @@ def test_node_onnx_session_matches_oracle_and_python_host(addon_built, pkg, tmp_
         model = M.modnet_like()
         feeds = M.feeds_for(key)
         want = R.run(R.load(model), feeds)
+    elif key == "conv_tiles":
+        model = M.conv_tiles()
+        rng = np.random.default_rng(5)
+        feeds = {"x": rng.standard_normal((2, 40, 37, 70)).astype(np.float32),
+                 "x2": rng.standard_normal((2, 200, 9, 16)).astype(np.float32)}
+        want = R.run(R.load(model), feeds, conv_operands=precision)
     else:
         model, feeds, want, _ = M.load_golden(os.path.join(ROOT, "tests", "golden", key + ".npz"))
     bad = R.make_model([R.make_node("Einsum", ["x", "x"], ["y"], equation="ij,jk->ik")], {},
@@ -188,14 +197,14 @@ def test_node_onnx_session_matches_oracle_and_python_host(addon_built, pkg, tmp_
     bp.write_bytes(bad)
     np.concatenate([np.ascontiguousarray(v, np.float32).ravel() for v in feeds.values()]).tofile(ip)
     out = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "run_onnx.js"), str(mp), str(ip),
-                          str(tmp_path / "out"), str(bp)], capture_output=True, text=True, timeout=300)
+                          str(tmp_path / "out"), str(bp), precision], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     info = json.loads(out.stdout.strip().splitlines()[-1])
     assert info["inputNames"] == list(feeds) and info["outputNames"] == list(want)
     assert info["replaySame"] and info["badDimsRejected"] and info["afterReject"] and info["releasedRejects"]
     assert info["unsupported"]["code"] == "-4" and "Einsum" in info["unsupported"]["message"]
     from vss_amd import ort as pyort
-    with pyort.InferenceSession(model) as s:
+    with pyort.InferenceSession(model, precision=precision) as s:
         py = s.run(feeds)
     for k, (name, w) in enumerate(want.items()):
         assert info["outputDims"][k] == list(w.shape) and info["outputTypes"][k] == "float32"

@@ -34,7 +34,7 @@
 //       -> Promise<{alpha: Float32Array, alphaU8: Uint8Array}>   (processFrame :78-169)
 //   segmentComposite(handle, post, frames, n, height, width, channels, rowStride)
 //       -> Promise<Uint8Array>   RGBA output canvases, n * height * width * 4 (:78-178)
-//   ortCreate(modelBytes: Uint8Array, inputDims: number[] | null, deviceId) -> session
+//   ortCreate(modelBytes: Uint8Array, inputDims: number[] | null, deviceId, convPrecision) -> session
 //       ONNX sessions (include/vso.h) behind InferenceSession.create (model.ts:14, :38, :61)
 //   ortInfo(session) -> {inputNames, outputNames, inputShapes, outputShapes}
 //   ortRun(session, inputs: Float32Array[]) -> Promise<Float32Array[]>   (session.run)
@@ -867,12 +867,13 @@ size_t elem_count(const std::vector<int64_t>& d) {
 }
 
 napi_value OrtCreate(napi_env env, napi_callback_info info) {
-  size_t argc = 3;
-  napi_value argv[3];
+  size_t argc = 4;
+  napi_value argv[4];
   NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
   bool is_ta = false;
   if (argc < 1 || napi_is_typedarray(env, argv[0], &is_ta) != napi_ok || !is_ta) {
-    napi_throw_type_error(env, nullptr, "ortCreate(modelBytes: Uint8Array, inputDims?: number[], deviceId?: number)");
+    napi_throw_type_error(env, nullptr,
+                          "ortCreate(modelBytes: Uint8Array, inputDims?: number[], deviceId?: number, convPrecision?: number)");
     return nullptr;
   }
   napi_typedarray_type tt;
@@ -895,8 +896,11 @@ napi_value OrtCreate(napi_env env, napi_callback_info info) {
   }
   int device = 0;
   if (argc >= 3) napi_get_value_int32(env, argv[2], &device);
+  vso_options opts;
+  vso_options_default(&opts);
+  if (argc >= 4) napi_get_value_int32(env, argv[3], &opts.conv_precision);
   vso_session* s = nullptr;
-  const int rc = vso_create(data, len, dims.empty() ? nullptr : dims.data(), (int)dims.size(), device, &s);
+  const int rc = vso_create_ex(data, len, dims.empty() ? nullptr : dims.data(), (int)dims.size(), device, &opts, &s);
   if (rc != VSO_OK) {
     throw_vss(env, "vso_create", rc, vso_last_error(nullptr));
     return nullptr;
