@@ -879,20 +879,37 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     if (gg < G) {
       // the lane's terms are integers (rint of v*2^32, v*v*2^24); their f64 sum
       // is exact while it stays below 2^53 — T = ceil(P_OUT/G) <= 16 terms:
-      // |v| < 2^17 and |v| < 5792 (the int64 frame totals overflow near the
-      // same magnitudes: |v| < 7.7k at d3) — so one f64 -> i64 conversion per
-      // sum replaces one f32 -> i64 sequence per term, with the same integers
+      // |v| < 2^17 and |v| < 5792 — so one f64 -> i64 conversion per sum
+      // replaces one f32 -> i64 sequence per term, with the same integers.  A
+      // lane holding any |v| >= 5792 takes the per-term int64 sums instead
+      // (exact up to where the int64 frame totals themselves overflow), so
+      // large pre-norm activations cannot round silently or make the totals
+      // depend on the tiling.
       double s = 0.0, q = 0.0;
+      bool big = false;
 #pragma unroll
       for (int pix = 0; pix < P_OUT; pix += G) {
         if (pix + gg < P_OUT) {
           const float v = work[(pix + gg) * RS + c];
+          big |= fabsf(v) >= 5792.f;
           s += (double)__builtin_rintf(v * 0x1p32f);
           q += (double)__builtin_rintf(v * v * 0x1p24f);
         }
       }
-      st64[gg * COUT + c] = (long long)s;
-      st64[256 + gg * COUT + c] = (long long)q;
+      long long si = (long long)s, qi = (long long)q;
+      if (big) {
+        si = 0;
+        qi = 0;
+        for (int pix = 0; pix < P_OUT; pix += G) {
+          if (pix + gg < P_OUT) {
+            const float v = work[(pix + gg) * RS + c];
+            si += (long long)__builtin_rintf(v * 0x1p32f);
+            qi += (long long)__builtin_rintf(v * v * 0x1p24f);
+          }
+        }
+      }
+      st64[gg * COUT + c] = si;
+      st64[256 + gg * COUT + c] = qi;
     }
     __syncthreads();
     if (tid < 2 * COUT) {
