@@ -877,27 +877,27 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     long long* st64 = reinterpret_cast<long long*>(stt);
     const int c = tid % COUT, gg = tid / COUT;
     if (gg < G) {
-      // the lane's terms are integers (rint of v*2^32, v*v*2^24); their f64 sum
-      // is exact while it stays below 2^53 — T = ceil(P_OUT/G) <= 16 terms:
-      // |v| < 2^17 and |v| < 5792 — so one f64 -> i64 conversion per sum
-      // replaces one f32 -> i64 sequence per term, with the same integers.  A
-      // lane holding any |v| >= 5792 takes the per-term int64 sums instead
-      // (exact up to where the int64 frame totals themselves overflow), so
-      // large pre-norm activations cannot round silently or make the totals
-      // depend on the tiling.
+      // the lane's terms are integers (rint of v*2^32, v*v*2^24); their f64 sums
+      // are exact while no partial sum reaches 2^53.  The q terms are >= 0, so
+      // q < 2^53 at the end means every partial q was exact, and then
+      // sum |s terms| <= sqrt(T * sum v^2 2^64) = sqrt(T q 2^40) < 2^53 for
+      // T = ceil(P_OUT/G) <= 16 — s was exact too.  One f64 -> i64
+      // conversion per sum then replaces one f32 -> i64 sequence per term,
+      // with the same integers; a lane whose q reaches 2^53 (|v| ~ 5.8k) adds
+      // its terms again as int64 (exact up to where the int64 frame totals
+      // overflow), so large pre-norm activations cannot round silently or
+      // make the totals depend on the tiling.
       double s = 0.0, q = 0.0;
-      bool big = false;
 #pragma unroll
       for (int pix = 0; pix < P_OUT; pix += G) {
         if (pix + gg < P_OUT) {
           const float v = work[(pix + gg) * RS + c];
-          big |= fabsf(v) >= 5792.f;
           s += (double)__builtin_rintf(v * 0x1p32f);
           q += (double)__builtin_rintf(v * v * 0x1p24f);
         }
       }
       long long si = (long long)s, qi = (long long)q;
-      if (big) {
+      if (q >= 0x1p53) {
         si = 0;
         qi = 0;
         for (int pix = 0; pix < P_OUT; pix += G) {
