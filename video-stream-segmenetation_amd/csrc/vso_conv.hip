@@ -111,10 +111,10 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   constexpr int NB = TH * TW / 16, PBW = NB / 4;   // 16-pixel blocks per tile / per wave
   constexpr int MI = BM / 16;
   static_assert(NB % 4 == 0 && TW % 16 == 0, "tile: a multiple of 64 pixels, rows of 16");
-  // 16-bit operands, k <= 3: the chunk's weights of all taps staged in LDS too
+  // 16-bit operands, k <= 3 (and 5x5 on 32-channel tiles: 51 KB): the chunk's weights of all taps staged in LDS too
   // ([tap][BM rows][NQ quads]), loaded once per workgroup instead of once
   // per wave and tap from L2 (whose latency the per-tap MFMAs cannot cover)
-  constexpr bool WL = PREC != PREC_F32 && KS <= 3;
+  constexpr bool WL = PREC != PREC_F32 && (KS <= 3 || BM == 32);
   constexpr int QW = NQ;
   constexpr int WITEMS = KS * KS * BM * NQ;
   constexpr int PERW = WL ? (WITEMS + 255) / 256 : 1;
@@ -355,7 +355,9 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   t.prec = prec;
   t.ks = ks;
   t.s = s;
-  t.bm = c.M <= 32 ? 32 : 64;
+  // 32-channel tiles for 16-bit 5x5: their 25 taps' weights then fit LDS
+  // (k_conv_tile's WL) instead of 25 exposed L2 round trips per chunk
+  t.bm = (c.M <= 32 || (ks == 5 && prec != PREC_F32)) ? 32 : 64;
   t.Mp = (c.M + t.bm - 1) / t.bm * t.bm;
   t.Cp = (c.C + CK - 1) / CK * CK;
   // candidate tiles, largest first: the first giving >= kWant workgroups wins,
