@@ -301,6 +301,8 @@ def main():
     ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host-buffer legs")
     ap.add_argument("--no-ts", action="store_true", help="skip the TypeScript (Node) leg")
     ap.add_argument("--no-sweep", action="store_true", help="skip the batch sweep")
+    ap.add_argument("--gather", action="store_true",
+                    help="run the multi-GPU step (RCCL clique all-gather) even at one rank (a rehearsal of N > 1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_traffic.json"),
                     help="per-kernel HBM traffic from tools/prof_summary.py (PMC passes)")
     args = ap.parse_args()
@@ -338,10 +340,13 @@ def main():
                        max_frame_h=fh, max_frame_w=fw, queue_depth=S)
     if args.no_graph:
         sess.set_option(pkg.VSS_OPT_USE_GRAPH, 0)
+    gather = world > 1 or args.gather
     if world > 1:
         ids = [sess.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
         sess.comm_init_rank(world, rank, ids[0])
+    elif gather:
+        sess.comm_init_rank(1, 0, sess.comm_unique_id())
     d_frames = torch.from_numpy(frames).to(dev)
     P = hm * wm
     # one output buffer per stream: step i writes buffer i % S on stream i % S
@@ -350,7 +355,7 @@ def main():
     rs, fs = fw * 3, fh * fw * 3
 
     def step(i, st):
-        if world > 1:
+        if gather:
             sess.segment_gather_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, outs[i % S].data_ptr(),
                                        st.cuda_stream)
         else:
@@ -369,7 +374,7 @@ def main():
         dist.barrier()
     last = (args.steps - 1) % S
     d_masks = outs[last][rank * B:(rank + 1) * B] if world > 1 else outs[last][:B]
-    if world > 1:  # the gathered batch holds every rank's masks in frame order
+    if gather:  # the gathered batch holds every rank's masks in frame order
         assert all(torch.equal(outs[last], o) for o in outs), "every step gathers the same masks"
     t = torch.tensor([el], dtype=torch.float64)
     if world > 1:
