@@ -129,6 +129,21 @@ def host_leg(pkg, frames, B, fh, fw, inflight, iters, d_ref=None):
         same = bool(np.array_equal(last, d_ref)) if d_ref is not None else None
         out["copy"] = {"value": round(B * iters / el, 1), "ms_per_batch": round(el * 1e3 / iters, 4),
                        "masks_equal_device_path": same}
+        # the same with the masks going to pinned blocks (host_empty / vss_host_alloc,
+        # what the N-API addon hands out): the D2H fills them, no completion copy
+        pinned = [pkg.host_empty((B, s.mask_h * s.mask_w)) for _ in range(inflight + 1)]
+        q = collections.deque()
+        t0 = time.perf_counter()
+        for i in range(iters):
+            if len(q) == inflight:
+                s.wait(q.popleft())
+            q.append(s.submit(frames, out=pinned[i % len(pinned)]))
+        while q:
+            last = s.wait(q.popleft())[0]
+        el = time.perf_counter() - t0
+        same = bool(np.array_equal(last, d_ref)) if d_ref is not None else None
+        out["copy_pinned_out"] = {"value": round(B * iters / el, 1), "ms_per_batch": round(el * 1e3 / iters, 4),
+                                  "masks_equal_device_path": same}
         # zero-copy: the frames are decoded straight into a leased slot's pinned
         # staging; the synthetic "decoder" fills each slot's buffer once, and
         # every later lease of that slot finds them there
@@ -152,6 +167,24 @@ def host_leg(pkg, frames, B, fh, fw, inflight, iters, d_ref=None):
         same = bool(np.array_equal(masks, d_ref)) if d_ref is not None else None
         out["zero_copy"] = {"value": round(B * iters / el, 1), "ms_per_batch": round(el * 1e3 / iters, 4),
                             "masks_equal_device_path": same}
+        # zero-copy both ways: frames decoded into the staging, masks into pinned blocks
+        tick = collections.deque()
+        for it in range(iters + inflight):
+            if it == inflight:
+                t0 = time.perf_counter()
+            if len(tick) == inflight:
+                s.wait(tick.popleft())
+            slot, buf = s.staging_acquire()
+            if slot not in filled:
+                buf[:flat.size] = flat
+                filled.add(slot)
+            tick.append(s.submit_staged(slot, B, fh, fw, 3, pinned[it % len(pinned)]))
+        while tick:
+            last = s.wait(tick.popleft())[0]
+        el = time.perf_counter() - t0
+        same = bool(np.array_equal(last, d_ref)) if d_ref is not None else None
+        out["zero_copy_pinned_out"] = {"value": round(B * iters / el, 1), "ms_per_batch": round(el * 1e3 / iters, 4),
+                                       "masks_equal_device_path": same}
     out.update({"unit": "frames/s", "frame": f"{fw}x{fh}x3", "batch": B, "inflight": inflight, "iters": iters,
                 "h2d_bytes_per_batch": int(frames.nbytes), "d2h_bytes_per_batch": int(B * 144 * 256 * 4),
                 "entry": "vss_submit / vss_wait (host frames -> host masks, queued, PCIe-inclusive)"})

@@ -202,6 +202,19 @@ int vss_staging_release(vss_handle* h, int slot);
 int vss_submit_staged(vss_handle* h, int slot, int n, int height, int width, int channels, size_t row_stride,
                       float* masks_out, int out_mode, vss_callback cb, void* user, vss_ticket* ticket);
 
+/* Pinned host memory for results (process-wide, any handle / GPU): a
+ * masks_out of vss_segment / vss_submit* / vss_segment_async that lies inside
+ * a vss_host_alloc block receives the batch's D2H directly — the completion
+ * copies nothing (otherwise the masks land in the slot's pinned buffer and the
+ * completion thread copies them to masks_out).  The JS side of the reference
+ * gets a fresh Float32Array per frame (squeezeMaskTo2D,
+ * frameProcessorTest.ts:190-201); the N-API addon hands out these blocks as
+ * its result ArrayBuffers.  vss_host_free: VSS_E_INVALID_ARG for a pointer
+ * vss_host_alloc did not return; freeing a block a batch still writes into is
+ * the caller's error, as for any masks_out. */
+int vss_host_alloc(size_t bytes, void** ptr);
+int vss_host_free(void* ptr);
+
 /* Device-resident variant: d_frames and d_masks are HBM pointers of the
  * handle's first GPU; the work is enqueued on `stream` (a hipStream_t; NULL =
  * the handle's stream) and not waited for.  frame_stride = bytes between

@@ -112,3 +112,40 @@ def test_row_fetch_bitwise(pkg, synthetic, torch_cuda, h, w, c):
         s.set_option(pkg.VSS_OPT_ROW_FETCH, 0)
         c_, _, _ = s.segment_frames(f)
         assert np.array_equal(a, ref) and np.array_equal(b, ref) and np.array_equal(c_, ref)
+
+
+def test_pinned_masks_out(pkg, synthetic, torch_cuda):
+    """masks_out inside a vss_host_alloc block takes the D2H directly (no
+    completion copy): bitwise the masks of the copying path, model and frame
+    outputs, queued with several in flight, and the zero-copy lease path."""
+    import ctypes
+    f = _frames(synthetic, 8, 480, 640, start=700)
+    g = _frames(synthetic, 8, 480, 640, start=710)
+    with pkg.Session(dtype="bf16x2", max_batch=8, max_frame_h=480, max_frame_w=640, queue_depth=3) as s:
+        ref_f, _, _ = s.segment_frames(f)
+        ref_g, _, _ = s.segment_frames(g)
+        ref_ff, _, _ = s.segment_frames(f, output_size="frame")
+        outs = [pkg.host_empty((8, s.mask_h * s.mask_w)) for _ in range(3)]
+        for o in outs:
+            o.fill(np.nan)
+        ts = [s.submit(x, out=o) for x, o in zip((f, g, f), outs)]
+        got = [s.wait(t)[0] for t in ts]
+        assert all(a is o for a, o in zip(got, outs))
+        assert np.array_equal(outs[0], ref_f) and np.array_equal(outs[1], ref_g) and np.array_equal(outs[2], ref_f)
+        fo = pkg.host_empty((8, 480 * 640))
+        fo.fill(np.nan)
+        s.wait(s.submit(f, output_size="frame", out=fo))
+        assert np.array_equal(fo, ref_ff)
+        slot, buf = s.staging_acquire()
+        buf[:g.size] = g.reshape(-1)
+        zo = pkg.host_empty((8, s.mask_h * s.mask_w))
+        zo.fill(np.nan)
+        s.wait(s.submit_staged(slot, 8, 480, 640, 3, zo))
+        assert np.array_equal(zo, ref_g)
+        # a block too small for the batch is not taken for the direct D2H
+        small = pkg.host_empty((4, s.mask_h * s.mask_w))
+        with pytest.raises(pkg.VssError):
+            s.submit(f, out=small)
+    L = pkg.lib()
+    assert L.vss_host_free(ctypes.c_void_p(0x1000)) == pkg.VSS_E_INVALID_ARG
+    assert L.vss_host_free(None) == pkg.VSS_OK

@@ -28,7 +28,9 @@ async function main() {
   const [h, w, b, it, depth] = process.argv.slice(2).map(Number);
   const frames = synthetic(b, h, w);
   const s = new seg.Segmenter({ maxBatch: b, maxFrameWidth: w, maxFrameHeight: h, queueDepth: depth || 0 });
-  for (let i = 0; i < 10; i++) await s.segmentFrames(frames);
+  // warm-up: long enough for V8 to collect results and their pinned blocks to
+  // come back to the addon's pool (the steady state of a video loop)
+  for (let i = 0; i < 150; i++) await s.segmentFrames(frames);
   // latency: one call at a time (the reference's serialised loop)
   const lat = [];
   for (let i = 0; i < Math.max(20, it / 5); i++) {

@@ -25,6 +25,7 @@ import ctypes
 import os
 import subprocess
 import threading
+import weakref
 
 import numpy as np
 
@@ -134,6 +135,8 @@ def lib() -> ctypes.CDLL:
                 "vss_submit_staged": ([P, I, I, I, I, I, S, P, I, CALLBACK, P, ctypes.POINTER(ctypes.c_uint64)], I),
                 "vss_submit_list": ([P, ctypes.POINTER(P), I, I, I, I, S, P, I, ctypes.POINTER(ctypes.c_uint64)], I),
                 "vss_segment_device": ([P, P, I, I, I, I, S, S, P, P], I),
+                "vss_host_alloc": ([S, ctypes.POINTER(P)], I),
+                "vss_host_free": ([P], I),
                 "vss_comm_unique_id": ([P, P, S, ctypes.POINTER(S)], I),
                 "vss_comm_init_rank": ([P, I, I, P, S], I),
                 "vss_segment_gather_device": ([P, P, I, I, I, I, S, S, P, P], I),
@@ -279,14 +282,19 @@ class Session:
                                        VSS_OUT_MODEL, cb, None), self._h)
         return out
 
-    def submit(self, frames: np.ndarray, output_size: str = "model") -> int:
+    def submit(self, frames: np.ndarray, output_size: str = "model", out: np.ndarray | None = None) -> int:
         """Queued host call: returns the batch's ticket once its frames are staged
         (VssError(VSS_E_BUSY) when queue_depth batches are in flight); wait(ticket)
-        returns (masks, maskW, maskH)."""
+        returns (masks, maskW, maskH).  out: where the masks go (e.g. host_empty()
+        memory, which the D2H fills directly); a new array by default."""
         f = _as_frames(frames)
         n, hh, ww, c = f.shape
         frame = output_size == "frame"
-        out = np.empty((n, hh * ww if frame else self.mask_h * self.mask_w), np.float32)
+        shape = (n, hh * ww if frame else self.mask_h * self.mask_w)
+        if out is None:
+            out = np.empty(shape, np.float32)
+        elif out.dtype != np.float32 or out.size < shape[0] * shape[1] or not out.flags.c_contiguous:
+            raise VssError(VSS_E_INVALID_ARG, f"out must be a C-contiguous float32 array of >= {shape} elements")
         t = ctypes.c_uint64()
         _check(lib().vss_submit(self._h, f.ctypes.data, n, hh, ww, c, ww * c, out.ctypes.data,
                                 VSS_OUT_FRAME if frame else VSS_OUT_MODEL, ctypes.byref(t)), self._h)
@@ -518,6 +526,28 @@ def composite_device(session: Session, frames_ptr: int, n: int, h: int, w: int, 
     ors = out_row_stride or w * 4
     _check(lib().vss_composite_device(session._h, frames_ptr, n, h, w, c, row_stride, frame_stride, alpha_u8_ptr,
                                       out_ptr, ors, out_frame_stride or ors * h, stream or None), session._h)
+
+
+class _PinnedBlock:
+    """A vss_host_alloc block, freed with its last numpy view."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        _check(lib().vss_host_alloc(max(16, nbytes), ctypes.byref(p)))
+        self.ptr = p.value
+        weakref.finalize(self, lib().vss_host_free, ctypes.c_void_p(p.value))
+
+
+def host_empty(shape, dtype=np.float32) -> np.ndarray:
+    """An uninitialised array in pinned host memory (vss_host_alloc): as the masks
+    `out` of Session.submit / submit_staged the batch's D2H lands in it directly
+    (no copy on the completion path)."""
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape))
+    blk = _PinnedBlock(count * dt.itemsize)
+    buf = (ctypes.c_uint8 * max(16, count * dt.itemsize)).from_address(blk.ptr)
+    buf._block = blk  # the memory lives as long as any view of it
+    return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
 
 
 def version() -> int:

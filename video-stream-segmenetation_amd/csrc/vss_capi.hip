@@ -987,6 +987,21 @@ void note_ticket(vss_handle* h, int k) {
   h->next_ticket = t + 1;
 }
 
+// Pinned result buffers (vss_host_alloc): a masks_out inside one of these
+// receives the batch's D2H directly, so the completion copies nothing.  The
+// registry is process-wide (any handle, any GPU), keyed by start address.
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pinned;
+
+bool pinned_range(const void* p, size_t bytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pinned.upper_bound(a);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  return a >= it->first && a + bytes <= it->first + it->second;
+}
+
 struct HostDone {
   float* out;
   const float* src;
@@ -1123,20 +1138,23 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   HIP_TRY(h, hipSetDevice(h->device));
   const float* src = s0.h_masks;
   size_t bytes = (size_t)n * P * 4;
+  if (out_mode == VSS_OUT_FRAME) bytes = (size_t)n * fh * fw * 4;
+  // masks_out from vss_host_alloc: the D2H lands there, nothing to copy after
+  const bool direct = pinned_range(masks_out, bytes);
   if (out_mode == VSS_OUT_FRAME) {
     enqueue_upmask(h, res, n, fh, fw, s0.d_fmasks, s0.stream);
     HIP_TRY(h, hipGetLastError());
-    bytes = (size_t)n * fh * fw * 4;
-    HIP_TRY(h, hipMemcpyAsync(s0.h_fmasks, s0.d_fmasks, bytes, hipMemcpyDeviceToHost, s0.stream));
     src = s0.h_fmasks;
+    HIP_TRY(h, hipMemcpyAsync(direct ? masks_out : s0.h_fmasks, s0.d_fmasks, bytes, hipMemcpyDeviceToHost,
+                              s0.stream));
   } else {
-    HIP_TRY(h, hipMemcpyAsync(s0.h_masks, res, bytes, hipMemcpyDeviceToHost, s0.stream));
+    HIP_TRY(h, hipMemcpyAsync(direct ? masks_out : s0.h_masks, res, bytes, hipMemcpyDeviceToHost, s0.stream));
   }
   if (!sync) {
     // completions in submission order: after the previous batch's
     Slot& prev = h->slots[h->ticket_slot[(t + vss_handle::kTicketRing - 1) % vss_handle::kTicketRing]];
     if (t > 0 && prev.used && &prev != &s0) HIP_TRY(h, hipStreamWaitEvent(s0.stream, prev.done, 0));
-    HostDone* c = new HostDone{masks_out, src, bytes, cb, user, &s0};
+    HostDone* c = new HostDone{direct ? nullptr : masks_out, src, bytes, cb, user, &s0};
     s0.status = 1;  // pending until the host function runs
     const hipError_t e = hipLaunchHostFunc(s0.stream, host_done, c);
     if (e != hipSuccess) {
@@ -1153,7 +1171,7 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   if (sync) {
     HIP_TRY(h, hipSetDevice(h->device));
     for (vss_handle* e : E) HIP_TRY(e, hipEventSynchronize(e->slots[k].done));
-    std::memcpy(masks_out, src, bytes);
+    if (!direct) std::memcpy(masks_out, src, bytes);
   }
   return VSS_OK;
 }
@@ -1539,6 +1557,26 @@ int vss_submit_staged(vss_handle* h, int slot, int n, int height, int width, int
   if (slot < 0 || slot >= (int)h->slots.size()) return fail(h, VSS_E_INVALID_ARG, "bad slot");
   return submit_host(h, h->slots[slot].h_frames, nullptr, n, height, width, channels, row_stride, masks_out, out_mode,
                      false, false, cb, user, ticket, slot);
+}
+
+int vss_host_alloc(size_t bytes, void** ptr) {
+  if (!ptr || bytes == 0) return VSS_E_INVALID_ARG;
+  *ptr = nullptr;
+  void* q = nullptr;
+  if (hipHostMalloc(&q, bytes, hipHostMallocPortable) != hipSuccess || !q) return VSS_E_OOM;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned[reinterpret_cast<uintptr_t>(q)] = bytes;
+  *ptr = q;
+  return VSS_OK;
+}
+
+int vss_host_free(void* ptr) {
+  if (!ptr) return VSS_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (g_pinned.erase(reinterpret_cast<uintptr_t>(ptr)) == 0) return VSS_E_INVALID_ARG;
+  }
+  return hipHostFree(ptr) == hipSuccess ? VSS_OK : VSS_E_HIP;
 }
 
 int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width, int channels,

@@ -54,6 +54,8 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -467,25 +469,101 @@ void QueuedComplete(napi_env env, napi_status, void* data) {
   delete w;
 }
 
-// The masks' ArrayBuffer: malloc'd (not zero-filled: Node 12's
+// The masks' ArrayBuffer: a pinned block (vss_host_alloc), so the batch's D2H
+// lands in it directly and the completion copies nothing — before, the masks
+// were copied out of the slot's pinned buffer into fresh malloc'd pages on the
+// HIP completion thread, one batch after another.  Pinning (and unpinning:
+// hipHostFree waits for the device) is far too slow for the per-call path, so
+// blocks are recycled: the finalizer V8 runs when a result is collected puts
+// its block on a free list by size, and blocks are never unpinned while the
+// process runs.  In steady state the live blocks are the results V8 has not
+// collected yet (its external-memory pressure — napi_adjust_external_memory —
+// sets the pace); past kPinnedCap bytes of pinned blocks, results fall back
+// to malloc'd memory (then the completion copies).  Not zero-filled (Node 12's
 // napi_create_arraybuffer spent ~0.19 ms clearing 1.2 MB on the JS thread per
-// call) and handed to V8 as external memory, freed by its finalizer; V8's GC
-// is told about the bytes so it collects results at the usual pace.
+// call).
+struct MaskBlock {
+  size_t bytes;
+  bool pinned;
+};
+
+std::mutex g_pool_mu;
+std::multimap<size_t, void*> g_pool;  // free pinned blocks by size
+size_t g_pinned_bytes = 0;             // every pinned block, free or live
+constexpr size_t kPinnedCap = size_t(1) << 30;
+
+// VSS_NAPI_PINNED=0: malloc'd results (the completion copies), for A/B runs
+const bool g_use_pinned = [] {
+  const char* e = std::getenv("VSS_NAPI_PINNED");
+  return !(e && e[0] == '0');
+}();
+
+void* pool_get(size_t bytes, bool* pinned) {
+  if (!g_use_pinned) {
+    *pinned = false;
+    return std::malloc(bytes);
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pool.find(bytes);
+    if (it != g_pool.end()) {
+      void* p = it->second;
+      g_pool.erase(it);
+      *pinned = true;
+      return p;
+    }
+    if (g_pinned_bytes + bytes > kPinnedCap) {
+      *pinned = false;
+      return std::malloc(bytes);
+    }
+    g_pinned_bytes += bytes;
+  }
+  void* p = nullptr;
+  if (vss_host_alloc(bytes, &p) == VSS_OK) {
+    *pinned = true;
+    return p;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pinned_bytes -= bytes;
+  }
+  *pinned = false;
+  return std::malloc(bytes);
+}
+
+void pool_put(void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool.emplace(bytes, p);
+}
+
 void free_masks(napi_env env, void* data, void* hint) {
-  std::free(data);
+  MaskBlock* b = static_cast<MaskBlock*>(hint);
+  if (b->pinned)
+    pool_put(data, b->bytes);
+  else
+    std::free(data);
   int64_t adj = 0;
-  napi_adjust_external_memory(env, -(int64_t)(uintptr_t)hint, &adj);
+  napi_adjust_external_memory(env, -(int64_t)b->bytes, &adj);
+  delete b;
 }
 
 bool masks_buffer(napi_env env, size_t bytes, void** data, napi_value* ab) {
-  void* p = std::malloc(std::max<size_t>(bytes, 16));
-  if (!p) return false;
-  if (napi_create_external_arraybuffer(env, p, bytes, free_masks, (void*)(uintptr_t)bytes, ab) != napi_ok) {
-    std::free(p);
+  MaskBlock* b = new MaskBlock{std::max<size_t>(bytes, 16), false};
+  void* p = pool_get(b->bytes, &b->pinned);
+  if (!p) {
+    delete b;
+    return false;
+  }
+  if (napi_create_external_arraybuffer(env, p, bytes, free_masks, b, ab) != napi_ok) {
+    if (b->pinned)
+      pool_put(p, b->bytes);
+    else
+      std::free(p);
+    delete b;
     return false;
   }
   int64_t adj = 0;
-  napi_adjust_external_memory(env, (int64_t)bytes, &adj);
+  napi_adjust_external_memory(env, (int64_t)b->bytes, &adj);
   *data = p;
   return true;
 }
