@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -987,6 +988,27 @@ void note_ticket(vss_handle* h, int k) {
   h->next_ticket = t + 1;
 }
 
+// VSS_TIME_SUBMIT=1: host time of each phase of the queued submit, summed over
+// the calls and printed when the handle is destroyed (where the calling
+// thread's time goes; tools/ts_prof.js showed the N-API call dominating).
+struct SubmitClock {
+  static constexpr int kPhases = 8;
+  bool on = std::getenv("VSS_TIME_SUBMIT") != nullptr;
+  double ns[kPhases] = {};
+  long calls = 0;
+  std::chrono::steady_clock::time_point t;
+  void start() {
+    if (on) t = std::chrono::steady_clock::now();
+  }
+  void mark(int k) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    ns[k] += std::chrono::duration<double, std::nano>(n - t).count();
+    t = n;
+  }
+};
+SubmitClock g_submit_clock;
+
 // Pinned result buffers (vss_host_alloc): a masks_out inside one of these
 // receives the batch's D2H directly, so the completion copies nothing.  The
 // registry is process-wide (any handle, any GPU), keyed by start address.
@@ -1047,7 +1069,10 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   if (out_mode == VSS_OUT_FRAME && (size_t)n * fh * fw > (size_t)h->user_max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w)
     return fail(h, VSS_E_INVALID_ARG, "frame-size masks exceed max_batch * max_frame_h * max_frame_w");
   const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
+  SubmitClock& clk = g_submit_clock;
+  clk.start();
   std::lock_guard<std::mutex> lk(h->mu);
+  clk.mark(0);
   const vss_ticket t = h->next_ticket;
   // a free slot: its previous batch is done on every GPU, so its staging may be rewritten
   int k = lease;
@@ -1064,6 +1089,7 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   }
   Slot& s0 = h->slots[k];
   if (out_mode == VSS_OUT_FRAME && (rc = ensure_frame_masks(h, s0))) return rc;
+  clk.mark(1);
   // only the rows the resize reads cross PCIe when that skips 60 % of them or
   // more (measured: 1080p, 20 % of the rows, 8.7k -> 23-29k frames/s; at
   // 640x480, 50 %, the kernel's reads of pinned memory lost to one DMA of the
@@ -1094,7 +1120,9 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
       }
     }
   }
+  clk.mark(2);
   h->pool->run(jobs);
+  clk.mark(3);
   for (int r = 0; r < R; ++r) {
     vss_handle* e = E[r];
     Slot& s = e->slots[k];
@@ -1119,6 +1147,7 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
       if ((rc = forward(e, k, s.d_frames, nr, fh, fw, fc, rs, fbytes, s.d_masks, s.stream))) return fail(h, rc, e->err);
     }
   }
+  clk.mark(4);
   const float* res = s0.d_masks;
   if (h->rccl) {
     // one all-gather of f32 masks per GPU, m frames each (padding rows of the
@@ -1150,7 +1179,15 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   } else {
     HIP_TRY(h, hipMemcpyAsync(direct ? masks_out : s0.h_masks, res, bytes, hipMemcpyDeviceToHost, s0.stream));
   }
-  if (!sync) {
+  clk.mark(5);
+  if (!sync && direct && !cb) {
+    // nothing to run on the host when the batch completes: the slot's done
+    // event (recorded below, after the D2H) is the completion.  A host
+    // function costs the submitting thread ~7 us alone and ~140 us while
+    // other threads block in vss_wait (the N-API addon's waiters; measured
+    // with VSS_TIME_SUBMIT), so it is only enqueued for a copy or a callback.
+    s0.status = VSS_OK;
+  } else if (!sync) {
     // completions in submission order: after the previous batch's
     Slot& prev = h->slots[h->ticket_slot[(t + vss_handle::kTicketRing - 1) % vss_handle::kTicketRing]];
     if (t > 0 && prev.used && &prev != &s0) HIP_TRY(h, hipStreamWaitEvent(s0.stream, prev.done, 0));
@@ -1162,11 +1199,14 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
       return fail(h, VSS_E_HIP, std::string("hipLaunchHostFunc: ") + hipGetErrorString(e));
     }
   }
+  clk.mark(6);
   for (vss_handle* e : E) {
     HIP_TRY(e, hipSetDevice(e->device));
     if ((rc = release_slot(e, e->slots[k], e->slots[k].stream))) return fail(h, rc, e->err);
   }
   note_ticket(h, k);
+  clk.mark(7);
+  clk.calls += clk.on ? 1 : 0;
   if (ticket) *ticket = t;
   if (sync) {
     HIP_TRY(h, hipSetDevice(h->device));
@@ -1318,6 +1358,16 @@ int create_engine(const vss_config* cfg, int device, int max_batch, int user_max
 
 void destroy_engine(vss_handle* h) {
   if (!h) return;
+  if (g_submit_clock.on && g_submit_clock.calls > 0) {
+    static const char* names[SubmitClock::kPhases] = {"lock", "slot", "plan", "copy", "h2d+fwd", "d2h", "hostfn",
+                                                      "release"};
+    std::fprintf(stderr, "vss submit phases (us/call over %ld calls):", g_submit_clock.calls);
+    for (int k = 0; k < SubmitClock::kPhases; ++k)
+      std::fprintf(stderr, " %s %.1f", names[k], g_submit_clock.ns[k] / 1e3 / g_submit_clock.calls);
+    std::fprintf(stderr, "\n");
+    g_submit_clock = SubmitClock();
+    g_submit_clock.on = true;
+  }
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
   for (Slot& s : h->slots) {
