@@ -16,4 +16,9 @@ echo smoke ok
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.log 2>&1 || { tail -20 gpurun_out/bench_$TAG.log; exit 1; }
 tail -1 gpurun_out/bench_$TAG.log > gpurun_out/bench_$TAG.json
 cut -c1-300 gpurun_out/bench_$TAG.json
+# the profiled runs replay the tiles the bench's autotuner chose: autotuning
+# under the profiler's per-dispatch overhead picks differently, and the
+# summary's durations must describe the kernels the bench line timed
+export VSS_TILE=$(python3 tools/tiles_of.py gpurun_out/bench_$TAG.json)
+echo "VSS_TILE=$VSS_TILE"
 bash tools/prof_run.sh "$TAG"
