@@ -67,6 +67,16 @@ def test_version_and_argument_validation(pkg):
     assert e.value.code == pkg.VSS_E_INVALID_ARG
     with pytest.raises(pkg.VssError):
         pkg.Session(max_batch=0)
+    # pinned result blocks: bad arguments and pointers vss_host_alloc did not
+    # return are refused from the registry alone (no HIP call)
+    import ctypes
+    L = pkg.lib()
+    p = ctypes.c_void_p()
+    assert L.vss_host_alloc(0, ctypes.byref(p)) == pkg.VSS_E_INVALID_ARG
+    assert L.vss_host_alloc(64, None) == pkg.VSS_E_INVALID_ARG
+    buf = ctypes.create_string_buffer(64)
+    assert L.vss_host_free(ctypes.cast(buf, ctypes.c_void_p)) == pkg.VSS_E_INVALID_ARG
+    assert L.vss_host_free(None) == pkg.VSS_OK
 
 
 def test_no_silent_cpu_fallback(pkg):
