@@ -156,6 +156,37 @@ __device__ __forceinline__ void prep_finish(const uint32_t v[12], float dy, floa
   }
 }
 
+// prep_finish for two pixels at once: lane 0 / 1 of every float2 is pixel a /
+// b, so each sub, mul and FMA is one packed-FP32 instruction (v_pk_add_f32,
+// v_pk_mul_f32, v_pk_fma_f32: per lane the same IEEE operation as the scalar
+// one) — the same floats as two prep_finish calls, in about half the VALU
+// issue slots (b1's prologue is bound by VALU issue at 4.5 waves per SIMD).
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 div255x2(f2 v) {
+#pragma clang fp contract(off)
+  constexpr float kInv = 1.0f / 255.0f;
+  const f2 inv = {kInv, kInv}, c255 = {255.0f, 255.0f};
+  const f2 q = v * inv;
+  return __builtin_elementwise_fma(__builtin_elementwise_fma(-q, c255, v), inv, q);
+}
+
+__device__ __forceinline__ void prep_finish2(const uint32_t va[12], const uint32_t vb[12], float dya, float dxa,
+                                             float dyb, float dxb, float outa[3], float outb[3]) {
+#pragma clang fp contract(off)
+  const f2 dy = {dya, dyb}, dx = {dxa, dxb};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const f2 tl = {(float)va[c], (float)vb[c]}, tr = {(float)va[3 + c], (float)vb[3 + c]};
+    const f2 bl = {(float)va[6 + c], (float)vb[6 + c]}, br = {(float)va[9 + c], (float)vb[9 + c]};
+    const f2 top = __builtin_elementwise_fma(tr - tl, dx, tl);
+    const f2 bot = __builtin_elementwise_fma(br - bl, dx, bl);
+    const f2 o = div255x2(__builtin_elementwise_fma(bot - top, dy, top));
+    outa[c] = o.x;
+    outb[c] = o.y;
+  }
+}
+
 __device__ __forceinline__ void prep_sample(const uint8_t* __restrict__ f, long rs, int fc, int fh, int fw,
                                             float ry, float rx, int y, int x, float& r, float& g, float& b) {
   const PrepTap t = prep_tap(f, rs, fc, fh, fw, ry, rx, y, x);
@@ -642,17 +673,24 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       dxs[u] = t.dx;
     }
     VSS_STAMP(6);  // every load issued
+    // this thread's resized pixels two at a time on packed FP32 (prep_finish2)
+    float o[NX][3];
+#pragma unroll
+    for (int u = 0; u < NX; u += 2) {
+      if (u + 1 < NX)
+        prep_finish2(raw[u], raw[u + 1], dys[u], dxs[u], dys[u + 1], dxs[u + 1], o[u], o[u + 1]);
+      else
+        prep_finish(raw[u], dys[u], dxs[u], o[u]);
+    }
 #pragma unroll
     for (int u = 0; u < NX; ++u) {
       const int i = tid + 256 * u;
       if (i < XH * XW) {
         const int ly = i / XW, lx = i - ly * XW;
         const int yy = r0 + ly, xx = c0 + lx;
-        float o[3];
-        prep_finish(raw[u], dys[u], dxs[u], o);
         const bool valid = yy >= 0 && yy < sp.Hm && xx >= 0 && xx < sp.Wm;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) x0s[(c * XH + ly) * XWP + lx] = valid ? o[c] : 0.f;
+        for (int c = 0; c < 3; ++c) x0s[(c * XH + ly) * XWP + lx] = valid ? o[u][c] : 0.f;
       }
     }
 #pragma unroll
