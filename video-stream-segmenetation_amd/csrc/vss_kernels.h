@@ -75,7 +75,7 @@ constexpr int kMaxAcc = 16;         // 16x16 project accumulators per wave
 __host__ __device__ constexpr int block_pix(int r) { return VSS_PERM ? (r < 4 ? r : (r < 12 ? r + 4 : r - 8)) : r; }
 // floats per pixel of an expand wave's hidden chunk in LDS (16 channels + pad)
 __host__ __device__ constexpr int hid_stride(int stride) { return stride == 2 ? 20 : VSS_HS1; }
-constexpr int kAccSlots = 16;       // instance-norm accumulator slots per frame and layer
+constexpr int kAccSlots = 4;        // instance-norm accumulator slots per frame and layer
                                     // (spreads the producers' atomics over 16x the cache lines)
 
 __host__ __device__ constexpr int r4(int v) { return (v + 3) & ~3; }
