@@ -290,3 +290,21 @@ def test_node_face_tracker_matches_python_host(addon_built, pkg, synthetic, tmp_
         pa, _, _, _ = chain.segment(frames)
     assert np.array_equal(np.fromfile(str(op) + ".f32", np.float32).reshape(n, -1), pa)
     assert sum(f["box"] is not None for f in info["faces"]) == 3
+
+
+@pytest.mark.gpu
+def test_node_result_blocks_recycled_safely(addon_built, synthetic, tmp_path):
+    """The addon's pinned result blocks return to its pool when V8 collects a
+    result: a result still held keeps its masks, and recycled blocks carry the
+    masks of the batch they were handed to (forced collections in between)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    frames = np.stack([synthetic.make_frame(900 + i, 480, 640, 3) for i in range(4)])
+    fp = tmp_path / "frames.bin"
+    frames.tofile(fp)
+    out = subprocess.run([NODE, "--expose-gc", os.path.join(ROOT, "tests", "node", "run_recycle.js"), str(fp), "2",
+                          "480", "640", "3", "30"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    assert info == {"heldIntact": True, "allEqual": True, "iters": 30}
