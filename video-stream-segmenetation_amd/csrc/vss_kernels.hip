@@ -621,21 +621,44 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     __syncthreads();
     // upsampled channels: PyTorch upsample_bilinear2d(scale 2, align_corners=False)
     // of relu(src * scale + shift) (the src's instance norm, applied per tap)
+    // Every read of this thread's items is issued before any of its writes:
+    // with a read -> write chain per item (the compiler cannot move an item's
+    // LDS reads above the previous item's write into the same array) the
+    // items ran one LDS round trip after another.  Reads are branch-free
+    // (outside-the-frame records read a valid dummy address; their value is
+    // dropped below).
+    constexpr int NU = (P_IN_PAD * C4L + 255) / 256;
+    uint4 rec[NU];
 #pragma unroll
-    for (int k = 0; k < (P_IN_PAD * C4L + 255) / 256; ++k) {
+    for (int k = 0; k < NU; ++k)
+      rec[k] = reinterpret_cast<const uint4*>(uc)[min(tid + 256 * k, P_IN_PAD * C4L - 1) / C4L];
+    f4 t00[NU], t01[NU], t10[NU], t11[NU];
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+      const int c4 = min(tid + 256 * k, P_IN_PAD * C4L - 1) % C4L;
+      const bool in = rec[k].x != 0xFFFFFFFFu;
+      const unsigned a = in ? rec[k].x : 0u, b = in ? rec[k].y : 0u;
+      t00[k] = *reinterpret_cast<const f4*>(lr + (a & 0xFFFFu) + 4 * c4);
+      t01[k] = *reinterpret_cast<const f4*>(lr + (a >> 16) + 4 * c4);
+      t10[k] = *reinterpret_cast<const f4*>(lr + (b & 0xFFFFu) + 4 * c4);
+      t11[k] = *reinterpret_cast<const f4*>(lr + (b >> 16) + 4 * c4);
+    }
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
       const int i = tid + 256 * k;
       if (i < P_IN_PAD * C4L) {
         const int pix = i / C4L, c4 = i % C4L;
-        const uint4 rec = reinterpret_cast<const uint4*>(uc)[pix];
         f4 v = {0.f, 0.f, 0.f, 0.f};
-        if (rec.x != 0xFFFFFFFFu) {
-          const float ly1 = __uint_as_float(rec.z), ly0 = 1.f - ly1;
-          const float lx1 = __uint_as_float(rec.w), lx0 = 1.f - lx1;
-          const f4 v00 = *reinterpret_cast<const f4*>(lr + (rec.x & 0xFFFFu) + 4 * c4);
-          const f4 v01 = *reinterpret_cast<const f4*>(lr + (rec.x >> 16) + 4 * c4);
-          const f4 v10 = *reinterpret_cast<const f4*>(lr + (rec.y & 0xFFFFu) + 4 * c4);
-          const f4 v11 = *reinterpret_cast<const f4*>(lr + (rec.y >> 16) + 4 * c4);
-          v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+        if (rec[k].x != 0xFFFFFFFFu) {
+          // the lerps as explicit FMAs: every tile variant compiles the same
+          // operations (left to contraction, variants fused differently)
+          const float ly1 = __uint_as_float(rec[k].z), ly0 = 1.f - ly1;
+          const float lx1 = __uint_as_float(rec[k].w), lx0 = 1.f - lx1;
+          const f4 lx0v = {lx0, lx0, lx0, lx0}, lx1v = {lx1, lx1, lx1, lx1};
+          const f4 ly0v = {ly0, ly0, ly0, ly0}, ly1v = {ly1, ly1, ly1, ly1};
+          const f4 top = __builtin_elementwise_fma(lx1v, t01[k], lx0v * t00[k]);
+          const f4 bot = __builtin_elementwise_fma(lx1v, t11[k], lx0v * t10[k]);
+          v = __builtin_elementwise_fma(ly1v, bot, ly0v * top);
         }
         *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
       }
