@@ -739,15 +739,24 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     {
       const StemTaps taps = stem_taps(sws, r, g, XH * XWP, XWP);
       const float bias = sbs[r];
+      // most tiles lie inside the image with their halo: then only the
+      // padding pixels past the tile are zeroed, no per-pixel row / column test
+      const bool interior = iy0 >= 0 && iy0 + L.IH <= H && ix0 >= 0 && ix0 + IW <= W;
       for (int blk = wave; blk < P_IN_PAD / 16; blk += 4) {
         const int pa = min(blk * 16 + r, P_IN - 1), py = pa / IW, px = pa - py * IW;
         const f4 acc = stem_mfma(taps, x0s + 2 * py * XWP + 2 * px, bias);
+        const int p0 = blk * 16 + 4 * g;
+        if (interior) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {  // D[pixel 4g+i][channel r]
-          const int pp = blk * 16 + 4 * g + i, qy = pp / IW, qx = pp - qy * IW;
-          const int yy = iy0 + qy, xx = ix0 + qx;
-          const bool valid = pp < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
-          xt[pp * XS + r] = valid ? relu6f(acc[i]) : 0.f;
+          for (int i = 0; i < 4; ++i) xt[(p0 + i) * XS + r] = p0 + i < P_IN ? relu6f(acc[i]) : 0.f;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {  // D[pixel 4g+i][channel r]
+            const int pp = p0 + i, qy = pp / IW, qx = pp - qy * IW;
+            const int yy = iy0 + qy, xx = ix0 + qx;
+            const bool valid = pp < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            xt[pp * XS + r] = valid ? relu6f(acc[i]) : 0.f;
+          }
         }
       }
     }
