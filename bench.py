@@ -283,10 +283,37 @@ def post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, st
             "composite": composite}
 
 
-def run_steps(sess, streams, n_steps, launch):
-    """Issue n_steps round-robin over the streams (launch(k, stream) per step)."""
-    for i in range(n_steps):
+def run_steps(sess, streams, n_steps, launch, start=0):
+    """Issue n_steps round-robin over the streams (launch(k, stream) per step).
+    `start` continues the global step count: step k uses stream, output buffer
+    and (the handle's round-robin over device calls) slot k % S, so a slot
+    always meets the same buffers and its graph is never patched."""
+    for i in range(start, start + n_steps):
         launch(i, streams[i % len(streams)])
+    return start + n_steps
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """--gpus N without a torch.distributed launcher: start N rank processes
+    (torch.distributed.run, one per GPU) from this process, which has not
+    touched the GPU (device_count() does not initialise HIP on this image),
+    and return their exit code.  Fewer than N visible GPUs is an error."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev < n:
+        print(f"bench.py: --gpus {n} needs {n} GPUs, {ndev} visible", file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def sweep(pkg, torch, dev, fh, fw, dtype, inflight, steps):
@@ -305,11 +332,13 @@ def sweep(pkg, torch, dev, fh, fw, dtype, inflight, steps):
                     s.segment_device(d.data_ptr(), B, fh, fw, 3, fw * 3, fh * fw * 3, masks[i % S].data_ptr(),
                                      st.cuda_stream)
 
-                run_steps(s, streams, 10, go)
+                s.prepare_device(B, fh, fw, 3, fw * 3, fh * fw * 3)
+
+                k = run_steps(s, streams, 10, go)
                 torch.cuda.synchronize(dev)
                 n = max(20, steps * 8 // B)
                 t0 = time.perf_counter()
-                run_steps(s, streams, n, go)
+                run_steps(s, streams, n, go, start=k)
                 torch.cuda.synchronize(dev)
                 el = time.perf_counter() - t0
                 out.append({"batch": B, "inflight": S, "value": round(B * n / el, 1),
@@ -340,7 +369,12 @@ def main():
                     help="per-kernel HBM traffic from tools/prof_summary.py (PMC passes)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks", file=sys.stderr, flush=True)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     fh, fw = (int(v) for v in args.frame.split("x"))
@@ -359,7 +393,10 @@ def main():
         # reduction (CPU tensors); the masks go over the handle's own RCCL clique
         dist.init_process_group("gloo")
     ndev = torch.cuda.device_count()
-    gpu = local % max(1, ndev)
+    if ndev < 1 or (world > 1 and local >= ndev):
+        print(f"bench.py: rank {rank} (local {local}) has no GPU ({ndev} visible)", file=sys.stderr, flush=True)
+        sys.exit(2)
+    gpu = local
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
 
@@ -394,18 +431,42 @@ def main():
         else:
             sess.segment_device(d_frames.data_ptr(), B, fh, fw, 3, rs, fs, outs[i % S].data_ptr(), st.cuda_stream)
 
-    run_steps(sess, streams, args.warmup, step)
+    # every slot's graph for this shape is built before the first step, so no
+    # build (and, with the buffer pairing of run_steps, no patch) happens in
+    # the timed region at any --warmup
+    sess.prepare_device(B, fh, fw, 3, rs, fs)
+    k = run_steps(sess, streams, args.warmup, step)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    builds0, patches0 = sess.graph_builds, sess.graph_patches
     t0 = time.perf_counter()
-    run_steps(sess, streams, args.steps, step)
+    k = run_steps(sess, streams, args.steps, step, start=k)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    last = (args.steps - 1) % S
+    timed_builds, timed_patches = sess.graph_builds - builds0, sess.graph_patches - patches0
+    last = (k - 1) % S
+    # per-step completion times (a second pass of the same K steps, events on
+    # each step's stream; kept out of the headline window): the median interval
+    ends = []
+
+    def step_ev(i, st):
+        step(i, st)
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(st)
+        ends.append(e)
+
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record(streams[k % S])
+    k = run_steps(sess, streams, args.steps, step_ev, start=k)
+    torch.cuda.synchronize(dev)
+    done_ms = sorted(e0.elapsed_time(e) for e in ends)
+    iv = np.diff(done_ms)
+    median_step_ms = float(np.median(iv)) if len(iv) else None
+    n_ranks = sess.comm_ranks if gather else world
     d_masks = outs[last][rank * B:(rank + 1) * B] if world > 1 else outs[last][:B]
     if gather:  # the gathered batch holds every rank's masks in frame order
         assert all(torch.equal(outs[last], o) for o in outs), "every step gathers the same masks"
@@ -474,10 +535,14 @@ def main():
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "frames/s",
-            "n_gpus": world,
+            "n_gpus": n_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el_max * 1e3 / args.steps, 5),
+            "median_step_ms": round(median_step_ms, 5) if median_step_ms else None,
+            "value_at_median_step": round(world * B / (median_step_ms * 1e-3), 1) if median_step_ms else None,
+            "graph_builds_in_timed_region": timed_builds,
+            "graph_patches_in_timed_region": timed_patches,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSS_VERSION 20000 /* 2.0.0: queued slots, multi-GPU handles, RCCL */
+#define VSS_VERSION 30000 /* 3.0.0: graphs patched per call, completion thread, shard plan */
 
 enum {
   VSS_OK = 0,
@@ -73,7 +73,9 @@ enum { VSS_OUT_MODEL = 0, VSS_OUT_FRAME = 1 };
  * removed; DESIGN.md keeps the numbers.  Setting them fails with
  * VSS_E_UNSUPPORTED.) */
 enum {
-  VSS_OPT_USE_GRAPH = 1, /* 1: replay a captured hipGraph per (slot, shape, buffers) (default 1) */
+  VSS_OPT_USE_GRAPH = 1, /* 1: replay a hipGraph per (slot, shape) (default 1); a call with other
+                            frame / mask buffers patches the graph's first and last kernel nodes
+                            (hipGraphExecKernelNodeSetParams) instead of building a new one */
   VSS_OPT_PROFILE = 2,   /* 1: time every kernel with HIP events (eager launches)         */
   VSS_OPT_KEEP_STEM = 6, /* 1: the stem fused into layer 1 also stores its activation, so
                             vss_read_layer(0) can report it (a debugging aid: 4.7 MB of HBM
@@ -81,13 +83,18 @@ enum {
                             the forward writes only what a later layer or the caller reads;
                             vss_read_layer(0) fails with VSS_E_INVALID_ARG unless the latest
                             forward ran with the option set. */
-  VSS_OPT_ROW_FETCH = 7  /* 1 (default): the queued host calls move only the frame rows the
+  VSS_OPT_ROW_FETCH = 7, /* 1 (default): the queued host calls move only the frame rows the
                             tfjs-legacy resize reads (frameProcessorTest.ts:80) across PCIe —
                             staged host-side and fetched by a kernel from pinned memory — when
                             that skips 60 % of the rows or more (four fifths at 720p and 1080p
                             for 144 model rows; at 640x480 half, where one DMA of the whole
                             frames is faster); 0: whole frames by DMA.  Masks are identical
                             either way. */
+  /* Read-only counters (vss_get_option; vss_set_option fails): */
+  VSS_OPT_GRAPH_BUILDS = 8,  /* executable graphs built (one per slot and shape)            */
+  VSS_OPT_GRAPH_PATCHES = 9, /* graph replays that patched their buffers' kernel parameters */
+  VSS_OPT_COMM_RANKS = 10    /* ranks of the handle's RCCL clique (ncclCommCount; the GPUs of a
+                                multi-GPU handle; 1 without a clique)                        */
 };
 
 typedef struct vss_handle vss_handle;
@@ -107,7 +114,7 @@ typedef struct vss_config {
   int n_gpus;
   const int* device_ids;
   int queue_depth;              /* batches in flight (slots per GPU); 0 = default 4, max 16 */
-  int staging_threads;          /* host threads for the pinned staging copies; 0 = default 4 */
+  int staging_threads;          /* host threads for the pinned staging copies; 0 = default 8 */
 } vss_config;
 
 /* vss_config.flags */
@@ -126,9 +133,10 @@ typedef struct vss_info {
   int rccl;                /* 1: the host calls all-gather the masks over RCCL */
 } vss_info;
 
-/* status callback for vss_segment_async: called on a runtime thread once the
- * masks are in masks_out (status = VSS_OK) or the call failed; in submission
- * order. */
+/* status callback for vss_segment_async: called on the handle's completion
+ * thread once the masks are in masks_out (status = VSS_OK) or the batch
+ * failed; in submission order.  No lock is held: the callback may call vss_*
+ * functions of its handle (a new submit, vss_query), except vss_destroy. */
 typedef void (*vss_callback)(void* user, int status);
 
 /* Submission ticket of a queued batch (vss_submit, vss_wait). */
@@ -223,6 +231,22 @@ int vss_host_free(void* ptr);
 int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width,
                        int channels, size_t row_stride, size_t frame_stride, float* d_masks,
                        void* stream);
+
+/* Build the executable graphs of every slot for this batch shape now (no
+ * launch), so the first calls of a steady loop replay instead of building
+ * (the graph is otherwise built by the slot's first call of that shape).
+ * The device pointers are bound by the first call. */
+int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels, size_t row_stride,
+                       size_t frame_stride);
+
+/* The batch sharding of SURVEY.md §8(e), host-only (no GPU needed): a batch
+ * of n frames over nranks GPUs in contiguous shards of *per_rank =
+ * ceil(n / nranks) frames; rank `rank` takes frames [*first, *first + *count)
+ * (the last ranks may get fewer, or none).  Every rank all-gathers *per_rank
+ * rows, so the gathered [nranks][per_rank] rows hold frame i at row i (only
+ * the last non-empty shard can be short; its padding rows follow frame n-1).
+ * The multi-GPU handle and vss_segment_gather_device callers use this plan. */
+int vss_shard_plan(int n, int nranks, int rank, int* first, int* count, int* per_rank);
 
 /* ---- one GPU per process (torchrun): an RCCL clique over the processes ------
  * Rank 0 calls vss_comm_unique_id (ids for every slot; *len bytes, at most

@@ -1,7 +1,14 @@
-"""CPU tests of the data-parallel path (world_size 2, gloo): frame sharding,
-ragged batches and the ordered all-gather of masks.  The per-frame compute is
-the CPU oracle here (the checker), so the gathered result must equal a
-single-process oracle run on the whole batch."""
+"""CPU tests of the product's multi-GPU batch plan.
+
+libvss's `vss_shard_plan` is the plan the multi-GPU handle (submit_host) and
+the one-GPU-per-process clique use: contiguous shards of ceil(n / R) frames,
+an all-gather of ceil(n / R) rows per rank, frame i at gathered row i.  It is
+host-only, so it is checked here exhaustively, and a world-size-2 gloo run
+drives the same plan end to end: each rank computes its shard (the CPU oracle
+stands in for the GPU forward — the checker), pads it to `per_rank` rows and
+all-gathers, exactly the collective the C ABI issues over RCCL; the first n
+gathered rows must equal a single-process run over the whole batch.  The RCCL
+exchange itself is measured only on an 8-GPU node (the driver's SCALE run)."""
 import os
 import socket
 
@@ -12,18 +19,32 @@ import torch.multiprocessing as mp
 from conftest import load_pkg
 
 
-def test_shard_range_partition():
+@pytest.mark.parametrize("R", range(1, 9))
+def test_shard_plan_exhaustive(R):
     pkg = load_pkg()
-    import vss_amd.parallel as par
-    for n in range(0, 20):
-        for world in (1, 2, 3, 4, 8):
-            covered = []
-            for r in range(world):
-                s, c = par.shard_range(n, r, world)
-                assert c <= par.shard_capacity(n, world)
-                covered.extend(range(s, s + c))
-            assert covered == list(range(n))
-    _ = pkg
+    for n in range(0, 71):
+        covered, gathered = [], []
+        per_all = set()
+        for r in range(R):
+            first, count, per = pkg.shard_plan(n, R, r)
+            per_all.add(per)
+            assert per == -(-n // R)
+            assert 0 <= count <= per
+            covered.extend(range(first, first + count))
+            # the rank's `per` gathered rows: its frames, then padding (None)
+            gathered.extend(list(range(first, first + count)) + [None] * (per - count))
+        assert len(per_all) == 1
+        assert covered == list(range(n)), (n, R)
+        # frame order: the first n gathered rows are frames 0..n-1, only padding after
+        assert gathered[:n] == list(range(n)), (n, R)
+        assert all(g is None for g in gathered[n:])
+
+
+def test_shard_plan_rejects_bad_args():
+    pkg = load_pkg()
+    for args in ((-1, 2, 0), (4, 0, 0), (4, 2, 2), (4, 2, -1)):
+        with pytest.raises(pkg.VssError):
+            pkg.shard_plan(*args)
 
 
 def _free_port():
@@ -39,28 +60,27 @@ def _worker(rank, world, port, n_total, blob_path, q):
     sys.path.insert(0, os.path.dirname(__file__))
     from conftest import load_pkg as lp
     import oracle_py
-    lp()
-    import vss_amd.parallel as par
+    pkg = lp()
     import vss_amd.synthetic as syn
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         blob = open(blob_path, "rb").read()
-        start, count = par.shard_range(n_total, rank, world)
-        frames = np.stack([syn.make_frame(i, 60, 80) for i in range(start, start + count)]) if count else None
+        first, count, per = pkg.shard_plan(n_total, world, rank)
+        send = torch.zeros((per, 32 * 48), dtype=torch.float32)  # padding rows stay zero
         if count:
-            local = torch.from_numpy(oracle_py.forward(blob, frames, 32, 48, mode=0).reshape(count, -1))
-        else:
-            local = torch.zeros((0, 32 * 48))
-        full = par.gather_masks(local, n_total)
-        q.put((rank, full.numpy()))
+            frames = np.stack([syn.make_frame(i, 60, 80) for i in range(first, first + count)])
+            send[:count] = torch.from_numpy(oracle_py.forward(blob, frames, 32, 48, mode=0).reshape(count, -1))
+        buf = torch.empty((world * per, 32 * 48), dtype=torch.float32)
+        dist.all_gather_into_tensor(buf, send)
+        q.put((rank, buf[:n_total].numpy()))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("n_total", [4, 5, 1])
-def test_gather_masks_gloo_world2(blob, n_total):
+def test_gather_plan_gloo_world2(blob, n_total):
     pkg = load_pkg()
     import oracle_py
     import vss_amd.synthetic as syn

@@ -42,7 +42,7 @@ def test_node_module_loads_and_fails_loudly_without_gpu(addon_built):
                          timeout=60)
     assert out.returncode == 0, out.stderr
     lines = out.stdout.split()
-    assert lines[0] == "20000"
+    assert lines[0] == "30000"
     if not torch.cuda.is_available():
         assert lines[1:] == ["error", "-2"]
 
@@ -61,7 +61,7 @@ def test_node_segment_matches_oracle_and_python_host(addon_built, pkg, oracle, b
     assert out.returncode == 0, out.stderr
     info = json.loads(out.stdout.strip().splitlines()[-1])
     assert info == {"width": 256, "height": 144, "count": 3, "singleMatchesBatch": True,
-                    "oversizeRejected": True, "version": 20000, "frameDims": [640, 480, 3 * 480 * 640]}
+                    "oversizeRejected": True, "version": 30000, "frameDims": [640, 480, 3 * 480 * 640]}
     masks = np.fromfile(op, np.float32).reshape(3, -1)
     ref = oracle.forward(blob, frames, 144, 256, mode=0).reshape(3, -1)
     assert np.abs(masks - ref).max() <= 1e-3

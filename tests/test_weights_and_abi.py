@@ -57,7 +57,7 @@ def test_library_exports_header_symbols(pkg):
 
 def test_version_and_argument_validation(pkg):
     pkg.build()
-    assert pkg.version() == 20000
+    assert pkg.version() == 30000
     # invalid configs are rejected before any HIP call
     with pytest.raises(pkg.VssError) as e:
         pkg.Session(model_h=100, model_w=256)

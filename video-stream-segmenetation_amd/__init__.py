@@ -40,6 +40,7 @@ VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_I
     0, -1, -2, -3, -4, -5, -6, -7)
 DTYPES = {"f32": 0, "bf16x2": 1}
 VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_KEEP_STEM, VSS_OPT_ROW_FETCH = 1, 2, 6, 7
+VSS_OPT_GRAPH_BUILDS, VSS_OPT_GRAPH_PATCHES, VSS_OPT_COMM_RANKS = 8, 9, 10  # read-only counters
 VSS_CREATE_NO_AUTOTUNE = 1
 VSS_OUT_MODEL, VSS_OUT_FRAME = 0, 1
 
@@ -135,6 +136,8 @@ def lib() -> ctypes.CDLL:
                 "vss_submit_staged": ([P, I, I, I, I, I, S, P, I, CALLBACK, P, ctypes.POINTER(ctypes.c_uint64)], I),
                 "vss_submit_list": ([P, ctypes.POINTER(P), I, I, I, I, S, P, I, ctypes.POINTER(ctypes.c_uint64)], I),
                 "vss_segment_device": ([P, P, I, I, I, I, S, S, P, P], I),
+                "vss_prepare_device": ([P, I, I, I, I, S, S], I),
+                "vss_shard_plan": ([I, I, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)], I),
                 "vss_host_alloc": ([S, ctypes.POINTER(P)], I),
                 "vss_host_free": ([P], I),
                 "vss_comm_unique_id": ([P, P, S, ctypes.POINTER(S)], I),
@@ -358,6 +361,25 @@ class Session:
         _check(lib().vss_segment_device(self._h, frames_ptr, n, h, w, c, row_stride, frame_stride, masks_ptr,
                                         stream or None), self._h)
 
+    def prepare_device(self, n: int, h: int, w: int, c: int, row_stride: int, frame_stride: int):
+        """Build every slot's executable graph for this batch shape now (no launch)."""
+        _check(lib().vss_prepare_device(self._h, n, h, w, c, row_stride, frame_stride), self._h)
+
+    @property
+    def graph_builds(self) -> int:
+        """Executable graphs built so far (one per slot and batch shape)."""
+        return self.get_option(VSS_OPT_GRAPH_BUILDS)
+
+    @property
+    def graph_patches(self) -> int:
+        """Replays that patched a graph's buffer pointers (callers rotating buffers)."""
+        return self.get_option(VSS_OPT_GRAPH_PATCHES)
+
+    @property
+    def comm_ranks(self) -> int:
+        """Ranks of the handle's RCCL clique (ncclCommCount), 1 without one."""
+        return self.get_option(VSS_OPT_COMM_RANKS)
+
     def mask_to_frame_device(self, masks_ptr: int, n: int, frame_h: int, frame_w: int, out_ptr: int,
                              stream: int = 0):
         """HBM masks [n][maskH][maskW] -> [n][frame_h][frame_w] (VSS_OUT_FRAME's upsample)."""
@@ -548,6 +570,15 @@ def host_empty(shape, dtype=np.float32) -> np.ndarray:
     buf = (ctypes.c_uint8 * max(16, count * dt.itemsize)).from_address(blk.ptr)
     buf._block = blk  # the memory lives as long as any view of it
     return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
+
+
+def shard_plan(n: int, nranks: int, rank: int):
+    """(first, count, per_rank) of `rank`'s contiguous shard of an n-frame batch
+    (vss_shard_plan); the gathered [nranks][per_rank] rows hold
+    frame i at row i.  Host-only: no GPU needed."""
+    f, c, m = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _check(lib().vss_shard_plan(n, nranks, rank, ctypes.byref(f), ctypes.byref(c), ctypes.byref(m)))
+    return f.value, c.value, m.value
 
 
 def version() -> int:

@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <map>
 #include <mutex>
@@ -79,7 +80,32 @@ struct LayerPlan {
   float head_b = 0.f;
 };
 
-using GraphKey = std::tuple<const void*, const void*, int, int, int, int, size_t, size_t>;
+// One kernel launch of the forward: function, grid, LDS and its parameter
+// block (every kernel takes one parameter struct by value).
+struct Launch {
+  const void* fn = nullptr;
+  dim3 grid;
+  size_t lds = 0;
+  int layer = 0;
+  union Prm {
+    StemParams stem;
+    BlockParams block;
+    HeadParams head;
+  } prm;
+};
+
+// A forward's executable graph per (slot, shape).  The caller's frame and
+// mask pointers are not part of the key: a call with other buffers patches the
+// kernel nodes whose parameters differ (hipGraphExecKernelNodeSetParams — the
+// first layer reads the frames, the head writes the masks) instead of
+// capturing a new graph, so callers that rotate buffers never rebuild.
+using GraphKey = std::tuple<int, int, int, int, size_t, size_t>;  // n, fh, fw, fc, row / frame stride
+struct GraphEntry {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  std::vector<hipGraphNode_t> nodes;  // one kernel node per launch, in order
+  std::vector<Launch> launches;       // the parameters the executable graph holds now
+};
 
 // The rows of an fh-row frame that the tfjs-legacy resize to the model's rows
 // reads (prep_tap's y0 / y1, the same float arithmetic), for the queued host
@@ -97,13 +123,19 @@ struct Slot {
   float* d_masks = nullptr;           // [max_batch][P]: host paths' masks (the all-gather's send buffer)
   float* d_gather = nullptr;          // RCCL handles: [nranks * max_batch][P]
   hipStream_t stream = nullptr;       // the slot's stream (queued host calls)
-  hipEvent_t done = nullptr;          // recorded after the slot's latest work
+  hipEvent_t done = nullptr;          // recorded after the slot's latest work (host or device call)
+  hipEvent_t host_done = nullptr;     // engine 0: recorded after the latest host batch's D2H
   bool used = false;
+  // Host-side state of the slot's latest host batch (guarded by the handle's mu):
   bool leased = false;                // reserved by vss_staging_acquire for its holder's next call
-  int status = VSS_OK;                // of the slot's latest queued batch (set by its callback)
-  vss_ticket ticket = 0;              // latest ticket that ran in this slot
+  bool host_busy = false;             // a host batch whose completion (copy / callback /
+                                      // synchronous wait) has not finished; the slot's pinned
+                                      // buffers belong to it until then
+  int status = VSS_OK;                // of the latest host batch
+  vss_ticket ticket = ~0ull;          // latest host ticket that ran in this slot (device calls
+                                      // take no ticket and leave it alone)
   bool stem_stored = false;           // the latest forward stored the fused stem (VSS_OPT_KEEP_STEM)
-  std::map<GraphKey, hipGraphExec_t> graphs;
+  std::map<GraphKey, GraphEntry> graphs;
   ncclComm_t comm = nullptr;          // this GPU's communicator of the slot (RCCL handles)
   // host-path staging, allocated on the slot's first host call
   uint8_t* d_frames = nullptr;
@@ -242,7 +274,6 @@ struct vss_handle {
   std::string err;
   int device = 0;
   hipStream_t stream = nullptr;          // NULL-stream device calls, post / composite, autotune
-  hipStream_t capture_stream = nullptr;  // hipGraph capture only (never executes)
   std::vector<Rec> recs;
   std::vector<float> hdata;
   float eps = 1e-5f;
@@ -289,12 +320,32 @@ struct vss_handle {
   // the caller's stream after the gather (vss_segment_gather_device)
   hipStream_t gather_stream = nullptr;
   std::vector<hipEvent_t> gather_ev;  // per slot: [2k] forward done, [2k+1] gather done
-  std::mutex mu;                   // serialises submissions (slot choice, staging, enqueue)
+  // Submissions (slot choice, staging, enqueue) are serialised by mu; no
+  // thread holds it while it waits for the GPU (waiters drop it first).
+  std::mutex mu;
+  std::condition_variable slot_cv;   // a slot's host_busy went false
   std::mutex post_mu;              // the synchronous post / composite calls share scratch
-  vss_ticket next_ticket = 0;
-  static constexpr int kTicketRing = 64;
-  int ticket_slot[kTicketRing] = {};  // slot of each of the latest tickets
+  vss_ticket next_ticket = 0;      // host batches (vss_submit*, vss_segment*)
+  unsigned long long device_calls = 0;  // vss_segment_device / _gather_device: slot = count % depth
+  long graph_builds = 0, graph_patches = 0;  // VSS_OPT_GRAPH_BUILDS / _PATCHES
   CopyPool* pool = nullptr;
+  // The completion thread (started on the first host batch that needs one):
+  // waits for the queued host batches in ticket order, copies their masks
+  // from the slot's pinned buffer into the caller's memory, fires callbacks.
+  struct Completion {
+    vss_ticket ticket;
+    int slot;
+    float* out;          // null: the D2H already went to the caller's pinned block
+    const float* src;
+    size_t bytes;
+    vss_callback cb;
+    void* user;
+  };
+  std::thread done_thread;
+  std::mutex done_mu;
+  std::condition_variable done_cv;
+  std::deque<Completion> done_q;
+  bool done_stop = false;
 };
 
 namespace {
@@ -646,6 +697,7 @@ int make_slot(vss_handle* h, Slot& s, int gather_ranks) {
   // N-API addon's libuv workers, vss_wait callers) would otherwise take the
   // cores the staging copies run on
   HIP_TRY(h, hipEventCreateWithFlags(&s.done, hipEventDisableTiming | hipEventBlockingSync));
+  HIP_TRY(h, hipEventCreateWithFlags(&s.host_done, hipEventDisableTiming | hipEventBlockingSync));
   return VSS_OK;
 }
 
@@ -766,40 +818,36 @@ BlockParams block_params(const vss_handle* h, const Slot& s, int li, int n) {
   return p;
 }
 
-// Enqueue the whole forward of n frames on stream st with slot s's buffers
-// (no sync, no alloc: graph-capturable).
-int enqueue_forward(vss_handle* h, Slot& s, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs,
-                    size_t fs, float* masks, hipStream_t st, int prof_slot) {
+// The forward of n frames with slot s's buffers as a list of launches (no
+// sync, no alloc): the eager path launches them, the graph path adds them as
+// kernel nodes.
+void forward_launches(vss_handle* h, Slot& s, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs,
+                      size_t fs, float* masks, std::vector<Launch>* out) {
   const int Hm = h->cfg.model_h, Wm = h->cfg.model_w;
   const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
   const int nl = (int)h->L.size();
+  out->clear();
   for (int i = 0; i < nl; ++i) {
     LayerPlan& l = h->L[i];
     const Rec& r = l.rec;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (prof_slot >= 0) {
-      e0 = h->ev[((size_t)prof_slot * nl + i) * 2];
-      e1 = h->ev[((size_t)prof_slot * nl + i) * 2 + 1];
-    }
-    auto go = [&](auto fn, dim3 grid, size_t lds, auto prm) {
-      if (prof_slot >= 0)
-        hipExtLaunchKernelGGL(fn, grid, dim3(kThreads), (uint32_t)lds, st, e0, e1, 0, prm);
-      else
-        hipLaunchKernelGGL(fn, grid, dim3(kThreads), lds, st, prm);
-    };
     if (l.fused) {  // runs inside its consumer's launch
 #ifdef VSS_TRACE
       h->trace_wgs[i] = 0;
 #endif
       continue;
     }
+    Launch L{};
+    L.layer = i;
     if (r.kind == K_STEM) {
       StemParams p = stem_params(h, s, i, frames, rs, fs, fh, fw, fc);
 #ifdef VSS_TRACE
       p.trace = h->trace[i];
       h->trace_wgs[i] = ((l.W + kStemTW - 1) / kStemTW) * ((l.H + kStemTH - 1) / kStemTH) * n;
 #endif
-      go(stem_kernel16(), dim3((l.W + kStemTW - 1) / kStemTW, (l.H + kStemTH - 1) / kStemTH, n), kStemLds * 4, p);
+      L.fn = (const void*)stem_kernel16();
+      L.grid = dim3((l.W + kStemTW - 1) / kStemTW, (l.H + kStemTH - 1) / kStemTH, n);
+      L.lds = kStemLds * 4;
+      L.prm.stem = p;
     } else if (r.kind == K_IR || r.kind == K_DEC) {
       BlockParams p = block_params(h, s, i, n);
       if (flags_stem_in(l.flags)) {
@@ -810,7 +858,10 @@ int enqueue_forward(vss_handle* h, Slot& s, const uint8_t* frames, int n, int fh
       p.trace = h->trace[i];
       h->trace_wgs[i] = l.tiles_x * l.tiles_y * n * l.ks;
 #endif
-      go(l.entry->fn[prec == PREC_F32 ? 0 : 1], dim3(l.tiles_x, l.tiles_y, n * l.ks), l.lds, p);
+      L.fn = (const void*)l.entry->fn[prec == PREC_F32 ? 0 : 1];
+      L.grid = dim3(l.tiles_x, l.tiles_y, n * l.ks);
+      L.lds = l.lds;
+      L.prm.block = p;
     } else if (r.kind == K_HEAD) {
       const LayerPlan& src = h->L[r.src];
       HeadParams p{};
@@ -824,7 +875,41 @@ int enqueue_forward(vss_handle* h, Slot& s, const uint8_t* frames, int n, int fh
       p.trace = h->trace[i];
       h->trace_wgs[i] = ((Wm + kHeadTW - 1) / kHeadTW) * ((Hm + kHeadTH - 1) / kHeadTH) * n;
 #endif
-      go(head_kernel16(), dim3((Wm + kHeadTW - 1) / kHeadTW, (Hm + kHeadTH - 1) / kHeadTH, n), kHeadLds * 4, p);
+      L.fn = (const void*)head_kernel16();
+      L.grid = dim3((Wm + kHeadTW - 1) / kHeadTW, (Hm + kHeadTH - 1) / kHeadTH, n);
+      L.lds = kHeadLds * 4;
+      L.prm.head = p;
+    } else {
+      continue;
+    }
+    out->push_back(L);
+  }
+}
+
+hipKernelNodeParams node_params(const Launch& L, void** args) {
+  hipKernelNodeParams kp{};
+  args[0] = const_cast<Launch::Prm*>(&L.prm);
+  kp.func = const_cast<void*>(L.fn);
+  kp.gridDim = L.grid;
+  kp.blockDim = dim3(kThreads);
+  kp.sharedMemBytes = (unsigned)L.lds;
+  kp.kernelParams = args;
+  kp.extra = nullptr;
+  return kp;
+}
+
+// Eager launches on stream st; prof_slot >= 0: each launch records its layer's
+// event pair of that profiling ring entry (hipExtLaunchKernel).
+int launch_eager(vss_handle* h, const std::vector<Launch>& ls, hipStream_t st, int prof_slot) {
+  const int nl = (int)h->L.size();
+  for (const Launch& L : ls) {
+    void* args[1] = {const_cast<Launch::Prm*>(&L.prm)};
+    if (prof_slot >= 0) {
+      hipEvent_t e0 = h->ev[((size_t)prof_slot * nl + L.layer) * 2];
+      hipEvent_t e1 = h->ev[((size_t)prof_slot * nl + L.layer) * 2 + 1];
+      HIP_TRY(h, hipExtLaunchKernel(L.fn, L.grid, dim3(kThreads), args, L.lds, st, e0, e1, 0));
+    } else {
+      HIP_TRY(h, hipLaunchKernel(L.fn, L.grid, dim3(kThreads), args, L.lds, st));
     }
   }
   hipError_t e = hipGetLastError();
@@ -852,14 +937,71 @@ bool has_fused_stem(const vss_handle* h) {
   return false;
 }
 
-// The forward of n frames with slot `si`'s buffers, on stream st: a captured
-// hipGraph per (slot, frames, masks, shape) replayed, or eager launches.
+void destroy_graph(GraphEntry& g) {
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g = GraphEntry();
+}
+
+// Build slot s's executable graph for these launches: one kernel node per
+// launch, each depending on the previous one (a linear chain).
+int build_graph(vss_handle* h, const std::vector<Launch>& ls, GraphEntry* out) {
+  GraphEntry g;
+  HIP_TRY(h, hipGraphCreate(&g.graph, 0));
+  g.launches = ls;
+  for (const Launch& L : g.launches) {
+    void* args[1];
+    const hipKernelNodeParams kp = node_params(L, args);
+    hipGraphNode_t node = nullptr;
+    const hipError_t e = hipGraphAddKernelNode(&node, g.graph, g.nodes.empty() ? nullptr : &g.nodes.back(),
+                                               g.nodes.empty() ? 0 : 1, &kp);
+    if (e != hipSuccess) {
+      destroy_graph(g);
+      return fail(h, VSS_E_HIP, std::string("hipGraphAddKernelNode: ") + hipGetErrorString(e));
+    }
+    g.nodes.push_back(node);
+  }
+  const hipError_t e = hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    destroy_graph(g);
+    return fail(h, VSS_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  }
+  h->graph_builds++;
+  *out = std::move(g);
+  return VSS_OK;
+}
+
+// Point slot si's graph at this call's launches: the kernel nodes whose
+// parameter blocks differ (the frames the first layer reads, the masks the
+// head writes) are updated in the executable graph.  An update must not race
+// a launch of the same graph still in flight, so it first waits for the
+// slot's previous work (only callers that change buffers ever get here).
+int patch_graph(vss_handle* h, Slot& s, GraphEntry& g, const std::vector<Launch>& ls) {
+  bool waited = false;
+  for (size_t i = 0; i < ls.size(); ++i) {
+    if (std::memcmp(&ls[i].prm, &g.launches[i].prm, sizeof(Launch::Prm)) == 0) continue;
+    if (!waited && s.used) HIP_TRY(h, hipEventSynchronize(s.done));
+    waited = true;
+    void* args[1];
+    const hipKernelNodeParams kp = node_params(ls[i], args);
+    HIP_TRY(h, hipGraphExecKernelNodeSetParams(g.exec, g.nodes[i], &kp));
+    g.launches[i] = ls[i];
+  }
+  if (waited) h->graph_patches++;
+  return VSS_OK;
+}
+
+// The forward of n frames with slot `si`'s buffers, on stream st: the slot's
+// executable graph for this shape replayed (built on first use, patched when
+// the buffers differ), or eager launches.
 int forward(vss_handle* h, int si, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, size_t fs,
             float* masks, hipStream_t st) {
   Slot& s = h->slots[si];
   h->last_n = n;
   h->last_slot = si;
   s.stem_stored = !has_fused_stem(h) || h->keep_stem;
+  std::vector<Launch> ls;
+  forward_launches(h, s, frames, n, fh, fw, fc, rs, fs, masks, &ls);
   if (h->profile) {
     const int ring = h->prof_next;
     h->prof_next = (h->prof_next + 1) % vss_handle::kProfRing;
@@ -867,40 +1009,31 @@ int forward(vss_handle* h, int si, const uint8_t* frames, int n, int fh, int fw,
       int rc = harvest_ring(h, ring);
       if (rc) return rc;
     }
-    int rc = enqueue_forward(h, s, frames, n, fh, fw, fc, rs, fs, masks, st, ring);
+    int rc = launch_eager(h, ls, st, ring);
     if (!rc) h->ring_pending[ring] = 1;
     return rc;
   }
-  if (!h->use_graph) return enqueue_forward(h, s, frames, n, fh, fw, fc, rs, fs, masks, st, -1);
-  GraphKey key{frames, masks, n, fh, fw, fc, rs, fs};
+  if (!h->use_graph) return launch_eager(h, ls, st, -1);
+  const GraphKey key{n, fh, fw, fc, rs, fs};
   auto it = s.graphs.find(key);
   if (it == s.graphs.end()) {
-    hipGraph_t g = nullptr;
-    hipGraphExec_t ge = nullptr;
-    HIP_TRY(h, hipStreamBeginCapture(h->capture_stream, hipStreamCaptureModeRelaxed));
-    int rc = enqueue_forward(h, s, frames, n, fh, fw, fc, rs, fs, masks, h->capture_stream, -1);
-    hipError_t e = hipStreamEndCapture(h->capture_stream, &g);
-    if (rc) {
-      if (g) (void)hipGraphDestroy(g);
-      return rc;
-    }
-    if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
-    e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
-    if (s.graphs.size() >= 16) {  // bound the cache
-      (void)hipGraphExecDestroy(s.graphs.begin()->second);
+    GraphEntry g;
+    if (int rc = build_graph(h, ls, &g)) return rc;
+    if (s.graphs.size() >= 16) {  // bound the cache (shapes per slot)
+      destroy_graph(s.graphs.begin()->second);
       s.graphs.erase(s.graphs.begin());
     }
-    it = s.graphs.emplace(key, ge).first;
+    it = s.graphs.emplace(key, std::move(g)).first;
+  } else if (int rc = patch_graph(h, s, it->second, ls)) {
+    return rc;
   }
-  HIP_TRY(h, hipGraphLaunch(it->second, st));
+  HIP_TRY(h, hipGraphLaunch(it->second.exec, st));
   return VSS_OK;
 }
 
 void drop_graphs(vss_handle* h) {
   for (Slot& s : h->slots) {
-    for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : s.graphs) destroy_graph(kv.second);
     s.graphs.clear();
   }
 }
@@ -937,9 +1070,10 @@ int release_slot(vss_handle* e, Slot& s, hipStream_t st) {
   return VSS_OK;
 }
 
-// Is slot k free on every GPU of the handle (its latest batch done, no lease)?
+// Is slot k free for a host batch on every GPU of the handle: no lease, no
+// host batch still completing, its latest work done?  (mu held)
 int slot_free(vss_handle* h, int k, bool* free_) {
-  *free_ = !h->slots[k].leased;
+  *free_ = !h->slots[k].leased && !h->slots[k].host_busy;
   if (!*free_) return VSS_OK;
   for (vss_handle* e : engines(h)) {
     Slot& s = e->slots[k];
@@ -955,37 +1089,114 @@ int slot_free(vss_handle* h, int k, bool* free_) {
   return VSS_OK;
 }
 
-// The slot for the next ticket: the first free one from its round-robin slot
-// on; if every slot is in flight, VSS_E_BUSY — or, with wait_free, the
-// round-robin slot once it is done.
-int pick_slot(vss_handle* h, bool wait_free, int* out) {
-  const int S = (int)h->slots.size();
-  const int k0 = (int)(h->next_ticket % S);
-  for (int j = 0; j < S; ++j) {
-    bool fr = false;
-    if (int rc = slot_free(h, (k0 + j) % S, &fr)) return rc;
-    if (fr) {
-      *out = (k0 + j) % S;
-      return VSS_OK;
-    }
+// Wait for events with mu released (lk is relocked before returning).
+int wait_events_unlocked(vss_handle* h, std::unique_lock<std::mutex>& lk,
+                         const std::vector<std::pair<int, hipEvent_t>>& evs) {
+  lk.unlock();
+  hipError_t e = hipSuccess;
+  for (const auto& de : evs) {
+    e = hipSetDevice(de.first);
+    if (e == hipSuccess) e = hipEventSynchronize(de.second);
+    if (e != hipSuccess) break;
   }
-  if (!wait_free) return fail(h, VSS_E_BUSY, "queue full: " + std::to_string(S) + " batches in flight");
-  int k = k0;
-  for (int j = 0; j < S && h->slots[k].leased; ++j) k = (k0 + j + 1) % S;
-  if (h->slots[k].leased) return fail(h, VSS_E_BUSY, "every slot is leased (vss_staging_acquire)");
-  for (vss_handle* e : engines(h)) {
-    HIP_TRY(e, hipSetDevice(e->device));
-    HIP_TRY(e, hipEventSynchronize(e->slots[k].done));
-  }
-  *out = k;
+  lk.lock();
+  if (e != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipEventSynchronize: ") + hipGetErrorString(e));
   return VSS_OK;
 }
 
-void note_ticket(vss_handle* h, int k) {
-  const vss_ticket t = h->next_ticket;
-  for (vss_handle* e : engines(h)) e->slots[k].ticket = t;
-  h->ticket_slot[t % vss_handle::kTicketRing] = k;
-  h->next_ticket = t + 1;
+// The slot for the next host batch (mu held through lk): the first free one
+// from the round-robin slot on; if every slot is in flight, VSS_E_BUSY — or,
+// with wait_free, wait for the round-robin slot (mu released meanwhile) and
+// look again.
+int pick_slot(vss_handle* h, std::unique_lock<std::mutex>& lk, bool wait_free, int* out) {
+  const int S = (int)h->slots.size();
+  for (;;) {
+    const int k0 = (int)(h->next_ticket % S);
+    for (int j = 0; j < S; ++j) {
+      bool fr = false;
+      if (int rc = slot_free(h, (k0 + j) % S, &fr)) return rc;
+      if (fr) {
+        *out = (k0 + j) % S;
+        return VSS_OK;
+      }
+    }
+    if (!wait_free) return fail(h, VSS_E_BUSY, "queue full: " + std::to_string(S) + " batches in flight");
+    int k = -1;
+    for (int j = 0; j < S && k < 0; ++j)
+      if (!h->slots[(k0 + j) % S].leased) k = (k0 + j) % S;
+    if (k < 0) return fail(h, VSS_E_BUSY, "every slot is leased (vss_staging_acquire)");
+    if (h->slots[k].host_busy) {  // its completion is still running: wait for it
+      h->slot_cv.wait(lk);
+      continue;
+    }
+    std::vector<std::pair<int, hipEvent_t>> evs;
+    for (vss_handle* e : engines(h))
+      if (e->slots[k].used) evs.push_back({e->device, e->slots[k].done});
+    if (int rc = wait_events_unlocked(h, lk, evs)) return rc;
+  }
+}
+
+// a batch of n frames over R GPUs in contiguous shards of
+// per = ceil(n / R); rank r takes [first, first + count) (the last ranks may
+// get fewer frames, or none).  Every rank all-gathers `per` rows, so the
+// gathered [R][per] rows hold frame i at row i and the padding rows after the
+// last frame (only the last non-empty shard can be short).
+void shard_plan(int n, int R, int r, int* first, int* count, int* per) {
+  const int m = R > 0 ? (n + R - 1) / R : 0;
+  const int f0 = r * m;
+  *first = std::min(f0, n);
+  *count = std::max(0, std::min(n - f0, m));
+  *per = m;
+}
+
+// Completion thread of a handle: host batches that need host work when they
+// finish (a copy out of the slot's pinned buffer, a callback) are queued in
+// ticket order; the thread waits for each batch's D2H, copies, marks the
+// slot free for reuse and fires the callback (outside every lock, so a
+// callback may call vss_* functions — except vss_destroy of its own handle).
+void completion_loop(vss_handle* h) {
+  (void)hipSetDevice(h->device);
+  for (;;) {
+    vss_handle::Completion c;
+    {
+      std::unique_lock<std::mutex> dl(h->done_mu);
+      h->done_cv.wait(dl, [&] { return h->done_stop || !h->done_q.empty(); });
+      if (h->done_q.empty()) return;  // stopping, and every queued batch completed
+      c = h->done_q.front();
+      h->done_q.pop_front();
+    }
+    Slot& s = h->slots[c.slot];
+    const hipError_t e = hipEventSynchronize(s.host_done);  // not re-recorded while host_busy
+    const int st = e == hipSuccess ? VSS_OK : VSS_E_HIP;
+    if (st == VSS_OK && c.out) std::memcpy(c.out, c.src, c.bytes);
+    {
+      std::lock_guard<std::mutex> lk(h->mu);
+      if (st != VSS_OK) h->err = std::string("batch failed: ") + hipGetErrorString(e);
+      s.status = st;
+      s.host_busy = false;
+    }
+    h->slot_cv.notify_all();
+    if (c.cb) c.cb(c.user, st);
+  }
+}
+
+void push_completion(vss_handle* h, const vss_handle::Completion& c) {  // mu held
+  if (!h->done_thread.joinable()) h->done_thread = std::thread(completion_loop, h);
+  {
+    std::lock_guard<std::mutex> dl(h->done_mu);
+    h->done_q.push_back(c);
+  }
+  h->done_cv.notify_one();
+}
+
+void stop_completions(vss_handle* h) {
+  if (!h->done_thread.joinable()) return;
+  {
+    std::lock_guard<std::mutex> dl(h->done_mu);
+    h->done_stop = true;
+  }
+  h->done_cv.notify_all();
+  h->done_thread.join();
 }
 
 // VSS_TIME_SUBMIT=1: host time of each phase of the queued submit, summed over
@@ -1024,30 +1235,17 @@ bool pinned_range(const void* p, size_t bytes) {
   return a >= it->first && a + bytes <= it->first + it->second;
 }
 
-struct HostDone {
-  float* out;
-  const float* src;
-  size_t bytes;
-  vss_callback cb;
-  void* user;
-  Slot* slot;
-};
-
-void host_done(void* p) {  // a HIP runtime thread, in stream order
-  HostDone* c = static_cast<HostDone*>(p);
-  if (c->out) std::memcpy(c->out, c->src, c->bytes);
-  c->slot->status = VSS_OK;
-  if (c->cb) c->cb(c->user, VSS_OK);
-  delete c;
-}
-
 // A queued host call: stage n host frames (each GPU its contiguous shard),
 // then on every GPU's slot stream H2D -> forward -> [RCCL all-gather] and on
-// engine 0's: [frame-size upsample] -> D2H -> the completion (host function,
-// after the previous batch's, so completions keep submission order).
-//   wait_free: block until the slot is free (else VSS_E_BUSY);
-//   sync: wait for the batch and copy the masks here (no host function).
-//   list: frame i at list[i] instead of frames + i * height * row_stride.
+// engine 0's: [frame-size upsample] -> D2H -> host_done.  What happens on the
+// host when the batch is done:
+//   * masks_out inside a vss_host_alloc block and no callback: nothing — the
+//     D2H wrote them there, the event is the completion (vss_wait syncs it);
+//   * otherwise the completion thread copies out of the slot's pinned buffer
+//     and fires the callback, in ticket order;
+//   * sync (vss_segment): the calling thread waits and copies, mu released.
+//   wait_free: block until a slot is free (else VSS_E_BUSY);
+//   list: frame i at list[i] instead of frames + i * height * row_stride;
 //   lease: the slot a vss_staging_acquire reserved (-1: pick a free one).
 int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list, int n, int fh, int fw, int fc,
                 size_t rs, float* masks_out, int out_mode, bool wait_free, bool sync, vss_callback cb, void* user,
@@ -1062,7 +1260,8 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   if (rc) return rc;
   const std::vector<vss_handle*> E = engines(h);
   const int R = (int)E.size();
-  const int m = (n + R - 1) / R;  // frames per GPU (the last GPUs may get fewer, or none)
+  int m = 0, f0_, n0_;
+  shard_plan(n, R, 0, &f0_, &n0_, &m);  // frames per GPU
   const size_t fbytes = (size_t)fh * rs;
   if ((size_t)m * fbytes > h->frame_cap)
     return fail(h, VSS_E_INVALID_ARG, "frames exceed the handle's staging capacity (max_frame_h/w)");
@@ -1071,16 +1270,15 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
   SubmitClock& clk = g_submit_clock;
   clk.start();
-  std::lock_guard<std::mutex> lk(h->mu);
+  std::unique_lock<std::mutex> lk(h->mu);
   clk.mark(0);
-  const vss_ticket t = h->next_ticket;
   // a free slot: its previous batch is done on every GPU, so its staging may be rewritten
   int k = lease;
   if (lease >= 0) {
     if (lease >= (int)h->slots.size() || !h->slots[lease].leased)
       return fail(h, VSS_E_INVALID_ARG, "not a leased slot (vss_staging_acquire)");
     h->slots[lease].leased = false;  // its batch runs now
-  } else if ((rc = pick_slot(h, wait_free, &k))) {
+  } else if ((rc = pick_slot(h, lk, wait_free, &k))) {
     return rc;
   }
   for (vss_handle* e : E) {
@@ -1103,7 +1301,8 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   // stage every GPU's shard (zero-copy when the caller wrote into this slot's buffer)
   std::vector<CopyPool::Job> jobs;
   for (int r = 0; r < R; ++r) {
-    const int f0 = r * m, nr = std::max(0, std::min(n - f0, m));
+    int f0, nr, per;
+    shard_plan(n, R, r, &f0, &nr, &per);
     uint8_t* dst = E[r]->slots[k].h_frames;
     for (int i = 0; i < nr; ++i) {
       const uint8_t* src = list ? list[f0 + i] : frames + (size_t)(f0 + i) * fbytes;
@@ -1123,12 +1322,28 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   clk.mark(2);
   h->pool->run(jobs);
   clk.mark(3);
+  // From the first claim on, every exit records each claimed slot's done event
+  // (so the slot's next user is ordered after whatever was enqueued) and a
+  // failure leaves the slot free with the error as its status.
+  int claimed = 0;
+  auto abort_batch = [&](int code) {
+    for (int r = 0; r < claimed; ++r) {
+      (void)hipSetDevice(E[r]->device);
+      (void)hipEventRecord(E[r]->slots[k].done, E[r]->slots[k].stream);
+      E[r]->slots[k].used = true;
+    }
+    (void)hipSetDevice(h->device);
+    s0.status = code;
+    return code;
+  };
   for (int r = 0; r < R; ++r) {
     vss_handle* e = E[r];
     Slot& s = e->slots[k];
-    const int f0 = r * m, nr = std::max(0, std::min(n - f0, m));
+    int f0, nr, per;
+    shard_plan(n, R, r, &f0, &nr, &per);
     HIP_TRY(e, hipSetDevice(e->device));
-    if ((rc = claim_slot(e, s, s.stream))) return fail(h, rc, e->err);
+    if ((rc = claim_slot(e, s, s.stream))) return abort_batch(fail(h, rc, e->err));
+    ++claimed;
     if (nr > 0) {
       if (plans[r]) {
         FetchRowsParams fp{};
@@ -1140,11 +1355,14 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
         fp.row_bytes = fw * fc;
         fp.vec16 = (rs % 16 == 0 && fbytes % 16 == 0 && (fw * fc) % 16 == 0) ? 1 : 0;
         launch_fetch_rows(fp, (int)plans[r]->rows.size(), nr, s.stream);
-        HIP_TRY(e, hipGetLastError());
+        const hipError_t e_ = hipGetLastError();
+        if (e_ != hipSuccess) return abort_batch(fail(h, VSS_E_HIP, std::string("k_fetch_rows: ") + hipGetErrorString(e_)));
       } else {
-        HIP_TRY(e, hipMemcpyAsync(s.d_frames, s.h_frames, (size_t)nr * fbytes, hipMemcpyHostToDevice, s.stream));
+        const hipError_t e_ = hipMemcpyAsync(s.d_frames, s.h_frames, (size_t)nr * fbytes, hipMemcpyHostToDevice, s.stream);
+        if (e_ != hipSuccess) return abort_batch(fail(h, VSS_E_HIP, std::string("H2D: ") + hipGetErrorString(e_)));
       }
-      if ((rc = forward(e, k, s.d_frames, nr, fh, fw, fc, rs, fbytes, s.d_masks, s.stream))) return fail(h, rc, e->err);
+      if ((rc = forward(e, k, s.d_frames, nr, fh, fw, fc, rs, fbytes, s.d_masks, s.stream)))
+        return abort_batch(fail(h, rc, e->err));
     }
   }
   clk.mark(4);
@@ -1152,16 +1370,14 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   if (h->rccl) {
     // one all-gather of f32 masks per GPU, m frames each (padding rows of the
     // last shards are gathered and dropped): [rank][m][P] = frame order
-    NCCL_TRY(h, ncclGroupStart());
-    for (int r = 0; r < R; ++r) {
+    ncclResult_t nr_ = ncclGroupStart();
+    for (int r = 0; r < R && nr_ == ncclSuccess; ++r) {
       Slot& s = E[r]->slots[k];
-      const ncclResult_t nr_ = ncclAllGather(s.d_masks, s.d_gather, (size_t)m * P, ncclFloat32, s.comm, s.stream);
-      if (nr_ != ncclSuccess) {
-        (void)ncclGroupEnd();
-        return fail(h, VSS_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr_));
-      }
+      nr_ = ncclAllGather(s.d_masks, s.d_gather, (size_t)m * P, ncclFloat32, s.comm, s.stream);
     }
-    NCCL_TRY(h, ncclGroupEnd());
+    const ncclResult_t ne = ncclGroupEnd();
+    if (nr_ == ncclSuccess) nr_ = ne;
+    if (nr_ != ncclSuccess) return abort_batch(fail(h, VSS_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr_)));
     res = s0.d_gather;
   }
   HIP_TRY(h, hipSetDevice(h->device));
@@ -1170,49 +1386,48 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   if (out_mode == VSS_OUT_FRAME) bytes = (size_t)n * fh * fw * 4;
   // masks_out from vss_host_alloc: the D2H lands there, nothing to copy after
   const bool direct = pinned_range(masks_out, bytes);
+  hipError_t e_ = hipSuccess;
   if (out_mode == VSS_OUT_FRAME) {
     enqueue_upmask(h, res, n, fh, fw, s0.d_fmasks, s0.stream);
-    HIP_TRY(h, hipGetLastError());
+    e_ = hipGetLastError();
     src = s0.h_fmasks;
-    HIP_TRY(h, hipMemcpyAsync(direct ? masks_out : s0.h_fmasks, s0.d_fmasks, bytes, hipMemcpyDeviceToHost,
-                              s0.stream));
+    if (e_ == hipSuccess)
+      e_ = hipMemcpyAsync(direct ? masks_out : s0.h_fmasks, s0.d_fmasks, bytes, hipMemcpyDeviceToHost, s0.stream);
   } else {
-    HIP_TRY(h, hipMemcpyAsync(direct ? masks_out : s0.h_masks, res, bytes, hipMemcpyDeviceToHost, s0.stream));
+    e_ = hipMemcpyAsync(direct ? masks_out : s0.h_masks, res, bytes, hipMemcpyDeviceToHost, s0.stream);
   }
+  if (e_ == hipSuccess) e_ = hipEventRecord(s0.host_done, s0.stream);
+  if (e_ != hipSuccess) return abort_batch(fail(h, VSS_E_HIP, std::string("D2H: ") + hipGetErrorString(e_)));
   clk.mark(5);
-  if (!sync && direct && !cb) {
-    // nothing to run on the host when the batch completes: the slot's done
-    // event (recorded below, after the D2H) is the completion.  A host
-    // function costs the submitting thread ~7 us alone and ~140 us while
-    // other threads block in vss_wait (the N-API addon's waiters; measured
-    // with VSS_TIME_SUBMIT), so it is only enqueued for a copy or a callback.
-    s0.status = VSS_OK;
-  } else if (!sync) {
-    // completions in submission order: after the previous batch's
-    Slot& prev = h->slots[h->ticket_slot[(t + vss_handle::kTicketRing - 1) % vss_handle::kTicketRing]];
-    if (t > 0 && prev.used && &prev != &s0) HIP_TRY(h, hipStreamWaitEvent(s0.stream, prev.done, 0));
-    HostDone* c = new HostDone{direct ? nullptr : masks_out, src, bytes, cb, user, &s0};
-    s0.status = 1;  // pending until the host function runs
-    const hipError_t e = hipLaunchHostFunc(s0.stream, host_done, c);
-    if (e != hipSuccess) {
-      delete c;
-      return fail(h, VSS_E_HIP, std::string("hipLaunchHostFunc: ") + hipGetErrorString(e));
-    }
-  }
-  clk.mark(6);
   for (vss_handle* e : E) {
     HIP_TRY(e, hipSetDevice(e->device));
-    if ((rc = release_slot(e, e->slots[k], e->slots[k].stream))) return fail(h, rc, e->err);
+    if ((rc = release_slot(e, e->slots[k], e->slots[k].stream))) return abort_batch(fail(h, rc, e->err));
   }
-  note_ticket(h, k);
+  HIP_TRY(h, hipSetDevice(h->device));
+  const vss_ticket t = h->next_ticket++;
+  s0.ticket = t;
+  s0.status = VSS_OK;
+  clk.mark(6);
+  if (sync) {
+    // the slot's pinned buffers stay ours until the copy below: host_busy
+    s0.host_busy = true;
+    std::vector<std::pair<int, hipEvent_t>> evs{{h->device, s0.host_done}};
+    rc = wait_events_unlocked(h, lk, evs);
+    if (!rc && !direct) std::memcpy(masks_out, src, bytes);
+    s0.status = rc;
+    s0.host_busy = false;
+    lk.unlock();
+    h->slot_cv.notify_all();
+    return rc;
+  }
+  if (!direct || cb) {
+    s0.host_busy = true;
+    s0.status = 1;  // pending until the completion thread has run
+    push_completion(h, {t, k, direct ? nullptr : masks_out, src, bytes, cb, user});
+  }
   clk.mark(7);
   clk.calls += clk.on ? 1 : 0;
   if (ticket) *ticket = t;
-  if (sync) {
-    HIP_TRY(h, hipSetDevice(h->device));
-    for (vss_handle* e : E) HIP_TRY(e, hipEventSynchronize(e->slots[k].done));
-    if (!direct) std::memcpy(masks_out, src, bytes);
-  }
   return VSS_OK;
 }
 
@@ -1333,7 +1548,6 @@ int create_engine(const vss_config* cfg, int device, int max_batch, int user_max
   if (!rc) rc = upload(h);
   if (rc) return rc;
   HIP_TRY(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-  HIP_TRY(h, hipStreamCreateWithFlags(&h->capture_stream, hipStreamNonBlocking));
   h->frame_cap = (size_t)max_batch * cfg->max_frame_h * cfg->max_frame_w * 4;
   h->slots.resize(depth);
   for (Slot& s : h->slots)
@@ -1359,8 +1573,8 @@ int create_engine(const vss_config* cfg, int device, int max_batch, int user_max
 void destroy_engine(vss_handle* h) {
   if (!h) return;
   if (g_submit_clock.on && g_submit_clock.calls > 0) {
-    static const char* names[SubmitClock::kPhases] = {"lock", "slot", "plan", "copy", "h2d+fwd", "d2h", "hostfn",
-                                                      "release"};
+    static const char* names[SubmitClock::kPhases] = {"lock", "slot", "plan", "copy", "h2d+fwd", "d2h", "release",
+                                                      "queue"};
     std::fprintf(stderr, "vss submit phases (us/call over %ld calls):", g_submit_clock.calls);
     for (int k = 0; k < SubmitClock::kPhases; ++k)
       std::fprintf(stderr, " %s %.1f", names[k], g_submit_clock.ns[k] / 1e3 / g_submit_clock.calls);
@@ -1368,13 +1582,15 @@ void destroy_engine(vss_handle* h) {
     g_submit_clock = SubmitClock();
     g_submit_clock.on = true;
   }
+  stop_completions(h);  // every queued batch completes (and its callback fires) first
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
   for (Slot& s : h->slots) {
-    for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : s.graphs) destroy_graph(kv.second);
     if (s.comm) (void)ncclCommDestroy(s.comm);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.done) (void)hipEventDestroy(s.done);
+    if (s.host_done) (void)hipEventDestroy(s.host_done);
   }
   for (auto e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1384,20 +1600,10 @@ void destroy_engine(vss_handle* h) {
   for (void* p : h->dev_allocs) (void)hipFree(p);
   for (void* p : h->host_allocs) (void)hipHostFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
-  if (h->capture_stream) (void)hipStreamDestroy(h->capture_stream);
   delete h->pool;
   delete h;
 }
 
-int wait_slot(vss_handle* h, int k) {
-  for (vss_handle* e : engines(h)) {
-    Slot& s = e->slots[k];
-    if (!s.used) continue;
-    HIP_TRY(e, hipSetDevice(e->device));
-    HIP_TRY(e, hipEventSynchronize(s.done));
-  }
-  return VSS_OK;
-}
 
 }  // namespace
 
@@ -1541,47 +1747,54 @@ int vss_submit_list(vss_handle* h, const uint8_t* const* frames, int n, int heig
                      nullptr, nullptr, ticket);
 }
 
+// The slot holding host ticket t, or -1 when no slot does any more: a slot
+// takes a new host batch only once it is free (its previous batch done and
+// completed), so a ticket no slot holds is done.  mu held.
+static int ticket_slot(const vss_handle* h, vss_ticket t) {
+  for (size_t k = 0; k < h->slots.size(); ++k)
+    if (h->slots[k].ticket == t) return (int)k;
+  return -1;
+}
+
 int vss_wait(vss_handle* h, vss_ticket ticket) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
-  int k;
-  {
-    std::lock_guard<std::mutex> lk(h->mu);
-    if (ticket >= h->next_ticket) return fail(h, VSS_E_INVALID_ARG, "unknown ticket");
-    if (h->next_ticket - ticket > (vss_ticket)vss_handle::kTicketRing) return VSS_OK;  // long done: its
-    // slot was taken again by a later batch, which is only picked once its slot is free
-    k = h->ticket_slot[ticket % vss_handle::kTicketRing];
-    if (h->slots[k].ticket != ticket) return VSS_OK;  // reused likewise
-  }
-  int rc = wait_slot(h, k);
-  if (rc) return rc;
-  const int st = h->slots[k].status;
-  return st > 0 ? VSS_OK : st;
+  std::unique_lock<std::mutex> lk(h->mu);
+  if (ticket >= h->next_ticket) return fail(h, VSS_E_INVALID_ARG, "unknown ticket");
+  const int k = ticket_slot(h, ticket);
+  if (k < 0) return VSS_OK;
+  Slot& s = h->slots[k];
+  // a batch with host work (copy / callback): the completion thread finishes it
+  h->slot_cv.wait(lk, [&] { return s.ticket != ticket || !s.host_busy; });
+  if (s.ticket != ticket) return VSS_OK;
+  // otherwise its D2H into the caller's pinned block is the completion
+  const std::vector<std::pair<int, hipEvent_t>> evs{{h->device, s.host_done}};
+  if (int rc = wait_events_unlocked(h, lk, evs)) return rc;
+  if (s.ticket != ticket) return VSS_OK;
+  return s.status > 0 ? VSS_OK : s.status;
 }
 
 int vss_query(vss_handle* h, vss_ticket ticket) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   std::lock_guard<std::mutex> lk(h->mu);
   if (ticket >= h->next_ticket) return fail(h, VSS_E_INVALID_ARG, "unknown ticket");
-  if (h->next_ticket - ticket > (vss_ticket)vss_handle::kTicketRing) return 1;
-  const int k = h->ticket_slot[ticket % vss_handle::kTicketRing];
-  if (h->slots[k].ticket != ticket) return 1;
-  for (vss_handle* e : engines(h)) {
-    Slot& s = e->slots[k];
-    HIP_TRY(e, hipSetDevice(e->device));
-    const hipError_t q = hipEventQuery(s.done);
-    if (q == hipErrorNotReady) return 0;
-    if (q != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
-  }
-  return 1;
+  const int k = ticket_slot(h, ticket);
+  if (k < 0) return 1;
+  Slot& s = h->slots[k];
+  if (s.host_busy) return 0;
+  HIP_TRY(h, hipSetDevice(h->device));
+  const hipError_t q = hipEventQuery(s.host_done);
+  if (q == hipErrorNotReady) return 0;
+  if (q != hipSuccess) return fail(h, VSS_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+  return s.status < 0 ? s.status : 1;
 }
 
 int vss_staging_acquire(vss_handle* h, int* slot, uint8_t** frames, size_t* capacity) {
   if (!h || !slot || !frames) return fail(h, VSS_E_INVALID_ARG, "null handle/slot/frames");
-  std::lock_guard<std::mutex> lk(h->mu);
+  std::unique_lock<std::mutex> lk(h->mu);
   if (!h->peers.empty())
     return fail(h, VSS_E_UNSUPPORTED, "zero-copy staging is per GPU: a multi-GPU handle stages its shards itself");
   int k = 0;
-  int rc = pick_slot(h, true, &k);  // a free slot (waits for one)
+  int rc = pick_slot(h, lk, true, &k);  // a free slot (waits for one, mu released meanwhile)
   if (rc) return rc;
   HIP_TRY(h, hipSetDevice(h->device));
   if ((rc = ensure_staging(h, h->slots[k]))) return rc;
@@ -1639,15 +1852,14 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
   HIP_TRY(h, hipSetDevice(h->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
   // round-robin slots, ordered on the device (no host wait): consecutive
-  // calls on different streams run concurrently
-  const int k = (int)(h->next_ticket % h->slots.size());
+  // calls on different streams run concurrently.  Device calls take no
+  // ticket: a host batch in the same slot keeps its ticket and completion.
+  const int k = (int)(h->device_calls++ % h->slots.size());
   Slot& sl = h->slots[k];
   if ((rc = claim_slot(h, sl, s))) return rc;
-  if ((rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, d_masks, s))) return rc;
-  if ((rc = release_slot(h, sl, s))) return rc;
-  sl.status = VSS_OK;
-  note_ticket(h, k);
-  return VSS_OK;
+  rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, d_masks, s);
+  const int rr = release_slot(h, sl, s);  // also after a failed enqueue: the next user orders after it
+  return rc ? rc : rr;
 }
 
 int vss_comm_unique_id(vss_handle* h, void* ids, size_t cap, size_t* len) {
@@ -1696,11 +1908,15 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(h, hipSetDevice(h->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
-  // round-robin, so every rank uses the same slot's communicator for the same call
-  const int k = (int)(h->next_ticket % h->slots.size());
+  // round-robin over the device calls, so every rank uses the same slot's
+  // communicator for the same call
+  const int k = (int)(h->device_calls++ % h->slots.size());
   Slot& sl = h->slots[k];
   if ((rc = claim_slot(h, sl, s))) return rc;
-  if ((rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, sl.d_masks, s))) return rc;
+  if ((rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, sl.d_masks, s))) {
+    (void)release_slot(h, sl, s);
+    return rc;
+  }
   const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
   // Default: each slot's own communicator on the slot's stream, so the
   // gathers of the batches in flight overlap (at one rank 170k frames/s vs
@@ -1712,23 +1928,24 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
   // slot 0's communicator and one stream instead (a total order, for systems
   // where concurrent communicators misbehave).
   static const bool serial = getenv("VSS_GATHER_SERIAL") && getenv("VSS_GATHER_SERIAL")[0] == '1';
+  ncclResult_t nr = ncclSuccess;
+  hipError_t he = hipSuccess;
   if (!serial) {
-    NCCL_TRY(h, ncclAllGather(sl.d_masks, d_gathered, (size_t)n * P, ncclFloat32, sl.comm, s));
-    if ((rc = release_slot(h, sl, s))) return rc;
-    sl.status = VSS_OK;
-    note_ticket(h, k);
-    return VSS_OK;
+    nr = ncclAllGather(sl.d_masks, d_gathered, (size_t)n * P, ncclFloat32, sl.comm, s);
+  } else {
+    hipEvent_t fwd = h->gather_ev[2 * k], gat = h->gather_ev[2 * k + 1];
+    he = hipEventRecord(fwd, s);
+    if (he == hipSuccess) he = hipStreamWaitEvent(h->gather_stream, fwd, 0);
+    if (he == hipSuccess) nr = ncclAllGather(sl.d_masks, d_gathered, (size_t)n * P, ncclFloat32, h->slots[0].comm,
+                                             h->gather_stream);
+    if (he == hipSuccess && nr == ncclSuccess) he = hipEventRecord(gat, h->gather_stream);
+    // the caller's stream (and the slot's release) after the gather
+    if (he == hipSuccess && nr == ncclSuccess) he = hipStreamWaitEvent(s, gat, 0);
   }
-  hipEvent_t fwd = h->gather_ev[2 * k], gat = h->gather_ev[2 * k + 1];
-  HIP_TRY(h, hipEventRecord(fwd, s));
-  HIP_TRY(h, hipStreamWaitEvent(h->gather_stream, fwd, 0));
-  NCCL_TRY(h, ncclAllGather(sl.d_masks, d_gathered, (size_t)n * P, ncclFloat32, h->slots[0].comm, h->gather_stream));
-  HIP_TRY(h, hipEventRecord(gat, h->gather_stream));
-  HIP_TRY(h, hipStreamWaitEvent(s, gat, 0));  // the caller's stream (and the slot's release) after the gather
-  if ((rc = release_slot(h, sl, s))) return rc;
-  sl.status = VSS_OK;
-  note_ticket(h, k);
-  return VSS_OK;
+  const int rr = release_slot(h, sl, s);
+  if (nr != ncclSuccess) return fail(h, VSS_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+  if (he != hipSuccess) return fail(h, VSS_E_HIP, std::string("gather ordering: ") + hipGetErrorString(he));
+  return rr;
 }
 
 int vss_mask_to_frame_device(vss_handle* h, const float* d_masks, int n, int frame_h, int frame_w, float* d_out,
@@ -1775,6 +1992,13 @@ int vss_synchronize(vss_handle* h) {
     }
   }
   HIP_TRY(h, hipSetDevice(h->device));
+  // and every host batch's completion (copy, callback) has run
+  std::unique_lock<std::mutex> lk(h->mu);
+  h->slot_cv.wait(lk, [&] {
+    for (const Slot& s : h->slots)
+      if (s.host_busy) return false;
+    return true;
+  });
   return VSS_OK;
 }
 
@@ -1782,13 +2006,15 @@ int vss_set_option(vss_handle* h, int option, int value) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (option == 3 || option == 4 || option == 5)
     return fail(h, VSS_E_UNSUPPORTED, "option removed (round-1 experiment measured slower; DESIGN.md)");
+  if (option == VSS_OPT_GRAPH_BUILDS || option == VSS_OPT_GRAPH_PATCHES || option == VSS_OPT_COMM_RANKS)
+    return fail(h, VSS_E_INVALID_ARG, "read-only option (vss_get_option)");
   if (option != VSS_OPT_KEEP_STEM && option != VSS_OPT_USE_GRAPH && option != VSS_OPT_PROFILE &&
       option != VSS_OPT_ROW_FETCH)
     return fail(h, VSS_E_INVALID_ARG, "unknown option");
   std::lock_guard<std::mutex> lk(h->mu);
   for (vss_handle* e : engines(h)) {
     if (option == VSS_OPT_KEEP_STEM) {
-      if ((value ? 1 : 0) != e->keep_stem) drop_graphs(e);  // the captured graphs hold the stem pointer
+      if ((value ? 1 : 0) != e->keep_stem) drop_graphs(e);  // the graphs hold the stem pointer
       e->keep_stem = value ? 1 : 0;
     } else if (option == VSS_OPT_USE_GRAPH) {
       e->use_graph = value ? 1 : 0;
@@ -1804,13 +2030,61 @@ int vss_set_option(vss_handle* h, int option, int value) {
 int vss_get_option(vss_handle* h, int option, int* value) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (!value) return fail(h, VSS_E_INVALID_ARG, "null value");
+  std::lock_guard<std::mutex> lk(h->mu);
   switch (option) {
     case VSS_OPT_USE_GRAPH: *value = h->use_graph; return VSS_OK;
     case VSS_OPT_PROFILE: *value = h->profile; return VSS_OK;
     case VSS_OPT_KEEP_STEM: *value = h->keep_stem; return VSS_OK;
     case VSS_OPT_ROW_FETCH: *value = h->row_fetch; return VSS_OK;
+    case VSS_OPT_GRAPH_BUILDS:
+    case VSS_OPT_GRAPH_PATCHES: {
+      long v = 0;
+      for (const vss_handle* e : engines(h)) v += option == VSS_OPT_GRAPH_BUILDS ? e->graph_builds : e->graph_patches;
+      *value = (int)std::min<long>(v, 0x7fffffff);
+      return VSS_OK;
+    }
+    case VSS_OPT_COMM_RANKS: {
+      if (h->rccl) {
+        *value = 1 + (int)h->peers.size();
+      } else if (h->clique) {
+        int c = 0;
+        NCCL_TRY(h, ncclCommCount(h->slots[0].comm, &c));
+        *value = c;
+      } else {
+        *value = 1;
+      }
+      return VSS_OK;
+    }
     default: return fail(h, VSS_E_INVALID_ARG, "unknown option");
   }
+}
+
+int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels, size_t row_stride,
+                       size_t frame_stride) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride, h->cfg.max_batch);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (!h->use_graph || h->profile) return VSS_OK;  // eager launches: nothing to build
+  const GraphKey key{n, height, width, channels, row_stride, frame_stride};
+  for (size_t k = 0; k < h->slots.size(); ++k) {
+    Slot& s = h->slots[k];
+    if (s.graphs.count(key)) continue;
+    std::vector<Launch> ls;
+    // null buffers: the first call patches in its own (the slot is idle then)
+    forward_launches(h, s, nullptr, n, height, width, channels, row_stride, frame_stride, nullptr, &ls);
+    GraphEntry g;
+    if ((rc = build_graph(h, ls, &g))) return rc;
+    s.graphs.emplace(key, std::move(g));
+  }
+  return VSS_OK;
+}
+
+int vss_shard_plan(int n, int nranks, int rank, int* first, int* count, int* per_rank) {
+  if (n < 0 || nranks < 1 || rank < 0 || rank >= nranks || !first || !count || !per_rank) return VSS_E_INVALID_ARG;
+  shard_plan(n, nranks, rank, first, count, per_rank);
+  return VSS_OK;
 }
 
 int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww) {
@@ -2026,9 +2300,12 @@ int post_enqueue(vss_post_state* st, const uint8_t* d_frames, int n, int fh, int
 }
 
 // The seam for the synchronous post / composite host calls on engine 0:
-// stage the frames into the next slot, H2D and forward on the handle's stream
-// (after that slot's previous batch); returns the slot.
-int seam_on_stream(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, int* slot) {
+// stage the frames into a free slot, H2D and forward on the handle's stream
+// (after that slot's previous work); returns the slot, claimed and marked
+// host_busy — the caller enqueues its own work and ends with finish_seam.
+// mu held through lk (released only while waiting for a slot).
+int seam_on_stream(vss_handle* h, std::unique_lock<std::mutex>& lk, const uint8_t* frames, int n, int fh, int fw,
+                   int fc, size_t rs, int* slot) {
   if (!frames) return fail(h, VSS_E_INVALID_ARG, "null frames");
   int rc = check_frames(h, n, fh, fw, fc, rs, rs * (size_t)fh, h->cfg.max_batch);
   if (rc) return rc;
@@ -2037,17 +2314,40 @@ int seam_on_stream(vss_handle* h, const uint8_t* frames, int n, int fh, int fw, 
     return fail(h, VSS_E_INVALID_ARG, "frames exceed the handle's staging capacity (max_frame_h/w)");
   HIP_TRY(h, hipSetDevice(h->device));
   int k = 0;
-  if ((rc = pick_slot(h, true, &k))) return rc;  // free: its staging is rewritten below
+  if ((rc = pick_slot(h, lk, true, &k))) return rc;  // free: its staging is rewritten below
   Slot& s = h->slots[k];
   if ((rc = ensure_staging(h, s))) return rc;
   if (frames != s.h_frames) h->pool->run({{s.h_frames, frames, (size_t)n * fbytes}});
   if ((rc = claim_slot(h, s, h->stream))) return rc;
-  HIP_TRY(h, hipMemcpyAsync(s.d_frames, s.h_frames, (size_t)n * fbytes, hipMemcpyHostToDevice, h->stream));
-  if ((rc = forward(h, k, s.d_frames, n, fh, fw, fc, rs, fbytes, s.d_masks, h->stream))) return rc;
-  s.status = VSS_OK;
-  note_ticket(h, k);
+  const hipError_t e = hipMemcpyAsync(s.d_frames, s.h_frames, (size_t)n * fbytes, hipMemcpyHostToDevice, h->stream);
+  if (e != hipSuccess) rc = fail(h, VSS_E_HIP, std::string("H2D: ") + hipGetErrorString(e));
+  if (!rc) rc = forward(h, k, s.d_frames, n, fh, fw, fc, rs, fbytes, s.d_masks, h->stream);
+  if (rc) {
+    (void)release_slot(h, s, h->stream);
+    return rc;
+  }
+  s.host_busy = true;
   *slot = k;
   return VSS_OK;
+}
+
+// End of a synchronous post / composite call on slot k (rc: its enqueue
+// status): record the slot's done event, wait for the handle's stream with mu
+// released, give the slot back.
+int finish_seam(vss_handle* h, std::unique_lock<std::mutex>& lk, int k, int rc) {
+  Slot& s = h->slots[k];
+  const int rr = release_slot(h, s, h->stream);
+  if (!rc) rc = rr;
+  if (!rc) {
+    lk.unlock();
+    const hipError_t e = hipStreamSynchronize(h->stream);
+    lk.lock();
+    if (e != hipSuccess) rc = fail(h, VSS_E_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+  }
+  s.host_busy = false;
+  lk.unlock();
+  h->slot_cv.notify_all();
+  return rc;
 }
 
 }  // namespace
@@ -2170,9 +2470,9 @@ int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, i
   if (!h || !st || st->h != h) return fail(h, VSS_E_INVALID_ARG, "handle / post state mismatch");
   if (!alpha_out && !alpha_u8_out) return fail(h, VSS_E_INVALID_ARG, "no output requested");
   std::lock_guard<std::mutex> pl(h->post_mu);
-  std::lock_guard<std::mutex> lk(h->mu);
+  std::unique_lock<std::mutex> lk(h->mu);
   int k = 0;
-  int rc = seam_on_stream(h, frames, n, height, width, channels, row_stride, &k);
+  int rc = seam_on_stream(h, lk, frames, n, height, width, channels, row_stride, &k);
   if (rc) return rc;
   Slot& s = h->slots[k];
   const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
@@ -2180,13 +2480,12 @@ int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, i
   uint8_t* d_u8 = alpha_u8_out ? h->d_post_u8 : nullptr;
   rc = post_enqueue(st, s.d_frames, n, height, width, channels, row_stride, row_stride * (size_t)height, s.d_masks,
                     d_alpha, d_u8, h->stream);
-  if (rc) return rc;
-  if (alpha_out) HIP_TRY(h, hipMemcpyAsync(alpha_out, d_alpha, (size_t)n * P * 4, hipMemcpyDeviceToHost, h->stream));
-  if (alpha_u8_out)
-    HIP_TRY(h, hipMemcpyAsync(alpha_u8_out, d_u8, (size_t)n * P, hipMemcpyDeviceToHost, h->stream));
-  if ((rc = release_slot(h, s, h->stream))) return rc;
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
-  return VSS_OK;
+  hipError_t e = hipSuccess;
+  if (!rc && alpha_out) e = hipMemcpyAsync(alpha_out, d_alpha, (size_t)n * P * 4, hipMemcpyDeviceToHost, h->stream);
+  if (!rc && e == hipSuccess && alpha_u8_out)
+    e = hipMemcpyAsync(alpha_u8_out, d_u8, (size_t)n * P, hipMemcpyDeviceToHost, h->stream);
+  if (!rc && e != hipSuccess) rc = fail(h, VSS_E_HIP, std::string("D2H: ") + hipGetErrorString(e));
+  return finish_seam(h, lk, k, rc);
 }
 
 }  // extern "C"
@@ -2252,7 +2551,7 @@ int vss_segment_composite(vss_handle* h, vss_post_state* st, const uint8_t* fram
   if (!h || !st || st->h != h) return fail(h, VSS_E_INVALID_ARG, "handle / post state mismatch");
   if (!out_rgba) return fail(h, VSS_E_INVALID_ARG, "null output");
   std::lock_guard<std::mutex> pl(h->post_mu);
-  std::lock_guard<std::mutex> lk(h->mu);
+  std::unique_lock<std::mutex> lk(h->mu);
   HIP_TRY(h, hipSetDevice(h->device));
   const size_t cap = (size_t)h->cfg.max_batch * h->cfg.max_frame_h * h->cfg.max_frame_w * 4;
   if (!h->d_comp) {
@@ -2263,19 +2562,19 @@ int vss_segment_composite(vss_handle* h, vss_post_state* st, const uint8_t* fram
   if ((size_t)n * ofs > cap)
     return fail(h, VSS_E_INVALID_ARG, "RGBA output exceeds the handle's capacity (max_batch, max_frame_h/w)");
   int k = 0;
-  int rc = seam_on_stream(h, frames, n, height, width, channels, row_stride, &k);
+  int rc = seam_on_stream(h, lk, frames, n, height, width, channels, row_stride, &k);
   if (rc) return rc;
   Slot& s = h->slots[k];
   rc = post_enqueue(st, s.d_frames, n, height, width, channels, row_stride, fs, s.d_masks, nullptr, h->d_post_u8,
                     h->stream);
-  if (rc) return rc;
-  rc = composite_enqueue(h, s.d_frames, n, height, width, channels, row_stride, fs, h->d_post_u8, h->d_comp, ors,
-                         ofs, h->stream);
-  if (rc) return rc;
-  HIP_TRY(h, hipMemcpyAsync(out_rgba, h->d_comp, (size_t)n * ofs, hipMemcpyDeviceToHost, h->stream));
-  if ((rc = release_slot(h, s, h->stream))) return rc;
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
-  return VSS_OK;
+  if (!rc)
+    rc = composite_enqueue(h, s.d_frames, n, height, width, channels, row_stride, fs, h->d_post_u8, h->d_comp, ors,
+                           ofs, h->stream);
+  if (!rc) {
+    const hipError_t e = hipMemcpyAsync(out_rgba, h->d_comp, (size_t)n * ofs, hipMemcpyDeviceToHost, h->stream);
+    if (e != hipSuccess) rc = fail(h, VSS_E_HIP, std::string("D2H: ") + hipGetErrorString(e));
+  }
+  return finish_seam(h, lk, k, rc);
 }
 
 }  // extern "C"

@@ -79,6 +79,12 @@ struct Handle {
   vss_handle* h = nullptr;
   int mask_h = 0, mask_w = 0;
   std::vector<Post*> posts;  // destroyed before the handle, whatever order the GC finalizes in
+  // Queued batches whose libuv work still holds h (JS thread only): destroy()
+  // or the GC finalizer while some are pending defers vss_destroy to the last
+  // one's completion, so no worker ever waits on a destroyed handle.
+  int pending = 0;
+  bool closing = false;    // destroy() / finalizer ran: no new work; release when pending == 0
+  bool finalized = false;  // the JS external is gone: the last completion deletes this
 };
 
 struct Post {
@@ -87,6 +93,8 @@ struct Post {
 };
 
 void release_handle(Handle* hd) {
+  hd->closing = true;
+  if (hd->pending > 0) return;  // work_done() of the last queued batch finishes the release
   for (Post* p : hd->posts) {
     if (p->st) vss_post_destroy(p->st);
     p->st = nullptr;
@@ -100,7 +108,16 @@ void release_handle(Handle* hd) {
 void finalize_handle(napi_env, void* data, void*) {
   Handle* hd = static_cast<Handle*>(data);
   release_handle(hd);
-  delete hd;
+  if (hd->pending > 0) hd->finalized = true;
+  else delete hd;
+}
+
+// A queued batch's async work finished (its Complete callback, JS thread).
+void work_done(Handle* hd) {
+  if (--hd->pending > 0 || !hd->closing) return;
+  const bool del = hd->finalized;
+  release_handle(hd);
+  if (del) delete hd;
 }
 
 void release_post(Post* p) {
@@ -123,7 +140,7 @@ Handle* get_handle(napi_env env, napi_value v) {
     return nullptr;
   }
   Handle* hd = static_cast<Handle*>(p);
-  if (!hd->h) {
+  if (!hd->h || hd->closing) {
     napi_throw_error(env, nullptr, "vss handle already destroyed");
     return nullptr;
   }
@@ -432,6 +449,7 @@ struct QueuedWork {
   napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
   napi_ref out_ref = nullptr;
+  Handle* hd = nullptr;  // pending counted until QueuedComplete
   vss_handle* h = nullptr;
   vss_ticket ticket = 0;
   size_t out_count = 0;
@@ -466,7 +484,9 @@ void QueuedComplete(napi_env env, napi_status, void* data) {
   }
   napi_delete_reference(env, w->out_ref);
   napi_delete_async_work(env, w->work);
+  Handle* hd = w->hd;
   delete w;
+  work_done(hd);
 }
 
 // The masks' ArrayBuffer: a pinned block (vss_host_alloc), so the batch's D2H
@@ -668,6 +688,8 @@ napi_value Segment(napi_env env, napi_callback_info info) {
   napi_create_string_utf8(env, "vss_wait", NAPI_AUTO_LENGTH, &name);
   NAPI_OK(env, napi_create_async_work(env, nullptr, name, QueuedExecute, QueuedComplete, w, &w->work));
   NAPI_OK(env, napi_queue_async_work(env, w->work));
+  w->hd = hd;
+  ++hd->pending;
   return promise;
 }
 
@@ -756,6 +778,8 @@ napi_value SegmentStaged(napi_env env, napi_callback_info info) {
   napi_create_string_utf8(env, "vss_wait", NAPI_AUTO_LENGTH, &name);
   NAPI_OK(env, napi_create_async_work(env, nullptr, name, QueuedExecute, QueuedComplete, w, &w->work));
   NAPI_OK(env, napi_queue_async_work(env, w->work));
+  w->hd = hd;
+  ++hd->pending;
   return promise;
 }
 
@@ -764,6 +788,7 @@ struct SegmentWork {
   napi_deferred deferred = nullptr;
   napi_ref frames_ref = nullptr, out_ref = nullptr;
   napi_ref u8_ref = nullptr;             // segmentPost: the alpha bytes
+  Handle* hd = nullptr;                  // pending counted until SegmentComplete
   vss_handle* h = nullptr;
   vss_post_state* post = nullptr;        // segmentPost / segmentComposite
   bool composite = false;                // segmentComposite: out_u8 holds the RGBA canvases
@@ -823,7 +848,9 @@ void SegmentComplete(napi_env env, napi_status, void* data) {
   napi_delete_reference(env, w->out_ref);
   if (w->u8_ref) napi_delete_reference(env, w->u8_ref);
   napi_delete_async_work(env, w->work);
+  Handle* hd = w->hd;
   delete w;
+  work_done(hd);
 }
 
 // segmentPost(handle, post, frames, ...) and segmentComposite(handle, post, frames, ...)
@@ -904,6 +931,8 @@ napi_value SegmentImpl(napi_env env, napi_callback_info info, bool with_post, bo
   napi_create_string_utf8(env, ps ? "vss_segment_post" : "vss_segment", NAPI_AUTO_LENGTH, &name);
   NAPI_OK(env, napi_create_async_work(env, nullptr, name, SegmentExecute, SegmentComplete, w, &w->work));
   NAPI_OK(env, napi_queue_async_work(env, w->work));
+  w->hd = hd;
+  ++hd->pending;
   return promise;
 }
 
