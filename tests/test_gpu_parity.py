@@ -202,13 +202,18 @@ def test_async_queue_order_and_busy(pkg, synthetic, torch_cuda):
                         done.set()
             return cb
 
-        _hold_slots(pkg, torch, s, 1, d, scratch)  # one slot held by a sleeping stream
+        # device calls take the slots round-robin: two held by a sleeping stream,
+        # the third is free and the async call finds it
+        _hold_slots(pkg, torch, s, 2, d, scratch)
         s.segment_frames_async(batches[0], cb_for(0))
-        s.segment_frames_async(batches[1], cb_for(1))
-        with pytest.raises(pkg.VssError) as e:  # three in flight: the queue is full
-            s.segment_frames_async(batches[2], cb_for(2))
+        s.synchronize()
+        # every slot in flight: the queue is full
+        _hold_slots(pkg, torch, s, 3, d, scratch)
+        with pytest.raises(pkg.VssError) as e:
+            s.segment_frames_async(batches[1], cb_for(1))
         assert e.value.code == pkg.VSS_E_BUSY
         s.synchronize()
+        s.segment_frames_async(batches[1], cb_for(1))
         s.segment_frames_async(batches[2], cb_for(2))
         assert done.wait(30)
         s.synchronize()

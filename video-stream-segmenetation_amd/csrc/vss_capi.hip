@@ -1166,9 +1166,14 @@ void completion_loop(vss_handle* h) {
       h->done_q.pop_front();
     }
     Slot& s = h->slots[c.slot];
-    const hipError_t e = hipEventSynchronize(s.host_done);  // not re-recorded while host_busy
+    hipError_t e = hipEventSynchronize(s.host_done);  // not re-recorded while host_busy
     const int st = e == hipSuccess ? VSS_OK : VSS_E_HIP;
     if (st == VSS_OK && c.out) std::memcpy(c.out, c.src, c.bytes);
+    // the slot counts as free once its done event has fired on every GPU too
+    // (recorded right after host_done): a submit after this completion finds it free
+    for (vss_handle* en : engines(h))
+      if (e == hipSuccess && hipSetDevice(en->device) == hipSuccess) e = hipEventSynchronize(en->slots[c.slot].done);
+    (void)hipSetDevice(h->device);
     {
       std::lock_guard<std::mutex> lk(h->mu);
       if (st != VSS_OK) h->err = std::string("batch failed: ") + hipGetErrorString(e);
@@ -1292,11 +1297,17 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   // more (measured: 1080p, 20 % of the rows, 8.7k -> 23-29k frames/s; at
   // 640x480, 50 %, the kernel's reads of pinned memory lost to one DMA of the
   // whole frames, 38-46k -> 31-39k)
-  std::vector<const RowPlan*> plans(R, nullptr);
+  //   Whatever moves the rows across PCIe, only the rows the resize reads are
+  // copied into the staging (the other rows of the staged frames are never
+  // read: the fused stem, k_prep and the post chain's guide all sample the
+  // same rows): at 640x480 that halves the host memcpy of the copy path.
+  std::vector<const RowPlan*> plans(R, nullptr);  // the rows (row_fetch on)
+  std::vector<bool> fetch(R, false);              // move them with k_fetch_rows (else one DMA)
   for (int r = 0; r < R; ++r) {
     HIP_TRY(E[r], hipSetDevice(E[r]->device));
+    if (!h->row_fetch) continue;
     if ((rc = row_plan(E[r], fh, &plans[r]))) return fail(h, rc, E[r]->err);
-    if (!h->row_fetch || plans[r]->rows.size() * 5 > (size_t)fh * 2) plans[r] = nullptr;
+    fetch[r] = plans[r]->rows.size() * 5 <= (size_t)fh * 2;
   }
   // stage every GPU's shard (zero-copy when the caller wrote into this slot's buffer)
   std::vector<CopyPool::Job> jobs;
@@ -1345,7 +1356,7 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
     if ((rc = claim_slot(e, s, s.stream))) return abort_batch(fail(h, rc, e->err));
     ++claimed;
     if (nr > 0) {
-      if (plans[r]) {
+      if (fetch[r]) {
         FetchRowsParams fp{};
         fp.src = s.h_frames;
         fp.dst = s.d_frames;
@@ -1412,6 +1423,7 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
     // the slot's pinned buffers stay ours until the copy below: host_busy
     s0.host_busy = true;
     std::vector<std::pair<int, hipEvent_t>> evs{{h->device, s0.host_done}};
+    for (vss_handle* e : E) evs.push_back({e->device, e->slots[k].done});
     rc = wait_events_unlocked(h, lk, evs);
     if (!rc && !direct) std::memcpy(masks_out, src, bytes);
     s0.status = rc;
@@ -1766,8 +1778,10 @@ int vss_wait(vss_handle* h, vss_ticket ticket) {
   // a batch with host work (copy / callback): the completion thread finishes it
   h->slot_cv.wait(lk, [&] { return s.ticket != ticket || !s.host_busy; });
   if (s.ticket != ticket) return VSS_OK;
-  // otherwise its D2H into the caller's pinned block is the completion
-  const std::vector<std::pair<int, hipEvent_t>> evs{{h->device, s.host_done}};
+  // otherwise its D2H into the caller's pinned block is the completion; the
+  // slot's done events (recorded after it) too, so the slot is free on return
+  std::vector<std::pair<int, hipEvent_t>> evs{{h->device, s.host_done}};
+  for (vss_handle* e : engines(h)) evs.push_back({e->device, e->slots[k].done});
   if (int rc = wait_events_unlocked(h, lk, evs)) return rc;
   if (s.ticket != ticket) return VSS_OK;
   return s.status > 0 ? VSS_OK : s.status;
