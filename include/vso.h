@@ -113,8 +113,6 @@ int vso_launch_count(const vso_session* s);
 int vso_launch_name(const vso_session* s, int k, char* buf, int cap);
 /* Convolutions planned on the LDS-tiled MFMA kernel (k_conv_tile). */
 int vso_tile_conv_count(const vso_session* s);
-/* MobileNetV2 inverted residuals (1x1 -> depthwise 3x3 -> 1x1 [+ x]) planned as one k_irb launch each. */
-int vso_fused_block_count(const vso_session* s);
 
 #ifdef __cplusplus
 }

@@ -137,10 +137,8 @@ def test_modnet_topology_288x512(ort, modnet_cases, q4f16, precision):
     with ort.InferenceSession(data, precision=precision) as s:
         got = s.run({"input": x})
         again = s.run({"input": x})
-        print(label, len(s.launches()), "launches,", s.tile_convs(), "tiled convolutions,", s.fused_blocks(),
-              "fused inverted residuals")
+        print(label, len(s.launches()), "launches,", s.tile_convs(), "tiled convolutions")
         assert s.tile_convs() >= 12  # every 3x3 / 5x5 of >= 8 MMAC (f32), every 3x3 / 5x5 (16-bit)
-        assert s.fused_blocks() == 0  # k_irb is opt-in (VSO_IRB=1; test_inverted_residual_fusion)
     for k, w in want.items():
         err, mean = float(np.abs(got[k] - w).max()), float(np.abs(got[k] - w).mean())
         print(f"{label}: vs the f32 oracle max abs err {err:.3e}, mean {mean:.3e}")
@@ -149,33 +147,6 @@ def test_modnet_topology_288x512(ort, modnet_cases, q4f16, precision):
         else:
             assert err <= MODNET_PRECISION_COST[precision][0] and mean <= MODNET_PRECISION_COST[precision][1], label
         assert np.array_equal(got[k], again[k])  # split-K reduction order is fixed
-
-
-@pytest.mark.parametrize("name", ["modnet_like", "modnet"])
-def test_inverted_residual_fusion(ort, name):
-    """The opt-in k_irb (VSO_IRB=1): modnet_like's four inverted residuals
-    (stride 1 and 2, with and without the residual Add) and the MODNet
-    topology's fifteen expanding blocks (288x512, the 320-channel one on the
-    unfused path) as one launch each, against the f64 oracle at the bar of
-    test_synthetic_models."""
-    import os as _os
-    data = M.modnet_like() if name == "modnet_like" else M.modnet()
-    feeds = M.feeds_for("modnet_like") if name == "modnet_like" else \
-        {"input": np.random.default_rng(21).random((1, 3, 288, 512), dtype=np.float32)}
-    want = R.run(R.load(data), feeds)
-    _os.environ["VSO_IRB"] = "1"
-    try:
-        with ort.InferenceSession(data) as s:
-            got = s.run(feeds)
-            again = s.run(feeds)
-            names = s.launches()
-            n = 4 if name == "modnet_like" else 15
-            assert s.fused_blocks() == n and sum("k_irb" in x for x in names) == n, names
-    finally:
-        del _os.environ["VSO_IRB"]
-    _check(got, want, f"{name} (k_irb)")
-    for k in got:
-        assert np.array_equal(got[k], again[k])
 
 
 def test_run_device(ort):

@@ -70,45 +70,6 @@ struct ConvTileParams {
   int* counters;       // ksplit > 1: arrivals per output block [N][M tiles][tiles], zero between runs
 };
 
-// A MobileNetV2 inverted-residual block in one launch (vso_irb.hip):
-// 1x1 expand (+act1) -> depthwise 3x3 stride s pad 1 (+act2) -> 1x1 project [+ x]
-struct IrbParams {
-  const float* x;  // [N][Cin][H][W]
-  float* y;        // [N][Cout][Ho][Wo]
-  const float *w1, *b1;  // [Ch][Cin], [Ch]
-  const float *wd, *bd;  // [Ch][9], [Ch]
-  const float *w2, *b2;  // [Cout][Ch], [Cout]
-  int N, Cin, H, W, Ch, Cout, Ho, Wo;
-  int act1, act2;        // ACT_NONE / ACT_RELU / ACT_CLIP
-  float lo1, hi1, lo2, hi2;
-  int res;               // y += x (stride 1, Cin == Cout)
-  int tiles_x, tiles;    // output tiles per row of tiles / per image
-  int ksplit, cps;       // hidden 16-channel chunks split over workgroups
-  float* part;           // ksplit > 1: partial project tiles (accumulator order)
-  int* counters;         // ksplit > 1: arrivals per output tile, zero between runs
-};
-
-struct IrbShape {
-  int s, th, cbw;        // stride, output tile rows (x 16 columns), output-channel blocks per wave
-  size_t lds;            // dynamic LDS bytes
-  int tiles_x, tiles, ksplit, cps;
-};
-
-// pixels of the staged input tile, padded to 16 and to 16 mod 32 (bank-free B reads)
-__host__ __device__ constexpr int irb_np(int S, int TH) {
-  int n = (((TH - 1) * S + 3) * (15 * S + 3) + 15) / 16 * 16;
-  return n % 32 == 16 ? n : n + 16;
-}
-
-// floats of one 16-hidden-channel chunk's weights in k_irb's LDS: w1 [16][Cin+1],
-// wd [16][9], b1 [16], bd [16], w2 [Cout][17]
-__host__ __device__ constexpr int irb_chunk_floats(int Cin, int Cout) { return 16 * (Cin + 1) + 144 + 32 + Cout * 17; }
-
-bool irb_shape(int N, int Cin, int Ch, int Cout, int Ho, int Wo, int S, IrbShape* sh);
-const char* irb_name(const IrbShape& t);
-void launch_irb(const IrbParams& p, const IrbShape& t, hipStream_t s);
-bool irb_set_lds_limit();
-
 constexpr int kDwPwMaxC = 256;  // channels a fused depthwise -> 1x1 pair may have
 
 enum BinOp : int { BIN_ADD = 0, BIN_SUB = 1, BIN_MUL = 2, BIN_DIV = 3, BIN_PRELU = 4 };

@@ -454,7 +454,6 @@ struct vso_session {
   int device = 0;
   int conv_precision = 0;  // ConvPrec
   int tile_convs = 0;      // convolutions planned on k_conv_tile
-  int irb_blocks = 0;      // inverted residuals planned on k_irb
   hipStream_t stream = nullptr;
   std::string err;
   std::vector<std::string> in_names, out_names;
@@ -875,134 +874,9 @@ struct Planner {
     return true;
   }
 
-  // A MobileNetV2 inverted residual — Conv 1x1 [-> Relu/Clip] -> depthwise
-  // 3x3 pad 1 stride 1/2 [-> Relu/Clip] -> Conv 1x1 [-> Add(block input)],
-  // every intermediate used once, no BatchNormalization left between — as one
-  // k_irb launch (vso_irb.hip), when env VSO_IRB=1 (opt-in: measured slower
-  // than the unfused launches).  1: planned, 0: not this pattern, -1: error.
-  int try_plan_irb(size_t ni) {
-    if (!irb_enabled) return 0;
-    const Node& e = g.nodes[ni];
-    Value* x = val(e.in[0]);
-    auto conv_w = [&](const Node& c) -> Value* {
-      Value* w = c.in.size() > 1 ? val(c.in[1]) : nullptr;
-      return (w && w->is_const && w->c.dims.size() == 4) ? w : nullptr;
-    };
-    auto conv_b = [&](const Node& c, int64_t m) -> const Const* {
-      if (c.in.size() < 3 || c.in[2].empty()) return nullptr;
-      Value* b = val(c.in[2]);
-      return (b && b->is_const && b->c.numel() == m) ? &b->c : nullptr;
-    };
-    auto ints_all = [&](const Node& c, const char* a, int64_t v) {
-      for (int64_t q : c.ais(a)) if (q != v) return false;
-      return true;
-    };
-    auto plain_1x1 = [&](const Node& c) {
-      Value* w = conv_w(c);
-      return c.op == "Conv" && w && w->c.dims[2] == 1 && w->c.dims[3] == 1 && c.ai("group", 1) == 1 &&
-             ints_all(c, "strides", 1) && ints_all(c, "pads", 0) && ints_all(c, "dilations", 1) &&
-             c.as("auto_pad", "NOTSET") == "NOTSET" && (c.in.size() < 3 || c.in[2].empty() || conv_b(c, w->c.dims[0]));
-    };
-    if (!x || x->is_const || x->shape.size() != 4 || !plain_1x1(e)) return 0;
-    // follow the single-consumer chain, skipping one activation after a conv
-    auto next_act = [&](const std::string& out, size_t after, int* act_node, Epilogue* ep) -> int {
-      int c = sole_consumer(out, after);
-      *act_node = -1;
-      if (c >= 0 && (g.nodes[c].op == "Relu" || g.nodes[c].op == "Clip")) {
-        if (!act_of(g.nodes[c], ep, 0)) return -2;
-        *act_node = c;
-        c = sole_consumer(g.nodes[c].out[0], (size_t)c);
-      }
-      return c;
-    };
-    Epilogue a1{}, a2{};
-    int n_a1, n_a2;
-    const int d = next_act(e.out[0], ni, &n_a1, &a1);
-    if (d < 0) return 0;
-    const Node& dw = g.nodes[d];
-    Value* wdv = conv_w(dw);
-    const int64_t Ch = conv_w(e)->c.dims[0], Cin = conv_w(e)->c.dims[1];
-    if (dw.op != "Conv" || !wdv || dw.ai("group", 1) != Ch || wdv->c.dims[0] != Ch || wdv->c.dims[1] != 1 ||
-        wdv->c.dims[2] != 3 || wdv->c.dims[3] != 3 || !ints_all(dw, "pads", 1) || !ints_all(dw, "dilations", 1) ||
-        dw.as("auto_pad", "NOTSET") != "NOTSET" || dw.in[0] != (n_a1 >= 0 ? g.nodes[n_a1].out[0] : e.out[0]))
-      return 0;
-    std::vector<int64_t> st = dw.ais("strides");
-    const int S = st.empty() ? 1 : (int)st[0];
-    if ((st.size() == 2 && st[1] != st[0]) || (S != 1 && S != 2)) return 0;
-    if (dw.in.size() > 2 && !dw.in[2].empty() && !conv_b(dw, Ch)) return 0;
-    const int pw = next_act(dw.out[0], (size_t)d, &n_a2, &a2);
-    if (pw < 0 || !plain_1x1(g.nodes[pw]) || conv_w(g.nodes[pw])->c.dims[1] != Ch) return 0;
-    const Node& pn = g.nodes[pw];
-    if (pn.in[0] != (n_a2 >= 0 ? g.nodes[n_a2].out[0] : dw.out[0])) return 0;
-    for (const Epilogue* a : {&a1, &a2})
-      if (a->act != ACT_NONE && a->act != ACT_RELU && a->act != ACT_CLIP) return 0;
-    const int64_t Cout = conv_w(pn)->c.dims[0];
-    std::string out = pn.out[0];
-    int add_node = -1;
-    const int c3 = sole_consumer(out, (size_t)pw);
-    if (c3 >= 0 && g.nodes[c3].op == "Add" && S == 1 && Cin == Cout) {
-      const Node& ad = g.nodes[c3];
-      const std::string& other = ad.in[0] == out ? ad.in[1] : ad.in[0];
-      if (other == e.in[0]) {
-        add_node = c3;
-        out = ad.out[0];
-      }
-    }
-    const int N = (int)x->shape[0], H = (int)x->shape[2], W = (int)x->shape[3];
-    if (x->shape[1] != Cin) return 0;
-    const int Ho = (H + 2 - 3) / S + 1, Wo = (W + 2 - 3) / S + 1;
-    IrbShape ts{};
-    if (!irb_shape(N, (int)Cin, (int)Ch, (int)Cout, Ho, Wo, S, &ts)) return 0;
-    if (!irb_lds_ok) {
-      if (!irb_set_lds_limit()) {
-        fail("hipFuncSetAttribute(k_irb) failed");
-        return -1;
-      }
-      irb_lds_ok = true;
-    }
-    auto zeros_or = [&](const Const* c, int64_t m) {
-      return c ? c->f : std::vector<float>((size_t)m, 0.f);
-    };
-    IrbParams q{};
-    q.x = dptr(*x);
-    q.w1 = upload(conv_w(e)->c);
-    q.b1 = upload_vec(zeros_or(conv_b(e, Ch), Ch));
-    q.wd = upload(wdv->c);
-    q.bd = upload_vec(zeros_or(conv_b(dw, Ch), Ch));
-    q.w2 = upload(conv_w(pn)->c);
-    q.b2 = upload_vec(zeros_or(conv_b(pn, Cout), Cout));
-    if (!q.w1 || !q.b1 || !q.wd || !q.bd || !q.w2 || !q.b2) return -1;
-    q.N = N; q.Cin = (int)Cin; q.H = H; q.W = W; q.Ch = (int)Ch; q.Cout = (int)Cout; q.Ho = Ho; q.Wo = Wo;
-    q.act1 = a1.act; q.lo1 = a1.a0; q.hi1 = a1.a1;
-    q.act2 = a2.act; q.lo2 = a2.a0; q.hi2 = a2.a1;
-    q.res = add_node >= 0;
-    q.tiles_x = ts.tiles_x; q.tiles = ts.tiles; q.ksplit = ts.ksplit; q.cps = ts.cps;
-    if (ts.ksplit > 1) {
-      const size_t blocks = (size_t)N * ts.tiles;
-      const size_t per = (size_t)ts.cbw * ts.th * 256 * 16;
-      if (!dalloc(&q.part, blocks * ts.ksplit * per) || !dalloc(&q.counters, blocks * 4)) return -1;
-      if (hipMemset(q.counters, 0, blocks * 4) != hipSuccess) {
-        fail("hipMemset failed");
-        return -1;
-      }
-    }
-    if (!set_runtime(out, {N, Cout, Ho, Wo})) return -1;
-    q.y = dptr(vals[out]);
-    for (int k : {n_a1, d, n_a2, pw, add_node})
-      if (k >= 0) done.insert((size_t)k);
-    add(irb_name(ts), [q, ts](hipStream_t st2) { launch_irb(q, ts, st2); });
-    s->irb_blocks++;
-    return 1;
-  }
-  bool irb_lds_ok = false;
-  const bool irb_enabled = getenv("VSO_IRB") && getenv("VSO_IRB")[0] == '1';  // opt-in (vso_irb.hip: measured slower)
 
   bool plan_conv(size_t ni) {
     const Node& nd = g.nodes[ni];
-    {
-      const int r = try_plan_irb(ni);
-      if (r != 0) return r > 0 && err.empty();
-    }
     Value* x = val(nd.in[0]);
     Value* w = val(nd.in[1]);
     Value* b = nd.in.size() > 2 ? val(nd.in[2]) : nullptr;
@@ -2139,7 +2013,6 @@ int vso_launch_count(const vso_session* s) { return s ? (int)s->launches.size() 
 
 int vso_tile_conv_count(const vso_session* s) { return s ? s->tile_convs : VSO_E_INVALID_ARG; }
 
-int vso_fused_block_count(const vso_session* s) { return s ? s->irb_blocks : VSO_E_INVALID_ARG; }
 
 int vso_launch_name(const vso_session* s, int k, char* buf, int cap) {
   if (!s || k < 0 || k >= (int)s->launches.size() || !buf || cap < 1) return VSO_E_INVALID_ARG;
