@@ -360,6 +360,8 @@ def main():
     ap.add_argument("--dtype", default="bf16x2", choices=["bf16x2", "f32"])
     ap.add_argument("--inflight", type=int, default=4, help="batches in flight (streams = the handle's queue depth)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--streams", default="slot", choices=["slot", "torch"],
+                    help="step streams: the handle's slot streams (distinct hardware queues) or new torch streams")
     ap.add_argument("--cpu-budget-s", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-post", action="store_true", help="skip the post-processing leg")
@@ -424,7 +426,10 @@ def main():
     P = hm * wm
     # one output buffer per stream: step i writes buffer i % S on stream i % S
     outs = [torch.empty((world * B, P), dtype=torch.float32, device=dev) for _ in range(S)]
-    streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
+    if args.streams == "slot":
+        streams = [torch.cuda.ExternalStream(sess.slot_stream(k), device=dev) for k in range(S)]
+    else:
+        streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
     rs, fs = fw * 3, fh * fw * 3
 
     def step(i, st):
@@ -465,8 +470,10 @@ def main():
     e0.record(streams[k % S])
     k = run_steps(sess, streams, args.steps, step_ev, start=k)
     torch.cuda.synchronize(dev)
-    done_ms = sorted(e0.elapsed_time(e) for e in ends)
-    iv = np.diff(done_ms)
+    # completions arrive in bursts (the batches in flight finish close
+    # together), so the step interval is taken over S consecutive completions
+    done_ms = np.sort(np.array([e0.elapsed_time(e) for e in ends]))
+    iv = (done_ms[S:] - done_ms[:-S]) / S if len(done_ms) > S else np.diff(done_ms)
     median_step_ms = float(np.median(iv)) if len(iv) else None
     n_ranks = sess.comm_ranks if gather else world
     d_masks = outs[last][rank * B:(rank + 1) * B] if world > 1 else outs[last][:B]

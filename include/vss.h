@@ -239,6 +239,13 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
 int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels, size_t row_stride,
                        size_t frame_stride);
 
+/* Slot k's HIP stream (a hipStream_t; k < queue_depth).  Device calls whose
+ * `stream` is the stream of the slot they take (device calls take slots
+ * round-robin: call i -> slot i % queue_depth) order after that slot's
+ * previous work for free, and the handle's slot streams sit on distinct
+ * hardware queues, so batches in flight on them run concurrently. */
+int vss_slot_stream(vss_handle* h, int k, void** stream);
+
 /* The batch sharding of SURVEY.md §8(e), host-only (no GPU needed): a batch
  * of n frames over nranks GPUs in contiguous shards of *per_rank =
  * ceil(n / nranks) frames; rank `rank` takes frames [*first, *first + *count)

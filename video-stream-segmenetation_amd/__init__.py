@@ -137,6 +137,7 @@ def lib() -> ctypes.CDLL:
                 "vss_submit_list": ([P, ctypes.POINTER(P), I, I, I, I, S, P, I, ctypes.POINTER(ctypes.c_uint64)], I),
                 "vss_segment_device": ([P, P, I, I, I, I, S, S, P, P], I),
                 "vss_prepare_device": ([P, I, I, I, I, S, S], I),
+                "vss_slot_stream": ([P, I, ctypes.POINTER(P)], I),
                 "vss_shard_plan": ([I, I, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)], I),
                 "vss_host_alloc": ([S, ctypes.POINTER(P)], I),
                 "vss_host_free": ([P], I),
@@ -364,6 +365,12 @@ class Session:
     def prepare_device(self, n: int, h: int, w: int, c: int, row_stride: int, frame_stride: int):
         """Build every slot's executable graph for this batch shape now (no launch)."""
         _check(lib().vss_prepare_device(self._h, n, h, w, c, row_stride, frame_stride), self._h)
+
+    def slot_stream(self, k: int) -> int:
+        """Slot k's hipStream_t (device call i takes slot i % queue_depth)."""
+        p = ctypes.c_void_p()
+        _check(lib().vss_slot_stream(self._h, k, ctypes.byref(p)), self._h)
+        return p.value
 
     @property
     def graph_builds(self) -> int:

@@ -85,6 +85,7 @@ struct LayerPlan {
 struct Launch {
   const void* fn = nullptr;
   dim3 grid;
+  int threads = kThreads;
   size_t lds = 0;
   int layer = 0;
   union Prm {
@@ -418,13 +419,19 @@ int ks_max(const LayerPlan& l) {
   return 1;
 }
 
+// LDS bytes of one workgroup of compiled shape e for layer l.
+size_t entry_lds_bytes(const LayerPlan& l, const BlockEntry& e) {
+  if (e.threads == kWideThreads) return (size_t)stem_b1_lds(e.TH, e.TW).total * 4;
+  return block_lds_bytes(l, e.TH, e.TW);
+}
+
 void set_tile(LayerPlan& l, const BlockEntry* e) {
   l.entry = e;
   l.TH = e->TH;
   l.TW = e->TW;
   l.tiles_x = (l.W + l.TW - 1) / l.TW;
   l.tiles_y = (l.H + l.TH - 1) / l.TH;
-  l.lds = block_lds_bytes(l, l.TH, l.TW);
+  l.lds = entry_lds_bytes(l, *e);
 }
 
 // Tile choice among the compiled shapes for this layer (csrc/vss_registry.inc):
@@ -441,8 +448,9 @@ int choose_tile(vss_handle* h, LayerPlan& l, int N) {
     if (e.mode != l.mode || e.stride != l.stride || e.cin != (int)l.rec.cin || e.cskip != cskip ||
         e.chid != l.chid / l.ks || e.cout != l.C || e.flags != l.flags)
       continue;
+    if (e.threads != kThreads) continue;  // the wide kernels are candidates of the autotuner only
     const long blocks = (long)((l.H + e.TH - 1) / e.TH) * ((l.W + e.TW - 1) / e.TW) * N;
-    const size_t lds = block_lds_bytes(l, e.TH, e.TW);
+    const size_t lds = entry_lds_bytes(l, e);
     // score: enough blocks first, then bigger tiles, then less LDS
     long score = (blocks >= 512 ? 1L << 40 : blocks << 20) + (long)e.TH * e.TW * 1024 - (long)(lds / 1024);
     if (blocks >= 512 && lds > 64 * 1024) score -= 1L << 39;
@@ -692,7 +700,20 @@ int make_slot(vss_handle* h, Slot& s, int gather_ranks) {
   HIP_TRY(h, hipMemset(s.acc, 0, acc));
   if ((rc = dalloc(h, &s.d_masks, (size_t)N * P * 4))) return rc;
   if (gather_ranks > 0 && (rc = dalloc(h, &s.d_gather, (size_t)gather_ranks * N * P * 4))) return rc;
-  HIP_TRY(h, hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  // VSS_SLOT_QUEUES=cumask: the slot's stream carries a CU mask of every CU,
+  // which gives it a hardware queue of its own (the runtime shares its pooled
+  // queues between plain streams — GPU_MAX_HW_QUEUES of them — so two slots
+  // could land on one queue and run one after the other)
+  static const char* q = std::getenv("VSS_SLOT_QUEUES");
+  if (q && !std::strcmp(q, "cumask")) {
+    int cus = 0;
+    HIP_TRY(h, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+    for (int c = 0; c < cus; ++c) mask[c / 32] |= 1u << (c % 32);
+    HIP_TRY(h, hipExtStreamCreateWithCUMask(&s.stream, (uint32_t)mask.size(), mask.data()));
+  } else {
+    HIP_TRY(h, hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  }
   // host waits on it sleep instead of spinning: several waiting threads (the
   // N-API addon's libuv workers, vss_wait callers) would otherwise take the
   // cores the staging copies run on
@@ -860,6 +881,7 @@ void forward_launches(vss_handle* h, Slot& s, const uint8_t* frames, int n, int 
 #endif
       L.fn = (const void*)l.entry->fn[prec == PREC_F32 ? 0 : 1];
       L.grid = dim3(l.tiles_x, l.tiles_y, n * l.ks);
+      L.threads = l.entry->threads;
       L.lds = l.lds;
       L.prm.block = p;
     } else if (r.kind == K_HEAD) {
@@ -891,7 +913,7 @@ hipKernelNodeParams node_params(const Launch& L, void** args) {
   args[0] = const_cast<Launch::Prm*>(&L.prm);
   kp.func = const_cast<void*>(L.fn);
   kp.gridDim = L.grid;
-  kp.blockDim = dim3(kThreads);
+  kp.blockDim = dim3(L.threads);
   kp.sharedMemBytes = (unsigned)L.lds;
   kp.kernelParams = args;
   kp.extra = nullptr;
@@ -907,9 +929,9 @@ int launch_eager(vss_handle* h, const std::vector<Launch>& ls, hipStream_t st, i
     if (prof_slot >= 0) {
       hipEvent_t e0 = h->ev[((size_t)prof_slot * nl + L.layer) * 2];
       hipEvent_t e1 = h->ev[((size_t)prof_slot * nl + L.layer) * 2 + 1];
-      HIP_TRY(h, hipExtLaunchKernel(L.fn, L.grid, dim3(kThreads), args, L.lds, st, e0, e1, 0));
+      HIP_TRY(h, hipExtLaunchKernel(L.fn, L.grid, dim3(L.threads), args, L.lds, st, e0, e1, 0));
     } else {
-      HIP_TRY(h, hipLaunchKernel(L.fn, L.grid, dim3(kThreads), args, L.lds, st));
+      HIP_TRY(h, hipLaunchKernel(L.fn, L.grid, dim3(L.threads), args, L.lds, st));
     }
   }
   hipError_t e = hipGetLastError();
@@ -1483,9 +1505,9 @@ int autotune(vss_handle* h) {
           p.stem.y = nullptr;  // timed as the forward runs it by default
         }
         const dim3 grid(l.tiles_x, l.tiles_y, N * l.ks);
-        for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(kThreads), l.lds, h->stream, p);
+        for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(e->threads), l.lds, h->stream, p);
         (void)hipEventRecord(e0, h->stream);
-        for (int k = 0; k < 8; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(kThreads), l.lds, h->stream, p);
+        for (int k = 0; k < 8; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(e->threads), l.lds, h->stream, p);
         (void)hipEventRecord(e1, h->stream);
         float ms = 0.f;
         if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess ||
@@ -2095,6 +2117,13 @@ int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels
   return VSS_OK;
 }
 
+int vss_slot_stream(vss_handle* h, int k, void** stream) {
+  if (!h || !stream) return fail(h, VSS_E_INVALID_ARG, "null handle/stream");
+  if (k < 0 || k >= (int)h->slots.size()) return fail(h, VSS_E_INVALID_ARG, "slot out of range");
+  *stream = h->slots[k].stream;
+  return VSS_OK;
+}
+
 int vss_shard_plan(int n, int nranks, int rank, int* first, int* count, int* per_rank) {
   if (n < 0 || nranks < 1 || rank < 0 || rank >= nranks || !first || !count || !per_rank) return VSS_E_INVALID_ARG;
   shard_plan(n, nranks, rank, first, count, per_rank);
@@ -2118,7 +2147,8 @@ int vss_layer_occupancy(const vss_handle* h, int layer, int* wg_per_cu, int* lds
   const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
   HIP_TRY(const_cast<vss_handle*>(h), hipSetDevice(h->device));
   HIP_TRY(const_cast<vss_handle*>(h),
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(wg_per_cu, (const void*)l.entry->fn[pi], kThreads, l.lds));
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(wg_per_cu, (const void*)l.entry->fn[pi], l.entry->threads,
+                                                       l.lds));
   // the API assumes a finer LDS granule than gfx950 allocates (kLdsGranule)
   *wg_per_cu = std::min(*wg_per_cu, lds_wg_per_cu((int)l.lds));
   return VSS_OK;
@@ -2149,8 +2179,11 @@ int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap) {
   else if (l.rec.kind == K_HEAD) std::snprintf(tmp, sizeof(tmp), "void vss::k_head<16>(vss::HeadParams)");
   else {
     const BlockEntry* e = l.entry;
-    std::snprintf(tmp, sizeof(tmp), "void vss::k_block<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>(vss::BlockParams)",
-                  e->mode, e->stride, e->TH, e->TW, e->cin, e->cskip, e->chid, e->cout, e->flags, prec);
+    if (e->threads == kWideThreads)
+      std::snprintf(tmp, sizeof(tmp), "void vss::k_stem_b1<%d, %d, %d>(vss::BlockParams)", e->TH, e->TW, prec);
+    else
+      std::snprintf(tmp, sizeof(tmp), "void vss::k_block<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>(vss::BlockParams)",
+                    e->mode, e->stride, e->TH, e->TW, e->cin, e->cskip, e->chid, e->cout, e->flags, prec);
   }
   const int len = (int)std::strlen(tmp);
   std::snprintf(buf, (size_t)cap, "%s", tmp);

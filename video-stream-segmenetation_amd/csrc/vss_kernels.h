@@ -245,7 +245,37 @@ using BlockFn = void (*)(BlockParams);
 struct BlockEntry {
   int mode, stride, TH, TW, cin, cskip, chid, cout, flags;
   BlockFn fn[2];  // [PREC_F32, PREC_BF16X2]
+  int threads = kThreads;  // workgroup size (kWideThreads: k_stem_b1)
 };
+
+// b1 with the stem fused on a wide workgroup (k_stem_b1, 16 waves): LDS
+// carve in floats — the resized region x0 [3][2*IH+1][2*IW+2], the stem
+// weights [27][16] + bias, the stem output tile xt [P_IN_PAD][16 + pad] and the
+// block's weight image (block_lds regions w1..b2 of the same shape).
+constexpr int kWideThreads = 1024;
+struct StemB1Lds {
+  int IH, IW, P_IN, P_IN_PAD, XS, XH, XW, XWP, x0, sw, sb, xt, wim, total;
+};
+__host__ __device__ constexpr StemB1Lds stem_b1_lds(int TH, int TW) {
+  StemB1Lds L{};
+  L.IH = TH + 2;
+  L.IW = TW + 2;
+  L.P_IN = L.IH * L.IW;
+  L.P_IN_PAD = (L.P_IN + 15) & ~15;
+  L.XS = 16 + VSS_XS_PAD;
+  L.XH = 2 * L.IH + 1;
+  L.XW = 2 * L.IW + 1;
+  L.XWP = L.XW + 1;
+  int o = 0;
+  L.x0 = o;  o += r4(3 * L.XH * L.XWP);
+  L.sw = o;  o += 27 * 16;
+  L.sb = o;  o += 16;
+  L.xt = o;  o += r4(L.P_IN_PAD * L.XS);
+  const BlockLds B = block_lds(1 /*MODE_IR_DIRECT*/, 1, TH, TW, 16, 0, 16, 16, 1);
+  L.wim = o; o += B.wimg_end - B.w1;
+  L.total = o;
+  return L;
+}
 const BlockEntry* block_registry(int* count);
 
 

@@ -1026,6 +1026,147 @@ __global__ __launch_bounds__(256) void k_block(BlockParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// b1 with the stem fused, on a wide workgroup (kWideThreads = 1024 threads, 16
+// waves) and a tile four to eight times block_body's.  The arithmetic is
+// block_body<MODE_IR_DIRECT, 1, .., 16, 0, 16, 16, STEM_IN | residual>'s,
+// operation for operation (prep_tap / prep_load / prep_finish of the resize,
+// stem_mfma, the dw taps in ky-major order, relu6, to_operand, one project
+// MFMA, + bias, + residual), so the activations are bitwise the same
+// (test_stem_fusion_bitwise, test_results_independent_of_tiling).  What
+// changes is the overlap: a 4 x 16 tile recomputes its resized region 1.9x
+// and its stem region 1.7x per output (the halo), an 8 x 32 tile 1.4x / 1.3x,
+// and each of the 1024 threads has fewer resized pixels to gather and lerp
+// (1.4 vs 1.9) — b1 is bound by the resize's VALU issue and byte gathers.
+// Only for this layer shape (16 -> 16 direct, stride 1), so it lives outside
+// the block registry's generator: block_registry() appends its entries.
+template <int TH, int TW, int PREC>
+__global__ __launch_bounds__(kWideThreads) void k_stem_b1(BlockParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int WT = kWideThreads, NWAVE = WT / 64;
+  constexpr StemB1Lds S = stem_b1_lds(TH, TW);
+  constexpr int IH = S.IH, IW = S.IW, P_IN = S.P_IN, P_IN_PAD = S.P_IN_PAD, XS = S.XS;
+  constexpr int XH = S.XH, XW = S.XW, XWP = S.XWP, NX = (XH * XW + WT - 1) / WT;
+  constexpr BlockLds B = block_lds(MODE_IR_DIRECT, 1, TH, TW, 16, 0, 16, 16, 1);
+  constexpr int WIMG4 = (B.wimg_end - B.w1) / 4;
+  static_assert(WIMG4 <= WT && 27 * 16 <= WT, "one weight element per thread");
+  float* x0s = smem + S.x0;
+  float* sws = smem + S.sw;
+  float* sbs = smem + S.sb;
+  float* xt = smem + S.xt;
+  float* wim = smem + S.wim;
+  const TileIdx tl = xcd_tile();
+  const int bx = tl.x, by = tl.y, n = tl.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int oy0 = by * TH, ox0 = bx * TW, iy0 = oy0 - 1, ix0 = ox0 - 1;
+  const StemParams& sp = p.stem;
+  const int H = p.H, W = p.W;  // the stem's output = b1's input
+  const uint8_t* fr = sp.frames + (long)n * sp.frame_stride;
+  const int r0 = 2 * iy0 - 1, c0 = 2 * ix0 - 1;  // x0 region origin (model resolution)
+  // every load issued first: the weight image, the stem's weights, the frame taps
+  const f4 wv = reinterpret_cast<const f4*>(p.wimg)[min(tid, WIMG4 - 1)];
+  const float swr = sp.w[min(tid, 27 * 16 - 1)];
+  const float sb = sp.b[min(tid, 15)];
+  uint32_t raw[NX][12];
+  float dys[NX], dxs[NX];
+#pragma unroll
+  for (int u = 0; u < NX; ++u) {
+    const int i = min(tid + WT * u, XH * XW - 1);
+    const int ly = i / XW, lx = i - ly * XW;
+    const int yy = min(max(r0 + ly, 0), sp.Hm - 1), xx = min(max(c0 + lx, 0), sp.Wm - 1);
+    const PrepTap t = prep_tap(fr, sp.row_stride, sp.fc, sp.fh, sp.fw, sp.ry, sp.rx, yy, xx);
+    prep_load(t, raw[u]);
+    dys[u] = t.dy;
+    dxs[u] = t.dx;
+  }
+  float o[NX][3];
+#pragma unroll
+  for (int u = 0; u < NX; u += 2) {
+    if (u + 1 < NX)
+      prep_finish2(raw[u], raw[u + 1], dys[u], dxs[u], dys[u + 1], dxs[u + 1], o[u], o[u + 1]);
+    else
+      prep_finish(raw[u], dys[u], dxs[u], o[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < NX; ++u) {
+    const int i = tid + WT * u;
+    if (i < XH * XW) {
+      const int ly = i / XW, lx = i - ly * XW;
+      const int yy = r0 + ly, xx = c0 + lx;
+      const bool valid = yy >= 0 && yy < sp.Hm && xx >= 0 && xx < sp.Wm;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) x0s[(c * XH + ly) * XWP + lx] = valid ? o[u][c] : 0.f;
+    }
+  }
+  if (tid < WIMG4) reinterpret_cast<f4*>(wim)[tid] = wv;
+  if (tid < 27 * 16) sws[(tid % 27) * 16 + tid / 27] = swr;  // sp.w is [c][27]
+  if (tid < 16) sbs[tid] = sb;
+  // start of the forward: zero this frame's decoder norm accumulators (the stem's job)
+  if (bx == 0 && by == 0)
+    for (int i = tid; i < sp.acc_stride; i += WT) sp.acc_zero[(long)n * sp.acc_stride + i] = 0ull;
+  __syncthreads();
+  // the stem over the region, 16-pixel blocks on the MFMA (stem_mfma), zero outside the image
+  {
+    const StemTaps taps = stem_taps(sws, r, g, XH * XWP, XWP);
+    const float bias = sbs[r];
+    const bool interior = iy0 >= 0 && iy0 + IH <= H && ix0 >= 0 && ix0 + IW <= W;
+    for (int blk = wave; blk < P_IN_PAD / 16; blk += NWAVE) {
+      const int pa = min(blk * 16 + r, P_IN - 1), py = pa / IW, px = pa - py * IW;
+      const f4 acc = stem_mfma(taps, x0s + 2 * py * XWP + 2 * px, bias);
+      const int p0 = blk * 16 + 4 * g;
+      if (interior) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xt[(p0 + i) * XS + r] = p0 + i < P_IN ? relu6f(acc[i]) : 0.f;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // D[pixel 4g+i][channel r]
+          const int pp = p0 + i, qy = pp / IW, qx = pp - qy * IW;
+          const int yy = iy0 + qy, xx = ix0 + qx;
+          const bool valid = pp < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+          xt[pp * XS + r] = valid ? relu6f(acc[i]) : 0.f;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // b1: dw 3x3 -> relu6 -> project 16 -> 16 (one MFMA) -> + bias -> + residual;
+  // lane (r, g) = pixel r of the wave's block, channels 4g..4g+3, in registers
+  // from the dw taps to the store
+  const uint16_t* w2s = reinterpret_cast<const uint16_t*>(wim + (B.w2 - B.w1));
+  const float* wdws = wim + (B.wdw - B.w1);
+  const float* bdws = wim + (B.bdw - B.w1);
+  const float* b2s = wim + (B.b2 - B.w1);
+  f4 wk[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wk[t] = *reinterpret_cast<const f4*>(wdws + t * 16 + 4 * g);
+  const f4 bb = *reinterpret_cast<const f4*>(bdws + 4 * g);
+  const typename AFrag<PREC>::T a2 = lds_a<PREC>(w2s, B.LD2, r, 4 * g);
+  const f4 bias2 = *reinterpret_cast<const f4*>(b2s + 4 * g);
+  const int Ho = p.Ho, Wo = p.Wo;
+  float* yn = p.y + (long)n * Ho * Wo * 16;
+  float* st = p.stem.y ? p.stem.y + (long)n * H * W * 16 : nullptr;  // VSS_OPT_KEEP_STEM
+  for (int pb = wave; pb < TH * TW / 16; pb += NWAVE) {
+    const int pix = pb * 16 + block_pix(r), ly = pix / TW, lx = pix % TW;
+    f4 a = bb;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+        a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx + kx) * XS + 4 * g) + a;
+    a = relu6v(a);
+    const f4 b = to_operand<PREC>(a);
+    f4 v = mma16_op<PREC>(f4{0.f, 0.f, 0.f, 0.f}, a2, b);
+    const f4 centre = *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + 4 * g);
+    v = v + bias2;
+    v = v + centre;
+    const int oy = oy0 + ly, ox = ox0 + lx;
+    if (oy < Ho && ox < Wo) {
+      *reinterpret_cast<f4*>(yn + ((long)oy * Wo + ox) * 16 + 4 * g) = v;
+      if (st) *reinterpret_cast<f4*>(st + ((long)oy * W + ox) * 16 + 4 * g) = centre;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Head: mask tile 16 x 64; logits over the (10 x 34) low-res region in LDS.
 template <int C, bool COH>
 __device__ __forceinline__ void head_body(const HeadParams& p, int bx, int by, int n, float* smem) {
@@ -1149,6 +1290,13 @@ const BlockEntry* VSS_CAT(registry_shard_, VSS_SHARD)(int* count) {
 #include "vss_registry_shards.inc"
 #undef VSS_SHARD_FN
 
+// The wide stem + b1 kernel's tiles (k_stem_b1): 16 -> 16 direct, stride 1,
+// residual, STEM_IN (block_flags(0, 1, 1, 1, 1, 1) = 258).
+#define VSS_STEM_B1(TH, TW) \
+  {1, 1, TH, TW, 16, 0, 16, 16, 258, {k_stem_b1<TH, TW, PREC_F32>, k_stem_b1<TH, TW, PREC_BF16X2>}, kWideThreads},
+static const BlockEntry kStemB1Blocks[] = {VSS_STEM_B1(8, 32) VSS_STEM_B1(4, 64) VSS_STEM_B1(8, 64)};
+#undef VSS_STEM_B1
+
 const BlockEntry* block_registry(int* count) {
   static const std::vector<BlockEntry> all = [] {
     std::vector<BlockEntry> v;
@@ -1159,6 +1307,7 @@ const BlockEntry* block_registry(int* count) {
     v.insert(v.end(), part, part + n);
 #include "vss_registry_shards.inc"
 #undef VSS_SHARD_FN
+    v.insert(v.end(), std::begin(kStemB1Blocks), std::end(kStemB1Blocks));
     return v;
   }();
   *count = (int)all.size();
