@@ -59,8 +59,9 @@ def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=False)
     f += r4(2 * cin) if mode == 2 else 0
     f += 4 * p_in_pad if mode == 2 else 0  # the decoder's upsample tap records (L.uc)
     # work: expand scratch / slabs / (decoder) the low-res src region; the
-    # decoder's norm slots and stats scratch live in xt
-    f += max(4 * p_in_pad * HID_STRIDE if mode == 0 else 1024, cs * p_out * (cout + 4),
+    # decoder's slabs go into xt when they fit (its stats scratch then in work)
+    slab_in_xt = mode == 2 and cs * p_out * (cout + 4) <= r4(p_in_pad * (cx + 4))
+    f += max(4 * p_in_pad * HID_STRIDE if mode == 0 else 1024, 0 if slab_in_xt else cs * p_out * (cout + 4),
              r4(sr * sc * cin) if mode == 2 else 0, stem_in_lds(ih, iw) if stem_in else 0)
     return f * 4, nacc
 

@@ -137,6 +137,9 @@ struct Slot {
                                       // take no ticket and leave it alone)
   bool stem_stored = false;           // the latest forward stored the fused stem (VSS_OPT_KEEP_STEM)
   std::map<GraphKey, GraphEntry> graphs;
+#ifdef VSS_TRACE
+  std::vector<unsigned long long*> trace;  // per layer, [workgroups][16] stamps of this slot's latest forward
+#endif
   ncclComm_t comm = nullptr;          // this GPU's communicator of the slot (RCCL handles)
   // host-path staging, allocated on the slot's first host call
   uint8_t* d_frames = nullptr;
@@ -289,7 +292,6 @@ struct vss_handle {
   std::map<int, RowPlan> row_plans;  // by frame height
   int row_fetch = 1;           // VSS_OPT_ROW_FETCH
 #ifdef VSS_TRACE
-  std::vector<unsigned long long*> trace;  // per layer, [grid][16] stamps
   std::vector<int> trace_wgs;              // workgroups of the layer's last launch
 #endif
   uint8_t* d_comp = nullptr;      // vss_segment_composite output, allocated on first use
@@ -670,14 +672,7 @@ int upload(vss_handle* h) {
     }
   }
 #ifdef VSS_TRACE
-  h->trace.assign(h->L.size(), nullptr);
   h->trace_wgs.assign(h->L.size(), 0);
-  for (size_t i = 0; i < h->L.size(); ++i) {
-    const LayerPlan& l = h->L[i];
-    const size_t bytes = (size_t)h->cfg.max_batch * l.H * l.W * 16 * 8;
-    if ((rc = dalloc(h, &h->trace[i], bytes))) return rc;
-    HIP_TRY(h, hipMemset(h->trace[i], 0, bytes));
-  }
 #endif
   return VSS_OK;
 }
@@ -719,6 +714,15 @@ int make_slot(vss_handle* h, Slot& s, int gather_ranks) {
   // cores the staging copies run on
   HIP_TRY(h, hipEventCreateWithFlags(&s.done, hipEventDisableTiming | hipEventBlockingSync));
   HIP_TRY(h, hipEventCreateWithFlags(&s.host_done, hipEventDisableTiming | hipEventBlockingSync));
+#ifdef VSS_TRACE
+  s.trace.assign(h->L.size(), nullptr);
+  for (size_t i = 0; i < h->L.size(); ++i) {
+    const LayerPlan& l = h->L[i];
+    const size_t bytes = (size_t)h->cfg.max_batch * l.H * l.W * 16 * 8;  // >= one record per workgroup
+    if ((rc = dalloc(h, &s.trace[i], bytes))) return rc;
+    HIP_TRY(h, hipMemset(s.trace[i], 0, bytes));
+  }
+#endif
   return VSS_OK;
 }
 
@@ -862,7 +866,7 @@ void forward_launches(vss_handle* h, Slot& s, const uint8_t* frames, int n, int 
     if (r.kind == K_STEM) {
       StemParams p = stem_params(h, s, i, frames, rs, fs, fh, fw, fc);
 #ifdef VSS_TRACE
-      p.trace = h->trace[i];
+      p.trace = s.trace[i];
       h->trace_wgs[i] = ((l.W + kStemTW - 1) / kStemTW) * ((l.H + kStemTH - 1) / kStemTH) * n;
 #endif
       L.fn = (const void*)stem_kernel16();
@@ -876,7 +880,7 @@ void forward_launches(vss_handle* h, Slot& s, const uint8_t* frames, int n, int 
         if (!h->keep_stem) p.stem.y = nullptr;  // no layer reads it (vss_read_layer(0) only)
       }
 #ifdef VSS_TRACE
-      p.trace = h->trace[i];
+      p.trace = s.trace[i];
       h->trace_wgs[i] = l.tiles_x * l.tiles_y * n * l.ks;
 #endif
       L.fn = (const void*)l.entry->fn[prec == PREC_F32 ? 0 : 1];
@@ -894,7 +898,7 @@ void forward_launches(vss_handle* h, Slot& s, const uint8_t* frames, int n, int 
       p.w = l.head_w; p.b = l.head_b; p.mask = masks;
       p.N = n; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
 #ifdef VSS_TRACE
-      p.trace = h->trace[i];
+      p.trace = s.trace[i];
       h->trace_wgs[i] = ((Wm + kHeadTW - 1) / kHeadTW) * ((Hm + kHeadTH - 1) / kHeadTH) * n;
 #endif
       L.fn = (const void*)head_kernel16();
@@ -1468,14 +1472,27 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
 // Autotune: time every compiled tile of every block layer at max_batch on
 // this device and keep the fastest.  The kernels' arithmetic does not depend
 // on the tile (see block_lds), so this changes speed only, never results.
+//   With several slots (queue_depth > 1) a candidate is timed as the engine
+// runs it in steady state: one launch per slot, all slots' streams at once
+// (each slot's own buffers), so what is measured is the layer's throughput
+// when its workgroups share the CUs with other batches' — there, a tile's
+// LDS x lifetime per output decides, not its latency alone (measured with
+// tools/trace_inflight.py: at 4 batches in flight the CUs hold ~3.3
+// workgroups each, LDS-full, ~4 % idle).  VSS_AUTOTUNE=latency times one
+// launch at a time instead (the round-2 criterion).
 int autotune(vss_handle* h) {
   const int N = h->cfg.max_batch;
   const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
   Slot& s = h->slots[0];
   if (int rc = ensure_staging(h, s)) return rc;  // the stem reads the staging buffer as frames
+  static const char* mode_env = std::getenv("VSS_AUTOTUNE");
+  const bool concurrent = h->slots.size() > 1 && !(mode_env && !std::strcmp(mode_env, "latency"));
+  const int S = concurrent ? (int)h->slots.size() : 1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   HIP_TRY(h, hipEventCreate(&e0));
   HIP_TRY(h, hipEventCreate(&e1));
+  std::vector<hipEvent_t> ends(S, nullptr);
+  for (auto& e : ends) HIP_TRY(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   int rc = VSS_OK;
   for (size_t li = 0; li < h->L.size(); ++li) {
     LayerPlan& l = h->L[li];
@@ -1497,17 +1514,33 @@ int autotune(vss_handle* h) {
           usable[c] = 0;
           continue;
         }
-        BlockParams p = block_params(h, s, (int)li, N);
-        if (flags_stem_in(l.flags)) {  // the staging buffer as frames: any bytes, valid memory
-          p.stem = stem_params(h, s, (int)l.rec.src, s.d_frames, (size_t)h->cfg.max_frame_w * 3,
-                               (size_t)h->cfg.max_frame_w * 3 * h->cfg.max_frame_h, h->cfg.max_frame_h,
-                               h->cfg.max_frame_w, 3);
-          p.stem.y = nullptr;  // timed as the forward runs it by default
+        std::vector<BlockParams> prm(S);
+        for (int k = 0; k < S; ++k) {
+          prm[k] = block_params(h, h->slots[k], (int)li, N);
+          if (flags_stem_in(l.flags)) {  // slot 0's staging buffer as frames: any bytes, valid memory
+            prm[k].stem = stem_params(h, h->slots[k], (int)l.rec.src, s.d_frames, (size_t)h->cfg.max_frame_w * 3,
+                                      (size_t)h->cfg.max_frame_w * 3 * h->cfg.max_frame_h, h->cfg.max_frame_h,
+                                      h->cfg.max_frame_w, 3);
+            prm[k].stem.y = nullptr;  // timed as the forward runs it by default
+          }
         }
         const dim3 grid(l.tiles_x, l.tiles_y, N * l.ks);
-        for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(e->threads), l.lds, h->stream, p);
+        auto run = [&](int reps) {
+          for (int k = 0; k < S; ++k) {
+            hipStream_t st = S > 1 ? h->slots[k].stream : h->stream;
+            if (S > 1) (void)hipStreamWaitEvent(st, e0, 0);
+            for (int q = 0; q < reps; ++q)
+              hipLaunchKernelGGL(e->fn[pi], grid, dim3(e->threads), l.lds, st, prm[k]);
+            if (S > 1) {
+              (void)hipEventRecord(ends[k], st);
+              (void)hipStreamWaitEvent(h->stream, ends[k], 0);
+            }
+          }
+        };
         (void)hipEventRecord(e0, h->stream);
-        for (int k = 0; k < 8; ++k) hipLaunchKernelGGL(e->fn[pi], grid, dim3(e->threads), l.lds, h->stream, p);
+        run(2);
+        (void)hipEventRecord(e0, h->stream);
+        run(8);
         (void)hipEventRecord(e1, h->stream);
         float ms = 0.f;
         if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess ||
@@ -1528,6 +1561,7 @@ int autotune(vss_handle* h) {
     set_tile(l, best);
     if (rc) break;
   }
+  for (auto e : ends) (void)hipEventDestroy(e);
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return rc;
@@ -2540,12 +2574,21 @@ int vss_segment_post(vss_handle* h, vss_post_state* st, const uint8_t* frames, i
 #ifdef VSS_TRACE
 // Trace build only: the stamps of `layer`'s last launch, [wgs][16] u64
 // (s_memrealtime ticks, 100 MHz).  Returns the workgroup count.
-extern "C" int vss_trace_read(vss_handle* h, int layer, unsigned long long* out, int cap) {
-  if (!h || layer < 0 || layer >= (int)h->L.size() || !out) return VSS_E_INVALID_ARG;
+// vss_trace_read_slot: the same for slot `slot`'s latest forward (several
+// batches in flight: tools/trace_inflight.py).  Stamp 7 holds the workgroup's
+// HW_ID register (cu, shader array, shader engine), stamp 15 its XCC_ID.
+extern "C" int vss_trace_read_slot(vss_handle* h, int slot, int layer, unsigned long long* out, int cap) {
+  if (!h || layer < 0 || layer >= (int)h->L.size() || !out || slot < 0 || slot >= (int)h->slots.size())
+    return VSS_E_INVALID_ARG;
   HIP_TRY(h, hipDeviceSynchronize());
   const int wgs = std::min(h->trace_wgs[layer], cap);
-  HIP_TRY(h, hipMemcpy(out, h->trace[layer], (size_t)wgs * 16 * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(h, hipMemcpy(out, h->slots[slot].trace[layer], (size_t)wgs * 16 * 8, hipMemcpyDeviceToHost));
   return wgs;
+}
+
+extern "C" int vss_trace_read(vss_handle* h, int layer, unsigned long long* out, int cap) {
+  if (!h || h->last_slot < 0) return VSS_E_INVALID_ARG;
+  return vss_trace_read_slot(h, h->last_slot, layer, out, cap);
 }
 #endif
 

@@ -89,6 +89,7 @@ struct BlockLds {
   int NCB, NPB, NCHUNK, PW, CS, NPBW, NACC;  // CS = chunk groups, PW = pixel-block groups
   int xt, xr, w1, w2, wdw, bdw, b1, b2, wimg_end, lr, nrm, uc, work, stt, total;  // [w1, wimg_end): the weight image
   int slab_stride;  // floats per wave slab = P_out * (cout + 4)
+  int slab;         // the epilogue's accumulator slabs: the work region, or (decoder) the input tile
 };
 
 // LDS the fused stem needs (x0 region [3][2*IH+1][2*IW+2] + stem weights), in the work region
@@ -137,21 +138,25 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   L.wimg_end = o;
   // per-wave scratch during the main loop (expand: each wave's hidden chunk
   // over the input tile), reused as the accumulator slabs after it.  The
-  // decoder's main loop needs no scratch, so its low-res src region (read
-  // only in the prologue) shares the space with the slabs (written only in
-  // the epilogue); the decoder stages the src's norm slots and, in the
-  // epilogue, its own stats scratch (int64 pairs) in xt, which is dead at
-  // both points (before the input tile is committed / after the main loop).
+  // decoder's main loop needs no scratch: its slabs go into the input tile
+  // xt (dead once the main loop is done) when they fit, and its low-res src
+  // region (read only in the prologue) then shares the work region with the
+  // epilogue's stats scratch (int64 pairs, 1024 floats); the decoder stages
+  // the src's norm slots in xt before the input tile is committed.  (Slabs in
+  // xt: d2 50 -> 39 KB of LDS, four workgroups per CU instead of three.)
+  const int xt_floats = r4(L.P_in_pad * L.XS);
+  const bool slab_in_xt = mode == 2 && L.CS * L.slab_stride <= xt_floats;
   L.work = o;
   L.lr = o;
-  o += cmax(cmax(cmax(mode == 0 ? 4 * L.P_in_pad * hid_stride(stride) : 1024, L.CS * L.slab_stride),
+  o += cmax(cmax(cmax(mode == 0 ? 4 * L.P_in_pad * hid_stride(stride) : 1024, slab_in_xt ? 0 : L.CS * L.slab_stride),
                  mode == 2 ? r4(L.SR * L.SC * cin) : 0),
             stem_in ? stem_in_lds(L.IH, L.IW) : 0);
   L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;
   // decoder: per input-tile pixel, its 2x-upsample taps (four lr offsets as
   // u16 pairs, ly1, lx1), built while the prologue loads are in flight
   L.uc = o;  o += mode == 2 ? 4 * L.P_in_pad : 0;
-  L.stt = L.xt;
+  L.slab = slab_in_xt ? L.xt : L.work;
+  L.stt = slab_in_xt ? L.work : L.xt;
   L.total = o;
   return L;
 }
@@ -176,6 +181,11 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
         unsigned long long* t_ = p.trace + (((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 16; \
         t_[(k)] = __builtin_amdgcn_s_memrealtime();                                                   \
         t_[8 + (k)] = __builtin_amdgcn_s_memtime();                                                   \
+        if ((k) == 0) {                                                                               \
+          /* where the workgroup runs: HW_ID (cu, sh, se, ...) and XCC_ID */                          \
+          t_[7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                                          \
+          t_[15] = __builtin_amdgcn_s_getreg((15 << 11) | 20);                                        \
+        }                                                                                             \
       }                                                                                               \
     }                                                                                                 \
   } while (0)

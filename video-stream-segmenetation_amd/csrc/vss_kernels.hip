@@ -498,9 +498,10 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   static_assert(!RES || (STRIDE == 1 && CIN == COUT && MODE != MODE_DEC), "residual shape");
   static_assert(MODE != MODE_IR_EXPAND || CS == 4, "expand deals its chunks to the 4 waves");
   static_assert(NPB % PW == 0, "pixel blocks must split evenly over the wave groups");
-  static_assert(MODE != MODE_DEC || (L.xt == L.stt && r4(P_IN_PAD * XS) >= 1024 &&
-                                     r4(P_IN_PAD * XS) >= (NORM_IN ? kAccSlots * 2 * CIN * 2 : 0)),
-                "decoder: xt holds the src's norm slots (prologue) and the stats scratch (epilogue)");
+  static_assert(MODE != MODE_DEC || (r4(P_IN_PAD * XS) >= (NORM_IN ? kAccSlots * 2 * CIN * 2 : 0) &&
+                                     (L.slab == L.xt ? L.stt == L.work : (L.stt == L.xt && r4(P_IN_PAD * XS) >= 1024))),
+                "decoder: xt holds the src's norm slots (prologue); the stats scratch (epilogue) sits in the "
+                "work region when the slabs take xt, else in xt");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n = KS == 1 ? bz : bz / KS;  // grid z = frame * KS + slice
@@ -516,6 +517,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   const float* b1s = smem + L.b1;
   const float* b2s = smem + L.b2;
   float* work = smem + L.work;
+  float* slabs = smem + L.slab;
   float* stt = smem + L.stt;
   VSS_STAMP(0);
 
@@ -893,7 +895,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   __syncthreads();  // every wave is done with its scratch (reused as slabs)
   VSS_STAMP(2);
   {
-    float* slab = work + cw * SS;
+    float* slab = slabs + cw * SS;
 #pragma unroll
     for (int i = 0; i < NPBW; ++i)
 #pragma unroll
@@ -917,9 +919,9 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       const int oy = oy0 + ly, ox = ox0 + lx;
       const bool valid = oy < Ho && ox < Wo;
       // slabs of the CS waves that own this pixel block, summed in wave order
-      f4 v = *reinterpret_cast<const f4*>(work + pix * RS + 4 * c4);
+      f4 v = *reinterpret_cast<const f4*>(slabs + pix * RS + 4 * c4);
 #pragma unroll
-      for (int s = 1; s < CS; ++s) v = v + *reinterpret_cast<const f4*>(work + s * SS + pix * RS + 4 * c4);
+      for (int s = 1; s < CS; ++s) v = v + *reinterpret_cast<const f4*>(slabs + s * SS + pix * RS + 4 * c4);
       if (KS == 1 || ks == 0) {  // bias and residual belong to part 0
         v = v + *reinterpret_cast<const f4*>(b2s + 4 * c4);
         if constexpr (RES) {
@@ -931,7 +933,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       }
       if constexpr (MODE == MODE_DEC) {
         outv[k] = v;
-        *reinterpret_cast<f4*>(work + pix * RS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(slabs + pix * RS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
       } else if (valid) {
         gy.st(((long)oy * Wo + ox) * COUT + 4 * c4, v);
       }
@@ -961,7 +963,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
       for (int pix = 0; pix < P_OUT; pix += G) {
         if (pix + gg < P_OUT) {
-          const float v = work[(pix + gg) * RS + c];
+          const float v = slabs[(pix + gg) * RS + c];
           s += (double)__builtin_rintf(v * 0x1p32f);
           q += (double)__builtin_rintf(v * v * 0x1p24f);
         }
@@ -972,7 +974,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         qi = 0;
         for (int pix = 0; pix < P_OUT; pix += G) {
           if (pix + gg < P_OUT) {
-            const float v = work[(pix + gg) * RS + c];
+            const float v = slabs[(pix + gg) * RS + c];
             si += (long long)__builtin_rintf(v * 0x1p32f);
             qi += (long long)__builtin_rintf(v * v * 0x1p24f);
           }
