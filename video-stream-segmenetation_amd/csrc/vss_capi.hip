@@ -1472,21 +1472,21 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
 // Autotune: time every compiled tile of every block layer at max_batch on
 // this device and keep the fastest.  The kernels' arithmetic does not depend
 // on the tile (see block_lds), so this changes speed only, never results.
-//   With several slots (queue_depth > 1) a candidate is timed as the engine
-// runs it in steady state: one launch per slot, all slots' streams at once
-// (each slot's own buffers), so what is measured is the layer's throughput
-// when its workgroups share the CUs with other batches' — there, a tile's
-// LDS x lifetime per output decides, not its latency alone (measured with
-// tools/trace_inflight.py: at 4 batches in flight the CUs hold ~3.3
-// workgroups each, LDS-full, ~4 % idle).  VSS_AUTOTUNE=latency times one
-// launch at a time instead (the round-2 criterion).
+//   Default: one launch at a time (latency).  VSS_AUTOTUNE=throughput times
+// a candidate as the engine runs it in steady state instead — one launch per
+// slot, all slots' streams at once (each slot's own buffers) — where a tile's
+// LDS x lifetime per output decides, not its latency alone (at 4 batches in
+// flight the CUs hold ~3.3 workgroups each, LDS-full, ~4 % idle:
+// tools/trace_inflight.py).  Measured (round 3, 2 x 2 interleaved runs):
+// 179.6k / 193.6k frames/s throughput-tuned against 192.5k / 188.9k — its
+// picks vary between runs, so latency stays the default.
 int autotune(vss_handle* h) {
   const int N = h->cfg.max_batch;
   const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
   Slot& s = h->slots[0];
   if (int rc = ensure_staging(h, s)) return rc;  // the stem reads the staging buffer as frames
   static const char* mode_env = std::getenv("VSS_AUTOTUNE");
-  const bool concurrent = h->slots.size() > 1 && !(mode_env && !std::strcmp(mode_env, "latency"));
+  const bool concurrent = h->slots.size() > 1 && mode_env && !std::strcmp(mode_env, "throughput");
   const int S = concurrent ? (int)h->slots.size() : 1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   HIP_TRY(h, hipEventCreate(&e0));
