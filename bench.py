@@ -360,8 +360,10 @@ def main():
     ap.add_argument("--dtype", default="bf16x2", choices=["bf16x2", "f32"])
     ap.add_argument("--inflight", type=int, default=4, help="batches in flight (streams = the handle's queue depth)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--streams", default="slot", choices=["slot", "torch"],
-                    help="step streams: the handle's slot streams (distinct hardware queues) or new torch streams")
+    ap.add_argument("--streams", default="torch", choices=["slot", "torch"],
+                    help="step streams: new torch streams (default; measured 184-187k vs 142-147k on plain slot "
+                         "streams, which share the runtime's pooled queues — see DESIGN.md) or the handle's slot "
+                         "streams (run with VSS_SLOT_QUEUES=cumask for dedicated queues)")
     ap.add_argument("--cpu-budget-s", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-post", action="store_true", help="skip the post-processing leg")

@@ -422,6 +422,22 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// dw pixel runs: the output pixels of XR consecutive pixel blocks are dealt
+// to lanes in horizontal runs — lane r of a "super-block" evaluates the XR
+// adjacent pixels (row, c0 .. c0 + XR - 1) — so the 3 x 3 taps those pixels
+// share are read from LDS once: per tap row STRIDE * (XR - 1) + 3 reads for
+// XR pixels instead of 3 * XR (stride 1, XR = 4: 18 reads per 4 pixels, not
+// 36).  Element j of the run is pixel block sb * XR + j's column r, so the
+// MFMAs still take one 16-pixel block per call, and every output pixel's
+// arithmetic is unchanged (bitwise the same activations for any XR / tile).
+// XR = the largest of 4, 2, 1 that tiles the TW-wide rows and deals evenly
+// to the PW pixel-block groups of waves.
+__host__ __device__ constexpr int dw_run(int TW, int NPB, int PW) {
+  return (TW % 4 == 0 && 16 % (TW / 4) == 0 && NPB % 4 == 0 && (NPB / 4) % PW == 0)   ? 4
+         : (TW % 2 == 0 && 16 % (TW / 2) == 0 && NPB % 2 == 0 && (NPB / 2) % PW == 0) ? 2
+                                                                                      : 1;
+}
+
 // Registers holding one thread's share of a TOTAL-item (16-B items) copy.
 // issue(): every load of the copy in flight (unconditional at clamped indices:
 // a conditional load makes hipcc branch and wait per element); commit():
@@ -806,6 +822,13 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
   for (int t = 0; t < L.NACC; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
   const int pw = wave % PW, cw = wave / PW;
+  // dw pixel runs (dw_run): element j of super-block sb for this lane
+  constexpr int XR = dw_run(TW, NPB, MODE == MODE_IR_EXPAND ? 1 : PW);
+  static_assert(NPB % XR == 0 && NPBW % XR == 0, "dw runs");
+  auto run_pix = [&](int sb, int j) {
+    if constexpr (XR == 1) return sb * 16 + block_pix(r);
+    else return (sb * (16 * XR / TW) + r / (TW / XR)) * TW + (r % (TW / XR)) * XR + j;
+  };
 
   if constexpr (MODE == MODE_IR_EXPAND) {
     constexpr int HSD = hid_stride(STRIDE);
@@ -840,20 +863,30 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) a2[cb] = lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g);
 #pragma unroll
-        for (int pb = 0; pb < NPB; ++pb) {
-          const int pix = pb * 16 + block_pix(r);
-          const int ly = pix / TW, lx = pix % TW;
-          f4 a = bb;
+        for (int q = 0; q < NPB / XR; ++q) {
+          const int pix0 = run_pix(q, 0), ly = pix0 / TW, lx0 = pix0 % TW;
+          f4 a[XR];
 #pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
+          for (int j = 0; j < XR; ++j) a[j] = bb;
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-              const int sp = (STRIDE * ly + ky) * IW + (STRIDE * lx + kx);
-              a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(hid + sp * HSD + 4 * g) + a;
-            }
-          const f4 b = to_operand<PREC>(relu6v(a));
+          for (int ky = 0; ky < 3; ++ky) {
+            constexpr int NT = STRIDE * (XR - 1) + 3;
+            f4 t[NT];
 #pragma unroll
-          for (int cb = 0; cb < NCB; ++cb) acc[pb * NCB + cb] = mma16_op<PREC>(acc[pb * NCB + cb], a2[cb], b);
+            for (int u = 0; u < NT; ++u)
+              t[u] = *reinterpret_cast<const f4*>(hid + ((STRIDE * ly + ky) * IW + STRIDE * lx0 + u) * HSD + 4 * g);
+#pragma unroll
+            for (int j = 0; j < XR; ++j)
+#pragma unroll
+              for (int kx = 0; kx < 3; ++kx) a[j] = __builtin_elementwise_fma(wk[ky * 3 + kx], t[STRIDE * j + kx], a[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < XR; ++j) {
+            const f4 b = to_operand<PREC>(relu6v(a[j]));
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb)
+              acc[(q * XR + j) * NCB + cb] = mma16_op<PREC>(acc[(q * XR + j) * NCB + cb], a2[cb], b);
+          }
         }
       }
       wave_sync();  // this chunk's hid reads before the next chunk's expand writes
@@ -874,19 +907,30 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) a2[cb] = lds_a<PREC>(w2s, L.LD2, cb * 16 + r, c0 + 4 * g);
 #pragma unroll
-      for (int i = 0; i < NPBW; ++i) {
-        const int pix = (pw + i * PW) * 16 + block_pix(r);
-        const int ly = pix / TW, lx = pix % TW;
-        f4 a = bb;
+      for (int q = 0; q < NPBW / XR; ++q) {
+        const int pix0 = run_pix(pw + q * PW, 0), ly = pix0 / TW, lx0 = pix0 % TW;
+        f4 a[XR];
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+        for (int j = 0; j < XR; ++j) a[j] = bb;
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx)
-            a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx + kx) * XS + c0 + 4 * g) + a;
-        if constexpr (MODE == MODE_IR_DIRECT) a = relu6v(a);
-        const f4 b = to_operand<PREC>(a);
+        for (int ky = 0; ky < 3; ++ky) {
+          f4 t[XR + 2];
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) acc[i * NCB + cb] = mma16_op<PREC>(acc[i * NCB + cb], a2[cb], b);
+          for (int u = 0; u < XR + 2; ++u)
+            t[u] = *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx0 + u) * XS + c0 + 4 * g);
+#pragma unroll
+          for (int j = 0; j < XR; ++j)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) a[j] = __builtin_elementwise_fma(wk[ky * 3 + kx], t[j + kx], a[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < XR; ++j) {
+          if constexpr (MODE == MODE_IR_DIRECT) a[j] = relu6v(a[j]);
+          const f4 b = to_operand<PREC>(a[j]);
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb)
+            acc[(q * XR + j) * NCB + cb] = mma16_op<PREC>(acc[(q * XR + j) * NCB + cb], a2[cb], b);
+        }
       }
     }
   }
@@ -897,12 +941,12 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   {
     float* slab = slabs + cw * SS;
 #pragma unroll
-    for (int i = 0; i < NPBW; ++i)
+    for (int q = 0; q < NPBW / XR; ++q)
 #pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        const int pb = pw + i * PW;
-        *reinterpret_cast<f4*>(slab + (pb * 16 + block_pix(r)) * RS + cb * 16 + 4 * g) = acc[i * NCB + cb];
-      }
+      for (int j = 0; j < XR; ++j)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+          *reinterpret_cast<f4*>(slab + run_pix(pw + q * PW, j) * RS + cb * 16 + 4 * g) = acc[(q * XR + j) * NCB + cb];
   }
   __syncthreads();
   constexpr int C4O = COUT / 4, NOUT = (P_OUT * C4O + 255) / 256;
@@ -1153,7 +1197,7 @@ __global__ __launch_bounds__(kWideThreads) void k_stem_b1(BlockParams p) {
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx)
-        a = wk[ky * 3 + kx] * *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx + kx) * XS + 4 * g) + a;
+        a = __builtin_elementwise_fma(wk[ky * 3 + kx], *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx + kx) * XS + 4 * g), a);
     a = relu6v(a);
     const f4 b = to_operand<PREC>(a);
     f4 v = mma16_op<PREC>(f4{0.f, 0.f, 0.f, 0.f}, a2, b);
