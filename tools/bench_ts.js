@@ -42,32 +42,42 @@ async function main() {
   // throughput: calls fired ahead of their results (a window of 2 x the queue
   // depth outstanding, so resolved results are dropped as a consumer would)
   const win = 2 * s.queueDepth;
-  const t0 = process.hrtime.bigint();
-  let ps = [];
-  for (let i = 0; i < it; i++) {
-    ps.push(s.segmentFrames(frames));
-    if (ps.length === win) { await ps[0]; ps = ps.slice(1); }
+  async function copyLoop(n) {
+    const t0 = process.hrtime.bigint();
+    let ps = [];
+    for (let i = 0; i < n; i++) {
+      ps.push(s.segmentFrames(frames));
+      if (ps.length === win) { await ps[0]; ps = ps.slice(1); }
+    }
+    await Promise.all(ps);
+    return Number(process.hrtime.bigint() - t0) / 1e9;
   }
-  await Promise.all(ps);
-  const el = Number(process.hrtime.bigint() - t0) / 1e9;
   // zero-copy: frames decoded straight into leased pinned staging (the
   // synthetic decoder fills each slot's buffer once; later leases find them)
   const filled = new Set();
   const fb = h * w * 3;
-  const z0 = process.hrtime.bigint();
-  let zs = [];
   let last = null;
-  for (let i = 0; i < it; i++) {
-    if (zs.length === s.queueDepth) { last = await zs[0]; zs = zs.slice(1); }  // a slot's batch is done
-    const lease = s.acquireFrames();
-    if (!filled.has(lease.slot)) {
-      for (let k = 0; k < b; k++) lease.data.set(frames[k].data, k * fb);
-      filled.add(lease.slot);
+  async function zeroCopyLoop(n) {
+    const z0 = process.hrtime.bigint();
+    let zs = [];
+    for (let i = 0; i < n; i++) {
+      if (zs.length === s.queueDepth) { last = await zs[0]; zs = zs.slice(1); }  // a slot's batch is done
+      const lease = s.acquireFrames();
+      if (!filled.has(lease.slot)) {
+        for (let k = 0; k < b; k++) lease.data.set(frames[k].data, k * fb);
+        filled.add(lease.slot);
+      }
+      zs.push(s.segmentLease(lease, b, w, h));
     }
-    zs.push(s.segmentLease(lease, b, w, h));
+    for (const p of zs) last = await p;
+    return Number(process.hrtime.bigint() - z0) / 1e9;
   }
-  for (const p of zs) last = await p;
-  const zel = Number(process.hrtime.bigint() - z0) / 1e9;
+  // each loop runs untimed once first: the first few hundred batches of a
+  // cold pipelined loop run up to 1.5x slower (copy threads, DMA queues)
+  await copyLoop(it);
+  const el = await copyLoop(it);
+  await zeroCopyLoop(it);
+  const zel = await zeroCopyLoop(it);
   const ref = (await s.segmentFrames(frames)).masks;
   const zsame = last.masks.every((v, k) => v === ref[k]);
   console.log(JSON.stringify({ value: Math.round(b * it / el * 10) / 10, unit: 'frames/s',
