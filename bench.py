@@ -480,6 +480,7 @@ def main():
     recs, _, _ = mw.parse_blob(blob)
     costs = cm.layer_costs(recs, hm, wm, fh, fw, 3, pw_weight_bytes=2 if args.dtype == "bf16x2" else 4)
     names = [sess.layer_kernel(i) for i in range(len(ms))]
+    tile_spec = sess.tile_spec()  # VSS_TILE pinning these kernels (tools/tiles_of.py, rocprof passes)
     occ = [sess.layer_occupancy(i) for i in range(len(ms))]
     per_layer = [{"layer": i, "kind": costs[i]["kind"], "kernel": names[i], "ms": round(m, 5),
                   "GBps": round(cm.launch_bytes(costs[i], B) / (m * 1e-3) / 1e9, 1) if m > 0 else None,
@@ -568,6 +569,7 @@ def main():
                 "step_frac_at_value": round(step_bytes / B * value / world / HBM_PEAK, 4),
             },
             "kernels": per_layer,
+            "tile_spec": tile_spec,
             "layer_launches_sum_ms": round(float(sum(ms)), 5),
             "launches_per_forward": sum(1 for n in names if not n.startswith("(fused")),
             "batch_sweep": batch_sweep,

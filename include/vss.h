@@ -296,9 +296,15 @@ int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap);
 /* The output tiles compiled for `layer`'s shape (csrc/vss_registry.inc), as
  * (tile h, tile w) pairs in th[k], tw[k]; returns how many (0 for the stem
  * and the head), at most `cap` written.  Any of them can be pinned with the
- * environment variable VSS_TILE="layer:THxTW[,...]" at vss_create; results
- * do not depend on the tile (bitwise). */
+ * environment variable VSS_TILE="layer:THxTW[,...]" at vss_create, or by
+ * index, VSS_TILE="layer:#k" (a tile can be compiled as more than one kernel:
+ * b1's k_block, k_stem_b1 and k_stem_b1s); results do not depend on the tile
+ * (bitwise). */
 int vss_layer_tiles(const vss_handle* h, int layer, int* th, int* tw, int cap);
+
+/* The kernel name (as vss_layer_kernel) of candidate `idx` of vss_layer_tiles'
+ * list for `layer`.  Returns the string length, or a negative code. */
+int vss_layer_tile_kernel(const vss_handle* h, int layer, int idx, char* buf, int cap);
 
 /* Workgroups of `layer`'s kernel that fit one CU at once (registers, from
  * hipOccupancyMaxActiveBlocksPerMultiprocessor, and the layer's dynamic LDS in

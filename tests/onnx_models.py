@@ -235,7 +235,7 @@ def q4f16_like(h=64, w=96):
     return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])], opset=21)
 
 
-def modnet(h=288, w=512, hr=32, q4f16=False, seed=7):
+def modnet(h=288, w=512, hr=32, q4f16=False, seed=7, in_eps=1e-5):
     """The public MODNet topology (Ke et al., "MODNet: Real-Time Trimap-Free
     Portrait Matting via Objective Decomposition", AAAI 2022; the authors'
     src/models/modnet.py) at inference, the graph an ONNX export of the
@@ -297,7 +297,7 @@ def modnet(h=288, w=512, hr=32, q4f16=False, seed=7):
                                          b.const((rng.standard_normal(nb) * 0.1).astype(dt)),
                                          b.const((rng.random(nb) + 0.5).astype(dt))], epsilon=1e-5)
         inn = b.op("InstanceNormalization", [hi, b.const(np.ones(cout - nb, dt)), b.const(np.zeros(cout - nb, dt))],
-                   epsilon=1e-5)
+                   epsilon=in_eps)
         return b.op("Relu", [b.op("Concat", [bn, inn], axis=1)])
 
     def resize(t, s):

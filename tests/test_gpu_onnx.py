@@ -99,26 +99,34 @@ def test_conv_tile_forms(ort, precision):
     _check(got, want, f"conv_tiles {precision}")
 
 
-# MODNet's matte (a sigmoid in [0, 1]) with 16-bit convolution operands.  This
-# seeded-weight net amplifies operand rounding (its InstanceNorms divide by
-# the small spread of some channels), so two roundings of the same values —
-# the GPU's and the oracle's after a slightly different f32 / f64 history —
-# land ~as far apart as either from f32: the kernels' parity is
-# test_conv_tile_forms; here the precision's cost is measured and bounded
-# (oracle with 16-bit operands vs f32: 0.20 / 0.023 max / mean for bf16,
-# 0.036 / 0.003 for f16).
-MODNET_TOL = {"f32": TOL}
-MODNET_PRECISION_COST = {"bf16": (0.35, 0.035), "f16": (0.07, 0.006)}  # (max, mean) vs the f32 oracle
+# MODNet's matte (a sigmoid in [0, 1]) with 16-bit convolution operands.  With
+# seeded weights some IBNorm InstanceNorm channels come out nearly constant
+# over the image, and at the export's epsilon 1e-5 the norm multiplies their
+# operand rounding by up to 1/sqrt(1e-5) ~ 316: the oracle itself then moves
+# by 0.018 max (f16) / 0.09 (bf16) between f32 and rounded operands, and two
+# roundings of the same values after slightly different f32 / f64 histories
+# land as far apart.  The 16-bit cases therefore run a well-conditioned seeded
+# MODNet (in_eps = 1e-3: the same graph with those channels' gain bounded by
+# ~32), where the precision's cost is 0.0013 max (f16) — the reference's
+# q4f16 arithmetic (main.ts:6, model.ts:12-29) — and the GPU is held to 1e-2
+# of the same-rounding oracle.  bf16 (8-bit mantissa) stays a measured
+# precision cost (0.09 max vs f32 in the oracle alone), bounded and reported.
+MODNET_TOL = {"f32": TOL, "f16": 1e-2}       # vs the oracle with the same operand rounding
+MODNET_BF16_COST = (0.15, 0.02)              # (max, mean) vs the f32 oracle: bf16 rounding, not parity
+MODNET_IN_EPS = {"f32": 1e-5, "f16": 1e-3, "bf16": 1e-3}
 
 
 @pytest.fixture(scope="module")
 def modnet_cases():
     cases = {}
     x = np.random.default_rng(21).random((1, 3, 288, 512), dtype=np.float32)
-    for q4f16, prec in ((False, "bf16"), (True, "f16")):
-        data = M.modnet(q4f16=q4f16)
+    for q4f16, prec in ((False, "f32"), (True, "f32"), (False, "bf16"), (True, "f16")):
+        data = M.modnet(q4f16=q4f16, in_eps=MODNET_IN_EPS[prec])
         m = R.load(data)
-        cases[q4f16] = (data, x, {"f32": R.run(m, {"input": x}), prec: R.run(m, {"input": x}, conv_operands=prec)})
+        want = {"f32": R.run(m, {"input": x})}
+        if prec != "f32":
+            want[prec] = R.run(m, {"input": x}, conv_operands=prec)
+        cases[(q4f16, prec)] = (data, x, want)
     return cases
 
 
@@ -126,26 +134,32 @@ def modnet_cases():
 def test_modnet_topology_288x512(ort, modnet_cases, q4f16, precision):
     """The public MODNet topology at the reference's 288x512
     (onnx_models.modnet; frameProcessorTest.ts:91), f32 and q4f16 forms, on
-    k_conv_tile with f32 operands and with bf16 / f16 ones (error reported)."""
-    data, x, wants = modnet_cases[q4f16]
-    want = wants["f32"]
+    k_conv_tile with f32 operands (1e-4 of the f32 oracle), f16 operands (the
+    reference's q4f16 arithmetic: 1e-2 of the same-rounding oracle, and of the
+    f32 one) and bf16 operands (the precision's cost, bounded and reported)."""
+    data, x, wants = modnet_cases[(q4f16, precision)]
     label = f"modnet {'q4f16' if q4f16 else 'f32'} {precision}"
-    if precision != "f32":
-        for k, w in wants[precision].items():
-            e = np.abs(w - want[k])
-            print(f"{label}: oracle with {precision} operands vs f32: max {e.max():.3e} mean {e.mean():.3e}")
     with ort.InferenceSession(data, precision=precision) as s:
         got = s.run({"input": x})
         again = s.run({"input": x})
         print(label, len(s.launches()), "launches,", s.tile_convs(), "tiled convolutions")
         assert s.tile_convs() >= 12  # every 3x3 / 5x5 of >= 8 MMAC (f32), every 3x3 / 5x5 (16-bit)
-    for k, w in want.items():
+    for k, w in wants["f32"].items():
         err, mean = float(np.abs(got[k] - w).max()), float(np.abs(got[k] - w).mean())
         print(f"{label}: vs the f32 oracle max abs err {err:.3e}, mean {mean:.3e}")
         if precision == "f32":
-            assert err <= MODNET_TOL[precision], (label, err)
+            assert err <= MODNET_TOL["f32"], (label, err)
+        elif precision == "f16":
+            same = wants["f16"][k]
+            e16 = float(np.abs(got[k] - same).max())
+            print(f"{label}: vs the f16-operand oracle max abs err {e16:.3e}; oracle f16 vs f32 "
+                  f"{float(np.abs(same - w).max()):.3e}")
+            assert e16 <= MODNET_TOL["f16"] and err <= MODNET_TOL["f16"], (label, e16, err)
         else:
-            assert err <= MODNET_PRECISION_COST[precision][0] and mean <= MODNET_PRECISION_COST[precision][1], label
+            same = wants["bf16"][k]
+            print(f"{label}: vs the bf16-operand oracle max abs err {float(np.abs(got[k] - same).max()):.3e}; "
+                  f"oracle bf16 vs f32 {float(np.abs(same - w).max()):.3e}")
+            assert err <= MODNET_BF16_COST[0] and mean <= MODNET_BF16_COST[1], (label, err, mean)
         assert np.array_equal(got[k], again[k])  # split-K reduction order is fixed
 
 

@@ -155,6 +155,7 @@ def lib() -> ctypes.CDLL:
                 "vss_profile_read": ([P, ctypes.POINTER(ctypes.c_double), I, ctypes.POINTER(I)], I),
                 "vss_layer_kernel": ([P, I, ctypes.c_char_p, I], I),
                 "vss_layer_tiles": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I), I], I),
+                "vss_layer_tile_kernel": ([P, I, I, ctypes.c_char_p, I], I),
                 "vss_layer_occupancy": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I)], I),
                 "vss_post_config_default": ([ctypes.POINTER(PostConfig)], None),
                 "vss_post_create": ([P, ctypes.POINTER(PostConfig), ctypes.POINTER(P)], I),
@@ -423,6 +424,25 @@ class Session:
         if n < 0:
             _check(n, self._h)
         return [(th[k], tw[k]) for k in range(n)]
+
+    def layer_tile_kernel(self, layer: int, idx: int) -> str:
+        """The kernel of candidate `idx` of layer_tiles(layer) (pin it with VSS_TILE="layer:#idx")."""
+        buf = ctypes.create_string_buffer(256)
+        n = lib().vss_layer_tile_kernel(self._h, layer, idx, buf, 256)
+        if n < 0:
+            _check(n, self._h)
+        return buf.value.decode()
+
+    def tile_spec(self) -> str:
+        """The VSS_TILE spec ("layer:#idx,...") that pins this handle's kernels."""
+        spec = []
+        for li in range(self.n_layers):
+            want = self.layer_kernel(li)
+            for k in range(len(self.layer_tiles(li))):
+                if self.layer_tile_kernel(li, k) == want:
+                    spec.append(f"{li}:#{k}")
+                    break
+        return ",".join(spec)
 
     def layer_occupancy(self, layer: int):
         """(workgroups per CU, LDS bytes per workgroup) of `layer`'s kernel."""

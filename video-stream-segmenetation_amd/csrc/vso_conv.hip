@@ -258,7 +258,16 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
         __hip_atomic_store(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+    // Ordering: the hardware side is the vmcnt(0) drain below (every sc1 store
+    // has left the CU before the arrival is counted) and sc1 loads on the
+    // consumer side (L1 bypassed) — the measured protocol of
+    // MI355X_MICROARCH.md's hand-off table, row 1.  The compiler side is the
+    // asm's memory clobber plus the signal fences (no load or store moves
+    // across them).  An acq_rel agent-scope fetch_add instead would add a
+    // buffer_wbl2 + buffer_inv per workgroup (~3.5 us each, measured 2x slower
+    // for the whole layer in round 1).
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __shared__ int last;
     __syncthreads();
     if (tid == 0) {
@@ -269,6 +278,7 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
     }
     __syncthreads();
     if (!last) return;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     const uint64_t* base = reinterpret_cast<const uint64_t*>(p.part) + blk * p.ksplit * (MI * PBW * 256 * 2);
 #pragma unroll
     for (int i = 0; i < MI; ++i)

@@ -423,7 +423,8 @@ int ks_max(const LayerPlan& l) {
 
 // LDS bytes of one workgroup of compiled shape e for layer l.
 size_t entry_lds_bytes(const LayerPlan& l, const BlockEntry& e) {
-  if (e.threads == kWideThreads) return (size_t)stem_b1_lds(e.TH, e.TW).total * 4;
+  if (e.variant == VAR_STEM_B1_WIDE) return (size_t)stem_b1_lds(e.TH, e.TW).total * 4;
+  if (e.variant == VAR_STEM_B1_STREAM) return (size_t)stem_b1s_lds(e.TW, e.sb).total * 4;
   return block_lds_bytes(l, e.TH, e.TW);
 }
 
@@ -450,7 +451,7 @@ int choose_tile(vss_handle* h, LayerPlan& l, int N) {
     if (e.mode != l.mode || e.stride != l.stride || e.cin != (int)l.rec.cin || e.cskip != cskip ||
         e.chid != l.chid / l.ks || e.cout != l.C || e.flags != l.flags)
       continue;
-    if (e.threads != kThreads) continue;  // the wide kernels are candidates of the autotuner only
+    if (e.variant != VAR_BLOCK) continue;  // the stem + b1 kernels are candidates of the autotuner only
     const long blocks = (long)((l.H + e.TH - 1) / e.TH) * ((l.W + e.TW - 1) / e.TW) * N;
     const size_t lds = entry_lds_bytes(l, e);
     // score: enough blocks first, then bigger tiles, then less LDS
@@ -1573,14 +1574,25 @@ int force_tiles(vss_handle* h, const char* spec) {
   const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
   const char* s = spec;
   while (*s) {
-    int layer = -1, th = 0, tw = 0, used = 0;
-    if (std::sscanf(s, "%d:%dx%d%n", &layer, &th, &tw, &used) != 3 || layer < 0 || layer >= (int)h->L.size())
+    // "layer:THxTW" (the first compiled shape with that tile) or "layer:#k"
+    // (candidate k of vss_layer_tiles' list: tiles can repeat across variants)
+    int layer = -1, th = 0, tw = 0, idx = -1, used = 0;
+    if (std::sscanf(s, "%d:#%d%n", &layer, &idx, &used) != 2 &&
+        std::sscanf(s, "%d:%dx%d%n", &layer, &th, &tw, &used) != 3)
       return fail(h, VSS_E_INVALID_ARG, std::string("VSS_TILE: bad entry in '") + spec + "'");
+    if (layer < 0 || layer >= (int)h->L.size())
+      return fail(h, VSS_E_INVALID_ARG, std::string("VSS_TILE: bad layer in '") + spec + "'");
     LayerPlan& l = h->L[layer];
     const BlockEntry* pick = nullptr;
-    if (l.mode >= 0)
-      for (const BlockEntry* e : tile_candidates(l))
-        if (e->TH == th && e->TW == tw) pick = e;
+    if (l.mode >= 0) {
+      const std::vector<const BlockEntry*> c = tile_candidates(l);
+      if (idx >= 0) {
+        if (idx < (int)c.size()) pick = c[idx];
+      } else {
+        for (const BlockEntry* e : c)
+          if (!pick && e->TH == th && e->TW == tw) pick = e;
+      }
+    }
     if (!pick)
       return fail(h, VSS_E_UNSUPPORTED, "VSS_TILE: layer " + std::to_string(layer) + " has no compiled " +
                                             std::to_string(th) + "x" + std::to_string(tw) + " tile");
@@ -2203,22 +2215,42 @@ int vss_layer_tiles(const vss_handle* h, int layer, int* th, int* tw, int cap) {
   return std::min(n, cap);
 }
 
+// The demangled kernel name of layer l run as compiled shape e (rocprofv3's spelling).
+static void entry_name(const vss_handle* h, const LayerPlan& l, int layer, const BlockEntry* e, char* tmp, size_t cap_) {
+  const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
+  if (l.fused) std::snprintf(tmp, cap_, "(fused into layer %d)", layer + 1);
+  else if (l.rec.kind == K_STEM) std::snprintf(tmp, cap_, "void vss::k_stem<16>(vss::StemParams)");
+  else if (l.rec.kind == K_HEAD) std::snprintf(tmp, cap_, "void vss::k_head<16>(vss::HeadParams)");
+  else {
+    if (e->variant == VAR_STEM_B1_WIDE)
+      std::snprintf(tmp, cap_, "void vss::k_stem_b1<%d, %d, %d>(vss::BlockParams)", e->TH, e->TW, prec);
+    else if (e->variant == VAR_STEM_B1_STREAM)
+      std::snprintf(tmp, cap_, "void vss::k_stem_b1s<%d, %d, %d, %d, %d>(vss::BlockParams)", e->TW, e->sb,
+                    e->TH / e->sb, e->threads, prec);
+    else
+      std::snprintf(tmp, cap_, "void vss::k_block<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>(vss::BlockParams)",
+                    e->mode, e->stride, e->TH, e->TW, e->cin, e->cskip, e->chid, e->cout, e->flags, prec);
+  }
+}
+
 int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap) {
   if (!h || layer < 0 || layer >= (int)h->L.size() || !buf || cap < 1) return VSS_E_INVALID_ARG;
   const LayerPlan& l = h->L[layer];
-  const int prec = h->cfg.dtype == VSS_DTYPE_F32 ? PREC_F32 : PREC_BF16X2;
   char tmp[160];
-  if (l.fused) std::snprintf(tmp, sizeof(tmp), "(fused into layer %d)", layer + 1);
-  else if (l.rec.kind == K_STEM) std::snprintf(tmp, sizeof(tmp), "void vss::k_stem<16>(vss::StemParams)");
-  else if (l.rec.kind == K_HEAD) std::snprintf(tmp, sizeof(tmp), "void vss::k_head<16>(vss::HeadParams)");
-  else {
-    const BlockEntry* e = l.entry;
-    if (e->threads == kWideThreads)
-      std::snprintf(tmp, sizeof(tmp), "void vss::k_stem_b1<%d, %d, %d>(vss::BlockParams)", e->TH, e->TW, prec);
-    else
-      std::snprintf(tmp, sizeof(tmp), "void vss::k_block<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>(vss::BlockParams)",
-                    e->mode, e->stride, e->TH, e->TW, e->cin, e->cskip, e->chid, e->cout, e->flags, prec);
-  }
+  entry_name(h, l, layer, l.entry, tmp, sizeof(tmp));
+  const int len = (int)std::strlen(tmp);
+  std::snprintf(buf, (size_t)cap, "%s", tmp);
+  return len;
+}
+
+int vss_layer_tile_kernel(const vss_handle* h, int layer, int idx, char* buf, int cap) {
+  if (!h || layer < 0 || layer >= (int)h->L.size() || !buf || cap < 1) return VSS_E_INVALID_ARG;
+  const LayerPlan& l = h->L[layer];
+  if (l.mode < 0) return VSS_E_INVALID_ARG;
+  const std::vector<const BlockEntry*> c = tile_candidates(l);
+  if (idx < 0 || idx >= (int)c.size()) return VSS_E_INVALID_ARG;
+  char tmp[160];
+  entry_name(h, l, layer, c[idx], tmp, sizeof(tmp));
   const int len = (int)std::strlen(tmp);
   std::snprintf(buf, (size_t)cap, "%s", tmp);
   return len;

@@ -1213,6 +1213,204 @@ __global__ __launch_bounds__(kWideThreads) void k_stem_b1(BlockParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// b1 with the stem fused, streamed down a column strip (stem_b1s_lds in
+// vss_kernels.h).  Workgroup (bx, by, n) owns b1 columns [TW*bx, TW*bx + TW)
+// and rows [y0, y0 + SB*NSTEP), y0 = SB*NSTEP*by, and walks down them SB rows
+// per step:
+//   pre-step : resized rows 2*y0-3 .. 2*y0+1 -> X[1], stem rows y0-1, y0 -> S[0]
+//   step k   : (b1 rows yk .. yk+SB-1, yk = y0 + k*SB)
+//     lerp   : the 2*SB new resized rows 2*yk+2 .. 2*yk+2*SB+1 -> X[k&1] rows
+//              1..2*SB (row 0 = 2*yk+1, carried from the previous step)
+//     issue  : step k+1's frame gathers (in flight during the rest of step k)
+//     stem   : the SB new stem rows yk+1 .. yk+SB -> S[k&1] rows 2..SB+1
+//              (rows 0, 1 = yk-1, yk carried)
+//     b1     : dw 3x3 over S[k&1] -> relu6 -> project -> + bias -> + residual
+// The rows a step hands to the next are written to both buffers by their
+// producer (no copies), and the buffers alternate, so two workgroup barriers
+// per step order everything.  Against k_block's 4 x 16 tile (the autotuner's
+// pick) the resized pixels are computed ~1.35x instead of 1.88x per output and
+// the stem outputs ~1.25x instead of 1.69x, and the gathers overlap compute
+// instead of every workgroup of the single round waiting for its loads at the
+// same moment.  The arithmetic per output is block_body<MODE_IR_DIRECT, ...,
+// STEM_IN | residual>'s, operation for operation (prep_* of the resize,
+// stem_mfma, ky-major dw taps, relu6, to_operand, one project MFMA, + bias, +
+// residual): bitwise the same activations (test_stem_fusion_bitwise,
+// test_results_independent_of_tiling).
+template <int TW, int SB, int NSTEP, int WT, int PREC>
+__global__ __launch_bounds__(WT) void k_stem_b1s(BlockParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr StemB1sLds S = stem_b1s_lds(TW, SB);
+  constexpr int IW = S.IW, XW = S.XW, XWP = S.XWP, XPL = S.XPL, SXS = S.SXS, NWAVE = WT / 64;
+  constexpr BlockLds B = block_lds(MODE_IR_DIRECT, 1, 1, 16, 16, 0, 16, 16, 1);
+  constexpr int WIMG4 = (B.wimg_end - B.w1) / 4;
+  constexpr int NPRE = 5 * XW, NSTP = 2 * SB * XW;
+  constexpr int NXP = (NPRE + WT - 1) / WT, NX = (NSTP + WT - 1) / WT;
+  static_assert(SB >= 2, "two stem rows carry over to the next step");
+  static_assert((SB * TW) % 16 == 0 && WT % 64 == 0, "b1 pixel blocks");
+  static_assert(WIMG4 <= WT, "one weight-image element per thread");
+  constexpr int NSW = (27 * 16 + WT - 1) / WT;  // stem weights per thread
+  const TileIdx tl = xcd_tile();
+  const int bx = tl.x, by = tl.y, n = tl.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const StemParams& sp = p.stem;
+  const int H = p.H, W = p.W, Hm = sp.Hm, Wm = sp.Wm;  // the stem's output = b1's input
+  const int ox0 = bx * TW, y0 = by * (SB * NSTEP);
+  const int c0 = 2 * ox0 - 3;  // resized column of X column 0
+  const uint8_t* fr = sp.frames + (long)n * sp.frame_stride;
+  float* xbuf[2] = {smem + S.x[0], smem + S.x[1]};
+  float* sbuf[2] = {smem + S.s[0], smem + S.s[1]};
+  float* sws = smem + S.sw;
+  float* sbs = smem + S.sb;
+  float* wim = smem + S.wim;
+
+  // item i of a block of resized rows starting at row0: its taps' loads
+  auto gather = [&](int i, int row0, uint32_t v[12], float& dy, float& dx) {
+    const int ly = i / XW, lx = i - ly * XW;
+    const int yy = min(max(row0 + ly, 0), Hm - 1), xx = min(max(c0 + lx, 0), Wm - 1);
+    const PrepTap t = prep_tap(fr, sp.row_stride, sp.fc, sp.fh, sp.fw, sp.ry, sp.rx, yy, xx);
+    prep_load(t, v);
+    dy = t.dy;
+    dx = t.dx;
+  };
+  // the finished item -> X buffer xb at row brow0 + ly (zero outside the
+  // image); the block's last row also to row 0 of the other buffer (carry)
+  auto put_x = [&](int i, int row0, const float o[3], float* xb, int brow0, int carry_ly, float* xc) {
+    const int ly = i / XW, lx = i - ly * XW;
+    const int yy = row0 + ly, xx = c0 + lx;
+    const bool valid = yy >= 0 && yy < Hm && xx >= 0 && xx < Wm;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = valid ? o[c] : 0.f;
+      xb[c * XPL + (brow0 + ly) * XWP + lx] = v;
+      if (ly == carry_ly) xc[c * XPL + lx] = v;
+    }
+  };
+
+  // ---- every load of the pre-step and step 0 issued first ----
+  const f4 wv = reinterpret_cast<const f4*>(p.wimg)[min(tid, WIMG4 - 1)];
+  float swr[NSW];
+#pragma unroll
+  for (int u = 0; u < NSW; ++u) swr[u] = sp.w[min(tid + WT * u, 27 * 16 - 1)];
+  const float sbv = sp.b[min(tid, 15)];
+  uint32_t rp[NXP][12];
+  float dyp[NXP], dxp[NXP];
+#pragma unroll
+  for (int u = 0; u < NXP; ++u) gather(min(tid + WT * u, NPRE - 1), 2 * y0 - 3, rp[u], dyp[u], dxp[u]);
+  uint32_t rs[NX][12];
+  float dys[NX], dxs[NX];
+#pragma unroll
+  for (int u = 0; u < NX; ++u) gather(min(tid + WT * u, NSTP - 1), 2 * y0 + 2, rs[u], dys[u], dxs[u]);
+  // start of the forward: zero this frame's decoder norm accumulators (the stem's job)
+  if (bx == 0 && by == 0)
+    for (int i = tid; i < sp.acc_stride; i += WT) sp.acc_zero[(long)n * sp.acc_stride + i] = 0ull;
+  if (tid < WIMG4) reinterpret_cast<f4*>(wim)[tid] = wv;
+#pragma unroll
+  for (int u = 0; u < NSW; ++u) {
+    const int i = tid + WT * u;  // sp.w is [c][27]
+    if (i < 27 * 16) sws[(i % 27) * 16 + i / 27] = swr[u];
+  }
+  if (tid < 16) sbs[tid] = sbv;
+  // ---- pre-step: resized rows 2*y0-3 .. 2*y0+1 -> X[1] rows 0..4 (row 4 carried to X[0]) ----
+  {
+    float o[NXP][3];
+#pragma unroll
+    for (int u = 0; u < NXP; u += 2) {
+      if (u + 1 < NXP) prep_finish2(rp[u], rp[u + 1], dyp[u], dxp[u], dyp[u + 1], dxp[u + 1], o[u], o[u + 1]);
+      else prep_finish(rp[u], dyp[u], dxp[u], o[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < NXP; ++u)
+      if (tid + WT * u < NPRE) put_x(tid + WT * u, 2 * y0 - 3, o[u], xbuf[1], 0, 4, xbuf[0]);
+  }
+  __syncthreads();
+  const StemTaps taps = stem_taps(sws, r, g, XPL, XWP);
+  const float sbias = sbs[r];
+  // stem rows s0 .. s0+nrows-1 of the X buffer xb (row 2i-th resized row at
+  // buffer row 2i), 16-pixel blocks on the MFMA, zero outside the stem image
+  auto stem_rows = [&](const float* xb, int nrows, int s0, auto&& put) {
+    const int npix = nrows * IW;
+    for (int blk = wave; blk < (npix + 15) / 16; blk += NWAVE) {
+      const int pa = min(blk * 16 + r, npix - 1), i = pa / IW, px = pa - i * IW;
+      const f4 acc = stem_mfma(taps, xb + 2 * i * XWP + 2 * px, sbias);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // D[pixel 4g+q][channel r]
+        const int pp = blk * 16 + 4 * g + q;
+        if (pp < npix) {
+          const int ii = pp / IW, px2 = pp - ii * IW;
+          const int sy = s0 + ii, sx = ox0 - 1 + px2;
+          const bool valid = sy >= 0 && sy < H && sx >= 0 && sx < W;
+          put(ii, px2, valid ? relu6f(acc[q]) : 0.f);
+        }
+      }
+    }
+  };
+  stem_rows(xbuf[1], 2, y0 - 1, [&](int ii, int px, float v) { sbuf[0][(ii * IW + px) * SXS + r] = v; });
+  // b1's weights, in registers for every step
+  const uint16_t* w2s = reinterpret_cast<const uint16_t*>(wim + (B.w2 - B.w1));
+  const float* wdws = wim + (B.wdw - B.w1);
+  f4 wk[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wk[t] = *reinterpret_cast<const f4*>(wdws + t * 16 + 4 * g);
+  const f4 bb = *reinterpret_cast<const f4*>(wim + (B.bdw - B.w1) + 4 * g);
+  const typename AFrag<PREC>::T a2 = lds_a<PREC>(w2s, B.LD2, r, 4 * g);
+  const f4 bias2 = *reinterpret_cast<const f4*>(wim + (B.b2 - B.w1) + 4 * g);
+  const int Ho = p.Ho, Wo = p.Wo;
+  float* yn = p.y + (long)n * Ho * Wo * 16;
+  float* stn = sp.y ? sp.y + (long)n * H * W * 16 : nullptr;  // VSS_OPT_KEEP_STEM
+  __syncthreads();  // the pre-step's stem read X[1] before step 0 writes its row 0
+
+  for (int k = 0; k < NSTEP; ++k) {
+    const int yk = y0 + k * SB;
+    if (yk >= H) break;  // uniform: the last segment of a frame may be short
+    float* xb = xbuf[k & 1];
+    float* sb_ = sbuf[k & 1];
+    float* sn = sbuf[(k + 1) & 1];
+    {
+      float o[NX][3];
+#pragma unroll
+      for (int u = 0; u < NX; u += 2) {
+        if (u + 1 < NX) prep_finish2(rs[u], rs[u + 1], dys[u], dxs[u], dys[u + 1], dxs[u + 1], o[u], o[u + 1]);
+        else prep_finish(rs[u], dys[u], dxs[u], o[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < NX; ++u)
+        if (tid + WT * u < NSTP) put_x(tid + WT * u, 2 * yk + 2, o[u], xb, 1, 2 * SB - 1, xbuf[(k + 1) & 1]);
+    }
+    if (k + 1 < NSTEP && yk + SB < H) {  // the next step's gathers, in flight from here
+#pragma unroll
+      for (int u = 0; u < NX; ++u) gather(min(tid + WT * u, NSTP - 1), 2 * (yk + SB) + 2, rs[u], dys[u], dxs[u]);
+    }
+    __syncthreads();
+    stem_rows(xb, SB, yk + 1, [&](int ii, int px, float v) {
+      sb_[((2 + ii) * IW + px) * SXS + r] = v;
+      if (ii >= SB - 2) sn[((ii - (SB - 2)) * IW + px) * SXS + r] = v;
+    });
+    __syncthreads();
+    // b1 rows yk .. yk+SB-1: lane (r, g) = pixel r of the wave's block, channels 4g..4g+3
+    for (int blk = wave; blk < SB * TW / 16; blk += NWAVE) {
+      const int pix = blk * 16 + r, j = pix / TW, lx = pix % TW;
+      f4 a = bb;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+          a = __builtin_elementwise_fma(wk[ky * 3 + kx], *reinterpret_cast<const f4*>(sb_ + ((j + ky) * IW + lx + kx) * SXS + 4 * g), a);
+      a = relu6v(a);
+      const f4 b = to_operand<PREC>(a);
+      f4 v = mma16_op<PREC>(f4{0.f, 0.f, 0.f, 0.f}, a2, b);
+      const f4 centre = *reinterpret_cast<const f4*>(sb_ + ((j + 1) * IW + lx + 1) * SXS + 4 * g);
+      v = v + bias2;
+      v = v + centre;
+      const int oy = yk + j, ox = ox0 + lx;
+      if (oy < Ho && ox < Wo) {
+        *reinterpret_cast<f4*>(yn + ((long)oy * Wo + ox) * 16 + 4 * g) = v;
+        if (stn) *reinterpret_cast<f4*>(stn + ((long)oy * W + ox) * 16 + 4 * g) = centre;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Head: mask tile 16 x 64; logits over the (10 x 34) low-res region in LDS.
 template <int C, bool COH>
 __device__ __forceinline__ void head_body(const HeadParams& p, int bx, int by, int n, float* smem) {
@@ -1338,10 +1536,19 @@ const BlockEntry* VSS_CAT(registry_shard_, VSS_SHARD)(int* count) {
 
 // The wide stem + b1 kernel's tiles (k_stem_b1): 16 -> 16 direct, stride 1,
 // residual, STEM_IN (block_flags(0, 1, 1, 1, 1, 1) = 258).
-#define VSS_STEM_B1(TH, TW) \
-  {1, 1, TH, TW, 16, 0, 16, 16, 258, {k_stem_b1<TH, TW, PREC_F32>, k_stem_b1<TH, TW, PREC_BF16X2>}, kWideThreads},
-static const BlockEntry kStemB1Blocks[] = {VSS_STEM_B1(8, 32) VSS_STEM_B1(4, 64) VSS_STEM_B1(8, 64)};
+#define VSS_STEM_B1(TH, TW)                                                                              \
+  {1, 1, TH, TW, 16, 0, 16, 16, 258, {k_stem_b1<TH, TW, PREC_F32>, k_stem_b1<TH, TW, PREC_BF16X2>}, kWideThreads, \
+   VAR_STEM_B1_WIDE, 0},
+// the streamed kernel (k_stem_b1s): TW columns, SB rows per step, NSTEP steps, WT threads
+#define VSS_STEM_B1S(TW, SB, NSTEP, WT)                                                                        \
+  {1, 1, SB * NSTEP, TW, 16, 0, 16, 16, 258,                                                                   \
+   {k_stem_b1s<TW, SB, NSTEP, WT, PREC_F32>, k_stem_b1s<TW, SB, NSTEP, WT, PREC_BF16X2>}, WT, VAR_STEM_B1_STREAM, SB},
+static const BlockEntry kStemB1Blocks[] = {
+    VSS_STEM_B1(8, 32) VSS_STEM_B1(4, 64) VSS_STEM_B1(8, 64)
+    VSS_STEM_B1S(32, 3, 3, 512) VSS_STEM_B1S(16, 3, 3, 256) VSS_STEM_B1S(32, 4, 2, 512) VSS_STEM_B1S(16, 4, 2, 256)
+    VSS_STEM_B1S(16, 2, 4, 256) VSS_STEM_B1S(32, 2, 3, 256)};
 #undef VSS_STEM_B1
+#undef VSS_STEM_B1S
 
 const BlockEntry* block_registry(int* count) {
   static const std::vector<BlockEntry> all = [] {
