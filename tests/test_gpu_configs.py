@@ -76,22 +76,6 @@ def test_config5_1080p_pipelined(pkg, oracle, blob, synthetic, torch_cuda):
         assert np.array_equal(outs[0], sync) and np.array_equal(outs[1], ref_g) and np.array_equal(outs[2], sync)
 
 
-def test_config5_whole_batch_64x1080p(pkg, oracle, blob, synthetic, torch_cuda):
-    """Config 5's whole batch (64 x 1920x1080, what 8 GPUs share) as ONE queued
-    host batch on one GPU (vss_submit: pinned staging, row fetch, forward, D2H)
-    against the oracle, and bitwise against the device path."""
-    torch = torch_cuda
-    f = _frames(synthetic, 64, 1080, 1920, start=800)
-    with pkg.Session(dtype="bf16x2", max_batch=64, max_frame_h=1080, max_frame_w=1920, queue_depth=2) as s:
-        m = s.wait(s.submit(f))[0]
-        _check(m, f, oracle, blob, what="config 5 (64 x 1080p, one batch)")
-        d = torch.from_numpy(f).cuda()
-        dev = torch.empty((64, 144 * 256), dtype=torch.float32, device="cuda")
-        s.segment_device(d.data_ptr(), 64, 1080, 1920, 3, 1920 * 3, 1080 * 1920 * 3, dev.data_ptr(), 0)
-        s.synchronize()
-        assert np.array_equal(m.reshape(64, -1), dev.cpu().numpy())
-
-
 @pytest.mark.parametrize("dtype", ["f32", "bf16x2"])
 def test_odd_model_resolution(pkg, oracle, blob, synthetic, torch_cuda, dtype):
     f = _frames(synthetic, 2, 480, 640, start=700)
