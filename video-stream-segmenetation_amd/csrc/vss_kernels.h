@@ -321,8 +321,37 @@ __host__ __device__ constexpr StemB1sLds stem_b1s_lds(int TW, int SB) {
   return L;
 }
 
+// A decoder block streamed down a column strip (k_dec_s): the workgroup owns
+// TW output columns and SB * NSTEP rows and walks down them SB rows per step.
+// The concat rows (2x upsample of relu(IN(src)) ++ skip) live in a ring of
+// R = 2*SB + 2 rows, so a step's new rows never overwrite the rows the
+// previous step's depthwise pass still reads, and each concat row is built
+// once per strip segment.  LDS carve in floats: ring [R][IW][XS], the step's
+// low-res src rows [SRS][SC][cin], the src norm scale / shift, the weight
+// image, the norm-statistics accumulators (int64 [2][cout]).
+struct DecSLds {
+  int IW, R, XS, SRS, SC, ring, lr, nrm, wim, stat, total;
+};
+__host__ __device__ constexpr DecSLds dec_s_lds(int TW, int SB, int cin, int cskip, int cout) {
+  DecSLds L{};
+  L.IW = TW + 2;
+  L.R = 2 * SB + 2;
+  L.XS = cin + cskip + VSS_XS_PAD;
+  L.SRS = SB / 2 + 2;
+  L.SC = (TW + 1) / 2 + 3;
+  int o = 0;
+  L.ring = o; o += r4(cmax(L.R * L.IW * L.XS, kAccSlots * 2 * cin * 2));  // also the prologue's norm slots
+  L.lr = o;   o += r4(L.SRS * L.SC * cin);
+  L.nrm = o;  o += r4(2 * cin);
+  const BlockLds B = block_lds(2 /*MODE_DEC*/, 1, 1, 16, cin, cskip, cin + cskip, cout);
+  L.wim = o;  o += B.wimg_end - B.w1;
+  L.stat = o; o += 4 * cout;
+  L.total = o;
+  return L;
+}
+
 // BlockEntry::variant
-enum BlockVariant : int { VAR_BLOCK = 0, VAR_STEM_B1_WIDE = 1, VAR_STEM_B1_STREAM = 2 };
+enum BlockVariant : int { VAR_BLOCK = 0, VAR_STEM_B1_WIDE = 1, VAR_STEM_B1_STREAM = 2, VAR_DEC_STREAM = 3 };
 
 const BlockEntry* block_registry(int* count);
 

@@ -1411,6 +1411,280 @@ __global__ __launch_bounds__(WT) void k_stem_b1s(BlockParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// A decoder block streamed down a column strip (dec_s_lds in vss_kernels.h).
+// Workgroup (bx, by, n) owns output columns [TW*bx, TW*bx + TW) and rows
+// [y0, y0 + SB*NSTEP) and walks down them SB rows per step:
+//   pre-step : concat rows y0-1, y0 -> ring
+//   step k   : (output rows yk .. yk+SB-1)
+//     commit : this step's low-res src rows (XP parts summed, then the src's
+//              instance norm + ReLU) -> lr; the skip rows of concat rows
+//              yk+1 .. yk+SB -> their ring rows
+//     issue  : the next step's src and skip loads (in flight from here)
+//     build  : the 2x upsample of lr -> the same ring rows' first cin channels
+//     dw     : each wave one 16-pixel block at a time: every 16-channel chunk's
+//              dw 3x3 (VALU) -> project (MFMA) into the chunk group's
+//              accumulator, the groups summed in order, + bias -> store; the
+//              block's fixed-point norm terms summed in the lane
+//   end      : the workgroup's norm sums -> one of the frame's kAccSlots
+// Two barriers per step; the ring of 2*SB + 2 rows keeps a step's writes off
+// the rows the previous step's dw pass still reads.  Against k_block's tile
+// the concat rows (upsample + skip) are built ~1.1x instead of ~1.5x per
+// output, the src norm, the weight image and the norm atomics once per strip
+// segment instead of once per tile, and the next step's loads overlap this
+// step's work.  The arithmetic per output is block_body<MODE_DEC, ...>'s
+// operation for operation (the same upsample FMAs, ky-major dw taps, chunk
+// groups CS summed in group order, + bias; integer norm sums, order-free):
+// bitwise the same activations for any tile (test_every_compiled_tile_bitwise).
+template <int CIN, int CSKIP, int COUT, int FLAGS, int TW, int SB, int NSTEP, int PREC>
+__global__ __launch_bounds__(256) void k_dec_s(BlockParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int CH = CIN + CSKIP;
+  constexpr DecSLds D = dec_s_lds(TW, SB, CIN, CSKIP, COUT);
+  constexpr BlockLds B = block_lds(MODE_DEC, 1, 1, 16, CIN, CSKIP, CH, COUT);
+  constexpr int IW = D.IW, R = D.R, XS = D.XS, SRS = D.SRS, SC = D.SC;
+  constexpr bool NORM_IN = (FLAGS & 1) != 0;
+  constexpr int XP = flags_xp(FLAGS), SP = flags_sp(FLAGS);
+  constexpr int NCHUNK = CH / 16, CS = NCHUNK >= 4 ? 4 : (NCHUNK >= 2 ? 2 : 1), NCB = COUT / 16;
+  constexpr int C4L = CIN / 4, C4S = CSKIP / 4;
+  constexpr int NLR = SRS * SC * C4L;  // src items (16 B) of a step, per part
+  constexpr int NSK = SB * IW * C4S;   // skip items of a step, per part
+  constexpr int NSK0 = 2 * IW * C4S;   // skip items of the pre-step
+  constexpr int NBLK = SB * TW / 16;   // output pixel blocks of a step
+  constexpr int WIMG4 = (B.wimg_end - B.w1) / 4;
+  static_assert(CIN % 16 == 0 && CSKIP % 16 == 0 && COUT % 16 == 0 && (SB * TW) % 16 == 0 && SB >= 2, "shape");
+  static_assert(SRS * SC * CIN < 65536, "lr offsets");
+  const TileIdx tl = xcd_tile();
+  const int bx = tl.x, by = tl.y, n = tl.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int h = p.H, w = p.W, Ho = p.Ho, Wo = p.Wo;  // src (low-res) and output dims
+  const int ox0 = bx * TW, y0 = by * (SB * NSTEP);
+  const int sx0 = max(0, (ox0 - 1) / 2 - 1);
+  float* ring = smem + D.ring;
+  float* lr = smem + D.lr;
+  float* nrm = smem + D.nrm;
+  float* wim = smem + D.wim;
+  unsigned long long* stat = reinterpret_cast<unsigned long long*>(smem + D.stat);
+  const float* xn = p.x + (long)n * h * w * CIN;
+  const float* sn = p.skip + (long)n * Ho * Wo * CSKIP;
+  auto pos = [&](int yy) { return (yy - y0 + 1) % R; };     // ring row of concat row yy (>= y0 - 1)
+  auto src_base = [&](int a) { return a > 0 ? (a - 1) >> 1 : 0; };  // first src row of concat rows a..
+
+  // loads of one step (concat rows a ..): src rows src_base(a) .. + SRS, skip rows a .. + rows
+  auto issue_lr = [&](Staged<NLR>(&st)[XP], int a) {
+    const int sb = src_base(a);
+#pragma unroll
+    for (int q = 0; q < XP; ++q) {
+      const float* gx = xn + q * p.x_part_stride;
+      st[q].issue([&](int i) {
+        const int pr = i / C4L, c4 = i % C4L;
+        const int yy = min(h - 1, sb + pr / SC), xx = min(w - 1, sx0 + pr % SC);
+        return *reinterpret_cast<const f4*>(gx + ((long)yy * w + xx) * CIN + 4 * c4);
+      });
+    }
+  };
+  auto issue_sk = [&](auto& st, int a) {
+#pragma unroll
+    for (int q = 0; q < SP; ++q) {
+      const float* gs = sn + q * p.skip_part_stride;
+      st[q].issue([&](int i) {
+        const int pix = i / C4S, c4 = i % C4S;
+        const int yy = min(max(a + pix / IW, 0), Ho - 1), xx = min(max(ox0 - 1 + pix % IW, 0), Wo - 1);
+        return *reinterpret_cast<const f4*>(gs + ((long)yy * Wo + xx) * CSKIP + 4 * c4);
+      });
+    }
+  };
+  auto commit_lr = [&](const Staged<NLR>(&st)[XP]) {
+    commit_sum(st, [&](int i, f4 v) {
+      if constexpr (NORM_IN) {
+        const int c4 = i % C4L;
+        v = reluv(__builtin_elementwise_fma(v, *reinterpret_cast<const f4*>(nrm + 4 * c4),
+                                            *reinterpret_cast<const f4*>(nrm + CIN + 4 * c4)));
+      }
+      reinterpret_cast<f4*>(lr)[i] = v;
+    });
+  };
+  auto commit_sk = [&](const auto& st, int a) {
+    commit_sum(st, [&](int i, f4 v) {
+      const int pix = i / C4S, c4 = i % C4S;
+      const int yy = a + pix / IW, px = pix % IW, xx = ox0 - 1 + px;
+      const bool valid = yy >= 0 && yy < Ho && xx >= 0 && xx < Wo;
+      *reinterpret_cast<f4*>(ring + (pos(yy) * IW + px) * XS + CIN + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+    });
+  };
+  // the upsampled channels of concat rows a .. a+nrows-1 from lr (PyTorch
+  // upsample_bilinear2d, scale 2, align_corners=False), block_body's taps and FMAs
+  auto build = [&](int a, int nrows) {
+    const int sb = src_base(a);
+    for (int i = tid; i < nrows * IW * C4L; i += 256) {
+      const int pix = i / C4L, c4 = i % C4L;
+      const int yy = a + pix / IW, px = pix % IW, xx = ox0 - 1 + px;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (yy >= 0 && yy < Ho && xx >= 0 && xx < Wo) {
+        const int ys = yy > 0 ? (yy - 1) >> 1 : 0, ys1 = ys + (ys < h - 1 ? 1 : 0);
+        const float ly1 = yy > 0 ? ((yy & 1) ? 0.25f : 0.75f) : 0.f;
+        const int xs = xx > 0 ? (xx - 1) >> 1 : 0, xs1 = xs + (xs < w - 1 ? 1 : 0);
+        const float lx1 = xx > 0 ? ((xx & 1) ? 0.25f : 0.75f) : 0.f;
+        const int r0 = min(max(ys - sb, 0), SRS - 1), r1 = min(max(ys1 - sb, 0), SRS - 1);
+        const int q0 = min(max(xs - sx0, 0), SC - 1), q1 = min(max(xs1 - sx0, 0), SC - 1);
+        const f4 t00 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q0) * CIN + 4 * c4);
+        const f4 t01 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q1) * CIN + 4 * c4);
+        const f4 t10 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q0) * CIN + 4 * c4);
+        const f4 t11 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q1) * CIN + 4 * c4);
+        const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+        const f4 lx0v = {lx0, lx0, lx0, lx0}, lx1v = {lx1, lx1, lx1, lx1};
+        const f4 ly0v = {ly0, ly0, ly0, ly0}, ly1v = {ly1, ly1, ly1, ly1};
+        const f4 top = __builtin_elementwise_fma(lx1v, t01, lx0v * t00);
+        const f4 bot = __builtin_elementwise_fma(lx1v, t11, lx0v * t10);
+        v = __builtin_elementwise_fma(ly1v, bot, ly0v * top);
+      }
+      *reinterpret_cast<f4*>(ring + (pos(yy) * IW + px) * XS + 4 * c4) = v;
+    }
+  };
+
+  // ---- prologue: every load of the weights, the src norm, the pre-step and step 0 ----
+  Staged<WIMG4> st_w;
+  st_w.issue([&](int i) { return reinterpret_cast<const f4*>(p.wimg)[i]; });
+  constexpr int NSLOT16 = NORM_IN ? kAccSlots * 2 * CIN / 2 : 0;
+  Staged<NSLOT16> st_slots;
+  if constexpr (NORM_IN)
+    st_slots.issue([&](int i) { return reinterpret_cast<const f4*>(p.in_acc + (long)n * p.acc_stride)[i]; });
+  Staged<NLR> pre_lr[XP];
+  Staged<NSK0> pre_sk[SP];
+  issue_lr(pre_lr, y0 - 1);
+  issue_sk(pre_sk, y0 - 1);
+  Staged<NLR> st_lr[XP];
+  Staged<NSK> st_sk[SP];
+  issue_lr(st_lr, y0 + 1);
+  issue_sk(st_sk, y0 + 1);
+  if (tid < 2 * COUT) stat[tid] = 0ull;
+  if constexpr (NORM_IN) {
+    const float gam = p.in_gamma[min(tid, CIN - 1)], bet = p.in_beta[min(tid, CIN - 1)];
+    st_slots.commit([&](int i, f4 v) { reinterpret_cast<f4*>(ring)[i] = v; });
+    __syncthreads();
+    const unsigned long long* sl = reinterpret_cast<const unsigned long long*>(ring);
+    if (tid < CIN) {
+      unsigned long long s_fx = 0, q_fx = 0;
+#pragma unroll
+      for (int k = 0; k < kAccSlots; ++k) {
+        s_fx += sl[k * 2 * CIN + tid];
+        q_fx += sl[k * 2 * CIN + CIN + tid];
+      }
+      norm_affine(s_fx, q_fx, p.in_hw, p.eps, gam, bet, nrm + tid, nrm + CIN + tid);
+    }
+  }
+  st_w.commit([&](int i, f4 v) { reinterpret_cast<f4*>(wim)[i] = v; });
+  __syncthreads();  // nrm and the weights ready; the norm slots' ring space free
+  // pre-step: concat rows y0-1, y0
+  commit_lr(pre_lr);
+  commit_sk(pre_sk, y0 - 1);
+  __syncthreads();
+  build(y0 - 1, 2);
+  const uint16_t* w2s = reinterpret_cast<const uint16_t*>(wim + (B.w2 - B.w1));
+  const float* wdws = wim + (B.wdw - B.w1);
+  const float* bdws = wim + (B.bdw - B.w1);
+  const float* b2s = wim + (B.b2 - B.w1);
+  float* yn = p.y + (long)n * Ho * Wo * COUT;
+  // the lane's norm terms: f64 sums of integers (exact below 2^53: at most
+  // NSTEP * NBLK / 4 <= 16 terms per lane while |v| < 4096) plus an int64 sum
+  // for the rare larger values — the same integers as block_body's, any order
+  constexpr int TERMS = NSTEP * ((NBLK + 3) / 4);
+  static_assert(TERMS <= 16, "f64 lane sums: at most 16 terms");
+  double sacc[NCB][4], qacc[NCB][4];
+  long long sbig[NCB][4], qbig[NCB][4];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sacc[cb][i] = qacc[cb][i] = 0.0;
+      sbig[cb][i] = qbig[cb][i] = 0;
+    }
+
+  for (int k = 0; k < NSTEP; ++k) {
+    const int yk = y0 + k * SB;
+    if (yk >= Ho) break;  // uniform: the last segment of a frame may be short
+    const int a = yk + 1;
+    __syncthreads();  // the previous build / pre-step build read lr
+    commit_lr(st_lr);
+    commit_sk(st_sk, a);
+    if (k + 1 < NSTEP && yk + SB < Ho) {  // the next step's loads, in flight from here
+      issue_lr(st_lr, a + SB);
+      issue_sk(st_sk, a + SB);
+    }
+    __syncthreads();
+    build(a, SB);
+    __syncthreads();
+    // dw 3x3 -> project for output rows yk .. yk+SB-1
+    for (int blk = wave; blk < NBLK; blk += 4) {
+      const int pix = blk * 16 + r, j = pix / TW, lx = pix % TW;
+      const float* rows[3];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) rows[ky] = ring + (pos(yk + j - 1 + ky) * IW + lx) * XS + 4 * g;
+      f4 acc[CS][NCB];
+#pragma unroll
+      for (int s = 0; s < CS; ++s)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) acc[s][cb] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ck = 0; ck < NCHUNK; ++ck) {
+        const int c0 = ck << 4;
+        f4 av = *reinterpret_cast<const f4*>(bdws + c0 + 4 * g);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx)
+            av = __builtin_elementwise_fma(*reinterpret_cast<const f4*>(wdws + (ky * 3 + kx) * CH + c0 + 4 * g),
+                                           *reinterpret_cast<const f4*>(rows[ky] + kx * XS + c0), av);
+        const f4 b = to_operand<PREC>(av);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+          acc[ck % CS][cb] = mma16_op<PREC>(acc[ck % CS][cb], lds_a<PREC>(w2s, B.LD2, cb * 16 + r, c0 + 4 * g), b);
+      }
+      // acc[.][cb][i] = output channel cb*16 + 4g + i of pixel (yk + j, ox0 + lx)
+      const int oy = yk + j, ox = ox0 + lx;
+      const bool valid = oy < Ho && ox < Wo;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        f4 v = acc[0][cb];
+#pragma unroll
+        for (int s = 1; s < CS; ++s) v = v + acc[s][cb];
+        v = v + *reinterpret_cast<const f4*>(b2s + cb * 16 + 4 * g);
+        if (valid) {
+          *reinterpret_cast<f4*>(yn + ((long)oy * Wo + ox) * COUT + cb * 16 + 4 * g) = v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float e = v[i];
+            if (__builtin_fabsf(e) < 4096.f) {
+              sacc[cb][i] += (double)__builtin_rintf(e * 0x1p32f);
+              qacc[cb][i] += (double)__builtin_rintf(e * e * 0x1p24f);
+            } else {
+              sbig[cb][i] += (long long)__builtin_rintf(e * 0x1p32f);
+              qbig[cb][i] += (long long)__builtin_rintf(e * e * 0x1p24f);
+            }
+          }
+        }
+      }
+    }
+  }
+  // the workgroup's exact sums -> one accumulator slot of the frame
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = cb * 16 + 4 * g + i;
+      __hip_atomic_fetch_add(stat + c, (unsigned long long)((long long)sacc[cb][i] + sbig[cb][i]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(stat + COUT + c, (unsigned long long)((long long)qacc[cb][i] + qbig[cb][i]),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  __syncthreads();
+  if (tid < 2 * COUT) {
+    const int slot = (by * (int)gridDim.x + bx) % kAccSlots;
+    __hip_atomic_fetch_add(p.out_acc + (long)n * p.acc_stride + slot * 2 * COUT + tid, stat[tid], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Head: mask tile 16 x 64; logits over the (10 x 34) low-res region in LDS.
 template <int C, bool COH>
 __device__ __forceinline__ void head_body(const HeadParams& p, int bx, int by, int n, float* smem) {
@@ -1543,12 +1817,21 @@ const BlockEntry* VSS_CAT(registry_shard_, VSS_SHARD)(int* count) {
 #define VSS_STEM_B1S(TW, SB, NSTEP, WT)                                                                        \
   {1, 1, SB * NSTEP, TW, 16, 0, 16, 16, 258,                                                                   \
    {k_stem_b1s<TW, SB, NSTEP, WT, PREC_F32>, k_stem_b1s<TW, SB, NSTEP, WT, PREC_BF16X2>}, WT, VAR_STEM_B1_STREAM, SB},
+// the streamed decoders (k_dec_s) of d2 (48 + 32 -> 32) and d3 (32 + 16 -> 16), src norm in (flags 1)
+#define VSS_DEC_S(CI, CK, CO, FL, TW, SB, NSTEP)                                                            \
+  {2, 1, SB * NSTEP, TW, CI, CK, CI + CK, CO, FL,                                                            \
+   {k_dec_s<CI, CK, CO, FL, TW, SB, NSTEP, PREC_F32>, k_dec_s<CI, CK, CO, FL, TW, SB, NSTEP, PREC_BF16X2>}, kThreads, \
+   VAR_DEC_STREAM, SB},
 static const BlockEntry kStemB1Blocks[] = {
     VSS_STEM_B1(8, 32) VSS_STEM_B1(4, 64) VSS_STEM_B1(8, 64)
     VSS_STEM_B1S(32, 3, 3, 512) VSS_STEM_B1S(16, 3, 3, 256) VSS_STEM_B1S(32, 4, 2, 512) VSS_STEM_B1S(16, 4, 2, 256)
-    VSS_STEM_B1S(16, 2, 4, 256) VSS_STEM_B1S(32, 2, 3, 256)};
+    VSS_STEM_B1S(16, 2, 4, 256) VSS_STEM_B1S(32, 2, 3, 256)
+    VSS_DEC_S(32, 16, 16, 1, 16, 4, 3) VSS_DEC_S(32, 16, 16, 1, 32, 2, 3) VSS_DEC_S(32, 16, 16, 1, 16, 2, 4)
+    VSS_DEC_S(32, 16, 16, 1, 32, 4, 2) VSS_DEC_S(32, 16, 16, 1, 16, 3, 3)
+    VSS_DEC_S(48, 32, 32, 1, 16, 2, 2) VSS_DEC_S(48, 32, 32, 1, 16, 2, 3) VSS_DEC_S(48, 32, 32, 1, 16, 4, 2)};
 #undef VSS_STEM_B1
 #undef VSS_STEM_B1S
+#undef VSS_DEC_S
 
 const BlockEntry* block_registry(int* count) {
   static const std::vector<BlockEntry> all = [] {
