@@ -411,12 +411,11 @@ def test_every_compiled_tile_bitwise(pkg, synthetic):
 
 
 @pytest.mark.parametrize("mh,mw", [(160, 272), (48, 80)])
-def test_streamed_kernels_ragged_bitwise(pkg, synthetic, mh, mw):
-    """Every kernel compiled for b1 (k_block, k_stem_b1, the streamed
-    k_stem_b1s) and for d2 / d3 (k_block, the streamed k_dec_s) at model sizes
-    where the strips and row segments do not divide the layer (b1 / d3 80 x
-    136: a short last segment, step and strip; 24 x 40: strips wider than part
-    of the image), bitwise equal layer by layer (masks included)."""
+def test_b1_kernels_ragged_bitwise(pkg, synthetic, mh, mw):
+    """Every kernel compiled for b1 (k_block and the wide k_stem_b1) at model
+    sizes where the tiles do not divide the stem image (80 x 136, 24 x 40),
+    bitwise equal layer by layer (masks included); pinned by candidate index
+    (VSS_TILE="1:#k": a tile shape can be compiled as more than one kernel)."""
     f = _frames(synthetic, 2, start=930)
     kw = dict(model_h=mh, model_w=mw, dtype="bf16x2", max_batch=2, autotune=False)
     with pkg.Session(**kw) as s:
@@ -424,23 +423,21 @@ def test_streamed_kernels_ragged_bitwise(pkg, synthetic, mh, mw):
         ref, _, _ = s.segment_frames(f)
         nl = s.n_layers
         ref_layers = [s.read_layer(li, 2) for li in range(nl - 1)]
-        layers = {li: [s.layer_tile_kernel(li, k) for k in range(len(s.layer_tiles(li)))] for li in (1, nl - 3, nl - 2)}
-    assert any("k_stem_b1s" in x for x in layers[1]) and any("k_dec_s" in x for x in layers[nl - 2]), layers
+        names = [s.layer_tile_kernel(1, k) for k in range(len(s.layer_tiles(1)))]
+    assert any("k_stem_b1<" in x for x in names), names
     bad = []
-    for li, names in layers.items():
-        for k, name in enumerate(names):
-            os.environ["VSS_TILE"] = f"{li}:#{k}"
-            try:
-                with pkg.Session(**kw) as s:
-                    assert s.layer_kernel(li) == name
-                    s.set_option(pkg.VSS_OPT_KEEP_STEM, 1)
-                    got, _, _ = s.segment_frames(f)
-                    first = next((q for q in range(nl - 1) if not np.array_equal(s.read_layer(q, 2), ref_layers[q])),
-                                 None)
-                    if first is not None or not np.array_equal(got, ref):
-                        bad.append((li, name, first))
-            finally:
-                del os.environ["VSS_TILE"]
+    for k, name in enumerate(names):
+        os.environ["VSS_TILE"] = f"1:#{k}"
+        try:
+            with pkg.Session(**kw) as s:
+                assert s.layer_kernel(1) == name
+                s.set_option(pkg.VSS_OPT_KEEP_STEM, 1)
+                got, _, _ = s.segment_frames(f)
+                first = next((q for q in range(nl - 1) if not np.array_equal(s.read_layer(q, 2), ref_layers[q])), None)
+                if first is not None or not np.array_equal(got, ref):
+                    bad.append((name, first))
+        finally:
+            del os.environ["VSS_TILE"]
     assert not bad, bad
 
 

@@ -424,8 +424,6 @@ int ks_max(const LayerPlan& l) {
 // LDS bytes of one workgroup of compiled shape e for layer l.
 size_t entry_lds_bytes(const LayerPlan& l, const BlockEntry& e) {
   if (e.variant == VAR_STEM_B1_WIDE) return (size_t)stem_b1_lds(e.TH, e.TW).total * 4;
-  if (e.variant == VAR_STEM_B1_STREAM) return (size_t)stem_b1s_lds(e.TW, e.sb).total * 4;
-  if (e.variant == VAR_DEC_STREAM) return (size_t)dec_s_lds(e.TW, e.sb, e.cin, e.cskip, e.cout).total * 4;
   return block_lds_bytes(l, e.TH, e.TW);
 }
 
@@ -2225,12 +2223,6 @@ static void entry_name(const vss_handle* h, const LayerPlan& l, int layer, const
   else {
     if (e->variant == VAR_STEM_B1_WIDE)
       std::snprintf(tmp, cap_, "void vss::k_stem_b1<%d, %d, %d>(vss::BlockParams)", e->TH, e->TW, prec);
-    else if (e->variant == VAR_STEM_B1_STREAM)
-      std::snprintf(tmp, cap_, "void vss::k_stem_b1s<%d, %d, %d, %d, %d>(vss::BlockParams)", e->TW, e->sb,
-                    e->TH / e->sb, e->threads, prec);
-    else if (e->variant == VAR_DEC_STREAM)
-      std::snprintf(tmp, cap_, "void vss::k_dec_s<%d, %d, %d, %d, %d, %d, %d, %d>(vss::BlockParams)", e->cin,
-                    e->cskip, e->cout, e->flags, e->TW, e->sb, e->TH / e->sb, prec);
     else
       std::snprintf(tmp, cap_, "void vss::k_block<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>(vss::BlockParams)",
                     e->mode, e->stride, e->TH, e->TW, e->cin, e->cskip, e->chid, e->cout, e->flags, prec);

@@ -256,8 +256,7 @@ struct BlockEntry {
   int mode, stride, TH, TW, cin, cskip, chid, cout, flags;
   BlockFn fn[2];  // [PREC_F32, PREC_BF16X2]
   int threads = kThreads;  // workgroup size
-  int variant = 0;         // BlockVariant: k_block, k_stem_b1 (wide), k_stem_b1s (streamed)
-  int sb = 0;              // k_stem_b1s: b1 rows per step (TH = sb * steps)
+  int variant = 0;         // BlockVariant: k_block or k_stem_b1 (wide)
 };
 
 // b1 with the stem fused on a wide workgroup (k_stem_b1, 16 waves): LDS
@@ -288,70 +287,8 @@ __host__ __device__ constexpr StemB1Lds stem_b1_lds(int TH, int TW) {
   L.total = o;
   return L;
 }
-// b1 with the stem fused, streamed down a column strip (k_stem_b1s): a
-// workgroup owns TW b1 columns and SB * NSTEP rows and walks down them SB rows
-// per step.  The resized rows and the two stem rows a step shares with the
-// next stay in LDS (ping-pong buffers), so the vertical halo is computed once
-// per strip segment instead of once per tile, and the next step's frame
-// gathers are in flight while this step's stem and b1 run.  LDS carve in
-// floats: X[2] = resized rows [3][2*SB+1][XWP], S[2] = stem rows
-// [SB+2][IW][SXS], the stem weights, the block's weight image.
-struct StemB1sLds {
-  int IW, XW, XWP, XHB, XPL, SXS, SPL, x[2], s[2], sw, sb, wim, total;
-};
-__host__ __device__ constexpr StemB1sLds stem_b1s_lds(int TW, int SB) {
-  StemB1sLds L{};
-  L.IW = TW + 2;
-  L.XW = 2 * L.IW + 1;
-  L.XWP = L.XW + 1;
-  L.XHB = 2 * SB + 1;
-  L.XPL = L.XHB * L.XWP;  // one colour plane of a resized-row buffer
-  L.SXS = 16 + VSS_XS_PAD;
-  L.SPL = (SB + 2) * L.IW * L.SXS;
-  int o = 0;
-  L.x[0] = o; o += r4(3 * L.XPL);
-  L.x[1] = o; o += r4(3 * L.XPL);
-  L.s[0] = o; o += r4(L.SPL);
-  L.s[1] = o; o += r4(L.SPL);
-  L.sw = o;   o += 27 * 16;
-  L.sb = o;   o += 16;
-  const BlockLds B = block_lds(1 /*MODE_IR_DIRECT*/, 1, 1, 16, 16, 0, 16, 16, 1);
-  L.wim = o;  o += B.wimg_end - B.w1;
-  L.total = o;
-  return L;
-}
-
-// A decoder block streamed down a column strip (k_dec_s): the workgroup owns
-// TW output columns and SB * NSTEP rows and walks down them SB rows per step.
-// The concat rows (2x upsample of relu(IN(src)) ++ skip) live in a ring of
-// R = 2*SB + 2 rows, so a step's new rows never overwrite the rows the
-// previous step's depthwise pass still reads, and each concat row is built
-// once per strip segment.  LDS carve in floats: ring [R][IW][XS], the step's
-// low-res src rows [SRS][SC][cin], the src norm scale / shift, the weight
-// image, the norm-statistics accumulators (int64 [2][cout]).
-struct DecSLds {
-  int IW, R, XS, SRS, SC, ring, lr, nrm, wim, stat, total;
-};
-__host__ __device__ constexpr DecSLds dec_s_lds(int TW, int SB, int cin, int cskip, int cout) {
-  DecSLds L{};
-  L.IW = TW + 2;
-  L.R = 2 * SB + 2;
-  L.XS = cin + cskip + VSS_XS_PAD;
-  L.SRS = SB / 2 + 2;
-  L.SC = (TW + 1) / 2 + 3;
-  int o = 0;
-  L.ring = o; o += r4(cmax(L.R * L.IW * L.XS, kAccSlots * 2 * cin * 2));  // also the prologue's norm slots
-  L.lr = o;   o += r4(L.SRS * L.SC * cin);
-  L.nrm = o;  o += r4(2 * cin);
-  const BlockLds B = block_lds(2 /*MODE_DEC*/, 1, 1, 16, cin, cskip, cin + cskip, cout);
-  L.wim = o;  o += B.wimg_end - B.w1;
-  L.stat = o; o += 4 * cout;
-  L.total = o;
-  return L;
-}
-
 // BlockEntry::variant
-enum BlockVariant : int { VAR_BLOCK = 0, VAR_STEM_B1_WIDE = 1, VAR_STEM_B1_STREAM = 2, VAR_DEC_STREAM = 3 };
+enum BlockVariant : int { VAR_BLOCK = 0, VAR_STEM_B1_WIDE = 1 };
 
 const BlockEntry* block_registry(int* count);
 

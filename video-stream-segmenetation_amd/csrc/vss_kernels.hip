@@ -1213,478 +1213,6 @@ __global__ __launch_bounds__(kWideThreads) void k_stem_b1(BlockParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// b1 with the stem fused, streamed down a column strip (stem_b1s_lds in
-// vss_kernels.h).  Workgroup (bx, by, n) owns b1 columns [TW*bx, TW*bx + TW)
-// and rows [y0, y0 + SB*NSTEP), y0 = SB*NSTEP*by, and walks down them SB rows
-// per step:
-//   pre-step : resized rows 2*y0-3 .. 2*y0+1 -> X[1], stem rows y0-1, y0 -> S[0]
-//   step k   : (b1 rows yk .. yk+SB-1, yk = y0 + k*SB)
-//     lerp   : the 2*SB new resized rows 2*yk+2 .. 2*yk+2*SB+1 -> X[k&1] rows
-//              1..2*SB (row 0 = 2*yk+1, carried from the previous step)
-//     issue  : step k+1's frame gathers (in flight during the rest of step k)
-//     stem   : the SB new stem rows yk+1 .. yk+SB -> S[k&1] rows 2..SB+1
-//              (rows 0, 1 = yk-1, yk carried)
-//     b1     : dw 3x3 over S[k&1] -> relu6 -> project -> + bias -> + residual
-// The rows a step hands to the next are written to both buffers by their
-// producer (no copies), and the buffers alternate, so two workgroup barriers
-// per step order everything.  Against k_block's 4 x 16 tile (the autotuner's
-// pick) the resized pixels are computed ~1.35x instead of 1.88x per output and
-// the stem outputs ~1.25x instead of 1.69x, and the gathers overlap compute
-// instead of every workgroup of the single round waiting for its loads at the
-// same moment.  The arithmetic per output is block_body<MODE_IR_DIRECT, ...,
-// STEM_IN | residual>'s, operation for operation (prep_* of the resize,
-// stem_mfma, ky-major dw taps, relu6, to_operand, one project MFMA, + bias, +
-// residual): bitwise the same activations (test_stem_fusion_bitwise,
-// test_results_independent_of_tiling).
-template <int TW, int SB, int NSTEP, int WT, int PREC>
-__global__ __launch_bounds__(WT) void k_stem_b1s(BlockParams p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr StemB1sLds S = stem_b1s_lds(TW, SB);
-  constexpr int IW = S.IW, XW = S.XW, XWP = S.XWP, XPL = S.XPL, SXS = S.SXS, NWAVE = WT / 64;
-  constexpr BlockLds B = block_lds(MODE_IR_DIRECT, 1, 1, 16, 16, 0, 16, 16, 1);
-  constexpr int WIMG4 = (B.wimg_end - B.w1) / 4;
-  constexpr int NPRE = 5 * XW, NSTP = 2 * SB * XW;
-  constexpr int NXP = (NPRE + WT - 1) / WT, NX = (NSTP + WT - 1) / WT;
-  static_assert(SB >= 2, "two stem rows carry over to the next step");
-  static_assert((SB * TW) % 16 == 0 && WT % 64 == 0, "b1 pixel blocks");
-  static_assert(WIMG4 <= WT, "one weight-image element per thread");
-  constexpr int NSW = (27 * 16 + WT - 1) / WT;  // stem weights per thread
-  const TileIdx tl = xcd_tile();
-  const int bx = tl.x, by = tl.y, n = tl.z;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-  const StemParams& sp = p.stem;
-  const int H = p.H, W = p.W, Hm = sp.Hm, Wm = sp.Wm;  // the stem's output = b1's input
-  const int ox0 = bx * TW, y0 = by * (SB * NSTEP);
-  const int c0 = 2 * ox0 - 3;  // resized column of X column 0
-  const uint8_t* fr = sp.frames + (long)n * sp.frame_stride;
-  float* xbuf[2] = {smem + S.x[0], smem + S.x[1]};
-  float* sbuf[2] = {smem + S.s[0], smem + S.s[1]};
-  float* sws = smem + S.sw;
-  float* sbs = smem + S.sb;
-  float* wim = smem + S.wim;
-
-  // item i of a block of resized rows starting at row0: its taps' loads
-  auto gather = [&](int i, int row0, uint32_t v[12], float& dy, float& dx) {
-    const int ly = i / XW, lx = i - ly * XW;
-    const int yy = min(max(row0 + ly, 0), Hm - 1), xx = min(max(c0 + lx, 0), Wm - 1);
-    const PrepTap t = prep_tap(fr, sp.row_stride, sp.fc, sp.fh, sp.fw, sp.ry, sp.rx, yy, xx);
-    prep_load(t, v);
-    dy = t.dy;
-    dx = t.dx;
-  };
-  // the finished item -> X buffer xb at row brow0 + ly (zero outside the
-  // image); the block's last row also to row 0 of the other buffer (carry)
-  auto put_x = [&](int i, int row0, const float o[3], float* xb, int brow0, int carry_ly, float* xc) {
-    const int ly = i / XW, lx = i - ly * XW;
-    const int yy = row0 + ly, xx = c0 + lx;
-    const bool valid = yy >= 0 && yy < Hm && xx >= 0 && xx < Wm;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float v = valid ? o[c] : 0.f;
-      xb[c * XPL + (brow0 + ly) * XWP + lx] = v;
-      if (ly == carry_ly) xc[c * XPL + lx] = v;
-    }
-  };
-
-  // ---- every load of the pre-step and step 0 issued first ----
-  const f4 wv = reinterpret_cast<const f4*>(p.wimg)[min(tid, WIMG4 - 1)];
-  float swr[NSW];
-#pragma unroll
-  for (int u = 0; u < NSW; ++u) swr[u] = sp.w[min(tid + WT * u, 27 * 16 - 1)];
-  const float sbv = sp.b[min(tid, 15)];
-  uint32_t rp[NXP][12];
-  float dyp[NXP], dxp[NXP];
-#pragma unroll
-  for (int u = 0; u < NXP; ++u) gather(min(tid + WT * u, NPRE - 1), 2 * y0 - 3, rp[u], dyp[u], dxp[u]);
-  uint32_t rs[NX][12];
-  float dys[NX], dxs[NX];
-#pragma unroll
-  for (int u = 0; u < NX; ++u) gather(min(tid + WT * u, NSTP - 1), 2 * y0 + 2, rs[u], dys[u], dxs[u]);
-  // start of the forward: zero this frame's decoder norm accumulators (the stem's job)
-  if (bx == 0 && by == 0)
-    for (int i = tid; i < sp.acc_stride; i += WT) sp.acc_zero[(long)n * sp.acc_stride + i] = 0ull;
-  if (tid < WIMG4) reinterpret_cast<f4*>(wim)[tid] = wv;
-#pragma unroll
-  for (int u = 0; u < NSW; ++u) {
-    const int i = tid + WT * u;  // sp.w is [c][27]
-    if (i < 27 * 16) sws[(i % 27) * 16 + i / 27] = swr[u];
-  }
-  if (tid < 16) sbs[tid] = sbv;
-  // ---- pre-step: resized rows 2*y0-3 .. 2*y0+1 -> X[1] rows 0..4 (row 4 carried to X[0]) ----
-  {
-    float o[NXP][3];
-#pragma unroll
-    for (int u = 0; u < NXP; u += 2) {
-      if (u + 1 < NXP) prep_finish2(rp[u], rp[u + 1], dyp[u], dxp[u], dyp[u + 1], dxp[u + 1], o[u], o[u + 1]);
-      else prep_finish(rp[u], dyp[u], dxp[u], o[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < NXP; ++u)
-      if (tid + WT * u < NPRE) put_x(tid + WT * u, 2 * y0 - 3, o[u], xbuf[1], 0, 4, xbuf[0]);
-  }
-  __syncthreads();
-  const StemTaps taps = stem_taps(sws, r, g, XPL, XWP);
-  const float sbias = sbs[r];
-  // stem rows s0 .. s0+nrows-1 of the X buffer xb (row 2i-th resized row at
-  // buffer row 2i), 16-pixel blocks on the MFMA, zero outside the stem image
-  auto stem_rows = [&](const float* xb, int nrows, int s0, auto&& put) {
-    const int npix = nrows * IW;
-    for (int blk = wave; blk < (npix + 15) / 16; blk += NWAVE) {
-      const int pa = min(blk * 16 + r, npix - 1), i = pa / IW, px = pa - i * IW;
-      const f4 acc = stem_mfma(taps, xb + 2 * i * XWP + 2 * px, sbias);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {  // D[pixel 4g+q][channel r]
-        const int pp = blk * 16 + 4 * g + q;
-        if (pp < npix) {
-          const int ii = pp / IW, px2 = pp - ii * IW;
-          const int sy = s0 + ii, sx = ox0 - 1 + px2;
-          const bool valid = sy >= 0 && sy < H && sx >= 0 && sx < W;
-          put(ii, px2, valid ? relu6f(acc[q]) : 0.f);
-        }
-      }
-    }
-  };
-  stem_rows(xbuf[1], 2, y0 - 1, [&](int ii, int px, float v) { sbuf[0][(ii * IW + px) * SXS + r] = v; });
-  // b1's weights, in registers for every step
-  const uint16_t* w2s = reinterpret_cast<const uint16_t*>(wim + (B.w2 - B.w1));
-  const float* wdws = wim + (B.wdw - B.w1);
-  f4 wk[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) wk[t] = *reinterpret_cast<const f4*>(wdws + t * 16 + 4 * g);
-  const f4 bb = *reinterpret_cast<const f4*>(wim + (B.bdw - B.w1) + 4 * g);
-  const typename AFrag<PREC>::T a2 = lds_a<PREC>(w2s, B.LD2, r, 4 * g);
-  const f4 bias2 = *reinterpret_cast<const f4*>(wim + (B.b2 - B.w1) + 4 * g);
-  const int Ho = p.Ho, Wo = p.Wo;
-  float* yn = p.y + (long)n * Ho * Wo * 16;
-  float* stn = sp.y ? sp.y + (long)n * H * W * 16 : nullptr;  // VSS_OPT_KEEP_STEM
-  __syncthreads();  // the pre-step's stem read X[1] before step 0 writes its row 0
-
-  for (int k = 0; k < NSTEP; ++k) {
-    const int yk = y0 + k * SB;
-    if (yk >= H) break;  // uniform: the last segment of a frame may be short
-    float* xb = xbuf[k & 1];
-    float* sb_ = sbuf[k & 1];
-    float* sn = sbuf[(k + 1) & 1];
-    {
-      float o[NX][3];
-#pragma unroll
-      for (int u = 0; u < NX; u += 2) {
-        if (u + 1 < NX) prep_finish2(rs[u], rs[u + 1], dys[u], dxs[u], dys[u + 1], dxs[u + 1], o[u], o[u + 1]);
-        else prep_finish(rs[u], dys[u], dxs[u], o[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < NX; ++u)
-        if (tid + WT * u < NSTP) put_x(tid + WT * u, 2 * yk + 2, o[u], xb, 1, 2 * SB - 1, xbuf[(k + 1) & 1]);
-    }
-    if (k + 1 < NSTEP && yk + SB < H) {  // the next step's gathers, in flight from here
-#pragma unroll
-      for (int u = 0; u < NX; ++u) gather(min(tid + WT * u, NSTP - 1), 2 * (yk + SB) + 2, rs[u], dys[u], dxs[u]);
-    }
-    __syncthreads();
-    stem_rows(xb, SB, yk + 1, [&](int ii, int px, float v) {
-      sb_[((2 + ii) * IW + px) * SXS + r] = v;
-      if (ii >= SB - 2) sn[((ii - (SB - 2)) * IW + px) * SXS + r] = v;
-    });
-    __syncthreads();
-    // b1 rows yk .. yk+SB-1: lane (r, g) = pixel r of the wave's block, channels 4g..4g+3
-    for (int blk = wave; blk < SB * TW / 16; blk += NWAVE) {
-      const int pix = blk * 16 + r, j = pix / TW, lx = pix % TW;
-      f4 a = bb;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
-          a = __builtin_elementwise_fma(wk[ky * 3 + kx], *reinterpret_cast<const f4*>(sb_ + ((j + ky) * IW + lx + kx) * SXS + 4 * g), a);
-      a = relu6v(a);
-      const f4 b = to_operand<PREC>(a);
-      f4 v = mma16_op<PREC>(f4{0.f, 0.f, 0.f, 0.f}, a2, b);
-      const f4 centre = *reinterpret_cast<const f4*>(sb_ + ((j + 1) * IW + lx + 1) * SXS + 4 * g);
-      v = v + bias2;
-      v = v + centre;
-      const int oy = yk + j, ox = ox0 + lx;
-      if (oy < Ho && ox < Wo) {
-        *reinterpret_cast<f4*>(yn + ((long)oy * Wo + ox) * 16 + 4 * g) = v;
-        if (stn) *reinterpret_cast<f4*>(stn + ((long)oy * W + ox) * 16 + 4 * g) = centre;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// A decoder block streamed down a column strip (dec_s_lds in vss_kernels.h).
-// Workgroup (bx, by, n) owns output columns [TW*bx, TW*bx + TW) and rows
-// [y0, y0 + SB*NSTEP) and walks down them SB rows per step:
-//   pre-step : concat rows y0-1, y0 -> ring
-//   step k   : (output rows yk .. yk+SB-1)
-//     commit : this step's low-res src rows (XP parts summed, then the src's
-//              instance norm + ReLU) -> lr; the skip rows of concat rows
-//              yk+1 .. yk+SB -> their ring rows
-//     issue  : the next step's src and skip loads (in flight from here)
-//     build  : the 2x upsample of lr -> the same ring rows' first cin channels
-//     dw     : each wave one 16-pixel block at a time: every 16-channel chunk's
-//              dw 3x3 (VALU) -> project (MFMA) into the chunk group's
-//              accumulator, the groups summed in order, + bias -> store; the
-//              block's fixed-point norm terms summed in the lane
-//   end      : the workgroup's norm sums -> one of the frame's kAccSlots
-// Two barriers per step; the ring of 2*SB + 2 rows keeps a step's writes off
-// the rows the previous step's dw pass still reads.  Against k_block's tile
-// the concat rows (upsample + skip) are built ~1.1x instead of ~1.5x per
-// output, the src norm, the weight image and the norm atomics once per strip
-// segment instead of once per tile, and the next step's loads overlap this
-// step's work.  The arithmetic per output is block_body<MODE_DEC, ...>'s
-// operation for operation (the same upsample FMAs, ky-major dw taps, chunk
-// groups CS summed in group order, + bias; integer norm sums, order-free):
-// bitwise the same activations for any tile (test_every_compiled_tile_bitwise).
-template <int CIN, int CSKIP, int COUT, int FLAGS, int TW, int SB, int NSTEP, int PREC>
-__global__ __launch_bounds__(256) void k_dec_s(BlockParams p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int CH = CIN + CSKIP;
-  constexpr DecSLds D = dec_s_lds(TW, SB, CIN, CSKIP, COUT);
-  constexpr BlockLds B = block_lds(MODE_DEC, 1, 1, 16, CIN, CSKIP, CH, COUT);
-  constexpr int IW = D.IW, R = D.R, XS = D.XS, SRS = D.SRS, SC = D.SC;
-  constexpr bool NORM_IN = (FLAGS & 1) != 0;
-  constexpr int XP = flags_xp(FLAGS), SP = flags_sp(FLAGS);
-  constexpr int NCHUNK = CH / 16, CS = NCHUNK >= 4 ? 4 : (NCHUNK >= 2 ? 2 : 1), NCB = COUT / 16;
-  constexpr int C4L = CIN / 4, C4S = CSKIP / 4;
-  constexpr int NLR = SRS * SC * C4L;  // src items (16 B) of a step, per part
-  constexpr int NSK = SB * IW * C4S;   // skip items of a step, per part
-  constexpr int NSK0 = 2 * IW * C4S;   // skip items of the pre-step
-  constexpr int NBLK = SB * TW / 16;   // output pixel blocks of a step
-  constexpr int WIMG4 = (B.wimg_end - B.w1) / 4;
-  static_assert(CIN % 16 == 0 && CSKIP % 16 == 0 && COUT % 16 == 0 && (SB * TW) % 16 == 0 && SB >= 2, "shape");
-  static_assert(SRS * SC * CIN < 65536, "lr offsets");
-  const TileIdx tl = xcd_tile();
-  const int bx = tl.x, by = tl.y, n = tl.z;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-  const int h = p.H, w = p.W, Ho = p.Ho, Wo = p.Wo;  // src (low-res) and output dims
-  const int ox0 = bx * TW, y0 = by * (SB * NSTEP);
-  const int sx0 = max(0, (ox0 - 1) / 2 - 1);
-  float* ring = smem + D.ring;
-  float* lr = smem + D.lr;
-  float* nrm = smem + D.nrm;
-  float* wim = smem + D.wim;
-  unsigned long long* stat = reinterpret_cast<unsigned long long*>(smem + D.stat);
-  const float* xn = p.x + (long)n * h * w * CIN;
-  const float* sn = p.skip + (long)n * Ho * Wo * CSKIP;
-  auto pos = [&](int yy) { return (yy - y0 + 1) % R; };     // ring row of concat row yy (>= y0 - 1)
-  auto src_base = [&](int a) { return a > 0 ? (a - 1) >> 1 : 0; };  // first src row of concat rows a..
-
-  // loads of one step (concat rows a ..): src rows src_base(a) .. + SRS, skip rows a .. + rows
-  auto issue_lr = [&](Staged<NLR>(&st)[XP], int a) {
-    const int sb = src_base(a);
-#pragma unroll
-    for (int q = 0; q < XP; ++q) {
-      const float* gx = xn + q * p.x_part_stride;
-      st[q].issue([&](int i) {
-        const int pr = i / C4L, c4 = i % C4L;
-        const int yy = min(h - 1, sb + pr / SC), xx = min(w - 1, sx0 + pr % SC);
-        return *reinterpret_cast<const f4*>(gx + ((long)yy * w + xx) * CIN + 4 * c4);
-      });
-    }
-  };
-  auto issue_sk = [&](auto& st, int a) {
-#pragma unroll
-    for (int q = 0; q < SP; ++q) {
-      const float* gs = sn + q * p.skip_part_stride;
-      st[q].issue([&](int i) {
-        const int pix = i / C4S, c4 = i % C4S;
-        const int yy = min(max(a + pix / IW, 0), Ho - 1), xx = min(max(ox0 - 1 + pix % IW, 0), Wo - 1);
-        return *reinterpret_cast<const f4*>(gs + ((long)yy * Wo + xx) * CSKIP + 4 * c4);
-      });
-    }
-  };
-  auto commit_lr = [&](const Staged<NLR>(&st)[XP]) {
-    commit_sum(st, [&](int i, f4 v) {
-      if constexpr (NORM_IN) {
-        const int c4 = i % C4L;
-        v = reluv(__builtin_elementwise_fma(v, *reinterpret_cast<const f4*>(nrm + 4 * c4),
-                                            *reinterpret_cast<const f4*>(nrm + CIN + 4 * c4)));
-      }
-      reinterpret_cast<f4*>(lr)[i] = v;
-    });
-  };
-  auto commit_sk = [&](const auto& st, int a) {
-    commit_sum(st, [&](int i, f4 v) {
-      const int pix = i / C4S, c4 = i % C4S;
-      const int yy = a + pix / IW, px = pix % IW, xx = ox0 - 1 + px;
-      const bool valid = yy >= 0 && yy < Ho && xx >= 0 && xx < Wo;
-      *reinterpret_cast<f4*>(ring + (pos(yy) * IW + px) * XS + CIN + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
-    });
-  };
-  // the upsampled channels of concat rows a .. a+nrows-1 from lr (PyTorch
-  // upsample_bilinear2d, scale 2, align_corners=False), block_body's taps and FMAs
-  auto build = [&](int a, int nrows) {
-    const int sb = src_base(a);
-    for (int i = tid; i < nrows * IW * C4L; i += 256) {
-      const int pix = i / C4L, c4 = i % C4L;
-      const int yy = a + pix / IW, px = pix % IW, xx = ox0 - 1 + px;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (yy >= 0 && yy < Ho && xx >= 0 && xx < Wo) {
-        const int ys = yy > 0 ? (yy - 1) >> 1 : 0, ys1 = ys + (ys < h - 1 ? 1 : 0);
-        const float ly1 = yy > 0 ? ((yy & 1) ? 0.25f : 0.75f) : 0.f;
-        const int xs = xx > 0 ? (xx - 1) >> 1 : 0, xs1 = xs + (xs < w - 1 ? 1 : 0);
-        const float lx1 = xx > 0 ? ((xx & 1) ? 0.25f : 0.75f) : 0.f;
-        const int r0 = min(max(ys - sb, 0), SRS - 1), r1 = min(max(ys1 - sb, 0), SRS - 1);
-        const int q0 = min(max(xs - sx0, 0), SC - 1), q1 = min(max(xs1 - sx0, 0), SC - 1);
-        const f4 t00 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q0) * CIN + 4 * c4);
-        const f4 t01 = *reinterpret_cast<const f4*>(lr + (r0 * SC + q1) * CIN + 4 * c4);
-        const f4 t10 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q0) * CIN + 4 * c4);
-        const f4 t11 = *reinterpret_cast<const f4*>(lr + (r1 * SC + q1) * CIN + 4 * c4);
-        const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
-        const f4 lx0v = {lx0, lx0, lx0, lx0}, lx1v = {lx1, lx1, lx1, lx1};
-        const f4 ly0v = {ly0, ly0, ly0, ly0}, ly1v = {ly1, ly1, ly1, ly1};
-        const f4 top = __builtin_elementwise_fma(lx1v, t01, lx0v * t00);
-        const f4 bot = __builtin_elementwise_fma(lx1v, t11, lx0v * t10);
-        v = __builtin_elementwise_fma(ly1v, bot, ly0v * top);
-      }
-      *reinterpret_cast<f4*>(ring + (pos(yy) * IW + px) * XS + 4 * c4) = v;
-    }
-  };
-
-  // ---- prologue: every load of the weights, the src norm, the pre-step and step 0 ----
-  Staged<WIMG4> st_w;
-  st_w.issue([&](int i) { return reinterpret_cast<const f4*>(p.wimg)[i]; });
-  constexpr int NSLOT16 = NORM_IN ? kAccSlots * 2 * CIN / 2 : 0;
-  Staged<NSLOT16> st_slots;
-  if constexpr (NORM_IN)
-    st_slots.issue([&](int i) { return reinterpret_cast<const f4*>(p.in_acc + (long)n * p.acc_stride)[i]; });
-  Staged<NLR> pre_lr[XP];
-  Staged<NSK0> pre_sk[SP];
-  issue_lr(pre_lr, y0 - 1);
-  issue_sk(pre_sk, y0 - 1);
-  Staged<NLR> st_lr[XP];
-  Staged<NSK> st_sk[SP];
-  issue_lr(st_lr, y0 + 1);
-  issue_sk(st_sk, y0 + 1);
-  if (tid < 2 * COUT) stat[tid] = 0ull;
-  if constexpr (NORM_IN) {
-    const float gam = p.in_gamma[min(tid, CIN - 1)], bet = p.in_beta[min(tid, CIN - 1)];
-    st_slots.commit([&](int i, f4 v) { reinterpret_cast<f4*>(ring)[i] = v; });
-    __syncthreads();
-    const unsigned long long* sl = reinterpret_cast<const unsigned long long*>(ring);
-    if (tid < CIN) {
-      unsigned long long s_fx = 0, q_fx = 0;
-#pragma unroll
-      for (int k = 0; k < kAccSlots; ++k) {
-        s_fx += sl[k * 2 * CIN + tid];
-        q_fx += sl[k * 2 * CIN + CIN + tid];
-      }
-      norm_affine(s_fx, q_fx, p.in_hw, p.eps, gam, bet, nrm + tid, nrm + CIN + tid);
-    }
-  }
-  st_w.commit([&](int i, f4 v) { reinterpret_cast<f4*>(wim)[i] = v; });
-  __syncthreads();  // nrm and the weights ready; the norm slots' ring space free
-  // pre-step: concat rows y0-1, y0
-  commit_lr(pre_lr);
-  commit_sk(pre_sk, y0 - 1);
-  __syncthreads();
-  build(y0 - 1, 2);
-  const uint16_t* w2s = reinterpret_cast<const uint16_t*>(wim + (B.w2 - B.w1));
-  const float* wdws = wim + (B.wdw - B.w1);
-  const float* bdws = wim + (B.bdw - B.w1);
-  const float* b2s = wim + (B.b2 - B.w1);
-  float* yn = p.y + (long)n * Ho * Wo * COUT;
-  // the lane's norm terms: f64 sums of integers (exact below 2^53: at most
-  // NSTEP * NBLK / 4 <= 16 terms per lane while |v| < 4096) plus an int64 sum
-  // for the rare larger values — the same integers as block_body's, any order
-  constexpr int TERMS = NSTEP * ((NBLK + 3) / 4);
-  static_assert(TERMS <= 16, "f64 lane sums: at most 16 terms");
-  double sacc[NCB][4], qacc[NCB][4];
-  long long sbig[NCB][4], qbig[NCB][4];
-#pragma unroll
-  for (int cb = 0; cb < NCB; ++cb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      sacc[cb][i] = qacc[cb][i] = 0.0;
-      sbig[cb][i] = qbig[cb][i] = 0;
-    }
-
-  for (int k = 0; k < NSTEP; ++k) {
-    const int yk = y0 + k * SB;
-    if (yk >= Ho) break;  // uniform: the last segment of a frame may be short
-    const int a = yk + 1;
-    __syncthreads();  // the previous build / pre-step build read lr
-    commit_lr(st_lr);
-    commit_sk(st_sk, a);
-    if (k + 1 < NSTEP && yk + SB < Ho) {  // the next step's loads, in flight from here
-      issue_lr(st_lr, a + SB);
-      issue_sk(st_sk, a + SB);
-    }
-    __syncthreads();
-    build(a, SB);
-    __syncthreads();
-    // dw 3x3 -> project for output rows yk .. yk+SB-1
-    for (int blk = wave; blk < NBLK; blk += 4) {
-      const int pix = blk * 16 + r, j = pix / TW, lx = pix % TW;
-      const float* rows[3];
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) rows[ky] = ring + (pos(yk + j - 1 + ky) * IW + lx) * XS + 4 * g;
-      f4 acc[CS][NCB];
-#pragma unroll
-      for (int s = 0; s < CS; ++s)
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) acc[s][cb] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ck = 0; ck < NCHUNK; ++ck) {
-        const int c0 = ck << 4;
-        f4 av = *reinterpret_cast<const f4*>(bdws + c0 + 4 * g);
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx)
-            av = __builtin_elementwise_fma(*reinterpret_cast<const f4*>(wdws + (ky * 3 + kx) * CH + c0 + 4 * g),
-                                           *reinterpret_cast<const f4*>(rows[ky] + kx * XS + c0), av);
-        const f4 b = to_operand<PREC>(av);
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb)
-          acc[ck % CS][cb] = mma16_op<PREC>(acc[ck % CS][cb], lds_a<PREC>(w2s, B.LD2, cb * 16 + r, c0 + 4 * g), b);
-      }
-      // acc[.][cb][i] = output channel cb*16 + 4g + i of pixel (yk + j, ox0 + lx)
-      const int oy = yk + j, ox = ox0 + lx;
-      const bool valid = oy < Ho && ox < Wo;
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        f4 v = acc[0][cb];
-#pragma unroll
-        for (int s = 1; s < CS; ++s) v = v + acc[s][cb];
-        v = v + *reinterpret_cast<const f4*>(b2s + cb * 16 + 4 * g);
-        if (valid) {
-          *reinterpret_cast<f4*>(yn + ((long)oy * Wo + ox) * COUT + cb * 16 + 4 * g) = v;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float e = v[i];
-            if (__builtin_fabsf(e) < 4096.f) {
-              sacc[cb][i] += (double)__builtin_rintf(e * 0x1p32f);
-              qacc[cb][i] += (double)__builtin_rintf(e * e * 0x1p24f);
-            } else {
-              sbig[cb][i] += (long long)__builtin_rintf(e * 0x1p32f);
-              qbig[cb][i] += (long long)__builtin_rintf(e * e * 0x1p24f);
-            }
-          }
-        }
-      }
-    }
-  }
-  // the workgroup's exact sums -> one accumulator slot of the frame
-#pragma unroll
-  for (int cb = 0; cb < NCB; ++cb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = cb * 16 + 4 * g + i;
-      __hip_atomic_fetch_add(stat + c, (unsigned long long)((long long)sacc[cb][i] + sbig[cb][i]), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add(stat + COUT + c, (unsigned long long)((long long)qacc[cb][i] + qbig[cb][i]),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  __syncthreads();
-  if (tid < 2 * COUT) {
-    const int slot = (by * (int)gridDim.x + bx) % kAccSlots;
-    __hip_atomic_fetch_add(p.out_acc + (long)n * p.acc_stride + slot * 2 * COUT + tid, stat[tid], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Head: mask tile 16 x 64; logits over the (10 x 34) low-res region in LDS.
 template <int C, bool COH>
 __device__ __forceinline__ void head_body(const HeadParams& p, int bx, int by, int n, float* smem) {
@@ -1812,26 +1340,9 @@ const BlockEntry* VSS_CAT(registry_shard_, VSS_SHARD)(int* count) {
 // residual, STEM_IN (block_flags(0, 1, 1, 1, 1, 1) = 258).
 #define VSS_STEM_B1(TH, TW)                                                                              \
   {1, 1, TH, TW, 16, 0, 16, 16, 258, {k_stem_b1<TH, TW, PREC_F32>, k_stem_b1<TH, TW, PREC_BF16X2>}, kWideThreads, \
-   VAR_STEM_B1_WIDE, 0},
-// the streamed kernel (k_stem_b1s): TW columns, SB rows per step, NSTEP steps, WT threads
-#define VSS_STEM_B1S(TW, SB, NSTEP, WT)                                                                        \
-  {1, 1, SB * NSTEP, TW, 16, 0, 16, 16, 258,                                                                   \
-   {k_stem_b1s<TW, SB, NSTEP, WT, PREC_F32>, k_stem_b1s<TW, SB, NSTEP, WT, PREC_BF16X2>}, WT, VAR_STEM_B1_STREAM, SB},
-// the streamed decoders (k_dec_s) of d2 (48 + 32 -> 32) and d3 (32 + 16 -> 16), src norm in (flags 1)
-#define VSS_DEC_S(CI, CK, CO, FL, TW, SB, NSTEP)                                                            \
-  {2, 1, SB * NSTEP, TW, CI, CK, CI + CK, CO, FL,                                                            \
-   {k_dec_s<CI, CK, CO, FL, TW, SB, NSTEP, PREC_F32>, k_dec_s<CI, CK, CO, FL, TW, SB, NSTEP, PREC_BF16X2>}, kThreads, \
-   VAR_DEC_STREAM, SB},
-static const BlockEntry kStemB1Blocks[] = {
-    VSS_STEM_B1(8, 32) VSS_STEM_B1(4, 64) VSS_STEM_B1(8, 64)
-    VSS_STEM_B1S(32, 3, 3, 512) VSS_STEM_B1S(16, 3, 3, 256) VSS_STEM_B1S(32, 4, 2, 512) VSS_STEM_B1S(16, 4, 2, 256)
-    VSS_STEM_B1S(16, 2, 4, 256) VSS_STEM_B1S(32, 2, 3, 256)
-    VSS_DEC_S(32, 16, 16, 1, 16, 4, 3) VSS_DEC_S(32, 16, 16, 1, 32, 2, 3) VSS_DEC_S(32, 16, 16, 1, 16, 2, 4)
-    VSS_DEC_S(32, 16, 16, 1, 32, 4, 2) VSS_DEC_S(32, 16, 16, 1, 16, 3, 3)
-    VSS_DEC_S(48, 32, 32, 1, 16, 2, 2) VSS_DEC_S(48, 32, 32, 1, 16, 2, 3) VSS_DEC_S(48, 32, 32, 1, 16, 4, 2)};
+   VAR_STEM_B1_WIDE},
+static const BlockEntry kStemB1Blocks[] = {VSS_STEM_B1(8, 32) VSS_STEM_B1(4, 64) VSS_STEM_B1(8, 64)};
 #undef VSS_STEM_B1
-#undef VSS_STEM_B1S
-#undef VSS_DEC_S
 
 const BlockEntry* block_registry(int* count) {
   static const std::vector<BlockEntry> all = [] {
