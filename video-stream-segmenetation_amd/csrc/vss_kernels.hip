@@ -131,51 +131,6 @@ __device__ __forceinline__ void prep_load(const PrepTap& t, uint32_t v[12]) {
   }
 }
 
-// The same 12 bytes from two aligned 12-byte windows (VSS_WIDE_TAPS, default
-// on): a tap row's two pixels (columns x0, x1 = x0 or x0 + 1) are fc or 0 bytes
-// apart, so bytes [o0, o0 + 2] and [o1, o1 + 2] lie in the 12 bytes from the
-// dword at or below o0 — one global_load_dwordx3 per row (dword-aligned: no
-// split access) instead of six byte loads, and v_alignbyte to pick each
-// pixel's bytes.  Byte values are the same, so the floats are the same.  A
-// window that would end past the frame's last byte (`fend`) is read byte by
-// byte instead (the last pixels of the last row).
-#ifndef VSS_WIDE_TAPS
-#define VSS_WIDE_TAPS 1
-#endif
-__device__ __forceinline__ void tap_row(const uint8_t* row, int o0, int o1, const uint8_t* fend, uint32_t* a,
-                                        uint32_t* b) {
-  const uint8_t* p = row + o0;
-  const uintptr_t ad = reinterpret_cast<uintptr_t>(p);
-  const uint8_t* base = reinterpret_cast<const uint8_t*>(ad & ~(uintptr_t)3);
-  if (base + 12 <= fend) {
-    const uint3 w = *reinterpret_cast<const uint3*>(base);
-    const unsigned off = (unsigned)(ad & 3), off1 = off + (unsigned)(o1 - o0);  // <= 3 + 4
-    const unsigned lo = __builtin_amdgcn_alignbyte(w.y, w.x, off);                // bytes off .. off+3
-    const unsigned lo1 = off1 < 4 ? __builtin_amdgcn_alignbyte(w.y, w.x, off1)
-                                  : __builtin_amdgcn_alignbyte(w.z, w.y, off1 - 4);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      a[c] = (lo >> (8 * c)) & 0xFFu;
-      b[c] = (lo1 >> (8 * c)) & 0xFFu;
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      a[c] = row[o0 + c];
-      b[c] = row[o1 + c];
-    }
-  }
-}
-
-__device__ __forceinline__ void prep_load_w(const PrepTap& t, const uint8_t* fend, uint32_t v[12]) {
-  if constexpr (VSS_WIDE_TAPS) {
-    tap_row(t.t0, t.o0, t.o1, fend, v, v + 3);
-    tap_row(t.t1, t.o0, t.o1, fend, v + 6, v + 9);
-  } else {
-    prep_load(t, v);
-  }
-}
-
 // v / 255.0f, correctly rounded, without the IEEE division sequence (div_scale,
 // rcp, four FMAs, div_fmas, div_fixup): the reciprocal product corrected by one
 // FMA residual.  Equal to the division for EVERY float in [0, 256] (and by
@@ -307,7 +262,6 @@ __device__ __forceinline__ void stem_body(const StemParams& p, int bx, int by, i
   const int tid = threadIdx.x;
   const int oy0 = by * TH, ox0 = bx * TW;
   const uint8_t* f = p.frames + (long)n * p.frame_stride;
-  const uint8_t* fend = f + (long)(p.fh - 1) * p.row_stride + (long)p.fw * p.fc;
   const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
   VSS_STAMP(0);
   // all frame gathers of this thread issued before any is consumed
@@ -325,7 +279,7 @@ __device__ __forceinline__ void stem_body(const StemParams& p, int bx, int by, i
     const int ly = i / IW, lx = i - ly * IW;
     const int yy = min(max(iy0 + ly, 0), p.Hm - 1), xx = min(max(ix0 + lx, 0), p.Wm - 1);
     const PrepTap t = prep_tap(f, p.row_stride, p.fc, p.fh, p.fw, p.ry, p.rx, yy, xx);
-    prep_load_w(t, fend, raw[u]);
+    prep_load(t, raw[u]);
     dys[u] = t.dy;
     dxs[u] = t.dx;
   }
@@ -737,7 +691,6 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     const StemParams& sp = p.stem;
     const int H = p.H, W = p.W;  // the stem's output = this block's input
     const uint8_t* fr = sp.frames + (long)n * sp.frame_stride;
-    const uint8_t* fend = fr + (long)(sp.fh - 1) * sp.row_stride + (long)sp.fw * sp.fc;
     const int r0 = 2 * iy0 - 1, c0 = 2 * ix0 - 1;  // x0 region origin (model resolution)
     float* x0s = work;                            // [3][XH][XWP]
     float* sws = work + r4(3 * XH * XWP);          // [tap][16]
@@ -756,7 +709,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       const int ly = i / XW, lx = i - ly * XW;
       const int yy = min(max(r0 + ly, 0), sp.Hm - 1), xx = min(max(c0 + lx, 0), sp.Wm - 1);
       const PrepTap t = prep_tap(fr, sp.row_stride, sp.fc, sp.fh, sp.fw, sp.ry, sp.rx, yy, xx);
-      prep_load_w(t, fend, raw[u]);
+      prep_load(t, raw[u]);
       dys[u] = t.dy;
       dxs[u] = t.dx;
     }
@@ -1154,7 +1107,6 @@ __global__ __launch_bounds__(kWideThreads) void k_stem_b1(BlockParams p) {
   const StemParams& sp = p.stem;
   const int H = p.H, W = p.W;  // the stem's output = b1's input
   const uint8_t* fr = sp.frames + (long)n * sp.frame_stride;
-  const uint8_t* fend = fr + (long)(sp.fh - 1) * sp.row_stride + (long)sp.fw * sp.fc;
   const int r0 = 2 * iy0 - 1, c0 = 2 * ix0 - 1;  // x0 region origin (model resolution)
   // every load issued first: the weight image, the stem's weights, the frame taps
   const f4 wv = reinterpret_cast<const f4*>(p.wimg)[min(tid, WIMG4 - 1)];
@@ -1168,7 +1120,7 @@ __global__ __launch_bounds__(kWideThreads) void k_stem_b1(BlockParams p) {
     const int ly = i / XW, lx = i - ly * XW;
     const int yy = min(max(r0 + ly, 0), sp.Hm - 1), xx = min(max(c0 + lx, 0), sp.Wm - 1);
     const PrepTap t = prep_tap(fr, sp.row_stride, sp.fc, sp.fh, sp.fw, sp.ry, sp.rx, yy, xx);
-    prep_load_w(t, fend, raw[u]);
+    prep_load(t, raw[u]);
     dys[u] = t.dy;
     dxs[u] = t.dx;
   }
