@@ -93,8 +93,13 @@ enum {
   /* Read-only counters (vss_get_option; vss_set_option fails): */
   VSS_OPT_GRAPH_BUILDS = 8,  /* executable graphs built (one per slot and shape)            */
   VSS_OPT_GRAPH_PATCHES = 9, /* graph replays that patched their buffers' kernel parameters */
-  VSS_OPT_COMM_RANKS = 10    /* ranks of the handle's RCCL clique (ncclCommCount; the GPUs of a
+  VSS_OPT_COMM_RANKS = 10,   /* ranks of the handle's RCCL clique (ncclCommCount; the GPUs of a
                                 multi-GPU handle; 1 without a clique)                        */
+  VSS_OPT_GATHER_CALLS = 11  /* vss_segment_gather_device calls so far: call i runs on slot (and
+                                that slot's communicator) i % queue_depth, counted apart from the
+                                other device calls, so ranks that interleave different
+                                vss_segment_device calls still agree on every collective's
+                                communicator */
 };
 
 typedef struct vss_handle vss_handle;

@@ -76,3 +76,35 @@ def test_clique_one_rank_gather_bitwise(pkg, synthetic, torch_cuda):
         torch.cuda.synchronize()
         for o in outs:
             assert np.array_equal(o.cpu().numpy(), ref)
+
+
+def test_gather_slot_order_independent_of_other_device_calls(pkg, synthetic, torch_cuda):
+    """Each rank's i-th vss_segment_gather_device runs on slot (and that slot's
+    communicator) i % queue_depth, counted apart from vss_segment_device calls:
+    ranks that interleave different plain device calls still issue every
+    collective on the same communicator (RCCL's ordering requirement).  At one
+    rank: the gather counter moves only with gathers, and interleaved calls of
+    both kinds on several streams keep every result bitwise."""
+    torch = torch_cuda
+    f = _frames(synthetic, 4, start=70)
+    with pkg.Session(dtype="bf16x2", max_batch=4, max_frame_h=480, max_frame_w=640, queue_depth=3) as s:
+        ref, _, _ = s.segment_frames(f)
+        s.comm_init_rank(1, 0, s.comm_unique_id())
+        assert s.get_option(pkg.VSS_OPT_GATHER_CALLS) == 0
+        with pytest.raises(pkg.VssError):
+            s.set_option(pkg.VSS_OPT_GATHER_CALLS, 0)  # read-only
+        d = torch.from_numpy(f).cuda()
+        outs = [torch.zeros((4, 144 * 256), dtype=torch.float32, device="cuda") for _ in range(10)]
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        gathers = 0
+        for i, kind in enumerate("gddgdgggdd"):
+            st = streams[i % 3].cuda_stream
+            if kind == "g":
+                s.segment_gather_device(d.data_ptr(), 4, 480, 640, 3, 640 * 3, 480 * 640 * 3, outs[i].data_ptr(), st)
+                gathers += 1
+            else:
+                s.segment_device(d.data_ptr(), 4, 480, 640, 3, 640 * 3, 480 * 640 * 3, outs[i].data_ptr(), st)
+            assert s.get_option(pkg.VSS_OPT_GATHER_CALLS) == gathers
+        torch.cuda.synchronize()
+        for o in outs:
+            assert np.array_equal(o.cpu().numpy(), ref)

@@ -40,7 +40,7 @@ VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_I
     0, -1, -2, -3, -4, -5, -6, -7)
 DTYPES = {"f32": 0, "bf16x2": 1}
 VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_KEEP_STEM, VSS_OPT_ROW_FETCH = 1, 2, 6, 7
-VSS_OPT_GRAPH_BUILDS, VSS_OPT_GRAPH_PATCHES, VSS_OPT_COMM_RANKS = 8, 9, 10  # read-only counters
+VSS_OPT_GRAPH_BUILDS, VSS_OPT_GRAPH_PATCHES, VSS_OPT_COMM_RANKS, VSS_OPT_GATHER_CALLS = 8, 9, 10, 11  # read-only
 VSS_CREATE_NO_AUTOTUNE = 1
 VSS_OUT_MODEL, VSS_OUT_FRAME = 0, 1
 

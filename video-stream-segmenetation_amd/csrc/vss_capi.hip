@@ -329,7 +329,8 @@ struct vss_handle {
   std::condition_variable slot_cv;   // a slot's host_busy went false
   std::mutex post_mu;              // the synchronous post / composite calls share scratch
   vss_ticket next_ticket = 0;      // host batches (vss_submit*, vss_segment*)
-  unsigned long long device_calls = 0;  // vss_segment_device / _gather_device: slot = count % depth
+  unsigned long long device_calls = 0;  // vss_segment_device: slot = count % depth
+  unsigned long long gather_calls = 0;  // vss_segment_gather_device: slot (and communicator) = count % depth
   long graph_builds = 0, graph_patches = 0;  // VSS_OPT_GRAPH_BUILDS / _PATCHES
   CopyPool* pool = nullptr;
   // The completion thread (started on the first host batch that needs one):
@@ -1989,9 +1990,10 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(h, hipSetDevice(h->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
-  // round-robin over the device calls, so every rank uses the same slot's
-  // communicator for the same call
-  const int k = (int)(h->device_calls++ % h->slots.size());
+  // round-robin over the gather calls alone (a counter of their own), so every
+  // rank uses the same slot's communicator for its i-th gather whatever other
+  // device calls it interleaves
+  const int k = (int)(h->gather_calls++ % h->slots.size());
   Slot& sl = h->slots[k];
   if ((rc = claim_slot(h, sl, s))) return rc;
   if ((rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, sl.d_masks, s))) {
@@ -2087,7 +2089,8 @@ int vss_set_option(vss_handle* h, int option, int value) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (option == 3 || option == 4 || option == 5)
     return fail(h, VSS_E_UNSUPPORTED, "option removed (round-1 experiment measured slower; DESIGN.md)");
-  if (option == VSS_OPT_GRAPH_BUILDS || option == VSS_OPT_GRAPH_PATCHES || option == VSS_OPT_COMM_RANKS)
+  if (option == VSS_OPT_GRAPH_BUILDS || option == VSS_OPT_GRAPH_PATCHES || option == VSS_OPT_COMM_RANKS ||
+      option == VSS_OPT_GATHER_CALLS)
     return fail(h, VSS_E_INVALID_ARG, "read-only option (vss_get_option)");
   if (option != VSS_OPT_KEEP_STEM && option != VSS_OPT_USE_GRAPH && option != VSS_OPT_PROFILE &&
       option != VSS_OPT_ROW_FETCH)
@@ -2124,6 +2127,9 @@ int vss_get_option(vss_handle* h, int option, int* value) {
       *value = (int)std::min<long>(v, 0x7fffffff);
       return VSS_OK;
     }
+    case VSS_OPT_GATHER_CALLS:
+      *value = (int)(h->gather_calls & 0x7FFFFFFF);
+      return VSS_OK;
     case VSS_OPT_COMM_RANKS: {
       if (h->rccl) {
         *value = 1 + (int)h->peers.size();
