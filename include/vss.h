@@ -303,7 +303,7 @@ int vss_layer_kernel(const vss_handle* h, int layer, char* buf, int cap);
  * and the head), at most `cap` written.  Any of them can be pinned with the
  * environment variable VSS_TILE="layer:THxTW[,...]" at vss_create, or by
  * index, VSS_TILE="layer:#k" (a tile can be compiled as more than one kernel:
- * b1's k_block, k_stem_b1 and k_stem_b1s); results do not depend on the tile
+ * b1's k_block and the wide k_stem_b1); results do not depend on the tile
  * (bitwise). */
 int vss_layer_tiles(const vss_handle* h, int layer, int* th, int* tw, int cap);
 

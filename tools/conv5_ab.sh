@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-for v in 0 1 0 1; do
+for v in 0 1 2 0 1 2; do
   VSO_CONV_DEEP_TILE=$v timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/t$v" -o run -- \
     python3 "$R/tools/bench_onnx.py" --only-modnet --batch 8 --cases modnet_288x512_b8_bf16 --iters 20 --warmup 5 \
     > "$OUT/t$v.log" 2>&1
