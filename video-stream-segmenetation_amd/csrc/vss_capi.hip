@@ -165,7 +165,11 @@ thread_local std::string g_tls_error;
 // frames from the caches.  Plain memcpy where AVX2 is absent or the
 // destination is not 32-byte aligned (env VSS_PLAIN_MEMCPY=1 forces it).
 // Measured on the box's 16-CPU share (noisy): VGA copy path ~26k -> ~29k
-// frames/s, 1080p ~17k -> ~20k; the zero-copy path does not copy.
+// frames/s, 1080p ~17k -> ~20k; the zero-copy path does not copy.  Since the
+// staging copies only the rows the resize reads, a VGA batch is ~1150 row runs
+// of 3840 B each (two rows): the streaming path takes pieces from 512 B on
+// (it was 4 KiB, which sent every VGA run through plain memcpy and its
+// read-for-ownership of the destination).
 __attribute__((target("avx2"))) static void stream_copy_avx2(void* dst, const void* src, size_t len) {
   char* d = static_cast<char*>(dst);
   const char* s = static_cast<const char*>(src);
@@ -186,7 +190,7 @@ __attribute__((target("avx2"))) static void stream_copy_avx2(void* dst, const vo
 
 static void staging_copy(void* dst, const void* src, size_t len) {
   static const bool avx2 = __builtin_cpu_supports("avx2") && !getenv("VSS_PLAIN_MEMCPY");
-  if (avx2 && (reinterpret_cast<uintptr_t>(dst) & 31) == 0 && len >= 4096) stream_copy_avx2(dst, src, len);
+  if (avx2 && (reinterpret_cast<uintptr_t>(dst) & 31) == 0 && len >= 512) stream_copy_avx2(dst, src, len);
   else std::memcpy(dst, src, len);
 }
 

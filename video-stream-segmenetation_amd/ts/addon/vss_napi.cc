@@ -50,6 +50,10 @@
 // so the event loop is not blocked — as `await session.run` does not block.
 #include <node_api.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
@@ -1418,7 +1422,24 @@ napi_value FaceDestroy(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+// VSS_NAPI_SEGV_TRACE=1: a fatal signal prints the native backtrace to
+// stderr before the process dies (diagnosing crashes at process exit).
+void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "vss_napi: fatal signal, native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 napi_value Init(napi_env env, napi_value exports) {
+  if (const char* e = std::getenv("VSS_NAPI_SEGV_TRACE"))
+    if (e[0] == '1') {
+      signal(SIGSEGV, segv_trace);
+      signal(SIGABRT, segv_trace);
+    }
   const napi_property_descriptor props[] = {
       {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"create", nullptr, Create, nullptr, nullptr, nullptr, napi_default, nullptr},
