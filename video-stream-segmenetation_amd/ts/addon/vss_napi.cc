@@ -55,6 +55,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -511,9 +512,15 @@ struct MaskBlock {
   bool pinned;
 };
 
-std::mutex g_pool_mu;
-std::multimap<size_t, void*> g_pool;  // free pinned blocks by size
+// Never destroyed: result ArrayBuffers can be finalized while the process
+// exits (V8 tearing the environment down), after static destructors of this
+// module could otherwise have run.
+std::mutex& g_pool_mu = *new std::mutex;
+std::multimap<size_t, void*>& g_pool = *new std::multimap<size_t, void*>;  // free pinned blocks by size
 size_t g_pinned_bytes = 0;             // every pinned block, free or live
+// Set by the environment's cleanup hook: finalizers that run during teardown
+// make no more N-API calls (the env is going away).
+std::atomic<bool> g_env_closing{false};
 constexpr size_t kPinnedCap = size_t(1) << 30;
 
 // VSS_NAPI_PINNED=0: malloc'd results (the completion copies), for A/B runs
@@ -566,8 +573,10 @@ void free_masks(napi_env env, void* data, void* hint) {
     pool_put(data, b->bytes);
   else
     std::free(data);
-  int64_t adj = 0;
-  napi_adjust_external_memory(env, -(int64_t)b->bytes, &adj);
+  if (!g_env_closing.load()) {
+    int64_t adj = 0;
+    napi_adjust_external_memory(env, -(int64_t)b->bytes, &adj);
+  }
   delete b;
 }
 
@@ -1434,7 +1443,10 @@ void segv_trace(int sig) {
   raise(sig);
 }
 
+void env_cleanup(void*) { g_env_closing.store(true); }
+
 napi_value Init(napi_env env, napi_value exports) {
+  napi_add_env_cleanup_hook(env, env_cleanup, nullptr);
   if (const char* e = std::getenv("VSS_NAPI_SEGV_TRACE"))
     if (e[0] == '1') {
       signal(SIGSEGV, segv_trace);
