@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export VSS_NAPI_SEGV_TRACE=1
 timeout -k 10 300 python -u -m pytest tests/test_ts.py -x -q --timeout 200 --timeout-method thread > gpurun_out/tsx_tests.log 2>&1; rc=$?
 tail -2 gpurun_out/tsx_tests.log; [ $rc -ne 0 ] && exit $rc
-for k in 1 2; do
+for k in 1 2 3; do
   VSS_TIME_SUBMIT=1 timeout -k 10 150 node tools/ts_copy_probe.js 400 > gpurun_out/tsx_probe$k.log 2>&1; rc=$?
   echo "probe $k rc=$rc"; tail -4 gpurun_out/tsx_probe$k.log | cut -c1-220; [ $rc -ne 0 ] && exit $rc
 done
