@@ -19,8 +19,6 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-
 #include "vso_device.h"
 #include "vso_kernels.h"
 
@@ -173,41 +171,35 @@ __global__ __launch_bounds__(256) void k_conv_dwpw(ConvParams p) {
     }
   }
   __syncthreads();
-  // phase 2: the workgroup's output channels (blockIdx.y's share of the
-  // 64-channel groups: the launcher gives a workgroup several groups when
-  // there are enough pixel tiles to fill the chip, so the depthwise above is
-  // not recomputed once per 64 output channels), 16 at a time per wave, x
-  // the 16 pixels
-  const int groups = (p.M + 63) / 64, per = (groups + (int)gridDim.y - 1) / (int)gridDim.y;
-  const int mend = min(p.M, ((int)blockIdx.y + 1) * per * 64);
+  // phase 2: this wave's 16 output channels x the 16 pixels
+  const int m0 = blockIdx.y * 64 + wave * 16;
+  if (m0 >= p.M) return;
+  const int m = m0 + r;
+  const bool m_ok = m < p.M;
+  const float* wrow = p.w + (long)(m_ok ? m : 0) * K;
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  constexpr int CH = 8;
+  for (int k0 = 0; k0 < K; k0 += 4 * CH) {
+    float a[CH];
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const int k = k0 + 4 * s + g;
+      a[s] = (m_ok && k < K) ? wrow[k] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const int k = k0 + 4 * s + g;
+      if (k0 + 4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], k < K ? bs[k][r] : 0.f, acc, 0, 0, 0);
+    }
+  }
   const int pix = tp * 16 + r;
-  for (int m0 = (int)blockIdx.y * per * 64 + wave * 16; m0 < mend; m0 += 64) {
-    const int m = m0 + r;
-    const bool m_ok = m < p.M;
-    const float* wrow = p.w + (long)(m_ok ? m : 0) * K;
-    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-    constexpr int CH = 8;
-    for (int k0 = 0; k0 < K; k0 += 4 * CH) {
-      float a[CH];
+  if (pix >= P) return;
 #pragma unroll
-      for (int s = 0; s < CH; ++s) {
-        const int k = k0 + 4 * s + g;
-        a[s] = (m_ok && k < K) ? wrow[k] : 0.f;
-      }
-#pragma unroll
-      for (int s = 0; s < CH; ++s) {
-        const int k = k0 + 4 * s + g;
-        if (k0 + 4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], k < K ? bs[k][r] : 0.f, acc, 0, 0, 0);
-      }
-    }
-    if (pix >= P) continue;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int ch = m0 + 4 * g + v;
-      if (ch >= p.M) continue;
-      const long o = ((long)n * p.M + ch) * P + pix;
-      p.y[o] = epilogue(p.ep, acc[v], ch, o, n, pix);
-    }
+  for (int v = 0; v < 4; ++v) {
+    const int ch = m0 + 4 * g + v;
+    if (ch >= p.M) continue;
+    const long o = ((long)n * p.M + ch) * P + pix;
+    p.y[o] = epilogue(p.ep, acc[v], ch, o, n, pix);
   }
 }
 
@@ -388,20 +380,7 @@ const char* conv_kernel_name(const ConvParams& p) {
 void launch_conv(const ConvParams& p, hipStream_t s, const char** name) {
   if (name) *name = conv_kernel_name(p);
   if (p.pre.w) {
-    // 64-channel groups of the 1x1 per workgroup: one each while that is what
-    // fills the chip (>= 512 workgroups), else as few splits as keep >= 512,
-    // so the depthwise of a pixel tile is computed once per split, not once
-    // per 64 output channels (VSO_DWPW_SPLIT=1: the old one-group form)
-    static const bool one_group = [] {
-      const char* e = std::getenv("VSO_DWPW_SPLIT");
-      return e && std::atoi(e) == 1;
-    }();
-    const long tiles = (long)((p.Ho * p.Wo + 15) / 16) * p.N;
-    const int groups = (p.M + 63) / 64;
-    int split = groups;
-    if (!one_group)
-      while (split > 1 && tiles * (split - 1) >= 512) --split;
-    const dim3 grid((unsigned)((p.Ho * p.Wo + 15) / 16), (unsigned)split, (unsigned)p.N);
+    const dim3 grid((unsigned)((p.Ho * p.Wo + 15) / 16), (unsigned)((p.M + 63) / 64), (unsigned)p.N);
     hipLaunchKernelGGL(k_conv_dwpw, grid, dim3(256), 0, s, p);
     return;
   }
