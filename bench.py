@@ -369,6 +369,10 @@ def main():
     ts = None
     if rank == 0 and world == 1 and not args.no_ts:
         ts = ts_leg(B, fh, fw, max(100, min(args.steps, 400)), args.inflight)  # before this process touches the GPU
+        # the Node process's GPU context is torn down after it exits; one full
+        # bench (r03i) timed its headline 9 % under its own median step right
+        # after this leg, so the headline starts on a settled device
+        time.sleep(2.0)
 
     import torch
     import torch.distributed as dist
