@@ -204,6 +204,7 @@ void launch_norm_apply(const NormParams& p, hipStream_t s);
 constexpr int kNormChunk = 4096;  // elements per k_norm_stats / k_norm_apply workgroup
 void launch_softmax(const RowParams& p, hipStream_t s);
 void launch_affine(const AffineParams& p, hipStream_t s);
+const char* resize_kernel_name(const ResizeParams& p);  // the kernel launch_resize picks (profiles)
 void launch_resize(const ResizeParams& p, hipStream_t s);
 void launch_gemm(const GemmParams& p, hipStream_t s);
 bool gemm_vec(const GemmParams& p);

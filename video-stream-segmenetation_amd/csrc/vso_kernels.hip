@@ -665,25 +665,36 @@ __device__ __forceinline__ int nearest_idx(float v, int mode, int in) {
   return i < 0 ? 0 : (i > in - 1 ? in - 1 : i);
 }
 
+__device__ __forceinline__ float resize_one(const ResizeParams& p, const float* __restrict__ xc, int oy, int ox) {
+  const float fy = resize_src(oy, p.sy, p.H, p.Ho, p.ctm), fx = resize_src(ox, p.sx, p.W, p.Wo, p.ctm);
+  if (!p.linear) return xc[(long)nearest_idx(fy, p.nearest, p.H) * p.W + nearest_idx(fx, p.nearest, p.W)];
+  const float sy = fminf(fmaxf(fy, 0.f), (float)(p.H - 1)), sx = fminf(fmaxf(fx, 0.f), (float)(p.W - 1));
+  const int y0 = (int)sy, x0 = (int)sx;
+  const int y1 = min(y0 + 1, p.H - 1), x1 = min(x0 + 1, p.W - 1);
+  const float ly = sy - (float)y0, lx = sx - (float)x0;
+  const float v00 = xc[(long)y0 * p.W + x0], v01 = xc[(long)y0 * p.W + x1];
+  const float v10 = xc[(long)y1 * p.W + x0], v11 = xc[(long)y1 * p.W + x1];
+  return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+}
+
+// Four consecutive outputs of one row per thread (rows of a multiple of 4:
+// one index split and one source row per 4 outputs, one float4 store; other
+// widths one output per thread), 32-bit index math — the flat 64-bit index's
+// three 64-bit divisions per output were most of the old kernel's
+// instructions.  Same arithmetic per output (resize_one).
+template <bool QUAD>
 __global__ __launch_bounds__(256) void k_resize(ResizeParams p) {
-  const long total = (long)p.N * p.C * p.Ho * p.Wo;
-  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
-    const int ox = (int)(o % p.Wo);
-    const long t = o / p.Wo;
-    const int oy = (int)(t % p.Ho);
-    const long nc = t / p.Ho;
-    const float* xc = p.x + nc * p.H * p.W;
-    const float fy = resize_src(oy, p.sy, p.H, p.Ho, p.ctm), fx = resize_src(ox, p.sx, p.W, p.Wo, p.ctm);
-    if (!p.linear) {
-      p.y[o] = xc[(long)nearest_idx(fy, p.nearest, p.H) * p.W + nearest_idx(fx, p.nearest, p.W)];
+  const int total = p.N * p.C * p.Ho * p.Wo, step = QUAD ? 4 : 1;
+  for (long ol = (blockIdx.x * 256L + threadIdx.x) * step; ol < total; ol += gridDim.x * 256L * step) {
+    const int o = (int)ol, ox = o % p.Wo, t = o / p.Wo, oy = t % p.Ho, nc = t / p.Ho;
+    const float* xc = p.x + (long)nc * p.H * p.W;
+    if constexpr (QUAD) {
+      f4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = resize_one(p, xc, oy, ox + e);
+      *reinterpret_cast<f4*>(p.y + o) = v;
     } else {
-      const float sy = fminf(fmaxf(fy, 0.f), (float)(p.H - 1)), sx = fminf(fmaxf(fx, 0.f), (float)(p.W - 1));
-      const int y0 = (int)sy, x0 = (int)sx;
-      const int y1 = min(y0 + 1, p.H - 1), x1 = min(x0 + 1, p.W - 1);
-      const float ly = sy - (float)y0, lx = sx - (float)x0;
-      const float v00 = xc[(long)y0 * p.W + x0], v01 = xc[(long)y0 * p.W + x1];
-      const float v10 = xc[(long)y1 * p.W + x0], v11 = xc[(long)y1 * p.W + x1];
-      p.y[o] = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+      p.y[o] = resize_one(p, xc, oy, ox);
     }
   }
 }
@@ -800,8 +811,18 @@ void launch_softmax(const RowParams& p, hipStream_t s) {
 void launch_affine(const AffineParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_affine, dim3(grid_for(p.n)), dim3(256), 0, s, p);
 }
+static bool resize_quad(const ResizeParams& p) {
+  return (p.Wo & 3) == 0 && (reinterpret_cast<uintptr_t>(p.y) & 15) == 0;
+}
+const char* resize_kernel_name(const ResizeParams& p) {
+  return resize_quad(p) ? "void vso::k_resize<true>(vso::ResizeParams)" : "void vso::k_resize<false>(vso::ResizeParams)";
+}
 void launch_resize(const ResizeParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_resize, dim3(grid_for((long)p.N * p.C * p.Ho * p.Wo)), dim3(256), 0, s, p);
+  const long total = (long)p.N * p.C * p.Ho * p.Wo;  // < 2^31: checked by the planner
+  if (resize_quad(p))
+    hipLaunchKernelGGL(k_resize<true>, dim3(grid_for(total / 4)), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(k_resize<false>, dim3(grid_for(total)), dim3(256), 0, s, p);
 }
 void launch_gemm(const GemmParams& p, hipStream_t s) {
   const int tm = (p.M + 15) / 16, tn = (p.N + 15) / 16;

@@ -1502,7 +1502,8 @@ struct Planner {
       p.x = dptr(*x);
       if (!set_runtime(nd.out[0], {xs[0], xs[1], p.Ho, p.Wo})) return false;
       p.y = dptr(vals[nd.out[0]]);
-      add("vso::k_resize(vso::ResizeParams)", [p](hipStream_t st) { launch_resize(p, st); });
+      if ((long)p.N * p.C * p.Ho * p.Wo >= (1L << 31)) return fail("Resize: output of 2^31 elements or more");
+      add(resize_kernel_name(p), [p](hipStream_t st) { launch_resize(p, st); });
       return true;
     }
     if (op == "MatMul" || op == "Gemm") {
