@@ -120,6 +120,11 @@ def ops_zoo():
                coordinate_transformation_mode="asymmetric", nearest_mode="floor")
     upa = b.op("Resize", [x, "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
                coordinate_transformation_mode="align_corners")
+    # rows of a width that is not a multiple of 4: k_resize's one-output-per-thread form
+    upo = b.op("Resize", [x, "", "", b.const(np.array([2, 8, 15, 21], np.int64))], mode="linear",
+               coordinate_transformation_mode="pytorch_half_pixel")
+    upc = b.op("Resize", [x, "", "", b.const(np.array([2, 8, 7, 10], np.int64))], mode="nearest",
+               coordinate_transformation_mode="half_pixel", nearest_mode="round_prefer_ceil")
     inn = b.op("InstanceNormalization", [up, b.const(b.rng.random(8).astype(np.float32) + 0.5),
                                          b.const(b.rng.standard_normal(8).astype(np.float32))], epsilon=1e-5)
     gap = b.op("GlobalAveragePool", [x])                                    # [2, 8, 1, 1]
@@ -130,7 +135,7 @@ def ops_zoo():
     sq = b.op("Squeeze", [sq, b.const(np.array([1], np.int64))])            # [2, 5]
     return b.model([("x", [2, 8, 12, 16])],
                    [(smx, [2, 60, 4]), (inn, [2, 8, 24, 32]), (upn, [2, 8, 18, 24]), (upa, [2, 8, 24, 32]),
-                    (sq, [2, 5])])
+                    (sq, [2, 5]), (upo, [2, 8, 15, 21]), (upc, [2, 8, 7, 10])])
 
 
 def modnet_like(h=64, w=96):
