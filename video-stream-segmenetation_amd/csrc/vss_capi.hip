@@ -2167,6 +2167,12 @@ int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels
     forward_launches(h, s, nullptr, n, height, width, channels, row_stride, frame_stride, nullptr, &ls);
     GraphEntry g;
     if ((rc = build_graph(h, ls, &g))) return rc;
+    // the executable's device-side state now, not at its first launch
+    if (const hipError_t e = hipGraphUpload(g.exec, s.stream); e != hipSuccess) {
+      destroy_graph(g);
+      return fail(h, VSS_E_HIP, std::string("hipGraphUpload: ") + hipGetErrorString(e));
+    }
+    HIP_TRY(h, hipStreamSynchronize(s.stream));
     s.graphs.emplace(key, std::move(g));
   }
   return VSS_OK;
