@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--settle", type=float, default=0.0, help="seconds of sleep after prepare_device")
+    ap.add_argument("--spin", type=float, default=0.0, help="seconds of host busy-wait after prepare_device")
     ap.add_argument("--pre", default="none", choices=["none", "query", "sleep", "calls"])
     a = ap.parse_args()
     import torch
@@ -28,6 +30,10 @@ def main():
         outs = [torch.empty((B, s.mask_h * s.mask_w), device="cuda") for _ in range(S)]
         sts = [torch.cuda.Stream() for _ in range(S)]
         s.prepare_device(B, fh, fw, 3, fw * 3, fh * fw * 3)
+        time.sleep(a.settle)
+        t_end = time.perf_counter() + a.spin
+        while time.perf_counter() < t_end:
+            pass
 
         def step(i):
             s.segment_device(d.data_ptr(), B, fh, fw, 3, fw * 3, fh * fw * 3, outs[i % S].data_ptr(),
