@@ -232,7 +232,11 @@ int vss_host_free(void* ptr);
  * handle's first GPU; the work is enqueued on `stream` (a hipStream_t; NULL =
  * the handle's stream) and not waited for.  frame_stride = bytes between
  * frames.  Consecutive calls take consecutive slots, so calls on different
- * streams run concurrently (each stream sees its own calls in order). */
+ * streams run concurrently (each stream sees its own calls in order).  A
+ * call on the stream that ran the slot's previous work relies on stream order
+ * instead of an event wait (VSS_SAME_STREAM_SKIP=0 in the environment turns
+ * that off), so a stream destroyed with this handle's work in flight must not
+ * be replaced by a new stream at the same address until that work is done. */
 int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width,
                        int channels, size_t row_stride, size_t frame_stride, float* d_masks,
                        void* stream);
