@@ -249,25 +249,38 @@ __global__ __launch_bounds__(256) void k_conv_small(ConvParams p, int tiles_m, i
     const int iy = iy0 + ky * p.dh, ix = ix0 + kx * p.dw;
     return (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? xg[((long)c * p.H + iy) * p.W + ix] : 0.f;
   };
-  float a[CH], b[CH];
+  // A operands: with K % 4 == 0 and 16-B aligned weights, MFMA 4t + e of a
+  // chunk takes k = k0 + 16 t + 4 g + e, so a lane's four A elements of MFMAs
+  // 4t .. 4t+3 are one float4 of its weight row (a quarter of the load
+  // instructions); otherwise MFMA s takes k = k0 + 4 s + g, one float each.
+  const bool av = (K & 3) == 0 && (reinterpret_cast<uintptr_t>(p.w) & 15) == 0;
+  auto kof = [&](int k0, int s) { return av ? k0 + 16 * (s >> 2) + 4 * g + (s & 3) : k0 + 4 * s + g; };
+  auto load_chunk = [&](int k0, float* a, float* b) {
+    if (av) {
 #pragma unroll
-  for (int s = 0; s < CH; ++s) {
-    const int k = kbeg + 4 * s + g;
-    a[s] = (m_ok && k < kend) ? wrow[k] : 0.f;
-    b[s] = bval(k);
-  }
+      for (int t = 0; t < CH / 4; ++t) {
+        const int kb = k0 + 16 * t + 4 * g;  // kend % 4 == 0: all four or none
+        const f4 w4 = (m_ok && kb < kend) ? *reinterpret_cast<const f4*>(wrow + kb) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[4 * t + e] = w4[e];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        const int k = kof(k0, s);
+        a[s] = (m_ok && k < kend) ? wrow[k] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < CH; ++s) b[s] = bval(kof(k0, s));
+  };
+  float a[CH], b[CH];
+  load_chunk(kbeg, a, b);
   f4 acc = f4{0.f, 0.f, 0.f, 0.f};
   for (int k0 = kbeg; k0 < kend; k0 += 4 * CH) {
     const bool more = k0 + 4 * CH < kend;
     float an[CH], bn[CH];
-    if (more) {
-#pragma unroll
-      for (int s = 0; s < CH; ++s) {  // the next chunk's loads, in flight during this chunk's MFMAs
-        const int k = k0 + 4 * CH + 4 * s + g;
-        an[s] = (m_ok && k < kend) ? wrow[k] : 0.f;
-        bn[s] = bval(k);
-      }
-    }
+    if (more) load_chunk(k0 + 4 * CH, an, bn);  // the next chunk's loads, in flight during this chunk's MFMAs
 #pragma unroll
     for (int s = 0; s < CH; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
     if (more) {
