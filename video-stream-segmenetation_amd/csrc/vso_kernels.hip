@@ -179,17 +179,36 @@ __global__ __launch_bounds__(256) void k_conv_dwpw(ConvParams p) {
   const float* wrow = p.w + (long)(m_ok ? m : 0) * K;
   f4 acc = f4{0.f, 0.f, 0.f, 0.f};
   constexpr int CH = 8;
-  for (int k0 = 0; k0 < K; k0 += 4 * CH) {
-    float a[CH];
+  if ((K & 15) == 0 && (reinterpret_cast<uintptr_t>(p.w) & 15) == 0) {
+    // as k_conv_small: MFMA 4t + e takes k = k0 + 16 t + 4 g + e, a lane's
+    // four weights of MFMAs 4t .. 4t+3 one float4 (K % 16 == 0: every MFMA full)
+    for (int k0 = 0; k0 < K; k0 += 4 * CH) {
+      f4 a4[CH / 4];
 #pragma unroll
-    for (int s = 0; s < CH; ++s) {
-      const int k = k0 + 4 * s + g;
-      a[s] = (m_ok && k < K) ? wrow[k] : 0.f;
+      for (int t = 0; t < CH / 4; ++t) {
+        const int kb = k0 + 16 * t + 4 * g;
+        a4[t] = (m_ok && kb < K) ? *reinterpret_cast<const f4*>(wrow + kb) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int t = 0; t < CH / 4; ++t)
+        if (k0 + 16 * t < K)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[t][e], bs[k0 + 16 * t + 4 * g + e][r], acc, 0, 0, 0);
     }
+  } else {
+    for (int k0 = 0; k0 < K; k0 += 4 * CH) {
+      float a[CH];
 #pragma unroll
-    for (int s = 0; s < CH; ++s) {
-      const int k = k0 + 4 * s + g;
-      if (k0 + 4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], k < K ? bs[k][r] : 0.f, acc, 0, 0, 0);
+      for (int s = 0; s < CH; ++s) {
+        const int k = k0 + 4 * s + g;
+        a[s] = (m_ok && k < K) ? wrow[k] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        const int k = k0 + 4 * s + g;
+        if (k0 + 4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], k < K ? bs[k][r] : 0.f, acc, 0, 0, 0);
+      }
     }
   }
   const int pix = tp * 16 + r;
