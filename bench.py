@@ -281,14 +281,15 @@ def _free_port() -> int:
         return so.getsockname()[1]
 
 
-def launch_ranks(n: int) -> int:
+def launch_ranks(n: int, check_gpus: bool = True) -> int:
     """--gpus N without a torch.distributed launcher: start N rank processes
     (torch.distributed.run, one per GPU) from this process, which has not
     touched the GPU (device_count() does not initialise HIP on this image),
-    and return their exit code.  Fewer than N visible GPUs is an error."""
+    and return their exit code.  Fewer than N visible GPUs is an error (except
+    for --dry-run-dist, which never reaches a GPU call)."""
     import torch
     ndev = torch.cuda.device_count()
-    if ndev < n:
+    if check_gpus and ndev < n:
         print(f"bench.py: --gpus {n} needs {n} GPUs, {ndev} visible", file=sys.stderr, flush=True)
         return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -350,12 +351,16 @@ def main():
     ap.add_argument("--no-sweep", action="store_true", help="skip the batch sweep")
     ap.add_argument("--gather", action="store_true",
                     help="run the multi-GPU step (RCCL clique all-gather) even at one rank (a rehearsal of N > 1)")
+    ap.add_argument("--dry-run-dist", action="store_true",
+                    help="rehearse the multi-rank plumbing only (launch_ranks -> torch.distributed.run -> gloo "
+                         "-> the clique-id broadcast, with placeholder id bytes) and stop before the first GPU "
+                         "call: each rank prints one JSON line; runs on a machine without GPUs")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_traffic.json"),
                     help="per-kernel HBM traffic from tools/prof_summary.py (PMC passes)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus))
+        sys.exit(launch_ranks(args.gpus, check_gpus=not args.dry_run_dist))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks", file=sys.stderr, flush=True)
@@ -367,7 +372,7 @@ def main():
     B = args.batch
 
     ts = None
-    if rank == 0 and world == 1 and not args.no_ts:
+    if rank == 0 and world == 1 and not args.no_ts and not args.dry_run_dist:
         ts = ts_leg(B, fh, fw, max(100, min(args.steps, 400)), args.inflight)  # before this process touches the GPU
         # the Node process's GPU context is torn down after it exits; one full
         # bench (r03i) timed its headline 9 % under its own median step right
@@ -381,6 +386,21 @@ def main():
         # the process group carries only the clique id, barriers and the max-time
         # reduction (CPU tensors); the masks go over the handle's own RCCL clique
         dist.init_process_group("gloo")
+    if args.dry_run_dist:
+        # the same broadcast the GPU run makes (rank 0's clique ids -> every
+        # rank), with placeholder bytes of the real size: RCCL's ncclGetUniqueId
+        # needs a GPU.  4 slots x sizeof(ncclUniqueId) = 128 B each.
+        import hashlib
+        ids = [os.urandom(args.inflight * 128) if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(ids, src=0)
+            dist.barrier()
+        print(json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local,
+                          "env_world_size": os.environ.get("WORLD_SIZE"), "ids_len": len(ids[0]),
+                          "ids_sha256": hashlib.sha256(ids[0]).hexdigest()}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     ndev = torch.cuda.device_count()
     if ndev < 1 or (world > 1 and local >= ndev):
         print(f"bench.py: rank {rank} (local {local}) has no GPU ({ndev} visible)", file=sys.stderr, flush=True)

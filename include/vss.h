@@ -73,9 +73,10 @@ enum { VSS_OUT_MODEL = 0, VSS_OUT_FRAME = 1 };
  * removed; DESIGN.md keeps the numbers.  Setting them fails with
  * VSS_E_UNSUPPORTED.) */
 enum {
-  VSS_OPT_USE_GRAPH = 1, /* 1: replay a hipGraph per (slot, shape) (default 1); a call with other
-                            frame / mask buffers patches the graph's first and last kernel nodes
-                            (hipGraphExecKernelNodeSetParams) instead of building a new one */
+  VSS_OPT_USE_GRAPH = 1, /* 1: replay a hipGraph per (slot, shape) (default 1): up to 4 executables
+                            per (slot, shape), each bound to one (frames, masks) buffer pair; a
+                            call with a fifth pair patches the least recently used executable's
+                            first and last kernel nodes (hipGraphExecKernelNodeSetParams) */
   VSS_OPT_PROFILE = 2,   /* 1: time every kernel with HIP events (eager launches)         */
   VSS_OPT_KEEP_STEM = 6, /* 1: the stem fused into layer 1 also stores its activation, so
                             vss_read_layer(0) can report it (a debugging aid: 4.7 MB of HBM
@@ -91,7 +92,8 @@ enum {
                             frames is faster); 0: whole frames by DMA.  Masks are identical
                             either way. */
   /* Read-only counters (vss_get_option; vss_set_option fails): */
-  VSS_OPT_GRAPH_BUILDS = 8,  /* executable graphs built (one per slot and shape)            */
+  VSS_OPT_GRAPH_BUILDS = 8,  /* executable graphs built (per slot and shape, one per buffer pair,
+                                at most 4)                                                   */
   VSS_OPT_GRAPH_PATCHES = 9, /* graph replays that patched their buffers' kernel parameters */
   VSS_OPT_COMM_RANKS = 10,   /* ranks of the handle's RCCL clique (ncclCommCount; the GPUs of a
                                 multi-GPU handle; 1 without a clique)                        */
@@ -141,7 +143,11 @@ typedef struct vss_info {
 /* status callback for vss_segment_async: called on the handle's completion
  * thread once the masks are in masks_out (status = VSS_OK) or the batch
  * failed; in submission order.  No lock is held: the callback may call vss_*
- * functions of its handle (a new submit, vss_query), except vss_destroy. */
+ * functions of its handle (a new submit, vss_query), except vss_destroy.
+ * Only this thread completes host batches, so a call from a callback that
+ * would have to wait for a later batch's completion (vss_wait on it,
+ * vss_synchronize, a blocking vss_segment / vss_staging_acquire when every
+ * slot is still completing) returns VSS_E_BUSY instead of deadlocking. */
 typedef void (*vss_callback)(void* user, int status);
 
 /* Submission ticket of a queued batch (vss_submit, vss_wait). */
@@ -232,11 +238,10 @@ int vss_host_free(void* ptr);
  * handle's first GPU; the work is enqueued on `stream` (a hipStream_t; NULL =
  * the handle's stream) and not waited for.  frame_stride = bytes between
  * frames.  Consecutive calls take consecutive slots, so calls on different
- * streams run concurrently (each stream sees its own calls in order).  A
- * call on the stream that ran the slot's previous work relies on stream order
- * instead of an event wait (VSS_SAME_STREAM_SKIP=0 in the environment turns
- * that off), so a stream destroyed with this handle's work in flight must not
- * be replaced by a new stream at the same address until that work is done. */
+ * streams run concurrently (each stream sees its own calls in order).  Any
+ * caller stream may be used and destroyed at any time: a call waits on the
+ * device for its slot's previous work (an event wait), unless both are on that
+ * slot's own stream (vss_slot_stream), where stream order suffices. */
 int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width,
                        int channels, size_t row_stride, size_t frame_stride, float* d_masks,
                        void* stream);
@@ -244,7 +249,12 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
 /* Build the executable graphs of every slot for this batch shape now (no
  * launch), so the first calls of a steady loop replay instead of building
  * (the graph is otherwise built by the slot's first call of that shape).
- * The device pointers are bound by the first call. */
+ * The device pointers are bound by the first call.  Only the handle's first
+ * GPU is prepared: device calls (vss_segment_device, _gather_device) run
+ * there; a multi-GPU handle's peers run host batches, whose per-GPU shard
+ * shapes build their graphs on first use.  A slot keeps graphs for at most 16
+ * shapes (the oldest shape's are dropped), and up to 4 executables per shape,
+ * each bound to one (frames, masks) buffer pair. */
 int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels, size_t row_stride,
                        size_t frame_stride);
 
@@ -263,6 +273,17 @@ int vss_slot_stream(vss_handle* h, int k, void** stream);
  * the last non-empty shard can be short; its padding rows follow frame n-1).
  * The multi-GPU handle and vss_segment_gather_device callers use this plan. */
 int vss_shard_plan(int n, int nranks, int rank, int* first, int* count, int* per_rank);
+
+/* The multi-GPU handle's copy-out, host-only (no GPU needed): after the
+ * all-gather of a batch of n frames over nranks GPUs (vss_shard_plan), the
+ * gathered buffer holds nranks blocks of per_rank rows, rank r's block being
+ * its shard's frames then padding.  Writes the runs that move every frame's
+ * row to frame order in the caller's buffer — run j copies rows[j] rows from
+ * gathered row src_row[j] to output row dst_row[j]; runs never read a padding
+ * row — and returns their number (at most nranks; each array needs nranks
+ * entries), or VSS_E_INVALID_ARG.  submit_host's D2H (VSS_OUT_MODEL) and the
+ * frame-size upsample (VSS_OUT_FRAME) both follow these runs. */
+int vss_gather_runs(int n, int nranks, int* src_row, int* dst_row, int* rows);
 
 /* ---- one GPU per process (torchrun): an RCCL clique over the processes ------
  * Rank 0 calls vss_comm_unique_id (ids for every slot; *len bytes, at most

@@ -26,3 +26,20 @@ def test_world_size_must_match_gpus():
     r = _run(["--gpus", "4", "--steps", "2"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_gpus_2_dry_run_reaches_the_clique_id_broadcast():
+    """the whole multi-rank launch path of `bench.py --gpus 2`
+    — launch_ranks -> torch.distributed.run -> gloo init -> rank 0's clique-id
+    broadcast — runs here, stopping before the first GPU call: both ranks see
+    WORLD_SIZE=2 and rank 1 holds exactly rank 0's id bytes."""
+    import json
+    r = _run(["--gpus", "2", "--dry-run-dist"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{") and '"dry_run"' in x]
+    by_rank = {d["rank"]: d for d in lines}
+    assert sorted(by_rank) == [0, 1], r.stdout
+    for d in by_rank.values():
+        assert d["world"] == 2 and d["env_world_size"] == "2"
+        assert d["ids_len"] == 4 * 128
+    assert by_rank[0]["ids_sha256"] == by_rank[1]["ids_sha256"]

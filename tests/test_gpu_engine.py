@@ -51,22 +51,132 @@ def test_rotating_buffers_build_once_per_slot(pkg, synthetic, torch_cuda):
                 torch.cuda.synchronize()
                 ref = outs[0].cpu().numpy().copy()
         torch.cuda.synchronize()
-        assert s.graph_builds == 4, s.graph_builds  # one per slot, none per buffer
-        assert s.graph_patches > 0
+        # every slot sees all 3 buffers: one executable per (slot, buffer pair), never a patch
+        # (the single executable per slot waited on every call of this pattern)
+        assert s.graph_builds == 12, s.graph_builds
+        assert s.graph_patches == 0, s.graph_patches
         for o in outs:
             assert np.array_equal(o.cpu().numpy(), ref)
-        # another frame buffer (a patched first layer) computes the same masks
+        # another frame buffer (a new pair: slot 0's fourth executable) computes the same masks
         d2 = d.clone()
         o2 = torch.empty_like(outs[0])
         s.segment_device(d2.data_ptr(), B, h, w, 3, w * 3, h * w * 3, o2.data_ptr(), st)
         torch.cuda.synchronize()
         assert np.array_equal(o2.cpu().numpy(), ref)
-        assert s.graph_builds == 4
-        # a new batch shape builds again (once per slot)
+        assert s.graph_builds == 13
+        # a new batch shape builds again
         s.segment_device(d.data_ptr(), 2, h, w, 3, w * 3, h * w * 3, o2.data_ptr(), st)
         torch.cuda.synchronize()
-        assert s.graph_builds == 5
+        assert s.graph_builds == 14
         assert np.array_equal(o2.cpu().numpy()[:2], ref[:2])
+
+
+def test_graph_lru_patches_beyond_four_buffer_pairs(pkg, synthetic, torch_cuda):
+    """One slot, five buffer pairs in rotation: four executables are built, and
+    each later call with a pair no executable holds patches the least recently
+    used one (after its own last launch) — masks bitwise equal throughout."""
+    torch = torch_cuda
+    B, h, w = 2, 240, 320
+    f = _frames(synthetic, B, h, w, start=7)
+    d = torch.from_numpy(f).cuda()
+    with pkg.Session(max_batch=B, max_frame_h=h, max_frame_w=w, queue_depth=1) as s:
+        want, _, _ = s.segment_frames(f)
+        outs = [torch.empty((B, s.mask_h * s.mask_w), device="cuda") for _ in range(5)]
+        st = torch.cuda.Stream()
+        for i in range(20):
+            outs[i % 5].zero_()
+            s.segment_device(d.data_ptr(), B, h, w, 3, w * 3, h * w * 3, outs[i % 5].data_ptr(), st.cuda_stream)
+            st.synchronize()
+            assert np.array_equal(outs[i % 5].cpu().numpy(), want), i
+        assert s.graph_builds == 4, s.graph_builds
+        assert s.graph_patches == 16, s.graph_patches  # every call from the fifth on re-binds the LRU one
+        # four pairs in rotation: no patch once each has its executable
+        before = s.graph_patches
+        for i in range(12):
+            s.segment_device(d.data_ptr(), B, h, w, 3, w * 3, h * w * 3, outs[i % 4].data_ptr(), st.cuda_stream)
+        st.synchronize()
+        assert s.graph_patches - before <= 4
+        for o in outs[:4]:
+            assert np.array_equal(o.cpu().numpy(), want)
+
+
+def test_caller_stream_destroyed_and_recreated(pkg, synthetic, torch_cuda):
+    """a caller stream may be destroyed with the handle's work
+    queued on it and a new stream (often at the same address) used at once:
+    calls on caller streams always wait for their slot's previous work."""
+    import ctypes
+    torch = torch_cuda
+    hip = ctypes.CDLL("libamdhip64.so")
+    B, h, w = 8, 480, 640
+    f = _frames(synthetic, B, h, w, start=11)
+    d = torch.from_numpy(f).cuda()
+    with pkg.Session(max_batch=B, max_frame_h=h, max_frame_w=w, queue_depth=4) as s:
+        want, _, _ = s.segment_frames(f)
+        outs = [torch.empty((B, s.mask_h * s.mask_w), device="cuda") for _ in range(8)]
+        addrs = []
+        for rep in range(4):
+            stp = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(stp)) == 0
+            addrs.append(stp.value)
+            for i in range(8):
+                s.segment_device(d.data_ptr(), B, h, w, 3, w * 3, h * w * 3, outs[i].data_ptr(), stp.value)
+            assert hip.hipStreamDestroy(stp) == 0  # work still queued on it
+        torch.cuda.synchronize()
+        s.synchronize()
+        for o in outs:
+            assert np.array_equal(o.cpu().numpy(), want)
+
+
+def test_destroy_with_callbacks_pending(pkg, synthetic, torch_cuda):
+    """vss_destroy drains the completion thread before any
+    engine is torn down, so every queued batch's callback fires with its masks
+    before close() returns — on the plain handle and the RCCL (device_ids) one."""
+    B, h, w = 2, 240, 320
+    batches = [_frames(synthetic, B, h, w, start=20 + 3 * i) for i in range(4)]
+    for ids in (None, [0]):
+        s = pkg.Session(max_batch=B, max_frame_h=h, max_frame_w=w, queue_depth=4, device_ids=ids)
+        want = [s.segment_frames(b)[0] for b in batches]
+        fired = []
+        for i, b in enumerate(batches):
+            s.segment_frames_async(b, lambda m, mw, mh, st, i=i: fired.append((i, st, m.copy())))
+        s.close()  # immediately: the four batches are still queued or running
+        assert [x[0] for x in fired] == [0, 1, 2, 3], (ids, fired)
+        for i, st, m in fired:
+            assert st == 0
+            assert np.array_equal(m, want[i]), (ids, i)
+
+
+def test_blocking_calls_from_callback_return_busy(pkg, synthetic, torch_cuda):
+    """a callback runs on the completion thread, the only thread that
+    completes host batches; a blocking call that would wait for a later batch's
+    completion returns VSS_E_BUSY instead of deadlocking."""
+    B, h, w = 2, 240, 320
+    f0 = _frames(synthetic, B, h, w, start=1)
+    f1 = _frames(synthetic, B, h, w, start=2)
+    with pkg.Session(max_batch=B, max_frame_h=h, max_frame_w=w, queue_depth=2) as s:
+        want1, _, _ = s.segment_frames(f1)
+        submitted = threading.Event()
+        box = {}
+        done = threading.Event()
+
+        def cb(_m, _mw, _mh, _st):
+            submitted.wait(10)
+            for name, fn in (("wait", lambda: s.wait(box["t1"])), ("synchronize", s.synchronize)):
+                try:
+                    fn()
+                    box[name] = "returned"
+                except pkg.VssError as e:
+                    box[name] = e.code
+            done.set()
+
+        s.segment_frames_async(f0, cb)
+        box["t1"] = s.submit(f1)  # a copy-out batch: its completion is queued behind the callback
+        submitted.set()
+        assert done.wait(30), "callback deadlocked"
+        assert box["wait"] == pkg.VSS_E_BUSY, box
+        assert box["synchronize"] == pkg.VSS_E_BUSY, box
+        got, _, _ = s.wait(box["t1"])
+        assert np.array_equal(got, want1)
 
 
 def test_prepare_device_builds_ahead(pkg, synthetic, torch_cuda):

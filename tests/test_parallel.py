@@ -40,6 +40,40 @@ def test_shard_plan_exhaustive(R):
         assert all(g is None for g in gathered[n:])
 
 
+@pytest.mark.parametrize("R", range(1, 9))
+@pytest.mark.parametrize("out_mode", ["model", "frame"])
+def test_gather_copy_out_frame_order(R, out_mode):
+    """the multi-GPU handle's copy-out (vss_gather_runs, what
+    submit_host's D2H and frame-size upsample follow) applied to a simulated
+    all-gather — each rank's block = its shard's rows, then padding rows of
+    garbage — puts every frame's row at its frame index and reads no padding.
+    A row is P floats at model resolution or fh*fw after the upsample; the
+    runs are in rows, so both layouts are checked with their row size."""
+    pkg = load_pkg()
+    row = 6 if out_mode == "model" else 10  # elements per row (stand-ins for P / fh*fw)
+    for n in range(0, 71):
+        blocks = []
+        for r in range(R):
+            first, count, per = pkg.shard_plan(n, R, r)
+            blk = np.full((per, row), -1.0, np.float32)  # padding garbage
+            for i in range(count):
+                blk[i] = first + i + np.arange(row) / 100.0
+            blocks.append(blk)
+        gathered = np.concatenate(blocks) if blocks and blocks[0].size else np.zeros((0, row), np.float32)
+        out = np.full((n, row), np.nan, np.float32)
+        runs = pkg.gather_runs(n, R)
+        assert len(runs) <= R
+        for src, dst, rows in runs:
+            assert rows > 0 and 0 <= dst and dst + rows <= n
+            seg = gathered[src:src + rows]
+            assert (seg >= 0).all(), (n, R, src, rows)  # never a padding row
+            out[dst:dst + rows] = seg
+        want = np.arange(n)[:, None] + np.arange(row)[None, :] / 100.0
+        assert np.array_equal(out, want.astype(np.float32)), (n, R)
+        # contiguous shards: one run of n rows from row 0
+        assert runs == ([(0, 0, n)] if n else [])
+
+
 def test_shard_plan_rejects_bad_args():
     pkg = load_pkg()
     for args in ((-1, 2, 0), (4, 0, 0), (4, 2, 2), (4, 2, -1)):

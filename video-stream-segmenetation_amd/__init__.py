@@ -139,6 +139,7 @@ def lib() -> ctypes.CDLL:
                 "vss_prepare_device": ([P, I, I, I, I, S, S], I),
                 "vss_slot_stream": ([P, I, ctypes.POINTER(P)], I),
                 "vss_shard_plan": ([I, I, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)], I),
+                "vss_gather_runs": ([I, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)], I),
                 "vss_host_alloc": ([S, ctypes.POINTER(P)], I),
                 "vss_host_free": ([P], I),
                 "vss_comm_unique_id": ([P, P, S, ctypes.POINTER(S)], I),
@@ -606,6 +607,16 @@ def shard_plan(n: int, nranks: int, rank: int):
     f, c, m = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     _check(lib().vss_shard_plan(n, nranks, rank, ctypes.byref(f), ctypes.byref(c), ctypes.byref(m)))
     return f.value, c.value, m.value
+
+
+def gather_runs(n: int, nranks: int):
+    """The multi-GPU copy-out of an n-frame batch (vss_gather_runs): a list of
+    (src_row, dst_row, rows) runs moving the all-gathered [nranks][per_rank]
+    rows to frame order.  Host-only: no GPU needed."""
+    a, b, c = (ctypes.c_int * max(1, nranks))(), (ctypes.c_int * max(1, nranks))(), (ctypes.c_int * max(1, nranks))()
+    k = lib().vss_gather_runs(n, nranks, a, b, c)
+    _check(min(k, 0))
+    return [(a[j], b[j], c[j]) for j in range(k)]
 
 
 def version() -> int:

@@ -95,15 +95,26 @@ struct Launch {
   } prm;
 };
 
-// A forward's executable graph per (slot, shape).  The caller's frame and
-// mask pointers are not part of the key: a call with other buffers patches the
-// kernel nodes whose parameters differ (hipGraphExecKernelNodeSetParams — the
-// first layer reads the frames, the head writes the masks) instead of
-// capturing a new graph, so callers that rotate buffers never rebuild.
+// A forward's executable graphs per (slot, shape): up to kExecPerShape
+// executables, each bound to the caller buffers (frames, masks) it last ran
+// with.  A call whose buffers match one replays it as is; otherwise a new
+// executable is built while the set has room, and after that the least
+// recently used one is patched (hipGraphExecKernelNodeSetParams on the kernel
+// nodes whose parameters differ — the first layer reads the frames, the head
+// writes the masks) once ITS last launch is done (its own event: the wait is
+// normally over already, since three newer launches were issued after it).
+// So callers rotating up to kExecPerShape buffer pairs through a slot never
+// patch in steady state, and no caller ever waits for the slot's latest work
+// here (the round-3 single executable waited on every call of a
+// caller rotating 3 buffers over 4 slots, holding the handle's lock).
 using GraphKey = std::tuple<int, int, int, int, size_t, size_t>;  // n, fh, fw, fc, row / frame stride
+constexpr int kExecPerShape = 4;
 struct GraphEntry {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
+  hipEvent_t last = nullptr;          // recorded after this executable's latest launch
+  bool launched = false;
+  unsigned long long tick = 0;        // LRU clock of its latest launch
   std::vector<hipGraphNode_t> nodes;  // one kernel node per launch, in order
   std::vector<Launch> launches;       // the parameters the executable graph holds now
 };
@@ -137,7 +148,8 @@ struct Slot {
   vss_ticket ticket = ~0ull;          // latest host ticket that ran in this slot (device calls
                                       // take no ticket and leave it alone)
   bool stem_stored = false;           // the latest forward stored the fused stem (VSS_OPT_KEEP_STEM)
-  std::map<GraphKey, GraphEntry> graphs;
+  std::map<GraphKey, std::vector<GraphEntry>> graphs;
+  unsigned long long graph_tick = 0;
 #ifdef VSS_TRACE
   std::vector<unsigned long long*> trace;  // per layer, [workgroups][16] stamps of this slot's latest forward
 #endif
@@ -151,6 +163,11 @@ struct Slot {
 };
 
 thread_local std::string g_tls_error;
+// The handle whose completion thread this is (null on every other thread): a
+// callback runs there, and only that thread clears host_busy, so a call from a
+// callback that would wait for a host_busy slot returns VSS_E_BUSY instead of
+// waiting for itself.
+thread_local const ::vss_handle* g_tls_completing = nullptr;
 
 // Host threads for the pinned staging copies: a copy is cut into 256 KiB
 // pieces that the pool's threads and the caller take in turn.  Measured on the
@@ -970,9 +987,16 @@ bool has_fused_stem(const vss_handle* h) {
 }
 
 void destroy_graph(GraphEntry& g) {
+  if (g.last && g.launched) (void)hipEventSynchronize(g.last);  // never destroy an executable in flight
   if (g.exec) (void)hipGraphExecDestroy(g.exec);
   if (g.graph) (void)hipGraphDestroy(g.graph);
+  if (g.last) (void)hipEventDestroy(g.last);
   g = GraphEntry();
+}
+
+void destroy_graph_set(std::vector<GraphEntry>& v) {
+  for (GraphEntry& g : v) destroy_graph(g);
+  v.clear();
 }
 
 // Build slot s's executable graph for these launches: one kernel node per
@@ -993,7 +1017,8 @@ int build_graph(vss_handle* h, const std::vector<Launch>& ls, GraphEntry* out) {
     }
     g.nodes.push_back(node);
   }
-  const hipError_t e = hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0);
+  hipError_t e = hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&g.last, hipEventDisableTiming);
   if (e != hipSuccess) {
     destroy_graph(g);
     return fail(h, VSS_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
@@ -1003,16 +1028,21 @@ int build_graph(vss_handle* h, const std::vector<Launch>& ls, GraphEntry* out) {
   return VSS_OK;
 }
 
-// Point slot si's graph at this call's launches: the kernel nodes whose
-// parameter blocks differ (the frames the first layer reads, the masks the
-// head writes) are updated in the executable graph.  An update must not race
-// a launch of the same graph still in flight, so it first waits for the
-// slot's previous work (only callers that change buffers ever get here).
-int patch_graph(vss_handle* h, Slot& s, GraphEntry& g, const std::vector<Launch>& ls) {
+// Kernel nodes of g whose parameter blocks differ from this call's launches.
+int graph_diff(const GraphEntry& g, const std::vector<Launch>& ls) {
+  int d = 0;
+  for (size_t i = 0; i < ls.size(); ++i) d += std::memcmp(&ls[i].prm, &g.launches[i].prm, sizeof(Launch::Prm)) != 0;
+  return d;
+}
+
+// Point executable g at this call's launches: the kernel nodes whose parameter
+// blocks differ are updated.  An update must not race a launch of the same
+// executable still in flight, so it first waits for g's own latest launch.
+int patch_graph(vss_handle* h, GraphEntry& g, const std::vector<Launch>& ls) {
   bool waited = false;
   for (size_t i = 0; i < ls.size(); ++i) {
     if (std::memcmp(&ls[i].prm, &g.launches[i].prm, sizeof(Launch::Prm)) == 0) continue;
-    if (!waited && s.used) HIP_TRY(h, hipEventSynchronize(s.done));
+    if (!waited && g.launched) HIP_TRY(h, hipEventSynchronize(g.last));
     waited = true;
     void* args[1];
     const hipKernelNodeParams kp = node_params(ls[i], args);
@@ -1023,9 +1053,44 @@ int patch_graph(vss_handle* h, Slot& s, GraphEntry& g, const std::vector<Launch>
   return VSS_OK;
 }
 
-// The forward of n frames with slot `si`'s buffers, on stream st: the slot's
-// executable graph for this shape replayed (built on first use, patched when
-// the buffers differ), or eager launches.
+// The executable of slot s for this call (see GraphEntry): one bound to the
+// same buffers, else a new one while the shape's set has room, else the least
+// recently used one patched.
+int pick_graph(vss_handle* h, Slot& s, const GraphKey& key, const std::vector<Launch>& ls, GraphEntry** out) {
+  auto it = s.graphs.find(key);
+  if (it == s.graphs.end()) {
+    if (s.graphs.size() >= 16) {  // bound the cache (shapes per slot)
+      destroy_graph_set(s.graphs.begin()->second);
+      s.graphs.erase(s.graphs.begin());
+    }
+    it = s.graphs.emplace(key, std::vector<GraphEntry>()).first;
+  }
+  std::vector<GraphEntry>& v = it->second;
+  GraphEntry* lru = nullptr;
+  for (GraphEntry& g : v) {
+    if (graph_diff(g, ls) == 0) {
+      *out = &g;
+      return VSS_OK;
+    }
+    if (!lru || !g.launched || (lru->launched && g.tick < lru->tick)) lru = &g;  // never-launched first
+  }
+  if ((int)v.size() < kExecPerShape && !(lru && !lru->launched)) {
+    v.emplace_back();
+    if (int rc = build_graph(h, ls, &v.back())) {
+      v.pop_back();
+      return rc;
+    }
+    *out = &v.back();
+    return VSS_OK;
+  }
+  if (int rc = patch_graph(h, *lru, ls)) return rc;
+  *out = lru;
+  return VSS_OK;
+}
+
+// The forward of n frames with slot `si`'s buffers, on stream st: one of the
+// slot's executable graphs for this shape replayed (pick_graph), or eager
+// launches.
 int forward(vss_handle* h, int si, const uint8_t* frames, int n, int fh, int fw, int fc, size_t rs, size_t fs,
             float* masks, hipStream_t st) {
   Slot& s = h->slots[si];
@@ -1046,26 +1111,18 @@ int forward(vss_handle* h, int si, const uint8_t* frames, int n, int fh, int fw,
     return rc;
   }
   if (!h->use_graph) return launch_eager(h, ls, st, -1);
-  const GraphKey key{n, fh, fw, fc, rs, fs};
-  auto it = s.graphs.find(key);
-  if (it == s.graphs.end()) {
-    GraphEntry g;
-    if (int rc = build_graph(h, ls, &g)) return rc;
-    if (s.graphs.size() >= 16) {  // bound the cache (shapes per slot)
-      destroy_graph(s.graphs.begin()->second);
-      s.graphs.erase(s.graphs.begin());
-    }
-    it = s.graphs.emplace(key, std::move(g)).first;
-  } else if (int rc = patch_graph(h, s, it->second, ls)) {
-    return rc;
-  }
-  HIP_TRY(h, hipGraphLaunch(it->second.exec, st));
+  GraphEntry* g = nullptr;
+  if (int rc = pick_graph(h, s, GraphKey{n, fh, fw, fc, rs, fs}, ls, &g)) return rc;
+  HIP_TRY(h, hipGraphLaunch(g->exec, st));
+  HIP_TRY(h, hipEventRecord(g->last, st));
+  g->launched = true;
+  g->tick = ++s.graph_tick;
   return VSS_OK;
 }
 
 void drop_graphs(vss_handle* h) {
   for (Slot& s : h->slots) {
-    for (auto& kv : s.graphs) destroy_graph(kv.second);
+    for (auto& kv : s.graphs) destroy_graph_set(kv.second);
     s.graphs.clear();
   }
 }
@@ -1090,18 +1147,17 @@ std::vector<vss_handle*> engines(vss_handle* h) {
   return e;
 }
 
-// Stream-order a slot's next user after its previous one (device side).
-// A slot's next user on the stream that recorded its done event is ordered by
-// the stream itself: no hipStreamWaitEvent (5 us of host time per device call,
-// 14 -> 9 us measured with tools/window_probe.py; the headline unchanged,
-// tools/ab_env.sh).  Stream handles are compared by address (vss.h).
-static const bool g_same_stream_skip = [] {
-  const char* v = std::getenv("VSS_SAME_STREAM_SKIP");
-  return v ? std::atoi(v) != 0 : true;
-}();
-
+// Stream-order a slot's next user after its previous one (device side): the
+// caller's stream waits for the slot's done event — except when both this
+// call and the slot's previous work are on the slot's OWN stream
+// (vss_slot_stream), which the handle created and destroys, so no other
+// stream can ever carry its address while the handle lives: stream order then
+// already holds (5 us of host time per device call saved, 14 -> 9 us,
+// tools/window_probe.py).  Round 3 compared any caller stream by address,
+// which a destroyed-and-recreated stream or two threads' hipStreamPerThread
+// could fool; caller streams now always wait.
 int claim_slot(vss_handle* e, Slot& s, hipStream_t st) {
-  if (s.used && !(g_same_stream_skip && st == s.done_stream)) HIP_TRY(e, hipStreamWaitEvent(st, s.done, 0));
+  if (s.used && !(st == s.stream && s.done_stream == s.stream)) HIP_TRY(e, hipStreamWaitEvent(st, s.done, 0));
   return VSS_OK;
 }
 
@@ -1168,6 +1224,8 @@ int pick_slot(vss_handle* h, std::unique_lock<std::mutex>& lk, bool wait_free, i
       if (!h->slots[(k0 + j) % S].leased) k = (k0 + j) % S;
     if (k < 0) return fail(h, VSS_E_BUSY, "every slot is leased (vss_staging_acquire)");
     if (h->slots[k].host_busy) {  // its completion is still running: wait for it
+      if (g_tls_completing == h)
+        return fail(h, VSS_E_BUSY, "called from a completion callback: every slot is still completing");
       h->slot_cv.wait(lk);
       continue;
     }
@@ -1191,6 +1249,29 @@ void shard_plan(int n, int R, int r, int* first, int* count, int* per) {
   *per = m;
 }
 
+// The gathered [R][per] rows -> frame order (vss_gather_runs): rank r's
+// count frames sit at gathered rows r * per .. r * per + count - 1 and belong
+// at output rows first .. first + count - 1; adjacent runs merge (with
+// contiguous shards of per frames they all do: one run of n rows).
+int gather_runs(int n, int R, int* src_row, int* dst_row, int* rows) {
+  int nr = 0;
+  for (int r = 0; r < R; ++r) {
+    int first, count, per;
+    shard_plan(n, R, r, &first, &count, &per);
+    if (count == 0) continue;
+    const int src = r * per;
+    if (nr > 0 && src_row[nr - 1] + rows[nr - 1] == src && dst_row[nr - 1] + rows[nr - 1] == first) {
+      rows[nr - 1] += count;
+    } else {
+      src_row[nr] = src;
+      dst_row[nr] = first;
+      rows[nr] = count;
+      ++nr;
+    }
+  }
+  return nr;
+}
+
 // Completion thread of a handle: host batches that need host work when they
 // finish (a copy out of the slot's pinned buffer, a callback) are queued in
 // ticket order; the thread waits for each batch's D2H, copies, marks the
@@ -1198,6 +1279,7 @@ void shard_plan(int n, int R, int r, int* first, int* count, int* per) {
 // callback may call vss_* functions — except vss_destroy of its own handle).
 void completion_loop(vss_handle* h) {
   (void)hipSetDevice(h->device);
+  g_tls_completing = h;
   for (;;) {
     vss_handle::Completion c;
     {
@@ -1441,14 +1523,26 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   // masks_out from vss_host_alloc: the D2H lands there, nothing to copy after
   const bool direct = pinned_range(masks_out, bytes);
   hipError_t e_ = hipSuccess;
+  // gathered rows -> frame order (one run per rank at most; for the plain
+  // handle and contiguous shards a single run of n rows from row 0)
+  std::vector<int> run_src(R), run_dst(R), run_rows(R);
+  const int nruns = h->rccl ? gather_runs(n, R, run_src.data(), run_dst.data(), run_rows.data()) : (n > 0 ? 1 : 0);
+  if (!h->rccl && nruns) run_src[0] = run_dst[0] = 0, run_rows[0] = n;
   if (out_mode == VSS_OUT_FRAME) {
-    enqueue_upmask(h, res, n, fh, fw, s0.d_fmasks, s0.stream);
-    e_ = hipGetLastError();
+    const size_t F = (size_t)fh * fw;
+    for (int j = 0; j < nruns && e_ == hipSuccess; ++j) {
+      enqueue_upmask(h, res + (size_t)run_src[j] * P, run_rows[j], fh, fw, s0.d_fmasks + (size_t)run_dst[j] * F,
+                     s0.stream);
+      e_ = hipGetLastError();
+    }
     src = s0.h_fmasks;
     if (e_ == hipSuccess)
       e_ = hipMemcpyAsync(direct ? masks_out : s0.h_fmasks, s0.d_fmasks, bytes, hipMemcpyDeviceToHost, s0.stream);
   } else {
-    e_ = hipMemcpyAsync(direct ? masks_out : s0.h_masks, res, bytes, hipMemcpyDeviceToHost, s0.stream);
+    float* dst = direct ? masks_out : s0.h_masks;
+    for (int j = 0; j < nruns && e_ == hipSuccess; ++j)
+      e_ = hipMemcpyAsync(dst + (size_t)run_dst[j] * P, res + (size_t)run_src[j] * P, (size_t)run_rows[j] * P * 4,
+                          hipMemcpyDeviceToHost, s0.stream);
   }
   if (e_ == hipSuccess) e_ = hipEventRecord(s0.host_done, s0.stream);
   if (e_ != hipSuccess) return abort_batch(fail(h, VSS_E_HIP, std::string("D2H: ") + hipGetErrorString(e_)));
@@ -1682,7 +1776,7 @@ void destroy_engine(vss_handle* h) {
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
   for (Slot& s : h->slots) {
-    for (auto& kv : s.graphs) destroy_graph(kv.second);
+    for (auto& kv : s.graphs) destroy_graph_set(kv.second);
     if (s.comm) (void)ncclCommDestroy(s.comm);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.done) (void)hipEventDestroy(s.done);
@@ -1752,6 +1846,7 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
   auto bail = [&](vss_handle* bad, int rc) {
     g_tls_error = bad && !bad->err.empty() ? bad->err : g_tls_error;
     if (h) {
+      stop_completions(h);
       for (vss_handle* p : h->peers) destroy_engine(p);
       h->peers.clear();
       if (bad && bad != h) destroy_engine(bad);
@@ -1794,6 +1889,10 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
 
 void vss_destroy(vss_handle* h) {
   if (!h) return;
+  // drain the completion thread first: it reads h->peers and waits on the
+  // peers' slot events, so every queued batch completes (and its callback
+  // fires) while the peers still exist (use-after-free otherwise)
+  stop_completions(h);
   for (vss_handle* p : h->peers) destroy_engine(p);
   h->peers.clear();
   destroy_engine(h);
@@ -1860,6 +1959,8 @@ int vss_wait(vss_handle* h, vss_ticket ticket) {
   if (k < 0) return VSS_OK;
   Slot& s = h->slots[k];
   // a batch with host work (copy / callback): the completion thread finishes it
+  if (g_tls_completing == h && s.ticket == ticket && s.host_busy)
+    return fail(h, VSS_E_BUSY, "vss_wait from a completion callback on a batch that completes after it");
   h->slot_cv.wait(lk, [&] { return s.ticket != ticket || !s.host_busy; });
   if (s.ticket != ticket) return VSS_OK;
   // otherwise its D2H into the caller's pinned block is the completion; the
@@ -2093,11 +2194,14 @@ int vss_synchronize(vss_handle* h) {
   HIP_TRY(h, hipSetDevice(h->device));
   // and every host batch's completion (copy, callback) has run
   std::unique_lock<std::mutex> lk(h->mu);
-  h->slot_cv.wait(lk, [&] {
+  auto idle = [&] {
     for (const Slot& s : h->slots)
       if (s.host_busy) return false;
     return true;
-  });
+  };
+  if (g_tls_completing == h && !idle())
+    return fail(h, VSS_E_BUSY, "vss_synchronize from a completion callback while later batches complete");
+  h->slot_cv.wait(lk, idle);
   return VSS_OK;
 }
 
@@ -2174,6 +2278,10 @@ int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels
   for (size_t k = 0; k < h->slots.size(); ++k) {
     Slot& s = h->slots[k];
     if (s.graphs.count(key)) continue;
+    if (s.graphs.size() >= 16) {  // the same bound as pick_graph (shapes per slot)
+      destroy_graph_set(s.graphs.begin()->second);
+      s.graphs.erase(s.graphs.begin());
+    }
     std::vector<Launch> ls;
     // null buffers: the first call patches in its own (the slot is idle then)
     forward_launches(h, s, nullptr, n, height, width, channels, row_stride, frame_stride, nullptr, &ls);
@@ -2185,7 +2293,7 @@ int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels
       return fail(h, VSS_E_HIP, std::string("hipGraphUpload: ") + hipGetErrorString(e));
     }
     HIP_TRY(h, hipStreamSynchronize(s.stream));
-    s.graphs.emplace(key, std::move(g));
+    s.graphs[key].push_back(std::move(g));
   }
   return VSS_OK;
 }
@@ -2201,6 +2309,11 @@ int vss_shard_plan(int n, int nranks, int rank, int* first, int* count, int* per
   if (n < 0 || nranks < 1 || rank < 0 || rank >= nranks || !first || !count || !per_rank) return VSS_E_INVALID_ARG;
   shard_plan(n, nranks, rank, first, count, per_rank);
   return VSS_OK;
+}
+
+int vss_gather_runs(int n, int nranks, int* src_row, int* dst_row, int* rows) {
+  if (n < 0 || nranks < 1 || !src_row || !dst_row || !rows) return VSS_E_INVALID_ARG;
+  return gather_runs(n, nranks, src_row, dst_row, rows);
 }
 
 int vss_layer_shape(const vss_handle* h, int layer, int* c, int* hh, int* ww) {
