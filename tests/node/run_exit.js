@@ -1,0 +1,24 @@
+// VERDICT r3 #4: the 400-batch segmentFrames loop that once crashed Node 12 at
+// exit (in its GC-deferred N-API finalizers), run to a NATURAL exit — no
+// process.exit, no exit guard when VSS_NODE_EXIT_GUARD=0.  Prints one JSON
+// line; the caller asserts the exit status.
+//   node run_exit.js [batches]
+'use strict';
+const path = require('path');
+const seg = require(path.join(__dirname, '..', '..', 'video-stream-segmenetation_amd', 'ts', 'segment.js'));
+async function main() {
+  const it = Number(process.argv[2] || 400);
+  const b = 8, h = 480, w = 640;
+  const s = new seg.Segmenter({ maxBatch: b, maxFrameWidth: w, maxFrameHeight: h, queueDepth: 4 });
+  const frames = [];
+  for (let i = 0; i < b; i++) frames.push({ data: new Uint8Array(h * w * 3).fill(i * 20), width: w, height: h, channels: 3 });
+  let ps = [], done = 0;
+  for (let i = 0; i < 150 + it; i++) {
+    ps.push(s.segmentFrames(frames).then((r) => { done += r.count; }));
+    if (ps.length === 8) { await ps[0]; ps = ps.slice(1); }
+  }
+  await Promise.all(ps);
+  s.close();
+  console.log(JSON.stringify({ batches: 150 + it, frames: done, guard: process.env.VSS_NODE_EXIT_GUARD || 'default' }));
+}
+main();

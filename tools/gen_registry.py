@@ -57,7 +57,7 @@ def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=False)
     f += r4(chid * (cin + 8) // 2) if mode == 0 else 0
     f += r4(cout * (chid + 8) // 2) + r4(9 * chid) + r4(chid) + (r4(chid) if mode == 0 else 0) + r4(cout)
     f += r4(2 * cin) if mode == 2 else 0
-    f += 4 * p_in_pad if mode == 2 else 0  # the decoder's upsample tap records (L.uc)
+    f += 4 * p_in_pad if mode == 2 and (th % 2 or tw % 2) else 0  # the decoder's upsample tap records (L.uc; odd tiles)
     # work: expand scratch / slabs / (decoder) the low-res src region; the
     # decoder's slabs go into xt when they fit (its stats scratch then in work)
     slab_in_xt = mode == 2 and cs * p_out * (cout + 4) <= r4(p_in_pad * (cx + 4))

@@ -4,7 +4,7 @@
 # success, test failure, GPU fault, timeout — is returned as is, never retried.
 # Usage: tools/gpurun_retry.sh TIMEOUT 'command'
 T=$1; shift
-for attempt in 1 2 3 4 5 6 7 8 9 10 11 12; do
+for attempt in $(seq 1 ${GPURUN_ATTEMPTS:-12}); do
   out=$(/usr/local/graft/bin/gpurun --timeout "$T" -- "$@" 2>&1); rc=$?
   if [ $rc -eq 3 ] || echo "$out" | grep -q "status=transient"; then
     echo "[retry] attempt $attempt: box not acquired (nothing ran); waiting" >&2

@@ -153,8 +153,9 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
             stem_in ? stem_in_lds(L.IH, L.IW) : 0);
   L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;
   // decoder: per input-tile pixel, its 2x-upsample taps (four lr offsets as
-  // u16 pairs, ly1, lx1), built while the prologue loads are in flight
-  L.uc = o;  o += mode == 2 ? 4 * L.P_in_pad : 0;
+  // u16 pairs, ly1, lx1), built while the prologue loads are in flight — only
+  // for tiles with an odd side; even tiles upsample by 2x2 quads (dec_quads)
+  L.uc = o;  o += (mode == 2 && (TH % 2 || TW % 2)) ? 4 * L.P_in_pad : 0;
   L.slab = slab_in_xt ? L.xt : L.work;
   L.stt = slab_in_xt ? L.work : L.xt;
   L.total = o;

@@ -69,6 +69,15 @@ struct Gm {
     else
       return *reinterpret_cast<const f4*>(b + i);
   }
+  // 32-bit element offset off a wave-uniform base: one global_load with an
+  // SGPR base and a 32-bit VGPR byte offset, no 64-bit address arithmetic
+  // (every activation tensor of a frame is far below 4 GiB)
+  __device__ __forceinline__ f4 ldu(unsigned i) const {
+    if constexpr (COH)
+      return ld((long)i);
+    else
+      return *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(b) + (i << 2));
+  }
   __device__ __forceinline__ void st(long i, f4 v) const {
     if constexpr (COH)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)(i * 4), 0, 16);
@@ -83,12 +92,22 @@ struct Gm {
   }
 };
 
-__device__ __forceinline__ float relu6f(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
+// ReLU6 / ReLU as one v_med3_f32 per element (fminf(fmaxf()) compiles to a
+// NaN-quieting v_max_f32 x, x, x plus the med3 in IEEE mode; the activations
+// here are never NaN, and for every other input the value is the same)
+__device__ __forceinline__ float relu6f(float v) { return __builtin_amdgcn_fmed3f(v, 0.f, 6.f); }
 __device__ __forceinline__ f4 relu6v(f4 v) {
   return f4{relu6f(v.x), relu6f(v.y), relu6f(v.z), relu6f(v.w)};
 }
+// clamp to [0, lim]: ReLU6 where lim = 6, zero where lim = 0 (padding pixels)
+__device__ __forceinline__ f4 clampv(f4 v, float lim) {
+  return f4{__builtin_amdgcn_fmed3f(v.x, 0.f, lim), __builtin_amdgcn_fmed3f(v.y, 0.f, lim),
+            __builtin_amdgcn_fmed3f(v.z, 0.f, lim), __builtin_amdgcn_fmed3f(v.w, 0.f, lim)};
+}
 __device__ __forceinline__ f4 reluv(f4 v) {
-  return f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+  constexpr float inf = __builtin_inff();
+  return f4{__builtin_amdgcn_fmed3f(v.x, 0.f, inf), __builtin_amdgcn_fmed3f(v.y, 0.f, inf),
+            __builtin_amdgcn_fmed3f(v.z, 0.f, inf), __builtin_amdgcn_fmed3f(v.w, 0.f, inf)};
 }
 
 // ---------------------------------------------------------------------------
@@ -231,14 +250,35 @@ struct StemTaps {
   float w[7];  // w[channel r][tap 4s+g]
 };
 
-__device__ __forceinline__ StemTaps stem_taps(const float* ws /* [tap][16] */, int r, int g, int plane, int row) {
+// The four lane groups' offsets of tap 4s + g (g = 0..3) for one s, packed as
+// 16-bit fields of a compile-time constant: a lane picks its field with one
+// 64-bit shift by 16 g and a mask, instead of dividing 4s + g by 9 and 3 at
+// run time (~12 VALU per tap: the taps' setup was a fifth of b1's VALU).
+template <int PLANE, int ROW>
+struct StemTapTable {
+  static_assert(2 * PLANE + 2 * ROW + 2 < 65536, "tap offsets are 16-bit fields");
+  static constexpr unsigned long long field(int s) {
+    unsigned long long v = 0;
+    for (int g = 0; g < 4; ++g) {
+      const int k = 4 * s + g;
+      const unsigned long long o = k < 27 ? (unsigned long long)((k / 9) * PLANE + ((k % 9) / 3) * ROW + k % 3) : 0ull;
+      v |= o << (16 * g);
+    }
+    return v;
+  }
+  static constexpr unsigned long long c[7] = {field(0), field(1), field(2), field(3), field(4), field(5), field(6)};
+};
+
+template <int PLANE, int ROW>
+__device__ __forceinline__ StemTaps stem_taps(const float* ws /* [tap][16], then the bias */, int r, int g) {
   StemTaps t;
+  const unsigned sh = (unsigned)g << 4;
 #pragma unroll
   for (int s = 0; s < 7; ++s) {
-    const int k = 4 * s + g;
-    const int ci = k / 9, ky = (k % 9) / 3, kx = k % 3;
-    t.off[s] = k < 27 ? ci * plane + ky * row + kx : 0;
-    t.w[s] = k < 27 ? ws[min(k, 26) * 16 + r] : 0.f;
+    t.off[s] = (int)((StemTapTable<PLANE, ROW>::c[s] >> sh) & 0xFFFFu);
+    // tap 27 (s = 6, g = 3) is K's padding: weight 0 (its address reads the bias row, in bounds)
+    const float wv = ws[(4 * s + g) * 16 + r];
+    t.w[s] = (s == 6 && g == 3) ? 0.f : wv;
   }
   return t;
 }
@@ -316,7 +356,7 @@ __device__ __forceinline__ void stem_body(const StemParams& p, int bx, int by, i
   VSS_STAMP(1);
   VSS_STAMP(2);
   const int lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-  const StemTaps taps = stem_taps(ws, r, g, IH * IWP, IWP);
+  const StemTaps taps = stem_taps<IH * IWP, IWP>(ws, r, g);
   const float bias = bs[r];
   const Gm<COH> gy(p.y + (long)n * p.Ho * p.Wo * COUT);
 #pragma unroll
@@ -563,7 +603,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       st_lr[q].issue([&](int i) {
         const int pr = i / C4L, c4 = i % C4L;
         const int yy = min(h - 1, sy0 + pr / SC), xx = min(w - 1, sx0 + pr % SC);
-        return gx.ld(((long)yy * w + xx) * CL + 4 * c4);
+        return gx.ldu((unsigned)((yy * w + xx) * CL + 4 * c4));
       });
     }
 #pragma unroll
@@ -572,7 +612,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       st_sk[q].issue([&](int i) {
         const int pix = i / C4S, c4 = i % C4S;
         const int yy = min(max(iy0 + pix / IW, 0), Ho - 1), xx = min(max(ix0 + pix % IW, 0), Wo - 1);
-        return gs.ld(((long)yy * Wo + xx) * CSKIP + 4 * c4);
+        return gs.ldu((unsigned)((yy * Wo + xx) * CSKIP + 4 * c4));
       });
     }
     st_w.issue([&](int i) { return wsrc[i]; });
@@ -582,7 +622,12 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     // integers — o = 0 -> (0, 0); odd o -> ((o - 1) / 2, 0.25); even o > 0 ->
     // (o / 2 - 1, 0.75), the same floats the float formula gives
     static_assert(SR * SC * CL < 65536, "tap offsets are u16");
+    // even tiles start at an odd row and column of the output (iy0 = TH*by - 1),
+    // so their input tile is whole 2x2 quads that share one 2x2 source window:
+    // the upsample below runs per quad and needs no per-pixel tap records
+    constexpr bool QUADS = TH % 2 == 0 && TW % 2 == 0;
     unsigned* uc = reinterpret_cast<unsigned*>(smem + L.uc);
+    if constexpr (!QUADS)
     for (int pix = tid; pix < P_IN_PAD; pix += 256) {
       const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
       uint4 rec = {0xFFFFFFFFu, 0u, 0u, 0u};  // outside the frame / padding: zeros
@@ -628,17 +673,75 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       }
       reinterpret_cast<f4*>(lr)[i] = v;
     });
+    // the skip channels: zero outside the image (tiles at its edge only; the
+    // loads were clamped to real pixels, and padding pixels are never read)
+    const bool sk_interior = iy0 >= 0 && iy0 + L.IH <= Ho && ix0 >= 0 && ix0 + IW <= Wo;
     commit_sum(st_sk, [&](int i, f4 v) {
       const int pix = i / C4S, c4 = i % C4S;
-      const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
-      const bool valid = pix < P_IN && yy >= 0 && yy < Ho && xx >= 0 && xx < Wo;
-      *reinterpret_cast<f4*>(xt + pix * XS + CL + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+      if (!sk_interior) {
+        const int py = pix / IW, yy = iy0 + py, xx = ix0 + pix - py * IW;
+        const bool valid = ((unsigned)yy < (unsigned)Ho) & ((unsigned)xx < (unsigned)Wo);
+        v = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+      }
+      *reinterpret_cast<f4*>(xt + pix * XS + CL + 4 * c4) = v;
     });
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     VSS_STAMP(4);
     __syncthreads();
     // upsampled channels: PyTorch upsample_bilinear2d(scale 2, align_corners=False)
     // of relu(src * scale + shift) (the src's instance norm, applied per tap)
+    if constexpr (QUADS) {
+      // Output rows 2j+1, 2j+2 both lie between source rows j, j+1 (weights
+      // 0.75 / 0.25 and 0.25 / 0.75), and so do columns: one 2x2 source window
+      // per output quad.  Per source row the two horizontal interpolants
+      // H1 = fma(0.25, R, 0.75 L) (column 2i+1) and H2 = fma(0.75, R, 0.25 L)
+      // (column 2i+2), then each output = fma(ly1, H[j+1], ly0 H[j]) — exactly
+      // the per-pixel form's operations (top / bot lerps, then the vertical
+      // one), shared by the quad: the same floats with 4 tap reads per 4
+      // pixels instead of 16.  At the image's edges the source index clamps
+      // (row / column -1 -> 0, h -> h - 1), where both weights hit the same
+      // value and the FMA returns it exactly — as the per-pixel form's
+      // weight-0 taps do.  Outputs outside the image are zero (halo).
+      constexpr int QH = L.IH / 2, QW = IW / 2, NQI = QH * QW * C4L, NQ = (NQI + 255) / 256;
+      const int j0 = (iy0 - 1) / 2, i0 = (ix0 - 1) / 2;  // iy0, ix0 odd: exact (-1 -> -1)
+      const bool interior = iy0 >= 0 && iy0 + L.IH <= Ho && ix0 >= 0 && ix0 + IW <= Wo;
+      const f4 c25 = {0.25f, 0.25f, 0.25f, 0.25f}, c75 = {0.75f, 0.75f, 0.75f, 0.75f};
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) {
+        const int it = tid + 256 * k;
+        if (NQI % 256 == 0 || it < NQI) {
+          const int c4 = it % C4L, qq = it / C4L, qx = qq % QW, qy = qq / QW;
+          const int ra = min(max(min(max(j0 + qy, 0), h - 1) - sy0, 0), SR - 1);
+          const int rb = min(max(min(max(j0 + qy + 1, 0), h - 1) - sy0, 0), SR - 1);
+          const int ca = min(max(min(max(i0 + qx, 0), w - 1) - sx0, 0), SC - 1);
+          const int cb = min(max(min(max(i0 + qx + 1, 0), w - 1) - sx0, 0), SC - 1);
+          const f4 taa = *reinterpret_cast<const f4*>(lr + (ra * SC + ca) * CL + 4 * c4);
+          const f4 tab = *reinterpret_cast<const f4*>(lr + (ra * SC + cb) * CL + 4 * c4);
+          const f4 tba = *reinterpret_cast<const f4*>(lr + (rb * SC + ca) * CL + 4 * c4);
+          const f4 tbb = *reinterpret_cast<const f4*>(lr + (rb * SC + cb) * CL + 4 * c4);
+          const f4 h1a = __builtin_elementwise_fma(c25, tab, c75 * taa), h2a = __builtin_elementwise_fma(c75, tab, c25 * taa);
+          const f4 h1b = __builtin_elementwise_fma(c25, tbb, c75 * tba), h2b = __builtin_elementwise_fma(c75, tbb, c25 * tba);
+          f4 o00 = __builtin_elementwise_fma(c25, h1b, c75 * h1a), o01 = __builtin_elementwise_fma(c25, h2b, c75 * h2a);
+          f4 o10 = __builtin_elementwise_fma(c75, h1b, c25 * h1a), o11 = __builtin_elementwise_fma(c75, h2b, c25 * h2a);
+          if (!interior) {
+            const int yy = iy0 + 2 * qy, xx = ix0 + 2 * qx;  // the quad's top-left output pixel
+            // (yy >= -1: the quad's second row is never above the image; a
+            // partial tile's quads may lie past its bottom / right edge)
+            const bool r0 = yy >= 0 && yy < Ho, r1 = yy + 1 < Ho, x0v = xx >= 0 && xx < Wo, x1v = xx + 1 < Wo;
+            const f4 z = {0.f, 0.f, 0.f, 0.f};
+            o00 = r0 && x0v ? o00 : z;
+            o01 = r0 && x1v ? o01 : z;
+            o10 = r1 && x0v ? o10 : z;
+            o11 = r1 && x1v ? o11 : z;
+          }
+          float* dst = xt + ((2 * qy) * IW + 2 * qx) * XS + 4 * c4;
+          *reinterpret_cast<f4*>(dst) = o00;
+          *reinterpret_cast<f4*>(dst + XS) = o01;
+          *reinterpret_cast<f4*>(dst + IW * XS) = o10;
+          *reinterpret_cast<f4*>(dst + (IW + 1) * XS) = o11;
+        }
+      }
+    } else {
     // Every read of this thread's items is issued before any of its writes:
     // with a read -> write chain per item (the compiler cannot move an item's
     // LDS reads above the previous item's write into the same array) the
@@ -681,13 +784,14 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
       }
     }
+    }
   } else if constexpr (STEM_IN) {
     // The input tile is the stem's output region (IH x IW at half model
     // resolution, halo included), computed here from the frame: resize taps of
     // its x0 region -> LDS, then the stem's 3x3 s2 conv + ReLU6 -> xt, in the
     // same operation order as k_stem (bitwise the same activations).
     static_assert(MODE == MODE_IR_DIRECT && STRIDE == 1 && CIN == 16 && XP == 1, "stem fusion shape");
-    constexpr int IH = L.IH, XH = 2 * IH + 1, XW = 2 * IW + 1, XWP = XW + 1, NX = (XH * XW + 255) / 256;
+    constexpr int IH = L.IH, XH = 2 * IH + 1, XW = 2 * IW + 1, XWP = XW + 1;
     const StemParams& sp = p.stem;
     const int H = p.H, W = p.W;  // the stem's output = this block's input
     const uint8_t* fr = sp.frames + (long)n * sp.frame_stride;
@@ -701,37 +805,68 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
     for (int u = 0; u < 2; ++u) wr[u] = sp.w[min(tid + 256 * u, 27 * 16 - 1)];
     const float sb = sp.b[min(tid, 15)];
-    uint32_t raw[NX][12];
-    float dys[NX], dxs[NX];
+    // Each thread resizes two pixels of one row of the region, columns lx and
+    // lx + HW2: the row's source rows, its weight and their byte offsets are
+    // worked out once for both (the resize is separable), and every tap is a
+    // 32-bit byte offset off the frame's base (one saddr load, no 64-bit
+    // address arithmetic).  The per-pixel arithmetic is prep_tap / prep_finish's,
+    // operation for operation (bitwise the same floats).
+    constexpr int HW2 = (XW + 1) / 2, NPAIR = XH * HW2, NR = (NPAIR + 255) / 256;
+    // the frame as a raw buffer (wave-uniform base, range = the frame's bytes)
+    const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(uniform_ptr(fr)), 0, (int)min(sp.frame_stride, (long)0x7FFFFFF0), 0x00020000);
+    uint32_t raw[NR][2][12];
+    float dys[NR], dxs[NR][2];
+    int lys[NR], lxs[NR];
 #pragma unroll
-    for (int u = 0; u < NX; ++u) {
-      const int i = min(tid + 256 * u, XH * XW - 1);
-      const int ly = i / XW, lx = i - ly * XW;
-      const int yy = min(max(r0 + ly, 0), sp.Hm - 1), xx = min(max(c0 + lx, 0), sp.Wm - 1);
-      const PrepTap t = prep_tap(fr, sp.row_stride, sp.fc, sp.fh, sp.fw, sp.ry, sp.rx, yy, xx);
-      prep_load(t, raw[u]);
-      dys[u] = t.dy;
-      dxs[u] = t.dx;
+    for (int u = 0; u < NR; ++u) {
+#pragma clang fp contract(off)
+      const int i = min(tid + 256 * u, NPAIR - 1);
+      const int ly = i / HW2, lx = i - ly * HW2;
+      lys[u] = ly;
+      lxs[u] = lx;
+      const int yy = min(max(r0 + ly, 0), sp.Hm - 1);
+      const float fy = (float)yy * sp.ry;
+      const float y0f = floorf(fmaxf(fy, 0.f));
+      const unsigned y1 = (unsigned)min(sp.fh - 1, (int)ceilf(fy));
+      dys[u] = fy - y0f;
+      const unsigned rs = (unsigned)sp.row_stride;
+      const unsigned t0 = (unsigned)y0f * rs, t1 = y1 * rs;  // frame bytes < 4 GiB
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int xx = min(max(c0 + min(lx + e * HW2, XW - 1), 0), sp.Wm - 1);
+        const float fx = (float)xx * sp.rx;
+        const float x0f = floorf(fmaxf(fx, 0.f));
+        const unsigned x1 = (unsigned)min(sp.fw - 1, (int)ceilf(fx));
+        dxs[u][e] = fx - x0f;
+        const unsigned o0 = (unsigned)x0f * (unsigned)sp.fc, o1 = x1 * (unsigned)sp.fc;
+        // byte loads through the frame's buffer descriptor: the channel is the
+        // instruction's immediate offset, so a tap is one address add, not three
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          raw[u][e][c] = __builtin_amdgcn_raw_buffer_load_b8(frsrc, (int)(t0 + o0) + c, 0, 0);
+          raw[u][e][3 + c] = __builtin_amdgcn_raw_buffer_load_b8(frsrc, (int)(t0 + o1) + c, 0, 0);
+          raw[u][e][6 + c] = __builtin_amdgcn_raw_buffer_load_b8(frsrc, (int)(t1 + o0) + c, 0, 0);
+          raw[u][e][9 + c] = __builtin_amdgcn_raw_buffer_load_b8(frsrc, (int)(t1 + o1) + c, 0, 0);
+        }
+      }
     }
     VSS_STAMP(6);  // every load issued
-    // this thread's resized pixels two at a time on packed FP32 (prep_finish2)
-    float o[NX][3];
+    // the two pixels at once on packed FP32 (prep_finish2)
 #pragma unroll
-    for (int u = 0; u < NX; u += 2) {
-      if (u + 1 < NX)
-        prep_finish2(raw[u], raw[u + 1], dys[u], dxs[u], dys[u + 1], dxs[u + 1], o[u], o[u + 1]);
-      else
-        prep_finish(raw[u], dys[u], dxs[u], o[u]);
-    }
+    for (int u = 0; u < NR; ++u) {
+      float o[2][3];
+      prep_finish2(raw[u][0], raw[u][1], dys[u], dxs[u][0], dys[u], dxs[u][1], o[0], o[1]);
+      const int ly = lys[u], yy = r0 + ly;
 #pragma unroll
-    for (int u = 0; u < NX; ++u) {
-      const int i = tid + 256 * u;
-      if (i < XH * XW) {
-        const int ly = i / XW, lx = i - ly * XW;
-        const int yy = r0 + ly, xx = c0 + lx;
-        const bool valid = yy >= 0 && yy < sp.Hm && xx >= 0 && xx < sp.Wm;
+      for (int e = 0; e < 2; ++e) {
+        const int lx = lxs[u] + e * HW2, xx = c0 + lx;
+        const bool in = tid + 256 * u < NPAIR && lx < XW;
+        const bool valid = ((unsigned)yy < (unsigned)sp.Hm) & ((unsigned)xx < (unsigned)sp.Wm);
+        if (in) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) x0s[(c * XH + ly) * XWP + lx] = valid ? o[u][c] : 0.f;
+          for (int c = 0; c < 3; ++c) x0s[(c * XH + ly) * XWP + lx] = valid ? o[e][c] : 0.f;
+        }
       }
     }
 #pragma unroll
@@ -755,26 +890,30 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     // stem outputs of the region, 16-pixel blocks on the MFMA (stem_mfma,
     // bitwise k_stem's), zero outside the image
     {
-      const StemTaps taps = stem_taps(sws, r, g, XH * XWP, XWP);
+      const StemTaps taps = stem_taps<XH * XWP, XWP>(sws, r, g);
       const float bias = sbs[r];
-      // most tiles lie inside the image with their halo: then only the
-      // padding pixels past the tile are zeroed, no per-pixel row / column test
-      const bool interior = iy0 >= 0 && iy0 + L.IH <= H && ix0 >= 0 && ix0 + IW <= W;
+      // every pixel of the region first (the pixels past P_IN land in xt's
+      // padding, which nothing reads); the stem pixels outside the image are
+      // zeroed after, border only, in the tiles that have any (below)
       for (int blk = wave; blk < P_IN_PAD / 16; blk += 4) {
         const int pa = min(blk * 16 + r, P_IN - 1), py = pa / IW, px = pa - py * IW;
         const f4 acc = stem_mfma(taps, x0s + 2 * py * XWP + 2 * px, bias);
         const int p0 = blk * 16 + 4 * g;
-        if (interior) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) xt[(p0 + i) * XS + r] = p0 + i < P_IN ? relu6f(acc[i]) : 0.f;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {  // D[pixel 4g+i][channel r]
-            const int pp = p0 + i, qy = pp / IW, qx = pp - qy * IW;
-            const int yy = iy0 + qy, xx = ix0 + qx;
-            const bool valid = pp < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
-            xt[pp * XS + r] = valid ? relu6f(acc[i]) : 0.f;
-          }
+        for (int i = 0; i < 4; ++i) xt[(p0 + i) * XS + r] = relu6f(acc[i]);  // D[pixel 4g+i][channel r]
+      }
+      // a tile at the image's edge: its pixels outside the image (the halo
+      // row / column, and a partial tile's columns / rows past the image) are
+      // the dw's zero padding — one pass over the region, each pixel as 4
+      // float4s, in those tiles only
+      const bool interior = iy0 >= 0 && iy0 + L.IH <= H && ix0 >= 0 && ix0 + IW <= W;
+      if (!interior) {
+        __syncthreads();
+        for (int i = tid; i < P_IN * 4; i += 256) {
+          const int q = i & 3, e = i >> 2, qy = e / IW, qx = e - qy * IW;
+          const int yy = iy0 + qy, xx = ix0 + qx;
+          if (yy < 0 || yy >= H || xx < 0 || xx >= W)
+            *reinterpret_cast<f4*>(xt + (qy * IW + qx) * XS + 4 * q) = f4{0.f, 0.f, 0.f, 0.f};
         }
       }
     }
@@ -791,24 +930,28 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       st_x[q].issue([&](int i) {
         const int pix = i / C4, c4 = i % C4;
         const int yy = min(max(iy0 + pix / IW, 0), H - 1), xx = min(max(ix0 + pix % IW, 0), W - 1);
-        return gx.ld(((long)yy * W + xx) * CIN + 4 * c4);
+        return gx.ldu((unsigned)((yy * W + xx) * CIN + 4 * c4));
       });
     }
     st_w.issue([&](int i) { return wsrc[i]; });
     VSS_STAMP(6);  // every load issued
     commit_sum(st_x, [&](int i, f4 v) {
       const int pix = i / C4, c4 = i % C4;
-      const int py = pix / IW, px = pix % IW;
-      const int yy = iy0 + py, xx = ix0 + px;
-      const bool valid = pix < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
-      const f4 x = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
       if constexpr (MODE == MODE_IR_EXPAND) {
-        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = to_operand<PREC>(x);
-        if constexpr (RES)
+        // no validity test: an expand layer's input pixels outside the image
+        // only feed hidden pixels that the expand loop zeroes (its clamp
+        // limit is 0 there), and the loads were clamped to real pixels
+        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = to_operand<PREC>(v);
+        if constexpr (RES) {
+          const int py = pix / IW, px = pix - py * IW;
           if (py >= 1 && py <= TH && px >= 1 && px <= TW)
-            *reinterpret_cast<f4*>(smem + L.xr + ((py - 1) * TW + px - 1) * CIN + 4 * c4) = x;
+            *reinterpret_cast<f4*>(smem + L.xr + ((py - 1) * TW + px - 1) * CIN + 4 * c4) = v;
+        }
       } else {
-        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = x;
+        const int py = pix / IW, px = pix % IW;
+        const int yy = iy0 + py, xx = ix0 + px;
+        const bool valid = pix < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
       }
     });
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
@@ -834,22 +977,35 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     constexpr int HSD = hid_stride(STRIDE);
     float* hid = work + wave * P_IN_PAD * HSD;
     constexpr int NK = CIN / 16;
+    constexpr int NCBI = P_IN_PAD / 16, UNR = NCBI <= 6 ? NCBI : 2;
+    static_assert(NCBI <= 32, "one validity bit per input pixel block");
+    // bit cb: this lane's pixel cb * 16 + r of the input tile lies in the
+    // image (else its hidden values are the dw's zero padding).  Once per
+    // wave, and only in tiles at the image's edge; the chunk loop turns the
+    // bit into the clamp limit of its ReLU6 (6, or 0 for a padding pixel),
+    // one v_med3_f32 per element either way.  Pixels past P_IN are never read.
+    unsigned vmask = ~0u;
+    if (!(iy0 >= 0 && iy0 + L.IH <= p.H && ix0 >= 0 && ix0 + IW <= p.W)) {
+      vmask = 0u;
+#pragma unroll
+      for (int cb = 0; cb < NCBI; ++cb) {
+        const int pix = cb * 16 + r, py = pix / IW, yy = iy0 + py, xx = ix0 + pix - py * IW;
+        vmask |= (yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) ? 1u << cb : 0u;
+      }
+    }
     for (int ck = wave; ck < NCHUNK; ck += 4) {
       const int c0 = ck << 4;
       typename AFrag<PREC>::T aw[NK];
 #pragma unroll
       for (int s = 0; s < NK; ++s) aw[s] = lds_a<PREC>(w1s, L.LD1, c0 + r, 16 * s + 4 * g);
       const f4 bias = *reinterpret_cast<const f4*>(b1s + c0 + 4 * g);
-      constexpr int NCBI = P_IN_PAD / 16, UNR = NCBI <= 6 ? NCBI : 2;
 #pragma unroll UNR
       for (int cb = 0; cb < NCBI; ++cb) {
         const int pix = cb * 16 + r;
-        f4 d = {0.f, 0.f, 0.f, 0.f};
+        f4 d = bias;  // the expand's bias enters as the MFMA accumulator
 #pragma unroll
         for (int s = 0; s < NK; ++s) d = mma16_op<PREC>(d, aw[s], *reinterpret_cast<const f4*>(xt + pix * XS + 16 * s + 4 * g));
-        const int yy = iy0 + pix / IW, xx = ix0 + pix % IW;
-        const bool valid = pix < P_IN && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
-        *reinterpret_cast<f4*>(hid + pix * HSD + 4 * g) = valid ? relu6v(d + bias) : f4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(hid + pix * HSD + 4 * g) = clampv(d, (vmask >> cb) & 1u ? 6.f : 0.f);
       }
       wave_sync();
       // dw 3x3 computed straight into the project MFMA's B layout: lane (r, g)
@@ -936,6 +1092,27 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   }
 
   // ---- epilogue: slabs -> fixed-order sum, bias, residual, store ----
+  if constexpr (MODE == MODE_IR_DIRECT && CS == 1) {
+    // one wave computes every channel of its pixels (a single 16-channel
+    // chunk): bias and residual added in registers and stored straight from
+    // the accumulators — the same additions in the same order as the slab
+    // path, without its LDS round trip and two barriers (b1)
+    VSS_STAMP(2);
+    const Gm<COH> gy(p.y + (long)n * Ho * Wo * COUT);
+#pragma unroll
+    for (int q = 0; q < NPBW / XR; ++q)
+#pragma unroll
+      for (int j = 0; j < XR; ++j) {
+        const int pix = run_pix(pw + q * PW, j), ly = pix / TW, lx = pix % TW;
+        const int oy = oy0 + ly, ox = ox0 + lx;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          f4 v = acc[(q * XR + j) * NCB + cb] + *reinterpret_cast<const f4*>(b2s + cb * 16 + 4 * g);
+          if constexpr (RES) v = v + *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + cb * 16 + 4 * g);
+          if (oy < Ho && ox < Wo) gy.st(((long)oy * Wo + ox) * COUT + cb * 16 + 4 * g, v);
+        }
+      }
+  } else {
   __syncthreads();  // every wave is done with its scratch (reused as slabs)
   VSS_STAMP(2);
   {
@@ -1047,6 +1224,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       }
     }
   }
+  }  // slab epilogue
   if constexpr (STEM_IN) {
     // the stem activation itself (the tile centre of xt, intact through the
     // epilogue), only under VSS_OPT_KEEP_STEM (null otherwise: no layer reads
@@ -1152,7 +1330,7 @@ __global__ __launch_bounds__(kWideThreads) void k_stem_b1(BlockParams p) {
   __syncthreads();
   // the stem over the region, 16-pixel blocks on the MFMA (stem_mfma), zero outside the image
   {
-    const StemTaps taps = stem_taps(sws, r, g, XH * XWP, XWP);
+    const StemTaps taps = stem_taps<XH * XWP, XWP>(sws, r, g);
     const float bias = sbs[r];
     const bool interior = iy0 >= 0 && iy0 + IH <= H && ix0 >= 0 && ix0 + IW <= W;
     for (int blk = wave; blk < P_IN_PAD / 16; blk += NWAVE) {
@@ -1237,7 +1415,7 @@ __device__ __forceinline__ void head_body(const HeadParams& p, int bx, int by, i
     const int zr = i / ZC, zc = i - zr * ZC;
     const int yy = min(max(zr0 + zr, 0), h - 1), xx = min(max(zc0 + zc, 0), w - 1);
 #pragma unroll
-    for (int q = 0; q < C / 4; ++q) xv[u][q] = gx.ld(((long)yy * w + xx) * C + 4 * q);
+    for (int q = 0; q < C / 4; ++q) xv[u][q] = gx.ldu((unsigned)((yy * w + xx) * C + 4 * q));
   }
   // the d3 norm: all slots of the frame's exact totals (2 x C int64 per slot)
   {
