@@ -326,6 +326,7 @@ struct vss_handle {
   // expand layers with at most this many output pixels per frame split their
   // hidden channels over ks_max() workgroups (env VSS_KSPLIT_PIXELS overrides)
   long ksplit_pixels = kDefaultKsplitPixels;
+  bool ksplit_on = true;       // env VSS_KSPLIT=0 turns the hidden split off (both rules)
   // profiling: ring of event pairs per layer
   static constexpr int kProfRing = 32;
   std::vector<hipEvent_t> ev;  // [ring][layer][2]
@@ -593,7 +594,8 @@ int plan(vss_handle* h) {
     // hidden split: expand layers whose output has at most ksplit_pixels
     // pixels per frame (a function of the model resolution only, so results
     // never depend on the batch or the autotuner)
-    if (l.mode == MODE_IR_EXPAND &&
+    // (env VSS_KSPLIT=0: no hidden split at all, either rule — an A/B knob)
+    if (l.mode == MODE_IR_EXPAND && h->ksplit_on &&
         ((long)l.H * l.W <= h->ksplit_pixels || weight_image_bytes(l) > kKsplitWeightBytes))
       l.ks = ks_max(l);
     if (r.kind == K_IR || r.kind == K_DEC) l.xp = h->L[r.src].ks;
@@ -1732,6 +1734,7 @@ int create_engine(const vss_config* cfg, int device, int max_batch, int user_max
   h->user_max_batch = user_max_batch;
   if (hipSetDevice(h->device) != hipSuccess) return fail(h, VSS_E_HIP, "hipSetDevice failed");
   if (const char* ev = std::getenv("VSS_KSPLIT_PIXELS")) h->ksplit_pixels = std::atol(ev);
+  if (const char* ev = std::getenv("VSS_KSPLIT")) h->ksplit_on = std::atoi(ev) != 0;
   if (const char* ev = std::getenv("VSS_FUSE_STEM")) h->fuse_stem = std::atoi(ev) != 0;
   int rc = load_weights(h);
   if (!rc) rc = plan(h);

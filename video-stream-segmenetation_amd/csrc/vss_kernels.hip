@@ -704,6 +704,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       // weight-0 taps do.  Outputs outside the image are zero (halo).
       constexpr int QH = L.IH / 2, QW = IW / 2, NQI = QH * QW * C4L, NQ = (NQI + 255) / 256;
       const int j0 = (iy0 - 1) / 2, i0 = (ix0 - 1) / 2;  // iy0, ix0 odd: exact (-1 -> -1)
+      const int jr = j0 - sy0, ic = i0 - sx0;             // the quads' first source row / column in the region
       const bool interior = iy0 >= 0 && iy0 + L.IH <= Ho && ix0 >= 0 && ix0 + IW <= Wo;
       const f4 c25 = {0.25f, 0.25f, 0.25f, 0.25f}, c75 = {0.75f, 0.75f, 0.75f, 0.75f};
 #pragma unroll
@@ -711,14 +712,18 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         const int it = tid + 256 * k;
         if (NQI % 256 == 0 || it < NQI) {
           const int c4 = it % C4L, qq = it / C4L, qx = qq % QW, qy = qq / QW;
-          const int ra = min(max(min(max(j0 + qy, 0), h - 1) - sy0, 0), SR - 1);
-          const int rb = min(max(min(max(j0 + qy + 1, 0), h - 1) - sy0, 0), SR - 1);
-          const int ca = min(max(min(max(i0 + qx, 0), w - 1) - sx0, 0), SC - 1);
-          const int cb = min(max(min(max(i0 + qx + 1, 0), w - 1) - sx0, 0), SC - 1);
-          const f4 taa = *reinterpret_cast<const f4*>(lr + (ra * SC + ca) * CL + 4 * c4);
-          const f4 tab = *reinterpret_cast<const f4*>(lr + (ra * SC + cb) * CL + 4 * c4);
-          const f4 tba = *reinterpret_cast<const f4*>(lr + (rb * SC + ca) * CL + 4 * c4);
-          const f4 tbb = *reinterpret_cast<const f4*>(lr + (rb * SC + cb) * CL + 4 * c4);
+          // the source window's rows / columns, clamped to the region: the
+          // region's rows (columns) past the source's last one were loaded
+          // clamped, i.e. they hold that last row (column), and a row above
+          // (left of) the source only occurs where the region starts at 0
+          const int ra = min(max(qy + jr, 0), SR - 1), rb = min(max(qy + jr + 1, 0), SR - 1);
+          const int ca = min(max(qx + ic, 0), SC - 1), cb = min(max(qx + ic + 1, 0), SC - 1);
+          const float* la = lr + ra * (SC * CL) + 4 * c4;
+          const float* lb = lr + rb * (SC * CL) + 4 * c4;
+          const f4 taa = *reinterpret_cast<const f4*>(la + ca * CL);
+          const f4 tab = *reinterpret_cast<const f4*>(la + cb * CL);
+          const f4 tba = *reinterpret_cast<const f4*>(lb + ca * CL);
+          const f4 tbb = *reinterpret_cast<const f4*>(lb + cb * CL);
           const f4 h1a = __builtin_elementwise_fma(c25, tab, c75 * taa), h2a = __builtin_elementwise_fma(c75, tab, c25 * taa);
           const f4 h1b = __builtin_elementwise_fma(c25, tbb, c75 * tba), h2b = __builtin_elementwise_fma(c75, tbb, c25 * tba);
           f4 o00 = __builtin_elementwise_fma(c25, h1b, c75 * h1a), o01 = __builtin_elementwise_fma(c25, h2b, c75 * h2a);
