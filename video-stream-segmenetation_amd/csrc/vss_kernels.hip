@@ -520,6 +520,11 @@ __device__ __forceinline__ void commit_sum(const Staged<TOTAL> (&st)[XP], Store 
   }
 }
 
+template <bool B>
+struct ChunkTag {
+  static constexpr bool value = B;
+};
+
 // Fused inverted-residual / decoder block, specialised on its whole shape
 // (every tile and channel extent a compile-time constant: index math folds
 // to shifts/multiplies, loops unroll, accumulators stay in registers).
@@ -966,9 +971,10 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   VSS_STAMP(1);
 
   // ---- main: per-wave work units ----
+  // The accumulators start at a wave's first chunk, whose MFMAs take the
+  // inline constant 0 as their C operand (the first chunk is peeled off the
+  // chunk loop below): no zeroing moves (NACC x 4 VALU per wave).
   f4 acc[L.NACC];
-#pragma unroll
-  for (int t = 0; t < L.NACC; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
   const int pw = wave % PW, cw = wave / PW;
   // dw pixel runs (dw_run): element j of super-block sb for this lane
   constexpr int XR = dw_run(TW, NPB, MODE == MODE_IR_EXPAND ? 1 : PW);
@@ -982,7 +988,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     constexpr int HSD = hid_stride(STRIDE);
     float* hid = work + wave * P_IN_PAD * HSD;
     constexpr int NK = CIN / 16;
-    constexpr int NCBI = P_IN_PAD / 16, UNR = NCBI <= 6 ? NCBI : 2;
+    constexpr int NCBI = P_IN_PAD / 16;
     static_assert(NCBI <= 32, "one validity bit per input pixel block");
     // bit cb: this lane's pixel cb * 16 + r of the input tile lies in the
     // image (else its hidden values are the dw's zero padding).  Once per
@@ -998,13 +1004,19 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         vmask |= (yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) ? 1u << cb : 0u;
       }
     }
-    for (int ck = wave; ck < NCHUNK; ck += 4) {
+    auto expand_chunk = [&](int ck, auto first) {
+      constexpr bool FIRST = decltype(first)::value;
       const int c0 = ck << 4;
       typename AFrag<PREC>::T aw[NK];
 #pragma unroll
       for (int s = 0; s < NK; ++s) aw[s] = lds_a<PREC>(w1s, L.LD1, c0 + r, 16 * s + 4 * g);
       const f4 bias = *reinterpret_cast<const f4*>(b1s + c0 + 4 * g);
-#pragma unroll UNR
+      // (the unroll count from template parameters only: a lambda's pragma
+      // cannot name the enclosing function's constexpr locals)
+      constexpr int UNRL = block_lds(MODE, STRIDE, TH, TW, CIN, CSKIP, CH, COUT, STEM_IN).P_in_pad / 16 <= 6
+                               ? block_lds(MODE, STRIDE, TH, TW, CIN, CSKIP, CH, COUT, STEM_IN).P_in_pad / 16
+                               : 2;
+#pragma unroll UNRL
       for (int cb = 0; cb < NCBI; ++cb) {
         const int pix = cb * 16 + r;
         f4 d = bias;  // the expand's bias enters as the MFMA accumulator
@@ -1045,20 +1057,29 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
           for (int j = 0; j < XR; ++j) {
             const f4 b = to_operand<PREC>(relu6v(a[j]));
 #pragma unroll
-            for (int cb = 0; cb < NCB; ++cb)
-              acc[(q * XR + j) * NCB + cb] = mma16_op<PREC>(acc[(q * XR + j) * NCB + cb], a2[cb], b);
+            for (int cb = 0; cb < NCB; ++cb) {
+              f4& ac = acc[(q * XR + j) * NCB + cb];
+              if constexpr (FIRST)
+                ac = mma16_op<PREC>(f4{0.f, 0.f, 0.f, 0.f}, a2[cb], b);
+              else
+                ac = mma16_op<PREC>(ac, a2[cb], b);
+            }
           }
         }
       }
       wave_sync();  // this chunk's hid reads before the next chunk's expand writes
-    }
+    };
+    static_assert(NCHUNK >= 4, "every wave has a first chunk");
+    expand_chunk(wave, ChunkTag<true>{});
+    for (int ck = wave + 4; ck < NCHUNK; ck += 4) expand_chunk(ck, ChunkTag<false>{});
   } else {
     // dw 3x3 straight into the project MFMA's B layout (lane (r, g): pixel r
     // of the block, channels c0+4g..c0+4g+3); no LDS round trip, no syncs.
     // Chunk-outer: the chunk's dw taps and project fragments are read from
     // LDS once and reused for every pixel block of the wave (each
     // accumulator still sums its chunks in the same order).
-    for (int ck = cw; ck < NCHUNK; ck += CS) {
+    auto dw_chunk = [&](int ck, auto first) {
+      constexpr bool FIRST = decltype(first)::value;
       const int c0 = ck << 4;
       f4 wk[9];
 #pragma unroll
@@ -1089,11 +1110,19 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
           if constexpr (MODE == MODE_IR_DIRECT) a[j] = relu6v(a[j]);
           const f4 b = to_operand<PREC>(a[j]);
 #pragma unroll
-          for (int cb = 0; cb < NCB; ++cb)
-            acc[(q * XR + j) * NCB + cb] = mma16_op<PREC>(acc[(q * XR + j) * NCB + cb], a2[cb], b);
+          for (int cb = 0; cb < NCB; ++cb) {
+            f4& ac = acc[(q * XR + j) * NCB + cb];
+            if constexpr (FIRST)
+              ac = mma16_op<PREC>(f4{0.f, 0.f, 0.f, 0.f}, a2[cb], b);
+            else
+              ac = mma16_op<PREC>(ac, a2[cb], b);
+          }
         }
       }
-    }
+    };
+    static_assert(CS <= NCHUNK, "every wave has a first chunk");
+    dw_chunk(cw, ChunkTag<true>{});
+    for (int ck = cw + CS; ck < NCHUNK; ck += CS) dw_chunk(ck, ChunkTag<false>{});
   }
 
   // ---- epilogue: slabs -> fixed-order sum, bias, residual, store ----
