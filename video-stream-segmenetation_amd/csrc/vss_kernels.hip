@@ -505,20 +505,45 @@ struct Staged {
   }
 };
 
-// Commit XP staged copies of the same items as their sum, in part order.
-template <int TOTAL, int XP, class Store>
-__device__ __forceinline__ void commit_sum(const Staged<TOTAL> (&st)[XP], Store store) {
+// A staged copy of NI items of four consecutive float4s (16 channels of one
+// pixel) from NP parts (the hidden-split partial sums) at the same offsets:
+// one index computation per 16 channels instead of per 4, the four loads at
+// immediate offsets (16 B apart) off a 32-bit offset from each part's
+// wave-uniform base; commit_sum adds the parts in part order.
+template <int NI, int NP>
+struct Staged16 {
+  static constexpr int PER = (NI + 255) / 256;
+  f4 v[NP][PER > 0 ? PER : 1][4];
+  template <class Off>
+  __device__ __forceinline__ void issue(const float* const (&base)[NP], Off off) {
 #pragma unroll
-  for (int u = 0; u < Staged<TOTAL>::PER; ++u) {
-    const int i = (int)threadIdx.x + 256 * u;
-    if (i < TOTAL) {
-      f4 v = st[0].v[u];
+    for (int u = 0; u < PER; ++u) {
+      const int i = (int)threadIdx.x + 256 * u;
+      const unsigned o = off(i < NI ? i : NI - 1);  // float offset of the item's first channel
 #pragma unroll
-      for (int q = 1; q < XP; ++q) v = v + st[q].v[u];
-      store(i, v);
+      for (int q = 0; q < NP; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[q][u][k] = *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(base[q]) + ((o + 4u * k) << 2));
     }
   }
-}
+  template <class Store>  // store(item, k, the parts' sum of float4 k of the item)
+  __device__ __forceinline__ void commit_sum(Store st) const {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int i = (int)threadIdx.x + 256 * u;
+      if (NI % 256 == 0 || i < NI) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          f4 x = v[0][u][k];
+#pragma unroll
+          for (int q = 1; q < NP; ++q) x = x + v[q][u][k];
+          st(i, k, x);
+        }
+      }
+    }
+  }
+};
 
 template <bool B>
 struct ChunkTag {
@@ -587,7 +612,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   const f4* wsrc = reinterpret_cast<const f4*>(p.wimg + ks * p.wimg_stride);
   f4* wdst = reinterpret_cast<f4*>(smem + L.w1);
   if constexpr (MODE == MODE_DEC) {
-    constexpr int CL = CIN, C4L = CL / 4, C4S = CSKIP / 4, SR = L.SR, SC = L.SC;
+    constexpr int CL = CIN, C4L = CL / 4, SR = L.SR, SC = L.SC;
     const int h = p.H, w = p.W;
     float* lr = smem + L.lr;
     float* nrm = smem + L.nrm;
@@ -599,25 +624,27 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     Staged<NSLOT16> st_slots;
     const Gm<COH> g_slots(reinterpret_cast<const float*>(p.in_acc + (long)n * p.acc_stride));
     if constexpr (NORM_IN) st_slots.issue([&](int i) { return g_slots.ld(4L * i); });
-    Staged<SR * SC * C4L> st_lr[XP];
-    Staged<P_IN_PAD * C4S> st_sk[SP];
+    static_assert(CL % 16 == 0 && CSKIP % 16 == 0, "16-channel staging items");
+    constexpr int GL = CL / 16, GS = CSKIP / 16;  // 16-channel items per pixel
+    Staged16<SR * SC * GL, XP> st_lr;
+    Staged16<P_IN_PAD * GS, SP> st_sk;
     Staged<WIMG_F4> st_w;
+    {
+      const float* xb[XP];
 #pragma unroll
-    for (int q = 0; q < XP; ++q) {
-      const Gm<COH> gx(xn + q * p.x_part_stride);
-      st_lr[q].issue([&](int i) {
-        const int pr = i / C4L, c4 = i % C4L;
+      for (int q = 0; q < XP; ++q) xb[q] = xn + q * p.x_part_stride;
+      st_lr.issue(xb, [&](int i) {
+        const int pr = i / GL, gq = i - pr * GL;
         const int yy = min(h - 1, sy0 + pr / SC), xx = min(w - 1, sx0 + pr % SC);
-        return gx.ldu((unsigned)((yy * w + xx) * CL + 4 * c4));
+        return (unsigned)((yy * w + xx) * CL + 16 * gq);
       });
-    }
+      const float* sb[SP];
 #pragma unroll
-    for (int q = 0; q < SP; ++q) {
-      const Gm<COH> gs(sn + q * p.skip_part_stride);
-      st_sk[q].issue([&](int i) {
-        const int pix = i / C4S, c4 = i % C4S;
-        const int yy = min(max(iy0 + pix / IW, 0), Ho - 1), xx = min(max(ix0 + pix % IW, 0), Wo - 1);
-        return gs.ldu((unsigned)((yy * Wo + xx) * CSKIP + 4 * c4));
+      for (int q = 0; q < SP; ++q) sb[q] = sn + q * p.skip_part_stride;
+      st_sk.issue(sb, [&](int i) {
+        const int pix = i / GS, gq = i - pix * GS, py = pix / IW;
+        const int yy = min(max(iy0 + py, 0), Ho - 1), xx = min(max(ix0 + pix - py * IW, 0), Wo - 1);
+        return (unsigned)((yy * Wo + xx) * CSKIP + 16 * gq);
       });
     }
     st_w.issue([&](int i) { return wsrc[i]; });
@@ -671,24 +698,25 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     }
     // the low-res src region; with norm_in, relu(src * scale + shift) applied
     // once per element as it is committed
-    commit_sum(st_lr, [&](int i, f4 v) {
+    st_lr.commit_sum([&](int i, int k, f4 v) {
+      // item i = (region pixel, 16-channel group): its floats are contiguous in lr
       if constexpr (NORM_IN) {
-        const int c4 = i % C4L;
+        const int c4 = (i % GL) * 4 + k;
         v = reluv(v * *reinterpret_cast<const f4*>(nrm + 4 * c4) + *reinterpret_cast<const f4*>(nrm + CL + 4 * c4));
       }
-      reinterpret_cast<f4*>(lr)[i] = v;
+      reinterpret_cast<f4*>(lr)[4 * i + k] = v;
     });
     // the skip channels: zero outside the image (tiles at its edge only; the
     // loads were clamped to real pixels, and padding pixels are never read)
     const bool sk_interior = iy0 >= 0 && iy0 + L.IH <= Ho && ix0 >= 0 && ix0 + IW <= Wo;
-    commit_sum(st_sk, [&](int i, f4 v) {
-      const int pix = i / C4S, c4 = i % C4S;
+    st_sk.commit_sum([&](int i, int k, f4 v) {
+      const int pix = i / GS, gq = i - pix * GS;
       if (!sk_interior) {
         const int py = pix / IW, yy = iy0 + py, xx = ix0 + pix - py * IW;
         const bool valid = ((unsigned)yy < (unsigned)Ho) & ((unsigned)xx < (unsigned)Wo);
         v = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
       }
-      *reinterpret_cast<f4*>(xt + pix * XS + CL + 4 * c4) = v;
+      *reinterpret_cast<f4*>(xt + pix * XS + CL + 16 * gq + 4 * k) = v;
     });
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     VSS_STAMP(4);
@@ -929,24 +957,26 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     }
 
   } else {
-    constexpr int C4 = CIN / 4;
     const int H = p.H, W = p.W;
     const float* xn = p.x + (long)n * H * W * CIN;
-    Staged<P_IN_PAD * C4> st_x[XP];
+    static_assert(CIN % 16 == 0, "16-channel staging items");
+    constexpr int GI = CIN / 16;  // 16-channel items per pixel
+    Staged16<P_IN_PAD * GI, XP> st_x;
     Staged<WIMG_F4> st_w;
+    {
+      const float* xb[XP];
 #pragma unroll
-    for (int q = 0; q < XP; ++q) {
-      const Gm<COH> gx(xn + q * p.x_part_stride);
-      st_x[q].issue([&](int i) {
-        const int pix = i / C4, c4 = i % C4;
-        const int yy = min(max(iy0 + pix / IW, 0), H - 1), xx = min(max(ix0 + pix % IW, 0), W - 1);
-        return gx.ldu((unsigned)((yy * W + xx) * CIN + 4 * c4));
+      for (int q = 0; q < XP; ++q) xb[q] = xn + q * p.x_part_stride;
+      st_x.issue(xb, [&](int i) {
+        const int pix = i / GI, gq = i - pix * GI, py = pix / IW;
+        const int yy = min(max(iy0 + py, 0), H - 1), xx = min(max(ix0 + pix - py * IW, 0), W - 1);
+        return (unsigned)((yy * W + xx) * CIN + 16 * gq);
       });
     }
     st_w.issue([&](int i) { return wsrc[i]; });
     VSS_STAMP(6);  // every load issued
-    commit_sum(st_x, [&](int i, f4 v) {
-      const int pix = i / C4, c4 = i % C4;
+    st_x.commit_sum([&](int i, int k, f4 v) {
+      const int pix = i / GI, c4 = (i - pix * GI) * 4 + k;
       if constexpr (MODE == MODE_IR_EXPAND) {
         // no validity test: an expand layer's input pixels outside the image
         // only feed hidden pixels that the expand loop zeroes (its clamp
