@@ -99,21 +99,21 @@ def test_conv_tile_forms(ort, precision):
     _check(got, want, f"conv_tiles {precision}")
 
 
-# MODNet's matte (a sigmoid in [0, 1]) with 16-bit convolution operands.  With
-# seeded weights some IBNorm InstanceNorm channels come out nearly constant
-# over the image, and at the export's epsilon 1e-5 the norm multiplies their
-# operand rounding by up to 1/sqrt(1e-5) ~ 316: the oracle itself then moves
-# by 0.018 max (f16) / 0.09 (bf16) between f32 and rounded operands, and two
-# roundings of the same values after slightly different f32 / f64 histories
-# land as far apart.  The 16-bit cases therefore run a well-conditioned seeded
-# MODNet (in_eps = 1e-3: the same graph with those channels' gain bounded by
-# ~32), where the precision's cost is 0.0013 max (f16) — the reference's
-# q4f16 arithmetic (main.ts:6, model.ts:12-29) — and the GPU is held to 1e-2
-# of the same-rounding oracle.  bf16 (8-bit mantissa) stays a measured
-# precision cost (0.09 max vs f32 in the oracle alone), bounded and reported.
+# MODNet's matte (a sigmoid in [0, 1]) with 16-bit convolution operands, on
+# the graph as exported (InstanceNormalization epsilon 1e-5 everywhere; round 3
+# ran the 16-bit cases at 1e-3).  Every InstanceNorm input channel of the
+# seeded net has a variance far above that epsilon on the test frame (the
+# smallest, 0.018, in the 144x256 one; test_modnet_instance_norm_conditioning
+# checks it), so the norm does not blow up operand rounding.  The q4f16 form
+# (the reference's model_q4f16.onnx arithmetic, main.ts:6, model.ts:12-29)
+# carries f16 weights, so f16 operands round only its activations: the oracle
+# itself moves 0.0018 max between f32 and f16 operands, and the GPU is held to
+# 1e-2 of the same-rounding oracle and of the f32 one.  bf16 operands round
+# the f32-form weights too (8-bit mantissa): 0.089 max in the oracle alone,
+# a measured precision cost, bounded and reported.
 MODNET_TOL = {"f32": TOL, "f16": 1e-2}       # vs the oracle with the same operand rounding
 MODNET_BF16_COST = (0.15, 0.02)              # (max, mean) vs the f32 oracle: bf16 rounding, not parity
-MODNET_IN_EPS = {"f32": 1e-5, "f16": 1e-3, "bf16": 1e-3}
+MODNET_IN_EPS = {"f32": 1e-5, "f16": 1e-5, "bf16": 1e-5}  # the export's own epsilon
 
 
 @pytest.fixture(scope="module")

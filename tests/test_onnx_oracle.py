@@ -153,3 +153,20 @@ def test_q4f16_operators():
     with np.errstate(over="ignore"):
         want = v.astype(np.float16).astype(np.float32)
     assert np.array_equal(R.run(m, {"v": v})["y"].astype(np.float32), want)
+
+
+def test_modnet_instance_norm_conditioning():
+    """The seeded MODNet's InstanceNormalization inputs on the GPU tests' frame
+    (tests/test_gpu_onnx.py::modnet_cases): every channel's variance is far
+    above the export's epsilon (1e-5), so the 16-bit GPU cases run the graph as
+    exported without the norm amplifying operand rounding (VERDICT r3 #6)."""
+    import onnx_models as M
+    m = R.load(M.modnet(q4f16=True, in_eps=1e-5))
+    x = np.random.default_rng(21).random((1, 3, 288, 512), dtype=np.float32)
+    nodes = [nd for nd in m.nodes if nd["op"] == "InstanceNormalization"]
+    assert len(nodes) == 16
+    assert all(abs(nd["attrs"].get("epsilon", 1e-5) - 1e-5) < 1e-12 for nd in nodes)
+    got = R.run(m, {"input": x}, want=[nd["inputs"][0] for nd in nodes])
+    worst = min(float(v.astype(np.float64).var(axis=(2, 3)).min()) for v in got.values())
+    print(f"smallest InstanceNorm input variance {worst:.4g} (eps 1e-5)")
+    assert worst >= 100 * 1e-5
