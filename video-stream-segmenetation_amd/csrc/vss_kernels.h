@@ -72,6 +72,11 @@ constexpr int kMaxAcc = 16;         // 16x16 project accumulators per wave
 #ifndef VSS_HS1
 #define VSS_HS1 20
 #endif
+// decoders with even tiles upsample by 2x2 quads (VSS_QUADS=0: per pixel,
+// from tap records, as odd tiles always do — an A/B knob)
+#ifndef VSS_QUADS
+#define VSS_QUADS 1
+#endif
 __host__ __device__ constexpr int block_pix(int r) { return VSS_PERM ? (r < 4 ? r : (r < 12 ? r + 4 : r - 8)) : r; }
 // floats per pixel of an expand wave's hidden chunk in LDS (16 channels + pad)
 __host__ __device__ constexpr int hid_stride(int stride) { return stride == 2 ? 20 : VSS_HS1; }
@@ -155,7 +160,7 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   // decoder: per input-tile pixel, its 2x-upsample taps (four lr offsets as
   // u16 pairs, ly1, lx1), built while the prologue loads are in flight — only
   // for tiles with an odd side; even tiles upsample by 2x2 quads (dec_quads)
-  L.uc = o;  o += (mode == 2 && (TH % 2 || TW % 2)) ? 4 * L.P_in_pad : 0;
+  L.uc = o;  o += (mode == 2 && (!VSS_QUADS || TH % 2 || TW % 2)) ? 4 * L.P_in_pad : 0;
   L.slab = slab_in_xt ? L.xt : L.work;
   L.stt = slab_in_xt ? L.work : L.xt;
   L.total = o;

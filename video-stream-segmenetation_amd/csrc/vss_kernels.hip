@@ -506,24 +506,37 @@ struct Staged {
 };
 
 // A staged copy of NI items of four consecutive float4s (16 channels of one
-// pixel) from NP parts (the hidden-split partial sums) at the same offsets:
-// one index computation per 16 channels instead of per 4, the four loads at
-// immediate offsets (16 B apart) off a 32-bit offset from each part's
-// wave-uniform base; commit_sum adds the parts in part order.
+// pixel) from NP parts (the hidden-split partial sums) at the same offsets;
+// commit_sum adds the parts in part order.  Two lane mappings:
+//  VSS_STAGE16 = 1: a lane takes whole items — one index computation per 16
+//    channels, its four loads at immediate offsets (16 B apart) off a 32-bit
+//    offset from each part's wave-uniform base;
+//  VSS_STAGE16 = 0: float4 j of the copy goes to lane j % 256 (a wave's load
+//    instruction reads 1 KiB contiguous), one index computation per float4.
+#ifndef VSS_STAGE16
+#define VSS_STAGE16 1
+#endif
 template <int NI, int NP>
 struct Staged16 {
-  static constexpr int PER = (NI + 255) / 256;
-  f4 v[NP][PER > 0 ? PER : 1][4];
+  static constexpr int PER = VSS_STAGE16 ? (NI + 255) / 256 : (4 * NI + 255) / 256;
+  static constexpr int V = VSS_STAGE16 ? 4 : 1;
+  f4 v[NP][PER > 0 ? PER : 1][V];
   template <class Off>
   __device__ __forceinline__ void issue(const float* const (&base)[NP], Off off) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      const int i = (int)threadIdx.x + 256 * u;
-      const unsigned o = off(i < NI ? i : NI - 1);  // float offset of the item's first channel
+      const int j = (int)threadIdx.x + 256 * u;
+      unsigned o;
+      if constexpr (VSS_STAGE16) {
+        o = off(j < NI ? j : NI - 1);  // float offset of the item's first channel
+      } else {
+        const int jj = j < 4 * NI ? j : 4 * NI - 1;
+        o = off(jj >> 2) + 4u * (unsigned)(jj & 3);
+      }
 #pragma unroll
       for (int q = 0; q < NP; ++q)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < V; ++k)
           v[q][u][k] = *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(base[q]) + ((o + 4u * k) << 2));
     }
   }
@@ -531,14 +544,18 @@ struct Staged16 {
   __device__ __forceinline__ void commit_sum(Store st) const {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      const int i = (int)threadIdx.x + 256 * u;
-      if (NI % 256 == 0 || i < NI) {
+      const int j = (int)threadIdx.x + 256 * u;
+      constexpr int TOT = VSS_STAGE16 ? NI : 4 * NI;  // items, or float4s
+      if (TOT % 256 == 0 || j < TOT) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < V; ++k) {
           f4 x = v[0][u][k];
 #pragma unroll
           for (int q = 1; q < NP; ++q) x = x + v[q][u][k];
-          st(i, k, x);
+          if constexpr (VSS_STAGE16)
+            st(j, k, x);
+          else
+            st(j >> 2, j & 3, x);
         }
       }
     }
@@ -657,7 +674,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     // even tiles start at an odd row and column of the output (iy0 = TH*by - 1),
     // so their input tile is whole 2x2 quads that share one 2x2 source window:
     // the upsample below runs per quad and needs no per-pixel tap records
-    constexpr bool QUADS = TH % 2 == 0 && TW % 2 == 0;
+    constexpr bool QUADS = VSS_QUADS && TH % 2 == 0 && TW % 2 == 0;
     unsigned* uc = reinterpret_cast<unsigned*>(smem + L.uc);
     if constexpr (!QUADS)
     for (int pix = tid; pix < P_IN_PAD; pix += 256) {
