@@ -1531,25 +1531,42 @@ __device__ __forceinline__ void head_body(const HeadParams& p, int bx, int by, i
   }
   __syncthreads();
   VSS_STAMP(2);
+  // bilinear x2 (align_corners=False) by 2 x 2 output blocks: output rows 2m
+  // and 2m + 1 lie between logit rows (m - 1, m) at weights (0.25, 0.75) and
+  // (m, m + 1) at (0.75, 0.25), columns alike, so one block reads a 3 x 3
+  // logit window at constant weights: per logit row the two horizontal
+  // interpolants, then the four vertical ones.  The region's rows / columns
+  // outside the image hold the edge logits (clamped loads), which is the
+  // clamp of the source index.  One block per thread (16 x 64 = 256 blocks).
+  static_assert(OTH * OTW == 4 * 256 && OTW == 64 && ZR == OTH / 2 + 2 && ZC == OTW / 2 + 2, "head blocks");
+  {
+    const int by2 = tid >> 5, bx2 = tid & 31;
+    float hz[3][2];
 #pragma unroll
-  for (int k = 0; k < (OTH * OTW) / 256; ++k) {
-    const int idx = tid + 256 * k;
-    const int ly = idx / OTW, lx = idx - ly * OTW;
-    const int oy = oy0 + ly, ox = ox0 + lx;
-    if (oy < p.Hm && ox < p.Wm) {
-      float sy = ((float)oy + 0.5f) * 0.5f - 0.5f;
-      sy = fmaxf(sy, 0.f);
-      const int y0 = (int)sy, y1 = y0 + (y0 < h - 1 ? 1 : 0);
-      const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
-      float sx = ((float)ox + 0.5f) * 0.5f - 0.5f;
-      sx = fmaxf(sx, 0.f);
-      const int x0 = (int)sx, x1 = x0 + (x0 < w - 1 ? 1 : 0);
-      const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
-      const float v = ly0 * (lx0 * z[y0 - zr0][x0 - zc0] + lx1 * z[y0 - zr0][x1 - zc0]) +
-                      ly1 * (lx0 * z[y1 - zr0][x0 - zc0] + lx1 * z[y1 - zr0][x1 - zc0]);
-      // sigmoid from the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32: ~1e-7
-      // off the libm form, against the 1e-3 mask tolerance)
-      p.mask[((long)n * p.Hm + oy) * p.Wm + ox] = __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+    for (int r = 0; r < 3; ++r) {
+      const float a = z[by2 + r][bx2], b = z[by2 + r][bx2 + 1], c = z[by2 + r][bx2 + 2];
+      hz[r][0] = __builtin_fmaf(0.75f, b, 0.25f * a);  // column 2n
+      hz[r][1] = __builtin_fmaf(0.25f, c, 0.75f * b);  // column 2n + 1
+    }
+    const int oy = oy0 + 2 * by2, ox = ox0 + 2 * bx2;
+    float* mrow = p.mask + ((long)n * p.Hm + oy) * p.Wm + ox;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      float o[2];
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const float v = dy == 0 ? __builtin_fmaf(0.75f, hz[1][dx], 0.25f * hz[0][dx])
+                                : __builtin_fmaf(0.25f, hz[2][dx], 0.75f * hz[1][dx]);
+        // sigmoid from the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32:
+        // ~1e-7 off the libm form, against the 1e-3 mask tolerance)
+        o[dx] = __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+      }
+      if (oy + dy < p.Hm) {
+        if (ox + 1 < p.Wm)
+          *reinterpret_cast<float2*>(mrow + dy * p.Wm) = float2{o[0], o[1]};
+        else if (ox < p.Wm)
+          mrow[dy * p.Wm] = o[0];
+      }
     }
   }
   VSS_STAMP(3);
