@@ -1,6 +1,6 @@
 // VERDICT r3 #4: the 400-batch segmentFrames loop that once crashed Node 12 at
 // exit (in its GC-deferred N-API finalizers), run to a NATURAL exit — no
-// process.exit, no exit guard when VSS_NODE_EXIT_GUARD=0.  Prints one JSON
+// process.exit; the exit guard is opt-in (VSS_NODE_EXIT_GUARD=1).  Prints one JSON
 // line; the caller asserts the exit status.
 //   node run_exit.js [batches]
 'use strict';

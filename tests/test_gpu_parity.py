@@ -87,6 +87,27 @@ def test_masks_vs_oracle(pkg, sess_f32, sess_bf, oracle, blob, synthetic, mode):
     assert err <= MASK_TOL
 
 
+@pytest.mark.parametrize("mode", ["f32", "bf16x2"])
+def test_hidden_split_opt_in(pkg, oracle, blob, synthetic, mode, monkeypatch):
+    """The hidden-channel split (off by default since round 4: it loses at 4
+    batches in flight) stays correct when opted in (VSS_KSPLIT=1): the deep
+    expand layers run KS workgroups per tile and their consumers sum the parts
+    (kernel flags carry KS / XP), masks within the bar of the oracle, and the
+    results are independent of the tile as with the split off."""
+    monkeypatch.setenv("VSS_KSPLIT", "1")
+    f = _frames(synthetic, 8)
+    ref = oracle.forward(blob, f, 144, 256, mode=0).reshape(8, -1)
+    with pkg.Session(dtype=mode, max_batch=8, max_frame_h=480, max_frame_w=640) as s:
+        names = [s.layer_kernel(i) for i in range(s.n_layers)]
+        masks, _, _ = s.segment_frames(f)
+    flags = [int(n.split("<")[1].split(",")[8]) for n in names if "k_block<" in n]
+    assert any((fl >> 6) & 3 for fl in flags), names  # some layer split (KS > 1)
+    assert any((fl >> 2) & 3 for fl in flags), names  # some consumer summing parts (XP > 1)
+    err = float(np.abs(masks - ref).max())
+    print(f"{mode} with the hidden split: mask max abs err vs oracle = {err:.3e}")
+    assert err <= MASK_TOL
+
+
 @pytest.mark.parametrize("name", ["vga_2f_144x256", "odd_rgba_1f_32x48"])
 def test_masks_vs_golden(pkg, synthetic, name, torch_cuda):
     g = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)

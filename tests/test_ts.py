@@ -313,15 +313,17 @@ def test_node_result_blocks_recycled_safely(addon_built, synthetic, tmp_path):
 @pytest.mark.gpu
 def test_node_natural_exit_without_guard(addon_built):
     """the 400-batch loop that once crashed Node 12 at exit, run
-    to a natural exit with the exit guard off (VSS_NODE_EXIT_GUARD=0): the
-    addon's own fix (no N-API call from a finalizer after the environment's
-    cleanup hook, a never-destroyed result pool) must carry it alone."""
+    to a natural exit with the default settings (no exit guard since round 4;
+    VSS_NODE_EXIT_GUARD=1 opts back in): the addon's own fix (no N-API call
+    from a finalizer after the environment's cleanup hook, a never-destroyed
+    result pool) carries it alone."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = dict(os.environ, VSS_NODE_EXIT_GUARD="0")
+    env = dict(os.environ)
+    env.pop("VSS_NODE_EXIT_GUARD", None)
     out = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "run_exit.js"), "400"], capture_output=True,
                          text=True, timeout=200, env=env)
     assert out.returncode == 0, (out.returncode, out.stderr[-2000:])
     last = json.loads(out.stdout.strip().splitlines()[-1])
-    assert last["frames"] == 8 * 550 and last["guard"] == "0"
+    assert last["frames"] == 8 * 550 and last["guard"] == "default"

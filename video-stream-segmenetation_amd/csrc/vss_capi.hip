@@ -326,7 +326,13 @@ struct vss_handle {
   // expand layers with at most this many output pixels per frame split their
   // hidden channels over ks_max() workgroups (env VSS_KSPLIT_PIXELS overrides)
   long ksplit_pixels = kDefaultKsplitPixels;
-  bool ksplit_on = true;       // env VSS_KSPLIT=0 turns the hidden split off (both rules)
+  // The hidden-channel split (KS workgroups per tile of a deep low-res expand
+  // layer, consumers summing the parts) buys latency with one batch in flight
+  // and costs throughput with four: measured round 4 (profiles/r04a/session.txt,
+  // two interleaved pairs): headline 206.9 / 206.1k without against 194.7 /
+  // 203.7k with, batch sweep at 4 in flight +4 % (b8), +7.5 % (b32), +6 % (b64),
+  // at 1 in flight -3 % (b8).  Off by default; env VSS_KSPLIT=1 turns it on.
+  bool ksplit_on = false;
   // profiling: ring of event pairs per layer
   static constexpr int kProfRing = 32;
   std::vector<hipEvent_t> ev;  // [ring][layer][2]
@@ -594,7 +600,7 @@ int plan(vss_handle* h) {
     // hidden split: expand layers whose output has at most ksplit_pixels
     // pixels per frame (a function of the model resolution only, so results
     // never depend on the batch or the autotuner)
-    // (env VSS_KSPLIT=0: no hidden split at all, either rule — an A/B knob)
+    // (only with VSS_KSPLIT=1: see ksplit_on)
     if (l.mode == MODE_IR_EXPAND && h->ksplit_on &&
         ((long)l.H * l.W <= h->ksplit_pixels || weight_image_bytes(l) > kKsplitWeightBytes))
       l.ks = ks_max(l);
@@ -863,6 +869,7 @@ BlockParams block_params(const vss_handle* h, const Slot& s, int li, int n) {
       p.in_gamma = src.gamma;
       p.in_beta = src.beta;
       p.in_hw = src.H * src.W;
+      p.in_inv_hw = 1.0 / (double)p.in_hw;
     }
   }
   return p;
@@ -922,6 +929,7 @@ void forward_launches(vss_handle* h, Slot& s, const uint8_t* frames, int n, int 
       p.gamma = src.gamma; p.beta = src.beta; p.eps = h->eps;
       p.w = l.head_w; p.b = l.head_b; p.mask = masks;
       p.N = n; p.h = src.H; p.w_ = src.W; p.cin = src.C; p.Hm = Hm; p.Wm = Wm;
+      p.inv_hw = 1.0 / ((double)src.H * src.W);
 #ifdef VSS_TRACE
       p.trace = s.trace[i];
       h->trace_wgs[i] = ((Wm + kHeadTW - 1) / kHeadTW) * ((Hm + kHeadTH - 1) / kHeadTH) * n;

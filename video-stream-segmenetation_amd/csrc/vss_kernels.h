@@ -237,6 +237,7 @@ struct BlockParams {
   const float* in_gamma;             // src layer's norm affine [cin]
   const float* in_beta;
   int in_hw;                         // pixels per frame of the src
+  double in_inv_hw;                  // 1 / in_hw
   unsigned long long* out_acc;       // DEC: this layer's accumulator [N][acc_stride] + offset
                                      // (kAccSlots slots of [2][cout]; workgroup -> slot tile % kAccSlots)
   int acc_stride;                    // int64 elements per frame over all decoder layers
@@ -306,6 +307,7 @@ struct HeadParams {
   const float* gamma;    // its norm affine [cin]
   const float* beta;
   float eps;
+  double inv_hw;         // 1 / (h * w_)
   const float* w;        // [cin]
   float b;
   float* mask;           // [N][Hm][Wm] f32
@@ -322,12 +324,25 @@ constexpr int kHeadTH = 16, kHeadTW = 64, kHeadZR = 10, kHeadZC = 34, kHeadZCP =
 constexpr int kHeadLds = kAccSlots * 2 * 16 * 2 + r4(kHeadZR * kHeadZCP) + 3 * 16;
 
 // Instance-norm scale/shift of one channel from the exact fixed-point totals.
-__host__ __device__ inline void norm_affine(unsigned long long s_fx, unsigned long long q_fx, int hw, float eps,
-                                            float gamma, float beta, float* scale, float* shift) {
-  const double mean = (double)(long long)s_fx * 0x1p-32 / (double)hw;
-  const double ex2 = (double)(long long)q_fx * 0x1p-24 / (double)hw;
+// inv_hw = 1 / (pixels per frame), computed by the host: the mean and E[x^2]
+// take one f64 multiply each instead of an f64 division, and 1/sqrt(var + eps)
+// is v_rsq_f64 refined by two Newton steps (~2^-50 relative; rounded to f32
+// after) instead of an f64 sqrt and division — the norm's setup runs on the
+// prologue's critical path of every decoder workgroup and the head.
+__host__ __device__ inline void norm_affine(unsigned long long s_fx, unsigned long long q_fx, double inv_hw,
+                                            float eps, float gamma, float beta, float* scale, float* shift) {
+  const double mean = (double)(long long)s_fx * (0x1p-32 * inv_hw);
+  const double ex2 = (double)(long long)q_fx * (0x1p-24 * inv_hw);
   const double var = ex2 - mean * mean > 0.0 ? ex2 - mean * mean : 0.0;
-  const float rstd = (float)(1.0 / __builtin_sqrt(var + (double)eps));
+  const double x = var + (double)eps;
+#ifdef __HIP_DEVICE_COMPILE__
+  double r = __builtin_amdgcn_rsq(x);
+  r = r * __builtin_fma(-0.5 * x * r, r, 1.5);
+  r = r * __builtin_fma(-0.5 * x * r, r, 1.5);
+#else
+  const double r = 1.0 / __builtin_sqrt(x);
+#endif
+  const float rstd = (float)r;
   const float sc = rstd * gamma;
   *scale = sc;
   *shift = beta - (float)mean * sc;

@@ -708,7 +708,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
           s_fx += sl[k * 2 * CL + tid];
           q_fx += sl[k * 2 * CL + CL + tid];
         }
-        norm_affine(s_fx, q_fx, p.in_hw, p.eps, gam, bet, nrm + tid, nrm + CL + tid);
+        norm_affine(s_fx, q_fx, p.in_inv_hw, p.eps, gam, bet, nrm + tid, nrm + CL + tid);
       }
       __syncthreads();
       VSS_STAMP(5);
@@ -1512,7 +1512,7 @@ __device__ __forceinline__ void head_body(const HeadParams& p, int bx, int by, i
       s_fx += slots[k * 2 * C + tid];
       q_fx += slots[k * 2 * C + C + tid];
     }
-    norm_affine(s_fx, q_fx, h * w, p.eps, p.gamma[tid], p.beta[tid], sc + tid, sh + tid);
+    norm_affine(s_fx, q_fx, p.inv_hw, p.eps, p.gamma[tid], p.beta[tid], sc + tid, sh + tid);
   }
   __syncthreads();
   VSS_STAMP(1);
