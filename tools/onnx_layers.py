@@ -31,8 +31,14 @@ def run(key, out):
     bench._load_pkg()
     import vss_amd.ort as ort
     import onnx_models as M
-    model = M.load_golden(os.path.join(ROOT, "tests", "golden", key + ".npz"))[0]
-    with ort.InferenceSession(model) as s:
+    if key.startswith("modnet"):  # modnet[_q4f16]:B:PREC — the full topology at 288x512
+        name, b, prec = (key.split(":") + ["1", "bf16"])[:3]
+        model = M.modnet(288, 512, q4f16=name.endswith("q4f16"))
+        kw = {"input_shape": (int(b), 3, 288, 512), "precision": prec}
+    else:
+        model = M.load_golden(os.path.join(ROOT, "tests", "golden", key + ".npz"))[0]
+        kw = {}
+    with ort.InferenceSession(model, **kw) as s:
         din = [torch.rand(sh, dtype=torch.float32, device="cuda") for sh in s.input_shapes]
         dout = [torch.empty(sh, dtype=torch.float32, device="cuda") for sh in s.output_shapes]
         st = torch.cuda.Stream()

@@ -21,10 +21,11 @@ from collections import defaultdict
 d = defaultdict(lambda: defaultdict(list))
 for r in csv.DictReader(open(sys.argv[1])):
     d[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+hot = max(len(c.get("SQ_WAVES", [])) for c in d.values())
 for k, c in sorted(d.items(), key=lambda kv: -len(kv[1].get("SQ_WAVES", []))):
     m = {n: sum(v) / len(v) for n, v in c.items()}
     wc = m.get("SQ_WAVE_CYCLES", 0) or 1
-    if len(c.get("SQ_WAVES", [])) < 100:
+    if len(c.get("SQ_WAVES", [])) < 0.8 * hot:  # the timed forwards' kernels only
         continue
     print(f"wait {m.get('SQ_WAIT_ANY', 0) / wc:5.2f} issue-stall {m.get('SQ_WAIT_INST_ANY', 0) / wc:5.2f} active "
           f"{m.get('SQ_ACTIVE_INST_ANY', 0) / wc:5.2f} (valu {m.get('SQ_ACTIVE_INST_VALU', 0) / wc:5.2f} lds "

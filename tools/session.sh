@@ -3,7 +3,7 @@
 # time limit, and a GPU fault / abort / kill / time-out stops the script):
 #   1 the GPU test suite          2 interleaved A/B vs the base library
 #   3 an SQ PMC pass (VALU / LDS / MFMA per kernel)
-#   4 the hidden-split A/B (VSS_KSPLIT=0)   5 a MODNet b8 kernel trace
+#   4 a wave-state pass   5 a MODNet b8 kernel trace and its per-launch table
 # Usage: bash tools/session.sh TAG [LIB ...]   (default: every ablib/libvss_*.so)
 TAG=${1:-s}
 shift || true
@@ -23,11 +23,15 @@ echo "== SQ pass"
 timeout -k 10 200 bash tools/prof_sq.sh ${TAG}; fatal $?
 echo "== stall pass"
 timeout -k 10 200 bash tools/prof_stall.sh ${TAG}; fatal $?
-echo "== hidden split A/B"
-timeout -k 10 400 bash tools/ab_env.sh 2 "VSS_KSPLIT=1" "VSS_KSPLIT=0"; fatal $?
 echo "== MODNet b8 trace"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_modnet" -o run -- \
   python3 "$R/tools/bench_onnx.py" --only-modnet --batch 8 --iters 50 --cases b8_bf16 > "$R/gpurun_out/${TAG}_modnet.log" 2>&1
 rc=$?; cd "$R"; tail -2 gpurun_out/${TAG}_modnet.log; fatal $rc
 python3 tools/trace_top.py gpurun_out/${TAG}_modnet/run_kernel_stats.csv 25
+echo "== MODNet b8 bf16 per launch"
+cd /tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/${TAG}_ml" -o run -- \
+  python3 "$R/tools/onnx_layers.py" run modnet:8:bf16 "$R/gpurun_out/${TAG}_ml/launches.json" > "$R/gpurun_out/${TAG}_ml.log" 2>&1
+rc=$?; cd "$R"; fatal $rc
+python3 tools/onnx_layers.py report gpurun_out/${TAG}_ml/launches.json gpurun_out/${TAG}_ml/run_kernel_trace.csv 2>&1 | head -60

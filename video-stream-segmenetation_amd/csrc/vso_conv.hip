@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
         const int ch = m0 + 16 * i + 4 * g + v;
         if (ch >= c.M) continue;
         const long o = ((long)n * c.M + ch) * P + pix;
-        c.y[o] = epilogue(c.ep, acc[i][j][v], ch, o, n, pix);
+        c.y[o + n * c.y_nx] = epilogue(c.ep, acc[i][j][v], ch, o, n, pix);
       }
   }
 }

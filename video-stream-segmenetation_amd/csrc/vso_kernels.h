@@ -49,6 +49,10 @@ struct ConvParams {
   int kh, kw, sh, sw, dh, dw, pt, pl;
   Epilogue ep;
   DwPre pre;       // k_conv_dwpw only (x is then the depthwise input)
+  // extra output elements per image: y is a channel range of a wider
+  // [N][ctot][Ho][Wo] tensor (a Concat input written in place), image n's
+  // output at y + n * (M * Ho * Wo + y_nx); 0 = a tensor of its own
+  long y_nx;
 };
 
 // Operand precision of the dense convolutions (vso_conv.hip; vso_options.conv_precision)
@@ -170,6 +174,7 @@ struct ResizeParams {
   int N, C, H, W, Ho, Wo;
   float sy, sx;  // scales (output / input)
   int linear, ctm, nearest;
+  long y_nx;     // as ConvParams::y_nx (C * Ho * Wo + y_nx elements per image)
 };
 
 struct GemmParams {  // y[b][m][n] = alpha * sum_k A[b][m][k] B[b][k][n] + beta * c

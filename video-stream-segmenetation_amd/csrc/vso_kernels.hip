@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvParams p) {
       const int pix = p0 + 16 * j + r;
       if (pix < P) {
         const long o = ((long)n * p.M + ch) * P + pix;
-        p.y[o] = epilogue(p.ep, acc[j][v], ch, o, n, pix);
+        p.y[o + n * p.y_nx] = epilogue(p.ep, acc[j][v], ch, o, n, pix);
       }
     }
   }
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void k_conv_dwpw(ConvParams p) {
     const int ch = m0 + 4 * g + v;
     if (ch >= p.M) continue;
     const long o = ((long)n * p.M + ch) * P + pix;
-    p.y[o] = epilogue(p.ep, acc[v], ch, o, n, pix);
+    p.y[o + n * p.y_nx] = epilogue(p.ep, acc[v], ch, o, n, pix);
   }
 }
 
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void k_conv_small(ConvParams p, int tiles_m, i
     if (gm >= p.Mg) continue;
     const int ch = grp * p.Mg + gm;
     const long o = ((long)n * p.M + ch) * P + pix;
-    p.y[o] = epilogue(p.ep, acc[v], ch, o, n, pix);
+    p.y[o + n * p.y_nx] = epilogue(p.ep, acc[v], ch, o, n, pix);
   }
 }
 
@@ -373,7 +373,8 @@ __device__ __forceinline__ void conv_dw_body(const ConvParams& p, I total) {
         if (ix >= 0 && ix < p.W) acc = __builtin_fmaf(wc[ky * p.kw + kx], xc[(long)iy * p.W + ix], acc);
       }
     }
-    p.y[o] = epilogue(p.ep, acc, ch, (long)o, (int)(nc / (I)p.M), oy * p.Wo + ox);
+    const int n = (int)(nc / (I)p.M);
+    p.y[(long)o + n * p.y_nx] = epilogue(p.ep, acc, ch, (long)o, n, oy * p.Wo + ox);
   }
 }
 
@@ -415,9 +416,10 @@ __device__ __forceinline__ void conv_dw3_quad(const ConvParams& p, int total4) {
         }
     }
     f4 out;
+    const int n = nc / p.M;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) out[j] = epilogue(p.ep, acc[j], ch, (long)o + j, nc / p.M, oy * p.Wo + ox + j);
-    *reinterpret_cast<f4*>(p.y + o) = out;
+    for (int j = 0; j < 4; ++j) out[j] = epilogue(p.ep, acc[j], ch, (long)o + j, n, oy * p.Wo + ox + j);
+    *reinterpret_cast<f4*>(p.y + o + n * p.y_nx) = out;
   }
 }
 
@@ -818,9 +820,9 @@ __global__ __launch_bounds__(256) void k_resize(ResizeParams p) {
       f4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = resize_one(p, xc, oy, ox + e);
-      *reinterpret_cast<f4*>(p.y + o) = v;
+      *reinterpret_cast<f4*>(p.y + o + (nc / p.C) * p.y_nx) = v;
     } else {
-      p.y[o] = resize_one(p, xc, oy, ox);
+      p.y[o + (nc / p.C) * p.y_nx] = resize_one(p, xc, oy, ox);
     }
   }
 }

@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <map>
 #include <set>
 #include <string>
@@ -484,6 +485,14 @@ struct Planner {
   std::map<std::string, ResFuse> res_fuse;
   std::map<std::string, std::pair<const float*, DwPre>> pending_dw;  // dw outputs computed in their 1x1 consumer (input, producer)
   std::map<const void*, float*> dev_consts;
+  // Concat (axis 1) inputs whose producer — a convolution or a Resize — writes
+  // them straight into the concatenation (find_concat_direct): value name ->
+  // patches re-pointing the producing launches' output there, applied when the
+  // Concat is planned (base: the input's first channel of image 0; ctot: the
+  // concatenation's channels), which then copies only the other inputs.
+  // MODNet: 10 of its 13 Concat copies (the k_copy_rows launches).
+  std::set<std::string> cat_direct;
+  std::map<std::string, std::vector<std::function<void(float*, int)>>> cat_patch;
   std::string err;
 
   bool fail(const std::string& m) {
@@ -1023,26 +1032,35 @@ struct Planner {
     }
     ConvTileShape ts{};
     const double macs = (double)p.N * p.M * p.Ho * p.Wo * p.Cg * p.kh * p.kw;
+    const std::string* direct = cat_direct.count(out) ? &out : nullptr;
     if (!p.pre.w && conv_tile_shape(p, s->conv_precision, &ts) &&
         (s->conv_precision != PREC_F32 || macs >= kTileMinMacs)) {
-      if (!plan_conv_tile(p, ts, wf)) return false;
+      if (!plan_conv_tile(p, ts, wf, direct)) return false;
     } else {
-      add(conv_kernel_name(p), [p](hipStream_t st) { launch_conv(p, st, nullptr); });
+      auto pp = std::make_shared<ConvParams>(p);
+      add(conv_kernel_name(p), [pp](hipStream_t st) { launch_conv(*pp, st, nullptr); });
+      if (direct) cat_patch[out].push_back([pp](float* base, int ctot) { retarget(pp.get(), base, ctot); });
     }
     if (ib != ibn.end()) {
       const IbnFuse& f = ib->second;
       const Node& inn = g.nodes[f.inorm];
       return plan_norm(p.y, p.y, p.N, p.M - f.nb, f.nb, p.M, (int64_t)p.Ho * p.Wo, inn, val(inn.in[1]),
-                       val(inn.in[2]), f.relu >= 0 ? ACT_RELU : ACT_NONE);
+                       val(inn.in[2]), f.relu >= 0 ? ACT_RELU : ACT_NONE, direct);
     }
     return true;
+  }
+
+  static void retarget(ConvParams* p, float* base, int ctot) {
+    p->y = base;
+    p->y_nx = (long)(ctot - p->M) * p->Ho * p->Wo;
   }
 
   // A dense convolution on k_conv_tile (vso_conv.hip): weights (BatchNorm
   // folded) packed [tap][Mp][Cp] in the operand type, zero padded; a
   // partial-sum buffer when the channel chunks are split over workgroups.
   static constexpr double kTileMinMacs = 8e6;  // f32: smaller convs keep k_conv_small / k_conv_gemm
-  bool plan_conv_tile(const ConvParams& p, const ConvTileShape& ts, const std::vector<float>& wf) {
+  bool plan_conv_tile(const ConvParams& p, const ConvTileShape& ts, const std::vector<float>& wf,
+                      const std::string* direct) {
     const int taps = p.kh * p.kw;
     const size_t n = (size_t)taps * ts.Mp * ts.Cp;
     ConvTileParams tp{};
@@ -1077,7 +1095,9 @@ struct Planner {
         return false;
       if (hipMemset(tp.counters, 0, blocks * 4) != hipSuccess) return fail("hipMemset failed");
     }
-    add(conv_tile_name(ts), [tp, ts](hipStream_t st) { launch_conv_tile(tp, ts, st); });
+    auto tpp = std::make_shared<ConvTileParams>(tp);
+    add(conv_tile_name(ts), [tpp, ts](hipStream_t st) { launch_conv_tile(*tpp, ts, st); });
+    if (direct) cat_patch[*direct].push_back([tpp](float* base, int ctot) { retarget(&tpp->c, base, ctot); });
     s->tile_convs++;
     return true;
   }
@@ -1401,10 +1421,16 @@ struct Planner {
       for (Value* v : in) os[ax] += v->shape[ax];
       if (!set_runtime(nd.out[0], os)) return false;
       int64_t off = 0;
-      for (Value* v : in) {
+      for (size_t q = 0; q < in.size(); ++q) {
+        Value* v = in[q];
         std::vector<int64_t> doff(rk, 0);
         doff[ax] = off;
         off += v->shape[ax];
+        auto direct = cat_patch.find(nd.in[q]);
+        if (direct != cat_patch.end() && rk == 4 && ax == 1) {  // its producer writes it here
+          for (auto& f : direct->second) f(dptr(vals[nd.out[0]]) + doff[1] * os[2] * os[3], (int)os[1]);
+          continue;
+        }
         if (!plan_copy_into(operand(*v), v->shape, dptr(vals[nd.out[0]]), os, v->shape, doff,
                             std::vector<int64_t>(rk, 0), std::vector<int64_t>(rk, 1), {}, 0.f))
           return false;
@@ -1503,7 +1529,13 @@ struct Planner {
       if (!set_runtime(nd.out[0], {xs[0], xs[1], p.Ho, p.Wo})) return false;
       p.y = dptr(vals[nd.out[0]]);
       if ((long)p.N * p.C * p.Ho * p.Wo >= (1L << 31)) return fail("Resize: output of 2^31 elements or more");
-      add(resize_kernel_name(p), [p](hipStream_t st) { launch_resize(p, st); });
+      auto pp = std::make_shared<ResizeParams>(p);
+      add(resize_kernel_name(p), [pp](hipStream_t st) { launch_resize(*pp, st); });
+      if (cat_direct.count(nd.out[0]))
+        cat_patch[nd.out[0]].push_back([pp](float* base, int ctot) {
+          pp->y = base;
+          pp->y_nx = (long)(ctot - pp->C) * pp->Ho * pp->Wo;
+        });
       return true;
     }
     if (op == "MatMul" || op == "Gemm") {
@@ -1637,7 +1669,7 @@ struct Planner {
   // InstanceNormalization (node `nd`, constant scale / B) of planes c0 .. c0+C-1
   // of an [N][ctot][inner] tensor, as k_norm_stats + k_norm_apply
   bool plan_norm(const float* x, float* y, int N, int C, int c0, int ctot, int64_t inner, const Node& nd, Value* sc,
-                 Value* sh, int act) {
+                 Value* sh, int act, const std::string* direct = nullptr) {
     if (sc->c.numel() != C || sh->c.numel() != C) return fail("InstanceNormalization '" + nd.name + "': scale/B size");
     NormParams p{};
     p.x = x; p.y = y;
@@ -1651,8 +1683,11 @@ struct Planner {
     p.chunks = (int)((inner + kNormChunk - 1) / kNormChunk);
     if (!p.scale || !p.shift || !dalloc(&p.stats, (size_t)N * C * std::max(p.chunks, 1) * 3 * 4)) return false;
     if (inner == 0 || N * C == 0) return true;
-    add("vso::k_norm_stats(vso::NormParams)", [p](hipStream_t st) { launch_norm_stats(p, st); });
-    add("vso::k_norm_apply(vso::NormParams)", [p](hipStream_t st) { launch_norm_apply(p, st); });
+    auto pp = std::make_shared<NormParams>(p);
+    add("vso::k_norm_stats(vso::NormParams)", [pp](hipStream_t st) { launch_norm_stats(*pp, st); });
+    add("vso::k_norm_apply(vso::NormParams)", [pp](hipStream_t st) { launch_norm_apply(*pp, st); });
+    if (direct)  // in place on the conv's output, wherever that now lies
+      cat_patch[*direct].push_back([pp](float* base, int ctot) { pp->x = pp->y = base; pp->ctot = ctot; });
     return true;
   }
 
@@ -1771,6 +1806,23 @@ struct Planner {
     }
   }
 
+  // Inputs of the Concats that may be written in place: used by that Concat
+  // only, once, and neither a graph input / output nor a constant (whether the
+  // producer can, and the Concat is on axis 1 of 4-D tensors, is decided when
+  // they are planned: see cat_patch)
+  void find_concat_direct() {
+    std::set<std::string> fixed;
+    for (const IO& o : g.inputs) fixed.insert(o.name);
+    for (const IO& o : g.outputs) fixed.insert(o.name);
+    for (auto& kv : g.inits) fixed.insert(kv.first);
+    for (size_t k = 0; k < g.nodes.size(); ++k) {
+      const Node& cat = g.nodes[k];
+      if (cat.op != "Concat" || done.count(k)) continue;
+      for (const std::string& i : cat.in)
+        if (!i.empty() && !fixed.count(i) && consumers[i] == 1) cat_direct.insert(i);
+    }
+  }
+
   bool channel_pad_only(const Node& nd) {
     if (nd.as("mode", "constant") != "constant" || nd.in.size() < 2) return false;
     Value* pv = val(nd.in[1]);
@@ -1808,6 +1860,7 @@ struct Planner {
     }
     find_residual_fusions();
     find_ibnorm();
+    find_concat_direct();
     for (size_t k = 0; k < g.nodes.size(); ++k) {
       if (done.count(k)) continue;
       if (!plan_node(k)) return false;

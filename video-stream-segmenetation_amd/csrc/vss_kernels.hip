@@ -508,18 +508,24 @@ struct Staged {
 // A staged copy of NI items of four consecutive float4s (16 channels of one
 // pixel) from NP parts (the hidden-split partial sums) at the same offsets;
 // commit_sum adds the parts in part order.  Two lane mappings:
-//  VSS_STAGE16 = 1: a lane takes whole items — one index computation per 16
+//  WHOLE = true : a lane takes whole items — one index computation per 16
 //    channels, its four loads at immediate offsets (16 B apart) off a 32-bit
 //    offset from each part's wave-uniform base;
-//  VSS_STAGE16 = 0: float4 j of the copy goes to lane j % 256 (a wave's load
+//  WHOLE = false: float4 j of the copy goes to lane j % 256 (a wave's load
 //    instruction reads 1 KiB contiguous), one index computation per float4.
+// Measured (4 batches in flight, A/B on one box): whole items for the
+// inverted-residual input tile (fewer VALU, same time), float4s for the
+// decoder's low-res / skip tiles (d2 7.18 -> 6.51 us, d3 8.83 -> 8.30 us).
 #ifndef VSS_STAGE16
-#define VSS_STAGE16 1
+#define VSS_STAGE16 1      // the inverted-residual blocks' input tile
 #endif
-template <int NI, int NP>
+#ifndef VSS_STAGE16_DEC
+#define VSS_STAGE16_DEC 0  // the decoder's low-res source and skip tiles
+#endif
+template <int NI, int NP, bool WHOLE>
 struct Staged16 {
-  static constexpr int PER = VSS_STAGE16 ? (NI + 255) / 256 : (4 * NI + 255) / 256;
-  static constexpr int V = VSS_STAGE16 ? 4 : 1;
+  static constexpr int PER = WHOLE ? (NI + 255) / 256 : (4 * NI + 255) / 256;
+  static constexpr int V = WHOLE ? 4 : 1;
   f4 v[NP][PER > 0 ? PER : 1][V];
   template <class Off>
   __device__ __forceinline__ void issue(const float* const (&base)[NP], Off off) {
@@ -527,7 +533,7 @@ struct Staged16 {
     for (int u = 0; u < PER; ++u) {
       const int j = (int)threadIdx.x + 256 * u;
       unsigned o;
-      if constexpr (VSS_STAGE16) {
+      if constexpr (WHOLE) {
         o = off(j < NI ? j : NI - 1);  // float offset of the item's first channel
       } else {
         const int jj = j < 4 * NI ? j : 4 * NI - 1;
@@ -545,14 +551,14 @@ struct Staged16 {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int j = (int)threadIdx.x + 256 * u;
-      constexpr int TOT = VSS_STAGE16 ? NI : 4 * NI;  // items, or float4s
+      constexpr int TOT = WHOLE ? NI : 4 * NI;  // items, or float4s
       if (TOT % 256 == 0 || j < TOT) {
 #pragma unroll
         for (int k = 0; k < V; ++k) {
           f4 x = v[0][u][k];
 #pragma unroll
           for (int q = 1; q < NP; ++q) x = x + v[q][u][k];
-          if constexpr (VSS_STAGE16)
+          if constexpr (WHOLE)
             st(j, k, x);
           else
             st(j >> 2, j & 3, x);
@@ -643,8 +649,8 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     if constexpr (NORM_IN) st_slots.issue([&](int i) { return g_slots.ld(4L * i); });
     static_assert(CL % 16 == 0 && CSKIP % 16 == 0, "16-channel staging items");
     constexpr int GL = CL / 16, GS = CSKIP / 16;  // 16-channel items per pixel
-    Staged16<SR * SC * GL, XP> st_lr;
-    Staged16<P_IN_PAD * GS, SP> st_sk;
+    Staged16<SR * SC * GL, XP, VSS_STAGE16_DEC> st_lr;
+    Staged16<P_IN_PAD * GS, SP, VSS_STAGE16_DEC> st_sk;
     Staged<WIMG_F4> st_w;
     {
       const float* xb[XP];
@@ -978,7 +984,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     const float* xn = p.x + (long)n * H * W * CIN;
     static_assert(CIN % 16 == 0, "16-channel staging items");
     constexpr int GI = CIN / 16;  // 16-channel items per pixel
-    Staged16<P_IN_PAD * GI, XP> st_x;
+    Staged16<P_IN_PAD * GI, XP, VSS_STAGE16> st_x;
     Staged<WIMG_F4> st_w;
     {
       const float* xb[XP];
@@ -1253,14 +1259,17 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     if (gg < G) {
       // the lane's terms are integers (rint of v*2^32, v*v*2^24); their f64 sums
       // are exact while no partial sum reaches 2^53.  The q terms are >= 0, so
-      // q < 2^53 at the end means every partial q was exact, and then
-      // sum |s terms| <= sqrt(T * sum v^2 2^64) = sqrt(T q 2^40) < 2^53 for
-      // T = ceil(P_OUT/G) <= 16 — s was exact too.  One f64 -> i64
-      // conversion per sum then replaces one f32 -> i64 sequence per term,
-      // with the same integers; a lane whose q reaches 2^53 (|v| ~ 5.8k) adds
-      // its terms again as int64 (exact up to where the int64 frame totals
-      // overflow), so large pre-norm activations cannot round silently or
-      // make the totals depend on the tiling.
+      // q < 2^51 at the end means every partial q was exact, and then
+      // sum |s terms| <= sqrt(T * sum v^2 2^64) = sqrt(T q 2^40) < 2^48 for
+      // T = ceil(P_OUT/G) <= 16 — s was exact too.  Both sums are then
+      // integers below 2^51 in magnitude, read out as int64 by the 1.5 * 2^52
+      // bias (one f64 add and one 64-bit subtract, instead of an f64 -> i64
+      // conversion sequence), the same integers as summing the terms as int64.
+      // A lane whose q reaches 2^51 (|v| ~ 2.9k) adds its terms again as int64
+      // (exact up to where the int64 frame totals overflow), so large pre-norm
+      // activations cannot round silently or make the totals depend on the
+      // tiling.  The asm statement keeps that rare path a branch: if-converted,
+      // its int64 conversions ran on every lane (~60 VALU per wave).
       double s = 0.0, q = 0.0;
 #pragma unroll
       for (int pix = 0; pix < P_OUT; pix += G) {
@@ -1270,8 +1279,11 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
           q += (double)__builtin_rintf(v * v * 0x1p24f);
         }
       }
-      long long si = (long long)s, qi = (long long)q;
-      if (q >= 0x1p53) {
+      constexpr double kBias = 0x1.8p52;
+      long long si = __double_as_longlong(s + kBias) - __double_as_longlong(kBias);
+      long long qi = __double_as_longlong(q + kBias) - __double_as_longlong(kBias);
+      if (q >= 0x1p51) {
+        asm volatile("" ::: "memory");
         si = 0;
         qi = 0;
         for (int pix = 0; pix < P_OUT; pix += G) {
