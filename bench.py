@@ -395,9 +395,12 @@ def main():
         if world > 1:
             dist.broadcast_object_list(ids, src=0)
             dist.barrier()
-        print(json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local,
-                          "env_world_size": os.environ.get("WORLD_SIZE"), "ids_len": len(ids[0]),
-                          "ids_sha256": hashlib.sha256(ids[0]).hexdigest()}), flush=True)
+        # one write per line: the ranks share the launcher's stdout pipe, and
+        # print()'s separate newline write let two ranks' lines interleave
+        line = json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local,
+                           "env_world_size": os.environ.get("WORLD_SIZE"), "ids_len": len(ids[0]),
+                           "ids_sha256": hashlib.sha256(ids[0]).hexdigest()})
+        os.write(sys.stdout.fileno(), (line + "\n").encode())
         if world > 1:
             dist.destroy_process_group()
         return
