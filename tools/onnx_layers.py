@@ -45,6 +45,7 @@ def run(key, out):
         for _ in range(5 + ITERS):
             s.run_device([t.data_ptr() for t in din], [t.data_ptr() for t in dout], st.cuda_stream)
         st.synchronize()
+        os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
         json.dump({"key": key, "iters": ITERS, "launches": s.launches()}, open(out, "w"))
 
 

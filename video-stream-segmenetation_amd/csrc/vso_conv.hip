@@ -48,6 +48,9 @@ namespace vso {
 
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+// 16 bytes as a clang vector (HIP's uint4 is a struct with a union: arrays of
+// it in registers were not promoted by SROA and went to scratch)
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
 constexpr int CK = 32;  // input channels per staged chunk
 
@@ -57,29 +60,29 @@ template <> struct Elem<PREC_BF16> { using T = __bf16; };
 template <> struct Elem<PREC_F16> { using T = _Float16; };
 
 // 16 bytes of the LDS pixel row: 4 f32 or 8 16-bit channels
-template <int PREC> __device__ __forceinline__ uint4 pack_quad(const float* v);
-template <> __device__ __forceinline__ uint4 pack_quad<PREC_F32>(const float* v) {
-  return uint4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+template <int PREC> __device__ __forceinline__ u4 pack_quad(const float* v);
+template <> __device__ __forceinline__ u4 pack_quad<PREC_F32>(const float* v) {
+  return u4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
 }
-template <> __device__ __forceinline__ uint4 pack_quad<PREC_BF16>(const float* v) {
+template <> __device__ __forceinline__ u4 pack_quad<PREC_BF16>(const float* v) {
   bf8 b;
 #pragma unroll
   for (int e = 0; e < 8; ++e) b[e] = (__bf16)v[e];
-  return __builtin_bit_cast(uint4, b);
+  return __builtin_bit_cast(u4, b);
 }
-template <> __device__ __forceinline__ uint4 pack_quad<PREC_F16>(const float* v) {
+template <> __device__ __forceinline__ u4 pack_quad<PREC_F16>(const float* v) {
   h8 b;
 #pragma unroll
   for (int e = 0; e < 8; ++e) b[e] = (_Float16)v[e];
-  return __builtin_bit_cast(uint4, b);
+  return __builtin_bit_cast(u4, b);
 }
 
 // acc += A (16 out channels x 32 in channels) * B (32 in channels x 16 pixels).
 // a / b: this lane's fragments — 16-bit: one quad (channels 8g .. 8g+7);
 // f32: two quads (channels 4g .. 4g+3 and 16+4g .. 16+4g+3), MFMA s taking
 // element s (the same channel on both sides: the sum over all 32 channels).
-template <int PREC> __device__ __forceinline__ f4 mma32(const uint4* a, const uint4* b, f4 acc);
-template <> __device__ __forceinline__ f4 mma32<PREC_F32>(const uint4* a, const uint4* b, f4 acc) {
+template <int PREC> __device__ __forceinline__ f4 mma32(const u4* a, const u4* b, f4 acc);
+template <> __device__ __forceinline__ f4 mma32<PREC_F32>(const u4* a, const u4* b, f4 acc) {
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[h].x), __uint_as_float(b[h].x), acc, 0, 0, 0);
@@ -89,18 +92,36 @@ template <> __device__ __forceinline__ f4 mma32<PREC_F32>(const uint4* a, const 
   }
   return acc;
 }
-template <> __device__ __forceinline__ f4 mma32<PREC_BF16>(const uint4* a, const uint4* b, f4 acc) {
+template <> __device__ __forceinline__ f4 mma32<PREC_BF16>(const u4* a, const u4* b, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a[0]), __builtin_bit_cast(bf8, b[0]), acc,
                                                   0, 0, 0);
 }
-template <> __device__ __forceinline__ f4 mma32<PREC_F16>(const uint4* a, const uint4* b, f4 acc) {
+template <> __device__ __forceinline__ f4 mma32<PREC_F16>(const u4* a, const u4* b, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a[0]), __builtin_bit_cast(h8, b[0]), acc, 0,
                                                  0, 0);
 }
 
 #ifdef VSO_CONV_PREC
+// Workgroups per CU the kernel's LDS allows (160 KiB per CU), as a register
+// budget (amdgpu_waves_per_eu; one wave per SIMD per workgroup) — an A/B knob,
+// off: held to the LDS occupancy the compiler spills (8x32 tiles, 72-184 B of
+// scratch) and MODNet batch 8 bf16 measured 2.38 ms per run against 2.31
+// without the cap (r04c).
+#ifndef VSO_CONV_WPE
+#define VSO_CONV_WPE 0
+#endif
 template <int PREC, int KS, int S, int TH, int TW, int BM>
-__global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
+constexpr int conv_tile_wpe() {
+  if (!VSO_CONV_WPE) return 1;
+  constexpr int sz = PREC == PREC_F32 ? 4 : 2, NQ = CK * sz / 16, IH = (TH - 1) * S + KS, IW = (TW - 1) * S + KS;
+  constexpr bool WL = PREC != PREC_F32 && (KS <= 3 || BM == 32);
+  constexpr int lds = IH * IW * (NQ + 1) * 16 + (WL ? KS * KS * BM * NQ * 16 : 16);
+  return std::max(1, std::min(4, 163840 / lds));
+}
+
+template <int PREC, int KS, int S, int TH, int TW, int BM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv_tile_wpe<PREC, KS, S, TH, TW, BM>(), 8)))
+void k_conv_tile(ConvTileParams p) {
   using T = typename Elem<PREC>::T;
   constexpr int NQ = CK * (int)sizeof(T) / 16;     // quads of one pixel's chunk: 8 (f32) / 4
   constexpr int QS = NQ + 1;                       // LDS pixel stride in quads (odd)
@@ -119,8 +140,8 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   constexpr int QW = NQ;
   constexpr int WITEMS = KS * KS * BM * NQ;
   constexpr int PERW = WL ? (WITEMS + 255) / 256 : 1;
-  __shared__ uint4 xs[NPIX * QS];
-  __shared__ uint4 wsm[WL ? KS * KS * BM * QW : 1];
+  __shared__ u4 xs[NPIX * QS];
+  __shared__ u4 wsm[WL ? KS * KS * BM * QW : 1];
 
   const ConvParams& c = p.c;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -141,33 +162,57 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   const float* xn = c.x + (long)n * c.C * c.H * c.W;
   const long plane = (long)c.H * c.W;
 
+  // The image as a raw buffer (wave-uniform base, range = its C planes): every
+  // staging load is unconditional, at a 32-bit byte offset, and the hardware's
+  // range check returns 0 for the halo outside the image (its offset is moved
+  // past the range) and for channels past C (their offsets lie past the last
+  // plane).  The per-element conditional loads this replaced compiled to a
+  // branch and an exec-mask swap per element (~5k instructions per chunk).
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(uniform_ptr(xn)), 0, (int)((long)c.C * plane * 4), 0x00020000);
+  const unsigned plane4 = (unsigned)plane * 4u;
+  unsigned soff[PER];  // per item: the byte offset of (channel q * CG, pixel) in the chunk, or out of range
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int idx = tid + 256 * u;
+    const int q = idx / NPIX, pix = idx - q * NPIX;
+    const int iy = pix / IW, ix = pix - iy * IW;
+    const int gy = iy0 + iy, gx = ix0 + ix;
+    const bool in = idx < ITEMS && (unsigned)gy < (unsigned)c.H && (unsigned)gx < (unsigned)c.W;
+    soff[u] = in ? (unsigned)(q * CG) * plane4 + (unsigned)(gy * c.W + gx) * 4u : 0x80000000u;
+  }
   float st[PER][CG];
   auto load = [&](int ch) {
+    const unsigned cofs = (unsigned)(ch * CK) * plane4;  // the chunk's first plane
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      const int idx = tid + 256 * u;
-      const int q = idx / NPIX, pix = idx - q * NPIX;
-      const int iy = pix / IW, ix = pix - (pix / IW) * IW;
-      const int gy = iy0 + iy, gx = ix0 + ix;
-      const bool in = idx < ITEMS && gy >= 0 && gy < c.H && gx >= 0 && gx < c.W;
-      const int cb = ch * CK + q * CG;
-      const float* src = xn + (long)cb * plane + (long)gy * c.W + gx;
+      const unsigned o = soff[u] + cofs;  // out-of-range items stay out of range (no wrap: < 2 GiB added)
 #pragma unroll
-      for (int e = 0; e < CG; ++e) st[u][e] = (in && cb + e < c.C) ? src[e * plane] : 0.f;
+      for (int e = 0; e < CG; ++e)
+        st[u][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(o + e * plane4), 0, 0));
     }
   };
-  const uint4* wq = static_cast<const uint4*>(p.wp);  // [tap][Mp][Cp] in quads of T
+  const u4* wq = static_cast<const u4*>(p.wp);  // [tap][Mp][Cp] in quads of T
   const int cq = p.Cp / CG;                            // quads per weight row
-  uint4 stw[PERW];
-#define VSO_LOAD_W(CH)                                                                   \
-  if (WL) {                                                                              \
-    _Pragma("unroll") for (int u = 0; u < PERW; ++u) {                                   \
-      const int idx = tid + 256 * u;                                                     \
-      const int tap = idx / (BM * NQ), rem = idx - tap * (BM * NQ);                      \
-      const int m = rem / NQ, q = rem - (rem / NQ) * NQ;                                 \
-      stw[u] = idx < WITEMS ? wq[((long)tap * p.Mp + m0 + m) * cq + (CH) * NQ + q] : uint4{0, 0, 0, 0}; \
-    }                                                                                    \
+  // weight staging: item u of a chunk is quad idx of [tap][BM rows][NQ], its
+  // LDS slot; its global quad index at chunk 0 worked out once (the index is
+  // clamped: items past WITEMS load a valid quad and store nothing).  A lambda
+  // with a fully unrolled loop: the macro form left stw[] in scratch.
+  unsigned woff[PERW];
+  u4 stw[PERW];
+#pragma unroll
+  for (int u = 0; u < PERW; ++u) {
+    const int idx = min(tid + 256 * u, WITEMS - 1);
+    const int tap = idx / (BM * NQ), rem = idx - tap * (BM * NQ);
+    const int m = rem / NQ, q = rem - m * NQ;
+    woff[u] = (unsigned)((tap * p.Mp + m0 + m) * cq + q);
   }
+  auto load_w = [&](int chw) {
+    if constexpr (WL) {
+#pragma unroll
+      for (int u = 0; u < PERW; ++u) stw[u] = wq[woff[u] + (unsigned)(chw * NQ)];
+    }
+  };
   f4 acc[MI][PBW];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -184,7 +229,7 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
   }
   if (cbeg < cend) {
     load(cbeg);
-    VSO_LOAD_W(cbeg)
+    load_w(cbeg);
   }
   for (int ch = cbeg; ch < cend; ++ch) {
     __syncthreads();  // the previous chunk's fragment reads are done
@@ -196,19 +241,18 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
         xs[pix * QS + q] = pack_quad<PREC>(st[u]);
       }
     }
-    if (WL) {
+    if constexpr (WL) {
+      static_assert(QW == NQ, "the weight item index is its LDS slot");
 #pragma unroll
       for (int u = 0; u < PERW; ++u) {
         const int idx = tid + 256 * u;
-        const int tap = idx / (BM * NQ), rem = idx - tap * (BM * NQ);
-        const int m = rem / NQ, q = rem - (rem / NQ) * NQ;
-        if (idx < WITEMS) wsm[(tap * BM + m) * QW + q] = stw[u];
+        if (WITEMS % 256 == 0 || idx < WITEMS) wsm[idx] = stw[u];
       }
     }
     __syncthreads();
     if (ch + 1 < cend) {  // in flight during this chunk's MFMAs
       load(ch + 1);
-      VSO_LOAD_W(ch + 1)
+      load_w(ch + 1);
     }
     const int wc = ch * (CK / CG);    // this chunk's first quad in a weight row
 #pragma unroll
@@ -216,21 +260,21 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
 #pragma unroll
       for (int kx = 0; kx < KS; ++kx) {
         const int tap = ky * KS + kx;
-        uint4 a[MI][NF];
+        u4 a[MI][NF];
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           if (WL) {
             a[i][0] = wsm[(tap * BM + 16 * i + r) * QW + g];
           } else {
-            const uint4* row = wq + ((long)tap * p.Mp + m0 + 16 * i + r) * cq + wc;
+            const u4* row = wq + ((long)tap * p.Mp + m0 + 16 * i + r) * cq + wc;
 #pragma unroll
             for (int f = 0; f < NF; ++f) a[i][f] = row[g + 4 * f];
           }
         }
 #pragma unroll
         for (int j = 0; j < PBW; ++j) {
-          uint4 b[NF];
-          const uint4* px = xs + (bpix[j] + ky * IW + kx) * QS;
+          u4 b[NF];
+          const u4* px = xs + (bpix[j] + ky * IW + kx) * QS;
 #pragma unroll
           for (int f = 0; f < NF; ++f) b[f] = px[g + 4 * f];
 #pragma unroll
@@ -305,24 +349,71 @@ __global__ __launch_bounds__(256) void k_conv_tile(ConvTileParams p) {
         acc[i][j] = sum;
       }
   }
+  // epilogue: bias, residual, then the activation over all the lane's outputs
+  // under one uniform switch (act_block), then the stores.  Output k = (i, j,
+  // v): channel m0 + 16 i + 4 g + v, pixel r of block j.
+  const Epilogue& ep = c.ep;
+  constexpr int NO = MI * PBW * 4;
+  float o[NO];
+  auto ch_of = [&](int k) { return m0 + 16 * (k / (PBW * 4)) + 4 * g + (k & 3); };
+  int pixj[PBW];
+  bool okj[PBW];
 #pragma unroll
   for (int j = 0; j < PBW; ++j) {
     const int b = wave * PBW + j;
     const int oy = oy0 + b / (TW / 16), ox = ox0 + (b % (TW / 16)) * 16 + r;
-    if (oy >= c.Ho || ox >= c.Wo) continue;
-    const int pix = oy * c.Wo + ox;
+    okj[j] = oy < c.Ho && ox < c.Wo;
+    pixj[j] = okj[j] ? oy * c.Wo + ox : 0;
+  }
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int ch = m0 + 16 * i + 4 * g + v;
+      const float bv = ep.bias ? ep.bias[min(ch, c.M - 1)] : 0.f;
+#pragma unroll
+      for (int j = 0; j < PBW; ++j) o[(i * PBW + j) * 4 + v] = acc[i][j][v] + bv;
+    }
+  // 32-bit offsets off the image's planes (uniform bases)
+  if (ep.res) {
+    if (ep.res_mode == 0) {
+      const float* rn = ep.res + (long)n * c.M * P;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < PBW; ++j)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int ch = m0 + 16 * i + 4 * g + v;
+            if (okj[j] && ch < c.M) o[(i * PBW + j) * 4 + v] += rn[ch * P + pixj[j]];
+          }
+    } else {  // the fused Pad / MaxPool residuals (face models): rare, one copy of the code
+      each_rare(o, [&](int k, float v) {
+        const int j = (k >> 2) % PBW, ch = ch_of(k);
+        int pj = pixj[0];
+        bool ok = okj[0];
+#pragma unroll
+        for (int t = 1; t < PBW; ++t) {
+          pj = j == t ? pixj[t] : pj;
+          ok = j == t ? okj[t] : ok;
+        }
+        ok = ok && ch < c.M;
+        return ok ? v + residual(ep, ch, ((long)n * c.M + ch) * P + pj, n, pj) : v;
+      });
+    }
+  }
+  act_block(o, ch_of, ep);
+  float* yn = c.y + (long)n * ((long)c.M * P + c.y_nx);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < PBW; ++j)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int ch = m0 + 16 * i + 4 * g + v;
-        if (ch >= c.M) continue;
-        const long o = ((long)n * c.M + ch) * P + pix;
-        c.y[o + n * c.y_nx] = epilogue(c.ep, acc[i][j][v], ch, o, n, pix);
+        if (okj[j] && ch < c.M) yn[ch * P + pixj[j]] = o[(i * PBW + j) * 4 + v];
       }
-  }
 }
-#undef VSO_LOAD_W
 #endif
 
 // ---- instantiations (one precision per compile unit) and dispatch ---------------

@@ -11,6 +11,16 @@ namespace vso {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// The same pointer, provably wave-uniform (in SGPRs) for a buffer descriptor
+// (the caller guarantees it is uniform; hipcc would otherwise waterfall every
+// buffer op whose descriptor it cannot prove uniform).
+__device__ __forceinline__ const void* uniform_ptr(const void* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return reinterpret_cast<const void*>(((unsigned long long)hi << 32) | lo);
+}
+
 __device__ __forceinline__ float act_apply(float v, int act, float a0, float a1, const float* slope, int ch,
                                            int slope_stride) {
   switch (act) {
@@ -22,6 +32,62 @@ __device__ __forceinline__ float act_apply(float v, int act, float a0, float a1,
     case ACT_TANH: return tanhf(v);
     case ACT_F16: return __half2float(__float2half_rn(v));
     default: return v;
+  }
+}
+
+// The fused residual source's value for output (ch, idx) — n / pix: the
+// output's image and pixel (res_mode 1 / 2 are addressed by them).
+__device__ __forceinline__ float residual(const Epilogue& e, int ch, long idx, int n, int pix) {
+  if (e.res_mode == 0) return e.res[idx];
+  if (ch >= e.res_c) return 0.f;
+  const long plane = (long)n * e.res_c + ch;
+  if (e.res_mode == 1) return e.res[plane * e.out_hw + pix];
+  const int y = pix / e.out_w, x = pix - y * e.out_w;
+  const float* b = e.res + (plane * e.res_h + 2 * y) * e.res_w + 2 * x;
+  return fmaxf(fmaxf(b[0], b[1]), fmaxf(b[e.res_w], b[e.res_w + 1]));
+}
+
+// o[k] = f(k, o[k]) for every k, in a loop that is NOT unrolled (one copy of
+// f's code), each element moved in and out of the loop by selects over the
+// array (a dynamic register index would go through scratch): for the rare
+// epilogue forms, whose code inlined per output set whole kernels' register
+// allocation.
+template <int N, class F>
+__device__ __forceinline__ void each_rare(float (&o)[N], F f) {
+#pragma unroll 1
+  for (int k = 0; k < N; ++k) {
+    float v = o[0];
+#pragma unroll
+    for (int t = 1; t < N; ++t) v = k == t ? o[t] : v;
+    v = f(k, v);
+#pragma unroll
+    for (int t = 0; t < N; ++t) o[t] = k == t ? v : o[t];
+  }
+}
+
+// The activation over all N outputs a lane holds (channel ch_of(k) of output
+// k): ONE uniform switch, then a loop per case.  A per-output switch (as in
+// epilogue() below) inlined into each of k_conv_tile's 32 outputs per lane
+// made a 17k-instruction kernel whose tanhf / expf paths set its register
+// allocation (300+ VGPRs: one wave per SIMD).
+template <int N, class ChOf>
+__device__ __forceinline__ void act_block(float (&o)[N], ChOf ch_of, const Epilogue& e) {
+  auto on = [&](int k) { return !(e.act_c_end && ch_of(k) >= e.act_c_end); };
+  switch (e.act) {
+    case ACT_RELU:
+#pragma unroll
+      for (int k = 0; k < N; ++k) o[k] = on(k) ? fmaxf(o[k], 0.f) : o[k];
+      break;
+    case ACT_CLIP:
+#pragma unroll
+      for (int k = 0; k < N; ++k) o[k] = on(k) ? fminf(fmaxf(o[k], e.a0), e.a1) : o[k];
+      break;
+    case ACT_NONE:
+      break;
+    default:
+      each_rare(o, [&](int k, float v) {
+        return on(k) ? act_apply(v, e.act, e.a0, e.a1, e.slope, ch_of(k), e.slope_stride) : v;
+      });
   }
 }
 

@@ -260,13 +260,23 @@ __global__ __launch_bounds__(256) void k_conv_small(ConvParams p, int tiles_m, i
   const float* wrow = p.w + ((long)grp * p.Mg + (m_ok ? m : 0)) * K;
   const int oy = pix / p.Wo, ox = pix - oy * p.Wo;
   const int iy0 = oy * p.sh - p.pt, ix0 = ox * p.sw - p.pl;
+  // Branch-free: every element is loaded from a valid (clamped) address and
+  // selected afterwards — a conditional load compiled to a branch and an exec
+  // swap per element.
+  const int pixc = pix_ok ? pix : 0;
   auto bval = [&](int k) -> float {
-    if (!pix_ok || k >= kend) return 0.f;
-    if (PW) return xg[(long)k * P + pix];
-    const int c = k / khw, rr = k - c * khw;
+    const bool ok = pix_ok && k < kend;
+    const int kc = min(k, K - 1);
+    if (PW) {
+      const float v = xg[(long)kc * P + pixc];
+      return ok ? v : 0.f;
+    }
+    const int c = kc / khw, rr = kc - c * khw;
     const int ky = rr / p.kw, kx = rr - ky * p.kw;
     const int iy = iy0 + ky * p.dh, ix = ix0 + kx * p.dw;
-    return (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? xg[((long)c * p.H + iy) * p.W + ix] : 0.f;
+    const bool in = ok && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+    const float v = xg[((long)c * p.H + min(max(iy, 0), p.H - 1)) * p.W + min(max(ix, 0), p.W - 1)];
+    return in ? v : 0.f;
   };
   // A operands: with K % 4 == 0 and 16-B aligned weights, MFMA 4t + e of a
   // chunk takes k = k0 + 16 t + 4 g + e, so a lane's four A elements of MFMAs
@@ -279,7 +289,8 @@ __global__ __launch_bounds__(256) void k_conv_small(ConvParams p, int tiles_m, i
 #pragma unroll
       for (int t = 0; t < CH / 4; ++t) {
         const int kb = k0 + 16 * t + 4 * g;  // kend % 4 == 0: all four or none
-        const f4 w4 = (m_ok && kb < kend) ? *reinterpret_cast<const f4*>(wrow + kb) : f4{0.f, 0.f, 0.f, 0.f};
+        const f4 w4l = *reinterpret_cast<const f4*>(wrow + min(kb, K - 4));  // clamped, selected (no branch)
+        const f4 w4 = (m_ok && kb < kend) ? w4l : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int e = 0; e < 4; ++e) a[4 * t + e] = w4[e];
       }
@@ -287,7 +298,8 @@ __global__ __launch_bounds__(256) void k_conv_small(ConvParams p, int tiles_m, i
 #pragma unroll
       for (int s = 0; s < CH; ++s) {
         const int k = kof(k0, s);
-        a[s] = (m_ok && k < kend) ? wrow[k] : 0.f;
+        const float wl = wrow[min(k, K - 1)];
+        a[s] = (m_ok && k < kend) ? wl : 0.f;
       }
     }
 #pragma unroll
