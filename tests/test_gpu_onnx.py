@@ -8,6 +8,7 @@ Bar (float32 arithmetic, f32 MFMA accumulation, vs the f64-per-op oracle):
 max |gpu - oracle| <= 1e-4 * max(1, max |oracle|) per output.
 """
 import os
+import re
 
 import numpy as np
 import pytest
@@ -220,22 +221,30 @@ def test_cast_float16_bitwise(ort):
     assert np.array_equal(got, want)
 
 
+def _fused_pair(name):
+    """A depthwise -> 1x1 pair in one launch: k_conv_dwpw, or k_conv_pw with
+    its depthwise stage (DWK 3 / 5) where that pays (pixel-rich layers)."""
+    return "k_conv_dwpw" in name or re.search(r"k_conv_pw<\d, [35]>", name) is not None
+
+
 def test_conv_kernel_choice(ort):
-    """A depthwise conv feeding a 1x1 one runs with it as k_conv_dwpw;
-    k_conv_small takes convolutions with < 1024 64x64 output tiles (every other
-    conv_zoo layer at 64x80, incl. the K > 128 split-K form), k_conv_gemm the
-    large ones (conv_zoo at 512x512: the stem); all forms are checked against
-    the oracle by test_synthetic_models."""
+    """A depthwise conv feeding a 1x1 one runs with it in one launch
+    (k_conv_dwpw, or k_conv_pw's depthwise stage on pixel-rich layers); 1x1
+    convolutions run on k_conv_pw where it has the workgroups (or a shallow K),
+    k_conv_small takes the other convolutions with < 1024 64x64 output tiles
+    (incl. the K > 128 split-K form), k_conv_gemm the large ones (conv_zoo at
+    512x512: the stem); all forms are checked against the oracle by
+    test_synthetic_models."""
     with ort.InferenceSession(M.conv_zoo()) as s:
         small = s.launches()
     with ort.InferenceSession(M.conv_zoo(512, 512)) as s:
         large = s.launches()
     assert not any("k_conv_gemm" in n for n in small), small
     assert any("k_conv_small<false, 16, true>" in n for n in small)  # split-K (K = 288, 360)
-    assert sum("k_conv_dwpw" in n for n in small) == 2               # both depthwise -> 1x1 pairs
+    assert sum(_fused_pair(n) for n in small) == 2, small            # both depthwise -> 1x1 pairs
     assert not any("k_conv_dw(" in n for n in small)
     assert sum("k_conv_gemm" in n for n in large) == 1, large          # the 5x5 stem at 256x256 outputs
-    assert sum("k_conv_dwpw" in n for n in large) == 2 and any("k_conv_small" in n for n in large)
+    assert sum(_fused_pair(n) for n in large) == 2, large
 
 
 def test_residual_source_fusion(ort):
@@ -249,8 +258,8 @@ def test_residual_source_fusion(ort):
             names[key] = s.launches()
     assert sum("k_pool" in n for n in names["mediapipe_face_detector"]) == 0
     assert sum("k_pool" in n for n in names["mediapipe_face_landmarks"]) == 1
-    # and every depthwise conv runs inside its 1x1 consumer (k_conv_dwpw): 32 and 20 launches fewer
+    # and every depthwise conv runs inside its 1x1 consumer (k_conv_dwpw / k_conv_pw): 32 and 20 launches fewer
     for key, dw in (("mediapipe_face_detector", 32), ("mediapipe_face_landmarks", 20)):
-        assert sum("k_conv_dwpw" in n for n in names[key]) == dw
+        assert sum(_fused_pair(n) for n in names[key]) == dw, names[key]
         assert not any("k_conv_dw(" in n for n in names[key])
     assert len(names["mediapipe_face_detector"]) == 45 and len(names["mediapipe_face_landmarks"]) == 28

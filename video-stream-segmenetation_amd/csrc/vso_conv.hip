@@ -114,7 +114,7 @@ template <int PREC, int KS, int S, int TH, int TW, int BM>
 constexpr int conv_tile_wpe() {
   if (!VSO_CONV_WPE) return 1;
   constexpr int sz = PREC == PREC_F32 ? 4 : 2, NQ = CK * sz / 16, IH = (TH - 1) * S + KS, IW = (TW - 1) * S + KS;
-  constexpr bool WL = PREC != PREC_F32 && (KS <= 3 || BM == 32);
+  constexpr bool WL = PREC != PREC_F32 && (KS <= 3 || BM <= 32);
   constexpr int lds = IH * IW * (NQ + 1) * 16 + (WL ? KS * KS * BM * NQ * 16 : 16);
   return std::max(1, std::min(4, 163840 / lds));
 }
@@ -133,10 +133,10 @@ void k_conv_tile(ConvTileParams p) {
   constexpr int NB = TH * TW / 16, PBW = NB / 4;   // 16-pixel blocks per tile / per wave
   constexpr int MI = BM / 16;
   static_assert(NB % 4 == 0 && TW % 16 == 0, "tile: a multiple of 64 pixels, rows of 16");
-  // 16-bit operands, k <= 3 (and 5x5 on 32-channel tiles: 51 KB): the chunk's weights of all taps staged in LDS too
+  // 16-bit operands, k <= 3 (and 5x5 on 16 / 32-channel tiles: <= 51 KB): the chunk's weights of all taps staged in LDS too
   // ([tap][BM rows][NQ quads]), loaded once per workgroup instead of once
   // per wave and tap from L2 (whose latency the per-tap MFMAs cannot cover)
-  constexpr bool WL = PREC != PREC_F32 && (KS <= 3 || BM == 32);
+  constexpr bool WL = PREC != PREC_F32 && (KS <= 3 || BM <= 32);
   constexpr int QW = NQ;
   constexpr int WITEMS = KS * KS * BM * NQ;
   constexpr int PERW = WL ? (WITEMS + 255) / 256 : 1;
@@ -436,7 +436,8 @@ void launch_conv_tile_prec<VSO_CONV_PREC>(const ConvTileParams& p, const ConvTil
   if (t.ks == KSV && t.s == SV && t.th == THV && t.tw == TWV && t.bm == BMV) {                  \
     hipLaunchKernelGGL((k_conv_tile<PR, KSV, SV, THV, TWV, BMV>), grid, dim3(256), 0, s, p);   \
   } else
-  VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 32) VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 64) {
+  VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 16) VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 32)
+  VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 64) {
     std::fprintf(stderr, "vso: no k_conv_tile instance for %s\n", conv_tile_name(t));
   }
 #undef VSO_TILE_CASE
@@ -459,7 +460,9 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   t.s = s;
   // 32-channel tiles for 16-bit 5x5: their 25 taps' weights then fit LDS
   // (k_conv_tile's WL) instead of 25 exposed L2 round trips per chunk
-  t.bm = (c.M <= 32 || (ks == 5 && prec != PREC_F32)) ? 32 : 64;
+  // (16-channel tiles for M <= 16: MODNet's 35 -> 16 fusion layer at 288x512
+  // ran half its MFMAs and weight traffic on padding in a 32-channel tile)
+  t.bm = c.M <= 16 ? 16 : (c.M <= 32 || (ks == 5 && prec != PREC_F32)) ? 32 : 64;
   t.Mp = (c.M + t.bm - 1) / t.bm * t.bm;
   t.Cp = (c.C + CK - 1) / CK * CK;
   // candidate tiles, largest first: the first giving >= kWant workgroups wins,
@@ -471,8 +474,15 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   if (s == 1) { cand = c.Wo >= 32 ? s1w : s1n; nc = c.Wo >= 32 ? 3 : 2; }
   else { cand = c.Wo >= 32 ? s2w : s2n; nc = 1; }
   constexpr long kWant = 1024;  // ~4 workgroups per CU
+  // VSO_CONV_MAX_TH: an A/B knob capping the tile height (8x32 tiles take the
+  // most registers: 300 VGPRs at 64 channels, one workgroup per CU)
+  static const int max_th = [] {
+    const char* e = std::getenv("VSO_CONV_MAX_TH");
+    return e ? std::atoi(e) : 0;
+  }();
   long wgs = 0;
   for (int k = 0; k < nc; ++k) {
+    if (max_th > 0 && cand[k][0] > max_th && k + 1 < nc) continue;
     t.th = cand[k][0];
     t.tw = cand[k][1];
     t.tiles_x = (c.Wo + t.tw - 1) / t.tw;

@@ -84,6 +84,13 @@ __device__ __forceinline__ void act_block(float (&o)[N], ChOf ch_of, const Epilo
       break;
     case ACT_NONE:
       break;
+    case ACT_SIGMOID:
+      if constexpr (N <= 16) {  // (the matte's last 1x1: a whole 288x512 layer of them)
+#pragma unroll
+        for (int k = 0; k < N; ++k) o[k] = on(k) ? 1.f / (1.f + expf(-o[k])) : o[k];
+        break;
+      }
+      [[fallthrough]];
     default:
       each_rare(o, [&](int k, float v) {
         return on(k) ? act_apply(v, e.act, e.a0, e.a1, e.slope, ch_of(k), e.slope_stride) : v;

@@ -191,6 +191,9 @@ struct GemmParams {  // y[b][m][n] = alpha * sum_k A[b][m][k] B[b][k][n] + beta 
 };
 
 const char* conv_kernel_name(const ConvParams& p);
+// a depthwise -> 1x1 pair of N images of P pixels into M channels runs fused
+// on k_conv_pw (vso_kernels.hip: where that measured faster)
+bool pw_fused_pays(int N, long P, int M);
 // false: not a k_conv_tile convolution (grouped, dilated, other kernel sizes)
 bool conv_tile_shape(const ConvParams& p, int prec, ConvTileShape* sh);
 const char* conv_tile_name(const ConvTileShape& t);

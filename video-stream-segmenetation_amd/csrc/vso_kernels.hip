@@ -343,6 +343,221 @@ __global__ __launch_bounds__(256) void k_conv_small(ConvParams p, int tiles_m, i
   }
 }
 
+// 1x1 convolutions (stride 1, unpadded, ungrouped) as one GEMM per image,
+// Y[m][p] = sum_k W[m][k] X[k][p], on NCHW f32 with v_mfma_f32_16x16x4_f32
+// (exact f32 products, like k_conv_small).  DWK = 3 / 5: X is a depthwise
+// DWK x DWK convolution computed on the fly (a fused dw -> 1x1 pair: k_conv_dw's
+// arithmetic, taps in ky, kx order, then its bias / activation — an absent tap
+// adds w * 0, as k_conv_dwpw did).  A workgroup owns PT = 64 WP pixels x
+// BM = 16 WM output channels (WM x WP = 4 waves, WM from the channel count:
+// the 16-channel project layers keep every wave busy on pixels); wave (wm, wp)
+// computes 16 channels x 64 pixels (4 MFMA blocks).  K runs in chunks of 32
+// channels staged through LDS as [k][pixel]: a thread stages one pixel of the
+// tile for 32 / (256 / PT) channels — lanes on consecutive pixels, so every
+// load is coalesced along the row and its pixel / tap geometry is worked out
+// once — and the next chunk's loads are in flight during this chunk's MFMAs.
+// Replaces k_conv_dwpw (16 pixels per workgroup: its 18k workgroups at
+// 144x256 were launch- and latency-bound, 104 us for a 7 us layer), and
+// k_conv_gemm / k_conv_small for the 1x1 convolutions.
+template <int WM, int DWK>
+__global__ __launch_bounds__(256) void k_conv_pw(ConvParams p) {
+  constexpr int WP = 4 / WM, PT = 64 * WP, BM = 16 * WM, KC = 32;
+  constexpr int KPT = 256 / PT;       // channels staged per pass (threads per pixel column)
+  constexpr int NS = KC / KPT;        // staged elements per thread and chunk
+  constexpr int XSTR = PT + 4;        // LDS row stride: rows 4 apart land 16 banks apart
+  constexpr int KT = DWK * DWK;       // depthwise taps (0: none)
+  __shared__ float xs[KC * XSTR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int wm = wave % WM, wp = wave / WM;
+  const int P = p.Ho * p.Wo, K = p.C;
+  const int p0 = blockIdx.x * PT, n = blockIdx.z;
+  const int px = tid % PT, kq = tid / PT;  // this thread's staged pixel and its first channel in a chunk
+  const int pix = p0 + px;
+  const bool pix_ok = pix < P;
+  const int pixc = pix_ok ? pix : P - 1;
+  const int nch = (K + KC - 1) / KC;
+  // the depthwise taps of this pixel: offsets in the input plane, and validity
+  int toff[KT > 0 ? KT : 1];
+  bool tok[KT > 0 ? KT : 1];
+  const DwPre& q = p.pre;
+  if constexpr (KT > 0) {
+    const int oy = pixc / p.Wo, ox = pixc - oy * p.Wo;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const int iy = oy * q.sh - q.pt + (t / DWK) * q.dh, ix = ox * q.sw - q.pl + (t % DWK) * q.dw;
+      tok[t] = pix_ok && iy >= 0 && iy < q.H && ix >= 0 && ix < q.W;
+      toff[t] = min(max(iy, 0), q.H - 1) * q.W + min(max(ix, 0), q.W - 1);
+    }
+  }
+  const int plane_in = KT > 0 ? q.H * q.W : P;
+  const float* xn = p.x + (long)n * K * plane_in;  // image n's input (32-bit offsets below)
+  float st[NS];
+  auto stage = [&](int ch) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int k = ch * KC + kq + KPT * u;  // wave-uniform (PT >= 64)
+      const int kc = min(k, K - 1);
+      if constexpr (KT == 0) {
+        const float v = xn[kc * P + pixc];
+        st[u] = (k < K && pix_ok) ? v : 0.f;
+      } else {
+        const int cu = __builtin_amdgcn_readfirstlane(kc);
+        const float* xc = xn + cu * plane_in;
+        const float* wc = q.w + cu * KT;
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          const float v = xc[toff[t]];
+          acc = __builtin_fmaf(wc[t], tok[t] ? v : 0.f, acc);
+        }
+        st[u] = acc;
+      }
+    }
+  };
+  // the depthwise epilogue (bias, activation) at commit, then zero for k >= K
+  auto commit = [&](int ch) {
+    if constexpr (KT > 0) {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        const int k = min(ch * KC + kq + KPT * u, K - 1);
+        if (q.ep.bias) st[u] += q.ep.bias[__builtin_amdgcn_readfirstlane(k)];
+      }
+      act_block(st, [&](int u) { return ch * KC + kq + KPT * u; }, q.ep);
+    }
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int k = ch * KC + kq + KPT * u;
+      xs[(kq + KPT * u) * XSTR + px] = (k < K && pix_ok) ? st[u] : 0.f;
+    }
+  };
+  // A operands: lane (r, g) of MFMA 4t + e takes W[m][k0 + 16 t + 4 g + e]
+  // (as k_conv_small: four consecutive k per lane and t, one float4 when the
+  // rows are 16-B aligned), B the same k of pixel r of its block
+  const int m = blockIdx.y * BM + wm * 16 + r;
+  const bool m_ok = m < p.M;
+  const float* wrow = p.w + (long)(m_ok ? m : 0) * K;
+  const bool av = (K & 3) == 0 && (reinterpret_cast<uintptr_t>(p.w) & 15) == 0;
+  float a[8];
+  auto load_a = [&](int ch) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int kb = ch * KC + 16 * t + 4 * g;
+      if (av) {
+        const f4 w4 = *reinterpret_cast<const f4*>(wrow + min(kb, K - 4));
+        const bool ok = m_ok && kb < K;  // K % 4 == 0: all four or none
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[4 * t + e] = ok ? w4[e] : 0.f;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float w1 = wrow[min(kb + e, K - 1)];
+          a[4 * t + e] = (m_ok && kb + e < K) ? w1 : 0.f;
+        }
+      }
+    }
+  };
+  f4 acc[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) acc[b] = f4{0.f, 0.f, 0.f, 0.f};
+  stage(0);
+  for (int ch = 0; ch < nch; ++ch) {
+    if (ch > 0) __syncthreads();  // the previous chunk's B reads are done
+    commit(ch);
+    load_a(ch);
+    __syncthreads();
+    if (ch + 1 < nch) stage(ch + 1);  // in flight during this chunk's MFMAs
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float* row = xs + (16 * t + 4 * g + e) * XSTR + wp * 64 + r;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * t + e], row[16 * b], acc[b], 0, 0, 0);
+      }
+  }
+  // acc[b][v] = D[channel m0 + 4 g + v][pixel p0 + wp * 64 + 16 b + r]
+  const Epilogue& ep = p.ep;
+  const int m0 = blockIdx.y * BM + wm * 16;
+  float o[16];
+  auto ch_of = [&](int k) { return m0 + 4 * g + (k & 3); };
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int chn = m0 + 4 * g + v;
+    const float bv = ep.bias ? ep.bias[min(chn, p.M - 1)] : 0.f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) o[4 * b + v] = acc[b][v] + bv;
+  }
+  const int pb0 = p0 + wp * 64 + r;
+  if (ep.res) {
+    if (ep.res_mode == 0) {
+      const float* rn = ep.res + (long)n * p.M * P;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int chn = m0 + 4 * g + v, px2 = pb0 + 16 * b;
+          if (chn < p.M && px2 < P) o[4 * b + v] += rn[chn * P + px2];
+        }
+    } else {
+      each_rare(o, [&](int k, float v) {
+        const int chn = ch_of(k), px2 = pb0 + 16 * (k >> 2);
+        return chn < p.M && px2 < P ? v + residual(ep, chn, ((long)n * p.M + chn) * P + px2, n, px2) : v;
+      });
+    }
+  }
+  act_block(o, ch_of, ep);
+  float* yn = p.y + (long)n * ((long)p.M * P + p.y_nx);
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int chn = m0 + 4 * g + v, px2 = pb0 + 16 * b;
+      if (chn < p.M && px2 < P) yn[chn * P + px2] = o[4 * b + v];
+    }
+}
+
+// k_conv_pw's workgroups for a 1x1 convolution of M channels over N images of
+// P pixels (WM waves along the channels, PT = 64 (4 / WM) pixels per workgroup)
+static long pw_workgroups(int N, long P, int M, int* wm) {
+  *wm = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  const long pt = 64L * (4 / *wm), bm = 16L * *wm;
+  return ((P + pt - 1) / pt) * ((M + bm - 1) / bm) * N;
+}
+
+// Where k_conv_pw pays (MODNet batch 8, per layer against the kernels it
+// replaces, profiles/r04e): a plain 1x1 always when it has >= 256 workgroups
+// or a shallow K (expand layers 16 -> 96 at 144x256 61 -> 44 us, 96 -> 576 at
+// 18x32 28 -> 18 us); a fused depthwise -> 1x1 pair only with >= 512
+// workgroups — a workgroup walks all of K serially with its depthwise
+// recomputed per chunk, which won at 144x256 and 72x128 (104 -> 35, 86 -> 56
+// us) and lost below (a 960-channel pair at 9x16: 72 workgroups, 26 -> 157 us),
+// where k_conv_dwpw's 16-pixel workgroups or k_conv_dw + k_conv_small's
+// split K keep the chip busy.
+bool pw_fused_pays(int N, long P, int M) {
+  int wm;
+  return pw_workgroups(N, P, M, &wm) >= 512;
+}
+
+// k_conv_pw serves this 1x1 convolution (or dw -> 1x1 pair); WM: waves along
+// the output channels (the rest along pixels)
+static bool pw_kernel(const ConvParams& p, int* wm, int* dwk) {
+  const bool one = p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.pt == 0 && p.pl == 0 && p.Ho == p.H &&
+                   p.Wo == p.W && p.G == 1;
+  if (!one) return false;
+  if ((long)p.C * (p.pre.w ? (long)p.pre.H * p.pre.W : (long)p.Ho * p.Wo) >= (1L << 31) ||
+      (long)p.M * p.Ho * p.Wo >= (1L << 31))
+    return false;  // 32-bit offsets within an image
+  const long P = (long)p.Ho * p.Wo, wgs = pw_workgroups(p.N, P, p.M, wm);
+  *dwk = 0;
+  if (p.pre.w) {
+    if (p.pre.kh != p.pre.kw || (p.pre.kh != 3 && p.pre.kh != 5)) return false;
+    *dwk = p.pre.kh;
+    return pw_fused_pays(p.N, P, p.M);
+  }
+  return wgs >= 256 || p.C <= 192;
+}
+
 // Index arithmetic in 32 bits whenever the tensor allows (I = int): a 64-bit
 // division is a ~40-instruction software sequence on CDNA, a 32-bit one a few
 // VALU ops; the elementwise kernels below choose per launch (uniform branch).
@@ -461,6 +676,17 @@ static ConvKind conv_kind(const ConvParams& p) {
 }
 
 const char* conv_kernel_name(const ConvParams& p) {
+  int wm, dwk;
+  if (pw_kernel(p, &wm, &dwk)) {
+    static const char* names[3][3] = {
+        {"void vso::k_conv_pw<1, 0>(vso::ConvParams)", "void vso::k_conv_pw<2, 0>(vso::ConvParams)",
+         "void vso::k_conv_pw<4, 0>(vso::ConvParams)"},
+        {"void vso::k_conv_pw<1, 3>(vso::ConvParams)", "void vso::k_conv_pw<2, 3>(vso::ConvParams)",
+         "void vso::k_conv_pw<4, 3>(vso::ConvParams)"},
+        {"void vso::k_conv_pw<1, 5>(vso::ConvParams)", "void vso::k_conv_pw<2, 5>(vso::ConvParams)",
+         "void vso::k_conv_pw<4, 5>(vso::ConvParams)"}};
+    return names[dwk / 2][wm / 2];
+  }
   if (p.pre.w) return "vso::k_conv_dwpw(vso::ConvParams)";
   switch (conv_kind(p)) {
     case CONV_DW: return "vso::k_conv_dw(vso::ConvParams)";
@@ -484,6 +710,15 @@ const char* conv_kernel_name(const ConvParams& p) {
 
 void launch_conv(const ConvParams& p, hipStream_t s, const char** name) {
   if (name) *name = conv_kernel_name(p);
+  int wm, dwk;
+  if (pw_kernel(p, &wm, &dwk)) {
+    const dim3 grid((unsigned)((p.Ho * p.Wo + 64 * (4 / wm) - 1) / (64 * (4 / wm))),
+                    (unsigned)((p.M + 16 * wm - 1) / (16 * wm)), (unsigned)p.N);
+#define VSO_PW(WMV, DWKV) \
+  if (wm == WMV && dwk == DWKV) { hipLaunchKernelGGL((k_conv_pw<WMV, DWKV>), grid, dim3(256), 0, s, p); return; }
+    VSO_PW(1, 0) VSO_PW(2, 0) VSO_PW(4, 0) VSO_PW(1, 3) VSO_PW(2, 3) VSO_PW(4, 3) VSO_PW(1, 5) VSO_PW(2, 5) VSO_PW(4, 5)
+#undef VSO_PW
+  }
   if (p.pre.w) {
     const dim3 grid((unsigned)((p.Ho * p.Wo + 15) / 16), (unsigned)((p.M + 63) / 64), (unsigned)p.N);
     hipLaunchKernelGGL(k_conv_dwpw, grid, dim3(256), 0, s, p);
@@ -805,36 +1040,69 @@ __device__ __forceinline__ int nearest_idx(float v, int mode, int in) {
   return i < 0 ? 0 : (i > in - 1 ? in - 1 : i);
 }
 
-__device__ __forceinline__ float resize_one(const ResizeParams& p, const float* __restrict__ xc, int oy, int ox) {
-  const float fy = resize_src(oy, p.sy, p.H, p.Ho, p.ctm), fx = resize_src(ox, p.sx, p.W, p.Wo, p.ctm);
-  if (!p.linear) return xc[(long)nearest_idx(fy, p.nearest, p.H) * p.W + nearest_idx(fx, p.nearest, p.W)];
-  const float sy = fminf(fmaxf(fy, 0.f), (float)(p.H - 1)), sx = fminf(fmaxf(fx, 0.f), (float)(p.W - 1));
-  const int y0 = (int)sy, x0 = (int)sx;
-  const int y1 = min(y0 + 1, p.H - 1), x1 = min(x0 + 1, p.W - 1);
-  const float ly = sy - (float)y0, lx = sx - (float)x0;
-  const float v00 = xc[(long)y0 * p.W + x0], v01 = xc[(long)y0 * p.W + x1];
-  const float v10 = xc[(long)y1 * p.W + x0], v11 = xc[(long)y1 * p.W + x1];
+// The source coordinate with the division by the scale as a multiplication
+// when the scale is a power of two (2, 0.5, ...: the reciprocal is exact, so
+// the value is the division's bit for bit); other scales divide.
+__device__ __forceinline__ float resize_src_fast(int o, float scale, float inv, bool pow2, int in, int out, int ctm) {
+  if ((ctm == 0 || (ctm == 1 && out > 1)) && pow2) return ((float)o + 0.5f) * inv - 0.5f;
+  return resize_src(o, scale, in, out, ctm);
+}
+
+// One output row's source rows (linear) or row (nearest), worked out once
+// for all the outputs of a thread (they share oy).
+struct ResizeRow {
+  const float* r0;
+  const float* r1;
+  float ly;
+};
+
+__device__ __forceinline__ ResizeRow resize_row(const ResizeParams& p, const float* __restrict__ xc, int oy, float inv,
+                                                bool pow2) {
+  const float fy = resize_src_fast(oy, p.sy, inv, pow2, p.H, p.Ho, p.ctm);
+  if (!p.linear) {
+    const float* r = xc + nearest_idx(fy, p.nearest, p.H) * p.W;
+    return {r, r, 0.f};
+  }
+  const float sy = fminf(fmaxf(fy, 0.f), (float)(p.H - 1));
+  const int y0 = (int)sy, y1 = min(y0 + 1, p.H - 1);
+  return {xc + y0 * p.W, xc + y1 * p.W, sy - (float)y0};
+}
+
+__device__ __forceinline__ float resize_col(const ResizeParams& p, const ResizeRow& rw, int ox, float inv, bool pow2) {
+  const float fx = resize_src_fast(ox, p.sx, inv, pow2, p.W, p.Wo, p.ctm);
+  if (!p.linear) return rw.r0[nearest_idx(fx, p.nearest, p.W)];
+  const float sx = fminf(fmaxf(fx, 0.f), (float)(p.W - 1));
+  const int x0 = (int)sx, x1 = min(x0 + 1, p.W - 1);
+  const float ly = rw.ly, lx = sx - (float)x0;
+  const float v00 = rw.r0[x0], v01 = rw.r0[x1], v10 = rw.r1[x0], v11 = rw.r1[x1];
   return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
 }
+
+__device__ __forceinline__ bool pow2f(float v) { return v > 0.f && (__float_as_uint(v) & 0x7FFFFFu) == 0; }
 
 // Four consecutive outputs of one row per thread (rows of a multiple of 4:
 // one index split and one source row per 4 outputs, one float4 store; other
 // widths one output per thread), 32-bit index math — the flat 64-bit index's
 // three 64-bit divisions per output were most of the old kernel's
-// instructions.  Same arithmetic per output (resize_one).
+// instructions.  The row's coordinate once per thread; the same arithmetic
+// per output as before (a power-of-two scale's division is its reciprocal's
+// multiplication, exactly).
 template <bool QUAD>
 __global__ __launch_bounds__(256) void k_resize(ResizeParams p) {
   const int total = p.N * p.C * p.Ho * p.Wo, step = QUAD ? 4 : 1;
+  const float iy = 1.f / p.sy, ix = 1.f / p.sx;
+  const bool py = pow2f(p.sy), px = pow2f(p.sx);
   for (long ol = (blockIdx.x * 256L + threadIdx.x) * step; ol < total; ol += gridDim.x * 256L * step) {
     const int o = (int)ol, ox = o % p.Wo, t = o / p.Wo, oy = t % p.Ho, nc = t / p.Ho;
     const float* xc = p.x + (long)nc * p.H * p.W;
+    const ResizeRow rw = resize_row(p, xc, oy, iy, py);
     if constexpr (QUAD) {
       f4 v;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = resize_one(p, xc, oy, ox + e);
+      for (int e = 0; e < 4; ++e) v[e] = resize_col(p, rw, ox + e, ix, px);
       *reinterpret_cast<f4*>(p.y + o + (nc / p.C) * p.y_nx) = v;
     } else {
-      p.y[o + (nc / p.C) * p.y_nx] = resize_one(p, xc, oy, ox);
+      p.y[o + (nc / p.C) * p.y_nx] = resize_col(p, rw, ox, ix, px);
     }
   }
 }

@@ -1019,9 +1019,15 @@ struct Planner {
     p.x = dptr(*x);
     if (!set_runtime(out, oshape)) return false;
     p.y = dptr(vals[out]);
-    if (p.G == p.C && p.G == p.M && !ep.res && ib == ibn.end() && p.C <= kDwPwMaxC && feeds_pointwise(out, last, p.M)) {
+    // (k_conv_pw stages the pair's channels in chunks: any count for a 3x3 / 5x5
+    // depthwise on enough pixels; k_conv_dwpw, the rest, holds all of them in LDS)
+    const int pw_m = consumer_out_channels(out, last);
+    const bool pw_dw = p.kh == p.kw && (p.kh == 3 || p.kh == 5) && pw_m > 0 &&
+                       pw_fused_pays(p.N, (long)p.Ho * p.Wo, pw_m);
+    if (p.G == p.C && p.G == p.M && !ep.res && ib == ibn.end() && (pw_dw || p.C <= kDwPwMaxC) &&
+        feeds_pointwise(out, last, p.M)) {
       pending_dw[out] = {p.x, DwPre{p.w, p.H, p.W, p.kh, p.kw, p.sh, p.sw, p.dh, p.dw, p.pt, p.pl, ep}};
-      return true;  // no launch: its 1x1 consumer computes it (k_conv_dwpw)
+      return true;  // no launch: its 1x1 consumer computes it (k_conv_pw / k_conv_dwpw)
     }
     auto pre = pending_dw.find(nd.in[0]);
     if (pre != pending_dw.end()) {
@@ -1104,6 +1110,14 @@ struct Planner {
 
   // The output of a depthwise conv feeds exactly one Conv, 1x1 / stride 1 /
   // unpadded / ungrouped, on all its channels: the pair runs as k_conv_dwpw.
+  // output channels of the sole Conv consuming `out` (its weights' dims[0]), or 0
+  int consumer_out_channels(const std::string& out, size_t last) {
+    const int c = sole_consumer(out, last);
+    if (c < 0 || g.nodes[c].op != "Conv" || g.nodes[c].in.size() < 2) return 0;
+    Value* w = val(g.nodes[c].in[1]);
+    return (w && w->is_const && !w->c.dims.empty()) ? (int)w->c.dims[0] : 0;
+  }
+
   bool feeds_pointwise(const std::string& out, size_t last, int channels) {
     const int c = sole_consumer(out, last);
     if (c < 0 || g.nodes[c].op != "Conv" || g.nodes[c].in.empty() || g.nodes[c].in[0] != out) return false;
