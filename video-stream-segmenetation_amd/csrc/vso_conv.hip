@@ -473,7 +473,11 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   int nc;
   if (s == 1) { cand = c.Wo >= 32 ? s1w : s1n; nc = c.Wo >= 32 ? 3 : 2; }
   else { cand = c.Wo >= 32 ? s2w : s2n; nc = 1; }
-  constexpr long kWant = 1024;  // ~4 workgroups per CU
+  // ~4 workgroups per CU (VSO_CONV_WANT: an A/B knob)
+  static const long kWant = [] {
+    const char* e = std::getenv("VSO_CONV_WANT");
+    return e ? std::atol(e) : 1024L;
+  }();
   // VSO_CONV_MAX_TH: an A/B knob capping the tile height (8x32 tiles take the
   // most registers: 300 VGPRs at 64 channels, one workgroup per CU)
   static const int max_th = [] {
