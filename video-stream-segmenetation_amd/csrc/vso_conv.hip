@@ -462,7 +462,12 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   // (k_conv_tile's WL) instead of 25 exposed L2 round trips per chunk
   // (16-channel tiles for M <= 16: MODNet's 35 -> 16 fusion layer at 288x512
   // ran half its MFMAs and weight traffic on padding in a 32-channel tile)
-  t.bm = c.M <= 16 ? 16 : (c.M <= 32 || (ks == 5 && prec != PREC_F32)) ? 32 : 64;
+  // (VSO_CONV_BM_MAX=32: an A/B knob — 64-channel tiles take up to 300 VGPRs)
+  static const int bm_max = [] {
+    const char* e = std::getenv("VSO_CONV_BM_MAX");
+    return e ? std::atoi(e) : 64;
+  }();
+  t.bm = c.M <= 16 ? 16 : (c.M <= 32 || bm_max <= 32 || (ks == 5 && prec != PREC_F32)) ? 32 : 64;
   t.Mp = (c.M + t.bm - 1) / t.bm * t.bm;
   t.Cp = (c.C + CK - 1) / CK * CK;
   // candidate tiles, largest first: the first giving >= kWant workgroups wins,
@@ -478,11 +483,15 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
     const char* e = std::getenv("VSO_CONV_WANT");
     return e ? std::atol(e) : 1024L;
   }();
-  // VSO_CONV_MAX_TH: an A/B knob capping the tile height (8x32 tiles take the
-  // most registers: 300 VGPRs at 64 channels, one workgroup per CU)
+  // The tile height is capped at 2 rows (VSO_CONV_MAX_TH; 0 = no cap): the
+  // 8x32 / 4x32 tiles' 180-300 VGPRs leave one or two workgroups per CU, and
+  // the 2x32 tiles measured faster overall despite twice the halo rows —
+  // MODNet batch 8 bf16 2.054-2.057 against 2.070-2.072 ms, two interleaved
+  // rounds (profiles/r04l/); a cap of 4 measured 2.08, 32-channel tiles for the
+  // 64-channel layers (VSO_CONV_BM_MAX=32) 2.10-2.11
   static const int max_th = [] {
     const char* e = std::getenv("VSO_CONV_MAX_TH");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 2;
   }();
   long wgs = 0;
   for (int k = 0; k < nc; ++k) {
