@@ -483,16 +483,19 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
     const char* e = std::getenv("VSO_CONV_WANT");
     return e ? std::atol(e) : 1024L;
   }();
-  // The tile height is capped at 2 rows (VSO_CONV_MAX_TH; 0 = no cap): the
-  // 8x32 / 4x32 tiles' 180-300 VGPRs leave one or two workgroups per CU, and
-  // the 2x32 tiles measured faster overall despite twice the halo rows —
-  // MODNet batch 8 bf16 2.054-2.057 against 2.070-2.072 ms, two interleaved
-  // rounds (profiles/r04l/); a cap of 4 measured 2.08, 32-channel tiles for the
-  // 64-channel layers (VSO_CONV_BM_MAX=32) 2.10-2.11
-  static const int max_th = [] {
+  // With 16-bit operands the tile height is capped at 2 rows
+  // (VSO_CONV_MAX_TH; 0 = no cap): the 8x32 / 4x32 tiles' 180-300 VGPRs leave
+  // one or two workgroups per CU, and the 2x32 tiles measured faster overall
+  // despite twice the halo rows — MODNet batch 8 bf16 2.054-2.057 against
+  // 2.070-2.072 ms, two interleaved rounds (profiles/r04l/); a cap of 4
+  // measured 2.08, 32-channel tiles for the 64-channel layers
+  // (VSO_CONV_BM_MAX=32) 2.10-2.11.  f32 operands keep the uncapped choice
+  // (their 2x32 tiles measured 4.45 against 4.08 ms, profiles/r04m/).
+  static const int max_th_env = [] {
     const char* e = std::getenv("VSO_CONV_MAX_TH");
-    return e ? std::atoi(e) : 2;
+    return e ? std::atoi(e) : -1;
   }();
+  const int max_th = max_th_env >= 0 ? max_th_env : (prec == PREC_F32 ? 0 : 2);
   long wgs = 0;
   for (int k = 0; k < nc; ++k) {
     if (max_th > 0 && cand[k][0] > max_th && k + 1 < nc) continue;
