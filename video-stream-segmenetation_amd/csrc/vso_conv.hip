@@ -119,9 +119,16 @@ constexpr int conv_tile_wpe() {
   return std::max(1, std::min(4, 163840 / lds));
 }
 
-template <int PREC, int KS, int S, int TH, int TW, int BM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv_tile_wpe<PREC, KS, S, TH, TW, BM>(), 8)))
-void k_conv_tile(ConvTileParams p) {
+// UP: the 32-channel chunks in [p.up_c0, p.up_c1) of the input are not read
+// from c.x but computed while staging — the 2x linear upsample (ONNX Resize,
+// half_pixel / pytorch_half_pixel, scale 2) of p.up, k_resize's arithmetic: a
+// Resize whose output only feeds this convolution (directly or through a
+// Concat) runs inside it instead of writing and re-reading a 4x larger
+// tensor.  As in the seam's decoders, the chunk's low-resolution source region
+// (SR x SC pixels) is loaded once (coalesced along its rows) into LDS and the
+// tile's items interpolate from there.
+template <int PREC, int KS, int S, int TH, int TW, int BM, bool UP>
+__device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
   using T = typename Elem<PREC>::T;
   constexpr int NQ = CK * (int)sizeof(T) / 16;     // quads of one pixel's chunk: 8 (f32) / 4
   constexpr int QS = NQ + 1;                       // LDS pixel stride in quads (odd)
@@ -181,8 +188,38 @@ void k_conv_tile(ConvTileParams p) {
     const bool in = idx < ITEMS && (unsigned)gy < (unsigned)c.H && (unsigned)gx < (unsigned)c.W;
     soff[u] = in ? (unsigned)(q * CG) * plane4 + (unsigned)(gy * c.W + gx) * 4u : 0x80000000u;
   }
+  // UP: the chunk's source region [CK][SR][SC] from the low-resolution image
+  // (rows / columns clamped to it; the halo's zeros come from the items'
+  // validity), copied global -> LDS with no register stage (LDS-DMA: the
+  // destination is linear in the region's order) while the previous chunk's
+  // MFMAs run; the barrier that opens the next chunk waits for it
+  constexpr int SR = UP ? IH / 2 + 2 : 1, SC = UP ? IW / 2 + 2 : 1, SRC = SR * SC;
+  constexpr int RITEMS = SRC * CK, PR = UP ? (RITEMS + 255) / 256 : 1;
+  __shared__ float lrs[UP ? PR * 256 : 1];
+  const int up_plane = UP ? p.up_H * p.up_W : 0;
+  const int ry0 = max(0, (iy0 - 1) >> 1), rx0 = max(0, (ix0 - 1) >> 1);  // the region's origin
+  const float* upn = UP ? p.up + (long)n * (p.up_c1 - p.up_c0) * up_plane : xn;
+  // is chunk ch an upsampled one (uniform: the range is whole chunks)
+  auto up_chunk = [&](int ch) { return UP && ch * CK >= p.up_c0 && ch * CK < p.up_c1; };
+  auto load_region = [&](int ch) {
+    const int c0 = ch * CK - p.up_c0;
+    const int wbase = __builtin_amdgcn_readfirstlane((tid >> 6) << 6);
+#pragma unroll
+    for (int u = 0; u < PR; ++u) {
+      const int idx = min(tid + 256 * u, RITEMS - 1);
+      const int cc = idx / SRC, rem = idx - cc * SRC, a = rem / SC, b = rem - a * SC;
+      const int yy = min(ry0 + a, p.up_H - 1), xx = min(rx0 + b, p.up_W - 1);
+      __builtin_amdgcn_global_load_lds(
+          (__attribute__((address_space(1))) void*)(upn + (c0 + cc) * up_plane + yy * p.up_W + xx),
+          (__attribute__((address_space(3))) void*)(lrs + 256 * u + wbase), 4, 0, 0);
+    }
+  };
   float st[PER][CG];
   auto load = [&](int ch) {
+    if (up_chunk(ch)) {
+      load_region(ch);
+      return;
+    }
     const unsigned cofs = (unsigned)(ch * CK) * plane4;  // the chunk's first plane
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -233,12 +270,43 @@ void k_conv_tile(ConvTileParams p) {
   }
   for (int ch = cbeg; ch < cend; ++ch) {
     __syncthreads();  // the previous chunk's fragment reads are done
+    if (up_chunk(ch)) {
+      if constexpr (UP) {
+#pragma unroll 1
+        for (int u = 0; u < PER; ++u) {
+          const int idx = tid + 256 * u;
+          if (idx < ITEMS) {
+            const int q = idx / NPIX, pix = idx - q * NPIX;
+            const int iy = pix / IW, ix = pix - iy * IW;
+            const int gy = iy0 + iy, gx = ix0 + ix;
+            const bool in = (unsigned)gy < (unsigned)c.H && (unsigned)gx < (unsigned)c.W;
+            const float sy = fminf(fmaxf(((float)gy + 0.5f) * 0.5f - 0.5f, 0.f), (float)(p.up_H - 1));
+            const float sx = fminf(fmaxf(((float)gx + 0.5f) * 0.5f - 0.5f, 0.f), (float)(p.up_W - 1));
+            const int y0 = (int)sy, x0 = (int)sx;
+            const float ly = sy - (float)y0, lx = sx - (float)x0;
+            // region pixels (clamped into the region: only out-of-image items, whose value is dropped, clamp)
+            const int a0 = min(max(y0 - ry0, 0), SR - 1), a1 = min(max(min(y0 + 1, p.up_H - 1) - ry0, 0), SR - 1);
+            const int b0 = min(max(x0 - rx0, 0), SC - 1), b1 = min(max(min(x0 + 1, p.up_W - 1) - rx0, 0), SC - 1);
+            const int t00 = a0 * SC + b0, t01 = a0 * SC + b1, t10 = a1 * SC + b0, t11 = a1 * SC + b1;
+            const float* l = lrs + q * CG * SRC;
+            float v[CG];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int idx = tid + 256 * u;
-      if (idx < ITEMS) {
-        const int q = idx / NPIX, pix = idx - q * NPIX;
-        xs[pix * QS + q] = pack_quad<PREC>(st[u]);
+            for (int e = 0; e < CG; ++e)
+              v[e] = in ? (1.f - ly) * ((1.f - lx) * l[e * SRC + t00] + lx * l[e * SRC + t01]) +
+                              ly * ((1.f - lx) * l[e * SRC + t10] + lx * l[e * SRC + t11])
+                        : 0.f;
+            xs[pix * QS + q] = pack_quad<PREC>(v);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int idx = tid + 256 * u;
+        if (idx < ITEMS) {
+          const int q = idx / NPIX, pix = idx - q * NPIX;
+          xs[pix * QS + q] = pack_quad<PREC>(st[u]);
+        }
       }
     }
     if constexpr (WL) {
@@ -414,6 +482,18 @@ void k_conv_tile(ConvTileParams p) {
         if (okj[j] && ch < c.M) yn[ch * P + pixj[j]] = o[(i * PBW + j) * 4 + v];
       }
 }
+
+template <int PREC, int KS, int S, int TH, int TW, int BM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv_tile_wpe<PREC, KS, S, TH, TW, BM>(), 8)))
+void k_conv_tile(ConvTileParams p) {
+  conv_tile_body<PREC, KS, S, TH, TW, BM, false>(p);
+}
+
+template <int PREC, int KS, int S, int TH, int TW, int BM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv_tile_wpe<PREC, KS, S, TH, TW, BM>(), 8)))
+void k_conv_tile_up(ConvTileParams p) {
+  conv_tile_body<PREC, KS, S, TH, TW, BM, true>(p);
+}
 #endif
 
 // ---- instantiations (one precision per compile unit) and dispatch ---------------
@@ -433,14 +513,25 @@ template <>
 void launch_conv_tile_prec<VSO_CONV_PREC>(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s) {
   const dim3 grid((unsigned)((long)t.tiles * (t.Mp / t.bm) * p.c.N * t.ksplit));
 #define VSO_TILE_CASE(PR, KSV, SV, THV, TWV, BMV)                                              \
-  if (t.ks == KSV && t.s == SV && t.th == THV && t.tw == TWV && t.bm == BMV) {                  \
+  if (!t.up && t.ks == KSV && t.s == SV && t.th == THV && t.tw == TWV && t.bm == BMV) {         \
     hipLaunchKernelGGL((k_conv_tile<PR, KSV, SV, THV, TWV, BMV>), grid, dim3(256), 0, s, p);   \
   } else
+#define VSO_TILE_CASE_UP(PR, KSV, SV, THV, TWV, BMV)                                           \
+  if (t.up && t.ks == KSV && t.s == SV && t.th == THV && t.tw == TWV && t.bm == BMV) {          \
+    hipLaunchKernelGGL((k_conv_tile_up<PR, KSV, SV, THV, TWV, BMV>), grid, dim3(256), 0, s, p); \
+  } else
   VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 16) VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 32)
-  VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 64) {
+  VSO_TILE_SHAPES(VSO_TILE_CASE, VSO_CONV_PREC, 64)
+#if VSO_CONV_PREC != 0  // the fused upsample: 16-bit operands, stride 1
+  VSO_TILE_SHAPES_S1(VSO_TILE_CASE_UP, VSO_CONV_PREC, 3, 16) VSO_TILE_SHAPES_S1(VSO_TILE_CASE_UP, VSO_CONV_PREC, 3, 32)
+  VSO_TILE_SHAPES_S1(VSO_TILE_CASE_UP, VSO_CONV_PREC, 3, 64) VSO_TILE_SHAPES_S1(VSO_TILE_CASE_UP, VSO_CONV_PREC, 5, 16)
+  VSO_TILE_SHAPES_S1(VSO_TILE_CASE_UP, VSO_CONV_PREC, 5, 32) VSO_TILE_SHAPES_S1(VSO_TILE_CASE_UP, VSO_CONV_PREC, 5, 64)
+#endif
+  {
     std::fprintf(stderr, "vso: no k_conv_tile instance for %s\n", conv_tile_name(t));
   }
 #undef VSO_TILE_CASE
+#undef VSO_TILE_CASE_UP
 }
 #endif
 
@@ -455,6 +546,7 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   // layers 240 us per frame there, 630 here in f32 and 16-bit alike)
   if (ks == 1) return false;
   ConvTileShape t{};
+  t.up = sh->up;  // (input: the k_conv_tile_up shape is wanted)
   t.prec = prec;
   t.ks = ks;
   t.s = s;
@@ -495,7 +587,10 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
     const char* e = std::getenv("VSO_CONV_MAX_TH");
     return e ? std::atoi(e) : -1;
   }();
-  const int max_th = max_th_env >= 0 ? max_th_env : (prec == PREC_F32 ? 0 : 2);
+  // k_conv_tile_up keeps the uncapped choice: a taller tile interpolates each
+  // staged source region for more pixels (MODNet's 35 -> 16 layer at 288x512:
+  // 146 us at 2 x 32, 113 at 8 x 32; the 64 -> 32 at 144x256: 59.7 -> 49.1)
+  const int max_th = t.up ? 0 : max_th_env >= 0 ? max_th_env : (prec == PREC_F32 ? 0 : 2);
   long wgs = 0;
   for (int k = 0; k < nc; ++k) {
     if (max_th > 0 && cand[k][0] > max_th && k + 1 < nc) continue;
@@ -546,8 +641,8 @@ void launch_conv_tile(const ConvTileParams& p, const ConvTileShape& t, hipStream
 #ifdef VSO_CONV_DISPATCH
 const char* conv_tile_name(const ConvTileShape& t) {
   static thread_local char buf[128];
-  std::snprintf(buf, sizeof buf, "void vso::k_conv_tile<%d, %d, %d, %d, %d, %d>(vso::ConvTileParams)", t.prec, t.ks,
-                t.s, t.th, t.tw, t.bm);
+  std::snprintf(buf, sizeof buf, "void vso::k_conv_tile%s<%d, %d, %d, %d, %d, %d>(vso::ConvTileParams)",
+                t.up ? "_up" : "", t.prec, t.ks, t.s, t.th, t.tw, t.bm);
   return buf;
 }
 #endif

@@ -61,6 +61,7 @@ enum ConvPrec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_F16 = 2 };
 // k_conv_tile's plan: tile shape, padding of the packed weights, K split
 struct ConvTileShape {
   int prec, ks, s, th, tw, bm;
+  int up;              // k_conv_tile_up: channels [up_c0, up_c1) upsampled from ConvTileParams::up
   int tiles_x, tiles;  // pixel tiles per tile row / per image
   int Mp, Cp;          // output channels padded to bm, input channels to 32
   int ksplit, cps;     // workgroups splitting the 32-channel chunks, chunks per split
@@ -72,6 +73,10 @@ struct ConvTileParams {
   int Mp, Cp, tiles_x, tiles, mtiles, ksplit, cps;
   float* part;         // ksplit > 1: partial tiles [output block][ksplit][bm/16][th*tw/64][256 threads] as f4
   int* counters;       // ksplit > 1: arrivals per output block [N][M tiles][tiles], zero between runs
+  // k_conv_tile_up: input channels [up_c0, up_c1) (whole 32-channel chunks)
+  // are the 2x linear (half-pixel) upsample of up ([N][up_c1 - up_c0][up_H][up_W])
+  const float* up;
+  int up_c0, up_c1, up_H, up_W;
 };
 
 constexpr int kDwPwMaxC = 256;  // channels a fused depthwise -> 1x1 pair may have

@@ -492,6 +492,15 @@ struct Planner {
   // concatenation's channels), which then copies only the other inputs.
   // MODNet: 10 of its 13 Concat copies (the k_copy_rows launches).
   std::set<std::string> cat_direct;
+  // 2x linear Resizes computed inside their consumer convolution
+  // (k_conv_tile_up): candidates by graph structure (find_up_fusions); the
+  // planned ones not yet launched, by output name; and per Concat output, its
+  // pending inputs' channel ranges.  A consumer that cannot take one launches
+  // it just before itself (flush_up).
+  std::set<std::string> up_cand;
+  std::map<std::string, std::shared_ptr<ResizeParams>> up_pending;
+  struct UpRange { std::string name; int c0, c1; };
+  std::map<std::string, std::vector<UpRange>> cat_up;
   std::map<std::string, std::vector<std::function<void(float*, int)>>> cat_patch;
   std::string err;
 
@@ -1026,6 +1035,9 @@ struct Planner {
                        pw_fused_pays(p.N, (long)p.Ho * p.Wo, pw_m);
     if (p.G == p.C && p.G == p.M && !ep.res && ib == ibn.end() && (pw_dw || p.C <= kDwPwMaxC) &&
         feeds_pointwise(out, last, p.M)) {
+      flush_up(nd.in[0]);
+      if (cat_up.count(nd.in[0]))
+        for (const UpRange& u : cat_up[nd.in[0]]) flush_up(u.name);
       pending_dw[out] = {p.x, DwPre{p.w, p.H, p.W, p.kh, p.kw, p.sh, p.sw, p.dh, p.dw, p.pt, p.pl, ep}};
       return true;  // no launch: its 1x1 consumer computes it (k_conv_pw / k_conv_dwpw)
     }
@@ -1039,9 +1051,31 @@ struct Planner {
     ConvTileShape ts{};
     const double macs = (double)p.N * p.M * p.Ho * p.Wo * p.Cg * p.kh * p.kw;
     const std::string* direct = cat_direct.count(out) ? &out : nullptr;
-    if (!p.pre.w && conv_tile_shape(p, s->conv_precision, &ts) &&
-        (s->conv_precision != PREC_F32 || macs >= kTileMinMacs)) {
-      if (!plan_conv_tile(p, ts, wf, direct)) return false;
+    const bool tile = !p.pre.w && conv_tile_shape(p, s->conv_precision, &ts) &&
+                      (s->conv_precision != PREC_F32 || macs >= kTileMinMacs);
+    // an upsampled input (or one upsampled Concat input) computed while staging
+    std::vector<UpRange> ups;
+    if (up_pending.count(nd.in[0])) ups.push_back({nd.in[0], 0, p.C});
+    else if (cat_up.count(nd.in[0])) ups = cat_up[nd.in[0]];
+    const ResizeParams* up = nullptr;
+    // (one output-channel tile of at most 32 only: each tile would interpolate
+    // the whole input again, and at 64 output channels the interpolation
+    // measured slower than the Resize's own launch, MODNet 288x512 b8 bf16)
+    if (tile && ups.size() == 1 && ts.s == 1 && (ts.ks == 3 || ts.ks == 5) && ts.ksplit == 1 && ts.Mp == ts.bm &&
+        ts.bm <= 32 &&
+        ts.prec != PREC_F32 && ups[0].c0 % 32 == 0 && ups[0].c1 % 32 == 0 && up_fuse_enabled()) {
+      ConvTileShape tu{};
+      tu.up = 1;
+      if (conv_tile_shape(p, s->conv_precision, &tu) && tu.ksplit == 1) {
+        up = up_pending[ups[0].name].get();
+        ts = tu;
+      }
+    }
+    for (const UpRange& u : ups)
+      if (!up || u.name != ups[0].name) flush_up(u.name);
+    if (tile) {
+      if (!plan_conv_tile(p, ts, wf, direct, up, up ? ups[0].c0 : 0, up ? ups[0].c1 : 0)) return false;
+      if (up) up_pending.erase(ups[0].name);
     } else {
       auto pp = std::make_shared<ConvParams>(p);
       add(conv_kernel_name(p), [pp](hipStream_t st) { launch_conv(*pp, st, nullptr); });
@@ -1066,13 +1100,18 @@ struct Planner {
   // partial-sum buffer when the channel chunks are split over workgroups.
   static constexpr double kTileMinMacs = 8e6;  // f32: smaller convs keep k_conv_small / k_conv_gemm
   bool plan_conv_tile(const ConvParams& p, const ConvTileShape& ts, const std::vector<float>& wf,
-                      const std::string* direct) {
+                      const std::string* direct, const ResizeParams* up = nullptr, int up_c0 = 0, int up_c1 = 0) {
     const int taps = p.kh * p.kw;
     const size_t n = (size_t)taps * ts.Mp * ts.Cp;
     ConvTileParams tp{};
     tp.c = p;
     tp.Mp = ts.Mp; tp.Cp = ts.Cp; tp.tiles_x = ts.tiles_x; tp.ksplit = ts.ksplit; tp.cps = ts.cps;
     tp.tiles = ts.tiles; tp.mtiles = ts.Mp / ts.bm;
+    if (up) {
+      tp.up = up->x;
+      tp.up_H = up->H; tp.up_W = up->W;
+      tp.up_c0 = up_c0; tp.up_c1 = up_c1;
+    }
     auto src = [&](size_t tap, int m, int c) { return wf[((size_t)m * p.C + c) * taps + tap]; };
     void* d = nullptr;
     if (ts.prec == PREC_F32) {
@@ -1243,6 +1282,8 @@ struct Planner {
       in.push_back(v);
       all_const = all_const && v->is_const;
     }
+    if (op != "Conv" && op != "Concat")
+      for (const std::string& n : nd.in) flush_up(n);
     if (op == "Shape" || (all_const && !in.empty() && op != "Conv") || op == "Constant") return fold(nd, in);
     Value* x = in.empty() ? nullptr : in[0];
     const std::vector<int64_t>& xs = x->shape;
@@ -1443,8 +1484,11 @@ struct Planner {
         auto direct = cat_patch.find(nd.in[q]);
         if (direct != cat_patch.end() && rk == 4 && ax == 1) {  // its producer writes it here
           for (auto& f : direct->second) f(dptr(vals[nd.out[0]]) + doff[1] * os[2] * os[3], (int)os[1]);
+          if (up_pending.count(nd.in[q]))
+            cat_up[nd.out[0]].push_back({nd.in[q], (int)doff[1], (int)(doff[1] + v->shape[1])});
           continue;
         }
+        flush_up(nd.in[q]);
         if (!plan_copy_into(operand(*v), v->shape, dptr(vals[nd.out[0]]), os, v->shape, doff,
                             std::vector<int64_t>(rk, 0), std::vector<int64_t>(rk, 1), {}, 0.f))
           return false;
@@ -1544,7 +1588,11 @@ struct Planner {
       p.y = dptr(vals[nd.out[0]]);
       if ((long)p.N * p.C * p.Ho * p.Wo >= (1L << 31)) return fail("Resize: output of 2^31 elements or more");
       auto pp = std::make_shared<ResizeParams>(p);
-      add(resize_kernel_name(p), [pp](hipStream_t st) { launch_resize(*pp, st); });
+      if (up_cand.count(nd.out[0]) && p.linear && (p.ctm == 0 || p.ctm == 1) && p.sy == 2.f && p.sx == 2.f &&
+          p.Ho == 2 * p.H && p.Wo == 2 * p.W && p.C % 32 == 0 && s->conv_precision != PREC_F32)
+        up_pending[nd.out[0]] = pp;  // its consumer convolution computes it (or flush_up launches it)
+      else
+        add(resize_kernel_name(p), [pp](hipStream_t st) { launch_resize(*pp, st); });
       if (cat_direct.count(nd.out[0]))
         cat_patch[nd.out[0]].push_back([pp](float* base, int ctot) {
           pp->y = base;
@@ -1820,6 +1868,45 @@ struct Planner {
     }
   }
 
+  // VSO_UP_FUSE=0 keeps every Resize a launch of its own (A/B)
+  static bool up_fuse_enabled() {
+    static const bool on = [] {
+      const char* e = std::getenv("VSO_UP_FUSE");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+
+  // launch a pending fused Resize (by output name) after all: its consumer
+  // cannot compute it
+  void flush_up(const std::string& name) {
+    auto it = up_pending.find(name);
+    if (it == up_pending.end()) return;
+    auto pp = it->second;
+    add(resize_kernel_name(*pp), [pp](hipStream_t st) { launch_resize(*pp, st); });
+    up_pending.erase(it);
+  }
+
+  // Resizes whose output feeds one convolution's input, directly or as an
+  // input of a Concat (written in place) that feeds one: planned as pending
+  // (the Resize case of plan_node checks the kind: 2x linear half-pixel)
+  void find_up_fusions() {
+    for (size_t k = 0; k < g.nodes.size(); ++k) {
+      const Node& rs = g.nodes[k];
+      if (rs.op != "Resize" || done.count(k)) continue;
+      const std::string& o = rs.out[0];
+      const int c = sole_consumer(o, k);
+      if (c < 0) continue;
+      const Node& cn = g.nodes[c];
+      if (cn.op == "Conv" && cn.in[0] == o) {
+        up_cand.insert(o);
+      } else if (cn.op == "Concat" && cat_direct.count(o) && cn.ai("axis", 0) == 1) {
+        const int cc = sole_consumer(cn.out[0], (size_t)c);
+        if (cc >= 0 && g.nodes[cc].op == "Conv" && g.nodes[cc].in[0] == cn.out[0]) up_cand.insert(o);
+      }
+    }
+  }
+
   // Inputs of the Concats that may be written in place: used by that Concat
   // only, once, and neither a graph input / output nor a constant (whether the
   // producer can, and the Concat is on axis 1 of 4-D tensors, is decided when
@@ -1875,10 +1962,12 @@ struct Planner {
     find_residual_fusions();
     find_ibnorm();
     find_concat_direct();
+    if (s->conv_precision != PREC_F32) find_up_fusions();
     for (size_t k = 0; k < g.nodes.size(); ++k) {
       if (done.count(k)) continue;
       if (!plan_node(k)) return false;
     }
+    if (!up_pending.empty()) return fail("internal: Resize '" + up_pending.begin()->first + "' never launched");
     for (const IO& o : g.outputs) {
       Value* v = val(o.name);
       if (!v) return fail("graph output '" + o.name + "' is never produced");
