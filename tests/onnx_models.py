@@ -387,6 +387,28 @@ def conv_tiles():
                     (s2, [2, 24, 19, 35]), (ks, [2, 48, 9, 16])])
 
 
+def conv_up():
+    """The 2x linear Resize computed inside its consumer convolution
+    (k_conv_tile_up, vso_conv.hip; 16-bit operands): through a Concat with a
+    skip input (half_pixel, 3x3, 24 output channels), straight into a 5x5
+    (pytorch_half_pixel by sizes, 16 output channels), and one it must not
+    take (a 3x3 of 70 output channels: two channel tiles, the Resize keeps its
+    launch).  Odd low-resolution sizes put the edge clamps inside tiles."""
+    b = Builder(9)
+    up = b.op("Resize", ["lo", "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+              coordinate_transformation_mode="half_pixel")                  # [2, 64, 18, 34]
+    cat = b.op("Concat", [up, "skip"], axis=1)                              # [2, 69, 18, 34]
+    a = b.op("Relu", [b.conv(cat, 69, 24, 3)])
+    up2 = b.op("Resize", ["lo2", "", "", b.const(np.array([2, 32, 22, 26], np.int64))], mode="linear",
+               coordinate_transformation_mode="pytorch_half_pixel")
+    c = b.conv(up2, 32, 16, 5)
+    up3 = b.op("Resize", ["lo2", "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+               coordinate_transformation_mode="half_pixel")
+    d = b.conv(up3, 32, 70, 3)
+    return b.model([("lo", [2, 64, 9, 17]), ("skip", [2, 5, 18, 34]), ("lo2", [2, 32, 11, 13])],
+                   [(a, [2, 24, 18, 34]), (c, [2, 16, 22, 26]), (d, [2, 70, 22, 26])])
+
+
 def face_detector_like(S=256, A=896, score_bias=3.0, seed=5):
     """A stand-in with the I/O of the reference's face detector
     (MediaPipeFaceDetector.onnx: image [1,3,S,S] -> box_coords [1,A,16],

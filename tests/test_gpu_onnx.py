@@ -100,6 +100,35 @@ def test_conv_tile_forms(ort, precision):
     _check(got, want, f"conv_tiles {precision}")
 
 
+@pytest.mark.parametrize("precision", ["bf16", "f16"])
+def test_conv_upsample_fusion(ort, precision):
+    """A 2x linear Resize inside its consumer convolution (k_conv_tile_up)
+    against the oracle with the same operand rounding.  The interpolated
+    values are rounded to the operand type in the kernel, the oracle's are
+    its f64 Resize rounded: an operand may land one 16-bit step apart, so the
+    bound is 1e-3 of the output scale (measured 4e-5 bf16, 1.3e-4 f16; a wrong
+    tap or weight is O(1))."""
+    data = M.conv_up()
+    rng = np.random.default_rng(11)
+    feeds = {"lo": rng.standard_normal((2, 64, 9, 17)).astype(np.float32),
+             "skip": rng.standard_normal((2, 5, 18, 34)).astype(np.float32),
+             "lo2": rng.standard_normal((2, 32, 11, 13)).astype(np.float32)}
+    want = R.run(R.load(data), feeds, conv_operands=precision)
+    with ort.InferenceSession(data, precision=precision) as s:
+        got = s.run(feeds)
+        again = s.run(feeds)
+        names = s.launches()
+    print(precision, names)
+    assert sum("k_conv_tile_up<" in n for n in names) == 2, names
+    assert sum("k_resize" in n for n in names) == 1, names  # the 70-channel consumer's
+    for k, w in want.items():
+        err = float(np.abs(got[k] - w).max())
+        scale = max(1.0, float(np.abs(w).max()))
+        print(f"conv_up {precision} {k}: max abs err {err:.3e} (scale {scale:.2f})")
+        assert err <= 1e-3 * scale, (k, err)
+        assert np.array_equal(got[k], again[k])
+
+
 # MODNet's matte (a sigmoid in [0, 1]) with 16-bit convolution operands, on
 # the graph as exported (InstanceNormalization epsilon 1e-5 everywhere; round 3
 # ran the 16-bit cases at 1e-3).  Every InstanceNorm input channel of the

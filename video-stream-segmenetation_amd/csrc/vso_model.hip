@@ -1061,12 +1061,12 @@ struct Planner {
     // (one output-channel tile of at most 32 only: each tile would interpolate
     // the whole input again, and at 64 output channels the interpolation
     // measured slower than the Resize's own launch, MODNet 288x512 b8 bf16)
-    if (tile && ups.size() == 1 && ts.s == 1 && (ts.ks == 3 || ts.ks == 5) && ts.ksplit == 1 && ts.Mp == ts.bm &&
+    if (tile && ups.size() == 1 && ts.s == 1 && (ts.ks == 3 || ts.ks == 5) && ts.Mp == ts.bm &&
         ts.bm <= 32 &&
         ts.prec != PREC_F32 && ups[0].c0 % 32 == 0 && ups[0].c1 % 32 == 0 && up_fuse_enabled()) {
       ConvTileShape tu{};
       tu.up = 1;
-      if (conv_tile_shape(p, s->conv_precision, &tu) && tu.ksplit == 1) {
+      if (conv_tile_shape(p, s->conv_precision, &tu)) {
         up = up_pending[ups[0].name].get();
         ts = tu;
       }
