@@ -172,8 +172,13 @@ def test_modnet_topology_288x512(ort, modnet_cases, q4f16, precision):
     with ort.InferenceSession(data, precision=precision) as s:
         got = s.run({"input": x})
         again = s.run({"input": x})
-        print(label, len(s.launches()), "launches,", s.tile_convs(), "tiled convolutions")
+        names = s.launches()
+        print(label, len(names), "launches,", s.tile_convs(), "tiled convolutions")
         assert s.tile_convs() >= 12  # every 3x3 / 5x5 of >= 8 MMAC (f32), every 3x3 / 5x5 (16-bit)
+        # the matte head (IBNorm -> 1x1 16 -> 1 -> Sigmoid): its InstanceNorm
+        # applied inside k_conv_thin, one k_norm_apply fewer than k_norm_stats
+        assert any("k_conv_thin<1>" in n for n in names), names
+        assert sum("k_norm_apply" in n for n in names) + 1 == sum("k_norm_stats" in n for n in names)
     for k, w in wants["f32"].items():
         err, mean = float(np.abs(got[k] - w).max()), float(np.abs(got[k] - w).mean())
         print(f"{label}: vs the f32 oracle max abs err {err:.3e}, mean {mean:.3e}")

@@ -205,6 +205,17 @@ const char* conv_tile_name(const ConvTileShape& t);
 void launch_conv_tile(const ConvTileParams& p, const ConvTileShape& t, hipStream_t s);
 
 void launch_conv(const ConvParams& p, hipStream_t s, const char** name);
+
+// k_conv_thin: a 1x1 convolution to at most kThinMaxM output channels (a
+// matte / logit head) — a per-pixel dot product over the input channels on
+// the VALU, 4 pixels per thread — optionally normalising input channels
+// [norm.c0, norm.c0 + norm.C) on the way in: an InstanceNorm (+ Relu) whose
+// statistics k_norm_stats computed (NormParams, its apply step not launched:
+// the IBNorm in front of MODNet's matte head)
+constexpr int kThinMaxM = 4;
+bool thin_conv_fits(const ConvParams& p);
+void launch_conv_thin(const ConvParams& p, const NormParams* norm, hipStream_t s);
+const char* conv_thin_name(int M);
 void launch_binary(const BinParams& p, hipStream_t s);
 void launch_unary(const UnaryParams& p, hipStream_t s);
 void launch_copy(const CopyParams& p, hipStream_t s);

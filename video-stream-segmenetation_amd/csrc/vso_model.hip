@@ -498,6 +498,8 @@ struct Planner {
   // pending inputs' channel ranges.  A consumer that cannot take one launches
   // it just before itself (flush_up).
   std::set<std::string> up_cand;
+  // InstanceNorm apply steps left to their consumer (k_conv_thin), by value name
+  std::map<std::string, std::shared_ptr<NormParams>> norm_pending;
   std::map<std::string, std::shared_ptr<ResizeParams>> up_pending;
   struct UpRange { std::string name; int c0, c1; };
   std::map<std::string, std::vector<UpRange>> cat_up;
@@ -1048,6 +1050,22 @@ struct Planner {
       p.x = pre->second.first;
       p.pre = pre->second.second;
     }
+    if (ib == ibn.end() && thin_conv_fits(p) && p.C <= kThinMaxC && thin_enabled()) {
+      // (a matte / logit head: memory bound, on the VALU; its input's
+      // InstanceNorm apply step, when left pending, folded into the loads)
+      std::shared_ptr<NormParams> norm;
+      auto nt = norm_pending.find(nd.in[0]);
+      if (nt != norm_pending.end()) {
+        norm = nt->second;
+        norm_pending.erase(nt);
+      }
+      flush_up(nd.in[0]);
+      auto pp = std::make_shared<ConvParams>(p);
+      add(conv_thin_name(p.M), [pp, norm](hipStream_t st) { launch_conv_thin(*pp, norm.get(), st); });
+      if (cat_direct.count(out)) cat_patch[out].push_back([pp](float* base, int ctot) { retarget(pp.get(), base, ctot); });
+      return true;
+    }
+    flush_norm(nd.in[0]);  // (a pending InstanceNorm apply step: not taken here)
     ConvTileShape ts{};
     const double macs = (double)p.N * p.M * p.Ho * p.Wo * p.Cg * p.kh * p.kw;
     const std::string* direct = cat_direct.count(out) ? &out : nullptr;
@@ -1084,10 +1102,29 @@ struct Planner {
     if (ib != ibn.end()) {
       const IbnFuse& f = ib->second;
       const Node& inn = g.nodes[f.inorm];
+      // a thin 1x1 consumer normalises its input itself: statistics only here
+      const bool defer = !direct && thin_enabled() && feeds_thin(out, last);
       return plan_norm(p.y, p.y, p.N, p.M - f.nb, f.nb, p.M, (int64_t)p.Ho * p.Wo, inn, val(inn.in[1]),
-                       val(inn.in[2]), f.relu >= 0 ? ACT_RELU : ACT_NONE, direct);
+                       val(inn.in[2]), f.relu >= 0 ? ACT_RELU : ACT_NONE, direct, defer ? &out : nullptr);
     }
     return true;
+  }
+
+  // `out`'s sole consumer is a Conv k_conv_thin runs (thin_conv_fits, C <= kThinMaxC)
+  static constexpr int kThinMaxC = 256;
+  bool feeds_thin(const std::string& out, size_t last) {
+    const int c = sole_consumer(out, last);
+    if (c < 0) return false;
+    const Node& cv = g.nodes[c];
+    if (cv.op != "Conv" || cv.in.empty() || cv.in[0] != out || cv.in.size() < 2) return false;
+    Value* w = val(cv.in[1]);
+    if (!w || !w->is_const || w->c.dims.size() != 4) return false;
+    const std::vector<int64_t>& d = w->c.dims;
+    if (d[0] > kThinMaxM || d[1] > kThinMaxC || d[2] != 1 || d[3] != 1 || cv.ai("group", 1) != 1) return false;
+    for (int64_t v : cv.ais("strides")) if (v != 1) return false;
+    for (int64_t v : cv.ais("pads")) if (v != 0) return false;
+    const std::string ap = cv.as("auto_pad", "NOTSET");
+    return ap == "NOTSET" || ap == "VALID";
   }
 
   static void retarget(ConvParams* p, float* base, int ctot) {
@@ -1731,7 +1768,7 @@ struct Planner {
   // InstanceNormalization (node `nd`, constant scale / B) of planes c0 .. c0+C-1
   // of an [N][ctot][inner] tensor, as k_norm_stats + k_norm_apply
   bool plan_norm(const float* x, float* y, int N, int C, int c0, int ctot, int64_t inner, const Node& nd, Value* sc,
-                 Value* sh, int act, const std::string* direct = nullptr) {
+                 Value* sh, int act, const std::string* direct = nullptr, const std::string* defer = nullptr) {
     if (sc->c.numel() != C || sh->c.numel() != C) return fail("InstanceNormalization '" + nd.name + "': scale/B size");
     NormParams p{};
     p.x = x; p.y = y;
@@ -1747,6 +1784,10 @@ struct Planner {
     if (inner == 0 || N * C == 0) return true;
     auto pp = std::make_shared<NormParams>(p);
     add("vso::k_norm_stats(vso::NormParams)", [pp](hipStream_t st) { launch_norm_stats(*pp, st); });
+    if (defer) {  // the apply step runs in the consumer (k_conv_thin) or, failing that, flush_up
+      norm_pending[*defer] = pp;
+      return true;
+    }
     add("vso::k_norm_apply(vso::NormParams)", [pp](hipStream_t st) { launch_norm_apply(*pp, st); });
     if (direct)  // in place on the conv's output, wherever that now lies
       cat_patch[*direct].push_back([pp](float* base, int ctot) { pp->x = pp->y = base; pp->ctot = ctot; });
@@ -1877,9 +1918,26 @@ struct Planner {
     return on;
   }
 
-  // launch a pending fused Resize (by output name) after all: its consumer
-  // cannot compute it
+  // VSO_THIN=0: 1x1 heads of <= kThinMaxM outputs stay on the MFMA kernels (A/B)
+  static bool thin_enabled() {
+    static const bool on = [] {
+      const char* e = std::getenv("VSO_THIN");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+
+  // launch a pending InstanceNorm apply step / fused Resize (by output name)
+  // after all: its consumer cannot take it
+  void flush_norm(const std::string& name) {
+    auto nt = norm_pending.find(name);
+    if (nt == norm_pending.end()) return;
+    auto pp = nt->second;
+    add("vso::k_norm_apply(vso::NormParams)", [pp](hipStream_t st) { launch_norm_apply(*pp, st); });
+    norm_pending.erase(nt);
+  }
   void flush_up(const std::string& name) {
+    flush_norm(name);
     auto it = up_pending.find(name);
     if (it == up_pending.end()) return;
     auto pp = it->second;
@@ -1968,6 +2026,7 @@ struct Planner {
       if (!plan_node(k)) return false;
     }
     if (!up_pending.empty()) return fail("internal: Resize '" + up_pending.begin()->first + "' never launched");
+    if (!norm_pending.empty()) return fail("internal: InstanceNorm of '" + norm_pending.begin()->first + "' never applied");
     for (const IO& o : g.outputs) {
       Value* v = val(o.name);
       if (!v) return fail("graph output '" + o.name + "' is never produced");
