@@ -225,6 +225,11 @@ void launch_pool(const PoolParams& p, hipStream_t s);
 void launch_gap(const RowParams& p, hipStream_t s);
 void launch_norm_stats(const NormParams& p, hipStream_t s);
 void launch_norm_apply(const NormParams& p, hipStream_t s);
+// k_norm_plane: statistics and apply of planes up to kNormPlaneMax elements in one launch
+constexpr long kNormPlaneMax = 36864;
+bool norm_plane_fits(long inner);
+const char* norm_plane_name(long inner);
+void launch_norm_plane(const NormParams& p, hipStream_t s);
 constexpr int kNormChunk = 4096;  // elements per k_norm_stats / k_norm_apply workgroup
 void launch_softmax(const RowParams& p, hipStream_t s);
 void launch_affine(const AffineParams& p, hipStream_t s);

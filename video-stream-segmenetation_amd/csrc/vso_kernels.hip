@@ -920,6 +920,91 @@ __device__ __forceinline__ bool norm_vec(const NormParams& p) {
          (reinterpret_cast<uintptr_t>(p.y) & 15) == 0;
 }
 
+// InstanceNorm of planes of at most 256 x PER elements: one workgroup per
+// plane holds it in registers — statistics and apply in one launch, one read
+// and one write (k_norm_stats + k_norm_apply read it twice, launch twice:
+// ~5 us each at MODNet's /8 and /16 planes, where the launches, not the
+// bytes, set the time).
+template <int NT>
+__device__ __forceinline__ float block_sum_n(float v, float* sh) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) t += sh[w];
+  return t;
+}
+
+template <int PER, int NT>
+__global__ __launch_bounds__(NT) void k_norm_plane(NormParams p) {
+  static_assert(PER % 4 == 0, "float4 pieces");
+  __shared__ float sh[NT / 64];
+  const int row = blockIdx.x, n = row / p.C, c = row - n * p.C;
+  const long off = ((long)n * p.ctot + p.c0 + c) * p.inner;
+  const int cnt = (int)p.inner;
+  const bool vec = norm_vec(p);
+  auto elem = [&](int i) { return vec ? 4 * (int)threadIdx.x + 4 * NT * (i >> 2) + (i & 3) : (int)threadIdx.x + NT * i; };
+  float v[PER];
+  if (vec) {
+#pragma unroll
+    for (int i = 0; i < PER; i += 4) {
+      const int e = elem(i);
+      const f4 t = e < cnt ? *reinterpret_cast<const f4*>(p.x + off + e) : f4{0.f, 0.f, 0.f, 0.f};
+      v[i] = t[0]; v[i + 1] = t[1]; v[i + 2] = t[2]; v[i + 3] = t[3];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = elem(i) < cnt ? p.x[off + elem(i)] : 0.f;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) s += v[i];
+  const float mean = block_sum_n<NT>(s, sh) / (float)cnt;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const float d = v[i] - mean;
+    if (elem(i) < cnt) q += d * d;
+  }
+  q = block_sum_n<NT>(q, sh);
+  const float sc = p.scale[c] / sqrtf(q / (float)cnt + p.eps), sf = p.shift[c];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    v[i] = (v[i] - mean) * sc + sf;
+    if (p.act == ACT_RELU) v[i] = fmaxf(v[i], 0.f);
+  }
+  if (vec) {
+#pragma unroll
+    for (int i = 0; i < PER; i += 4) {
+      const int e = elem(i);
+      if (e < cnt) *reinterpret_cast<f4*>(p.y + off + e) = f4{v[i], v[i + 1], v[i + 2], v[i + 3]};
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (elem(i) < cnt) p.y[off + elem(i)] = v[i];
+  }
+}
+
+bool norm_plane_fits(long inner) { return inner > 0 && inner <= kNormPlaneMax; }
+
+// (256 threads x 16 / 48 elements up to 12288; 1024 x 36 up to 36864:
+// MODNet's 144x256 planes, 128-256 of them, one per CU)
+const char* norm_plane_name(long inner) {
+  return inner <= 4096    ? "void vso::k_norm_plane<16, 256>(vso::NormParams)"
+         : inner <= 12288 ? "void vso::k_norm_plane<48, 256>(vso::NormParams)"
+                          : "void vso::k_norm_plane<36, 1024>(vso::NormParams)";
+}
+
+void launch_norm_plane(const NormParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)(p.N * p.C));
+  if (p.inner <= 4096) hipLaunchKernelGGL((k_norm_plane<16, 256>), grid, dim3(256), 0, s, p);
+  else if (p.inner <= 12288) hipLaunchKernelGGL((k_norm_plane<48, 256>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((k_norm_plane<36, 1024>), grid, dim3(1024), 0, s, p);
+}
+
 // A plane's statistics from k_norm_stats' pieces ((mean, M2, count) each),
 // merged by one wave: every lane folds pieces lane, lane + 64, ... in order,
 // then the lanes' partials combine in a butterfly (Chan et al.'s pairwise

@@ -1783,12 +1783,16 @@ struct Planner {
     if (!p.scale || !p.shift || !dalloc(&p.stats, (size_t)N * C * std::max(p.chunks, 1) * 3 * 4)) return false;
     if (inner == 0 || N * C == 0) return true;
     auto pp = std::make_shared<NormParams>(p);
-    add("vso::k_norm_stats(vso::NormParams)", [pp](hipStream_t st) { launch_norm_stats(*pp, st); });
-    if (defer) {  // the apply step runs in the consumer (k_conv_thin) or, failing that, flush_up
-      norm_pending[*defer] = pp;
-      return true;
+    if (!defer && norm_plane_fits(inner) && norm_plane_enabled()) {
+      add(norm_plane_name(inner), [pp](hipStream_t st) { launch_norm_plane(*pp, st); });
+    } else {
+      add("vso::k_norm_stats(vso::NormParams)", [pp](hipStream_t st) { launch_norm_stats(*pp, st); });
+      if (defer) {  // the apply step runs in the consumer (k_conv_thin) or, failing that, flush_up
+        norm_pending[*defer] = pp;
+        return true;
+      }
+      add("vso::k_norm_apply(vso::NormParams)", [pp](hipStream_t st) { launch_norm_apply(*pp, st); });
     }
-    add("vso::k_norm_apply(vso::NormParams)", [pp](hipStream_t st) { launch_norm_apply(*pp, st); });
     if (direct)  // in place on the conv's output, wherever that now lies
       cat_patch[*direct].push_back([pp](float* base, int ctot) { pp->x = pp->y = base; pp->ctot = ctot; });
     return true;
@@ -1913,6 +1917,15 @@ struct Planner {
   static bool up_fuse_enabled() {
     static const bool on = [] {
       const char* e = std::getenv("VSO_UP_FUSE");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+
+  // VSO_NORM_PLANE=0: small InstanceNorm planes keep the stats + apply pair (A/B)
+  static bool norm_plane_enabled() {
+    static const bool on = [] {
+      const char* e = std::getenv("VSO_NORM_PLANE");
       return !(e && e[0] == '0');
     }();
     return on;
