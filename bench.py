@@ -331,7 +331,11 @@ def sweep(pkg, torch, dev, fh, fw, dtype, inflight, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    # (2000 steps: a ~75 ms window; 200-step windows (~8.5 ms) read 187-191k
+    # against 213-215k on the same box, the pipeline's fill / drain and the
+    # first calls' host costs spread over too few steps — DESIGN.md "Short
+    # windows"; the per-step work is the same)
+    ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=8, help="frames per GPU per step")
     ap.add_argument("--frame", default="480x640")
