@@ -255,6 +255,12 @@ def test_cast_float16_bitwise(ort):
     assert np.array_equal(got, want)
 
 
+def _standalone_dw(name):
+    """A depthwise convolution launched on its own (k_conv_dw or its
+    plane-mapped form k_conv_dw_plane)."""
+    return re.search(r"k_conv_dw(_plane<\d>)?\(", name) is not None
+
+
 def _fused_pair(name):
     """A depthwise -> 1x1 pair in one launch: k_conv_dwpw, or k_conv_pw with
     its depthwise stage (DWK 3 / 5) where that pays (pixel-rich layers)."""
@@ -276,7 +282,7 @@ def test_conv_kernel_choice(ort):
     assert not any("k_conv_gemm" in n for n in small), small
     assert any("k_conv_small<false, 16, true>" in n for n in small)  # split-K (K = 288, 360)
     assert sum(_fused_pair(n) for n in small) == 2, small            # both depthwise -> 1x1 pairs
-    assert not any("k_conv_dw(" in n for n in small)
+    assert not any(_standalone_dw(n) for n in small)
     assert sum("k_conv_gemm" in n for n in large) == 1, large          # the 5x5 stem at 256x256 outputs
     assert sum(_fused_pair(n) for n in large) == 2, large
 
@@ -295,5 +301,5 @@ def test_residual_source_fusion(ort):
     # and every depthwise conv runs inside its 1x1 consumer (k_conv_dwpw / k_conv_pw): 32 and 20 launches fewer
     for key, dw in (("mediapipe_face_detector", 32), ("mediapipe_face_landmarks", 20)):
         assert sum(_fused_pair(n) for n in names[key]) == dw, names[key]
-        assert not any("k_conv_dw(" in n for n in names[key])
+        assert not any(_standalone_dw(n) for n in names[key])
     assert len(names["mediapipe_face_detector"]) == 45 and len(names["mediapipe_face_landmarks"]) == 28

@@ -575,6 +575,15 @@ constexpr long kIdx32 = 1L << 30;  // totals below this index in int (grid-strid
 // rows of a multiple of 4 outputs, a 16-B aligned output, and at least 1024
 // workgroups of quads (4 per CU; MODNet's 648-workgroup layer measured 12.3 us
 // as quads against 10.1 us one output per thread)
+// VSO_DW_PLANE=0: the flat k_conv_dw for every quad-shaped depthwise (A/B)
+static bool dw_plane_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VSO_DW_PLANE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 __host__ __device__ inline bool dw_quad(const ConvParams& p) {
   const long total = (long)p.N * p.M * p.Ho * p.Wo;
   return p.kh == 3 && p.kw == 3 && p.dh == 1 && p.dw == 1 && (p.sw == 1 || p.sw == 2) && (p.Wo & 3) == 0 &&
@@ -650,6 +659,58 @@ __device__ __forceinline__ void conv_dw3_quad(const ConvParams& p, int total4) {
   }
 }
 
+// conv_dw3_quad with one (image, channel) plane per blockIdx.y and a wave
+// per workgroup: the channel, its 9 weights, bias and activation are uniform
+// (scalar loads, a uniform branch) and the only runtime division is by the
+// plane's quads per row — the flat form divides five times per quad and
+// loads the weights per lane.  Same taps, FMA order and epilogue: bit for
+// bit k_conv_dw's values.
+template <int SW>
+__global__ __launch_bounds__(64) void k_conv_dw_plane(ConvParams p) {
+  constexpr int NC = 3 * SW + 3;
+  const int nc = blockIdx.y;
+  const int qrow = p.Wo >> 2;
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  if (q >= qrow * p.Ho) return;
+  const int oy = q / qrow, ox = (q - oy * qrow) * 4;
+  const int n = nc / p.M, ch = nc - n * p.M;
+  const float* xc = p.x + (long)nc * p.H * p.W;
+  const float* wc = p.w + (long)ch * 9;
+  float wv[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wv[k] = wc[k];
+  const int ix0 = ox * SW - p.pl;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = oy * p.sh - p.pt + ky;
+    if (iy < 0 || iy >= p.H) continue;
+    float r[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ix = ix0 + c;
+      r[c] = (ix >= 0 && ix < p.W) ? xc[(long)iy * p.W + ix] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ix0 + j * SW + kx;
+        if (ix >= 0 && ix < p.W) acc[j] = __builtin_fmaf(wv[ky * 3 + kx], r[j * SW + kx], acc[j]);
+      }
+  }
+  const int pix = oy * p.Wo + ox;
+  const long o = (long)nc * p.Ho * p.Wo + pix;
+  f4 out;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) out[j] = epilogue(p.ep, acc[j], ch, o + j, n, pix + j);
+  *reinterpret_cast<f4*>(p.y + o + n * p.y_nx) = out;
+}
+
+__host__ inline bool dw_plane(const ConvParams& p) {
+  return dw_quad(p) && (long)p.N * p.M <= 65535 && dw_plane_enabled();
+}
+
 __global__ __launch_bounds__(256) void k_conv_dw(ConvParams p) {
   const long total = (long)p.N * p.M * p.Ho * p.Wo;
   if (dw_quad(p)) {
@@ -689,7 +750,10 @@ const char* conv_kernel_name(const ConvParams& p) {
   }
   if (p.pre.w) return "vso::k_conv_dwpw(vso::ConvParams)";
   switch (conv_kind(p)) {
-    case CONV_DW: return "vso::k_conv_dw(vso::ConvParams)";
+    case CONV_DW:
+      if (dw_plane(p))
+        return p.sw == 1 ? "void vso::k_conv_dw_plane<1>(vso::ConvParams)" : "void vso::k_conv_dw_plane<2>(vso::ConvParams)";
+      return "vso::k_conv_dw(vso::ConvParams)";
     case CONV_SMALL_PW:
     case CONV_SMALL: {
       static const char* names[2][4] = {
@@ -727,6 +791,12 @@ void launch_conv(const ConvParams& p, hipStream_t s, const char** name) {
   const ConvKind kind = conv_kind(p);
   if (kind == CONV_DW) {
     const long total = (long)p.N * p.M * p.Ho * p.Wo;
+    if (dw_plane(p)) {
+      const dim3 grid((unsigned)(((p.Wo >> 2) * p.Ho + 63) / 64), (unsigned)(p.N * p.M));
+      if (p.sw == 1) hipLaunchKernelGGL(k_conv_dw_plane<1>, grid, dim3(64), 0, s, p);
+      else hipLaunchKernelGGL(k_conv_dw_plane<2>, grid, dim3(64), 0, s, p);
+      return;
+    }
     hipLaunchKernelGGL(k_conv_dw, dim3(grid_for(dw_quad(p) ? total / 4 : total)), dim3(256), 0, s, p);
   } else if (kind == CONV_GEMM) {
     const dim3 grid((p.Ho * p.Wo + BP - 1) / BP, (p.Mg + BM - 1) / BM, p.N * p.G);
