@@ -387,6 +387,25 @@ def conv_tiles():
                     (s2, [2, 24, 19, 35]), (ks, [2, 48, 9, 16])])
 
 
+def norm_planes():
+    """InstanceNormalization on every k_norm_plane form (vso_kernels.hip) and
+    past it: planes of 2590 (scalar loads, 256 threads x 16), 9216 (float4,
+    256 x 48), 36750 (scalar, 1024 x 36) and 40000 elements (the statistics +
+    apply pair), with and without a following Relu (fused)."""
+    b = Builder(13)
+    outs = []
+    for name, shape, relu in (("a", [2, 3, 37, 70], False), ("b", [2, 4, 72, 128], True),
+                              ("c", [1, 2, 150, 245], True), ("d", [1, 2, 200, 200], False)):
+        C = shape[1]
+        y = b.op("InstanceNormalization", [name, b.const(b.rng.random(C).astype(np.float32) + 0.5),
+                                           b.const(b.rng.standard_normal(C).astype(np.float32))], epsilon=1e-5)
+        if relu:
+            y = b.op("Relu", [y])
+        outs.append((y, shape))
+    return b.model([("a", [2, 3, 37, 70]), ("b", [2, 4, 72, 128]), ("c", [1, 2, 150, 245]), ("d", [1, 2, 200, 200])],
+                   outs)
+
+
 def conv_up():
     """The 2x linear Resize computed inside its consumer convolution
     (k_conv_tile_up, vso_conv.hip; 16-bit operands): through a Concat with a

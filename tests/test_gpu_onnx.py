@@ -100,6 +100,23 @@ def test_conv_tile_forms(ort, precision):
     _check(got, want, f"conv_tiles {precision}")
 
 
+def test_norm_planes(ort):
+    """k_norm_plane's three forms and the two-launch path beyond it against the
+    oracle (f32: 1e-4 of the output scale)."""
+    data = M.norm_planes()
+    rng = np.random.default_rng(17)
+    feeds = {k: (rng.standard_normal(s) * 3 + 1).astype(np.float32)
+             for k, s in (("a", (2, 3, 37, 70)), ("b", (2, 4, 72, 128)), ("c", (1, 2, 150, 245)), ("d", (1, 2, 200, 200)))}
+    want = R.run(R.load(data), feeds)
+    with ort.InferenceSession(data) as s:
+        got = s.run(feeds)
+        names = s.launches()
+    print(names)
+    assert sum("k_norm_plane<" in n for n in names) == 3, names
+    assert sum("k_norm_stats" in n for n in names) == 1, names
+    _check(got, want, "norm_planes")
+
+
 @pytest.mark.parametrize("precision", ["bf16", "f16"])
 def test_conv_upsample_fusion(ort, precision):
     """A 2x linear Resize inside its consumer convolution (k_conv_tile_up)
