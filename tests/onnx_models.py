@@ -406,6 +406,18 @@ def norm_planes():
                    outs)
 
 
+def conv_thin():
+    """1x1 heads of <= 4 outputs on k_conv_thin (vso_kernels.h): 3 outputs
+    with a Sigmoid on a 37x70 plane (scalar pixel path), 4 outputs with a
+    fused residual Add on 36x64 (float4 path), 2 outputs plain."""
+    b = Builder(15)
+    h1 = b.op("Sigmoid", [b.conv("x", 24, 3, 1)])
+    h2 = b.op("Add", [b.conv("x2", 16, 4, 1), "r"])
+    h3 = b.conv("x2", 16, 2, 1)
+    return b.model([("x", [2, 24, 37, 70]), ("x2", [2, 16, 36, 64]), ("r", [2, 4, 36, 64])],
+                   [(h1, [2, 3, 37, 70]), (h2, [2, 4, 36, 64]), (h3, [2, 2, 36, 64])])
+
+
 def conv_up():
     """The 2x linear Resize computed inside its consumer convolution
     (k_conv_tile_up, vso_conv.hip; 16-bit operands): through a Concat with a

@@ -100,6 +100,24 @@ def test_conv_tile_forms(ort, precision):
     _check(got, want, f"conv_tiles {precision}")
 
 
+def test_conv_thin(ort):
+    """k_conv_thin's instances (2 / 3 / 4 outputs), scalar and float4 pixel
+    paths, Sigmoid and residual epilogues, against the oracle (f32: 1e-4)."""
+    data = M.conv_thin()
+    rng = np.random.default_rng(19)
+    feeds = {"x": rng.standard_normal((2, 24, 37, 70)).astype(np.float32),
+             "x2": rng.standard_normal((2, 16, 36, 64)).astype(np.float32),
+             "r": rng.standard_normal((2, 4, 36, 64)).astype(np.float32)}
+    want = R.run(R.load(data), feeds)
+    with ort.InferenceSession(data) as s:
+        got = s.run(feeds)
+        names = s.launches()
+    print(names)
+    assert sorted(n.split("(")[0] for n in names) == ["void vso::k_conv_thin<2>", "void vso::k_conv_thin<3>",
+                                                     "void vso::k_conv_thin<4>"], names
+    _check(got, want, "conv_thin")
+
+
 def test_norm_planes(ort):
     """k_norm_plane's three forms and the two-launch path beyond it against the
     oracle (f32: 1e-4 of the output scale)."""
