@@ -253,7 +253,8 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
  * GPU is prepared: device calls (vss_segment_device, _gather_device) run
  * there; a multi-GPU handle's peers run host batches, whose per-GPU shard
  * shapes build their graphs on first use.  A slot keeps graphs for at most 16
- * shapes (the oldest shape's are dropped), and up to 4 executables per shape,
+ * shapes (past that, the graphs of the shape least recently prepared or run
+ * are dropped), and up to 4 executables per shape,
  * each bound to one (frames, masks) buffer pair. */
 int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels, size_t row_stride,
                        size_t frame_stride);

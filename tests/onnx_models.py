@@ -440,6 +440,20 @@ def conv_up():
                    [(a, [2, 24, 18, 34]), (c, [2, 16, 22, 26]), (d, [2, 70, 22, 26])])
 
 
+def conv_up_thin():
+    """A pending 2x Resize through an in-place Concat into a thin 1x1 head
+    (<= 4 outputs, k_conv_thin: computes no upsample itself), so the planner
+    must launch the Resize in front of it (the thin path flushed
+    only its direct input, and the plan failed with 'Resize ... never
+    launched').  32-channel upsampled range, a 3-output Sigmoid head."""
+    b = Builder(10)
+    up = b.op("Resize", ["lo", "", b.const(np.array([1, 1, 2, 2], np.float32))], mode="linear",
+              coordinate_transformation_mode="half_pixel")                  # [2, 32, 18, 34]
+    cat = b.op("Concat", [up, "skip"], axis=1)                              # [2, 48, 18, 34]
+    h = b.op("Sigmoid", [b.conv(cat, 48, 3, 1)])
+    return b.model([("lo", [2, 32, 9, 17]), ("skip", [2, 16, 18, 34])], [(h, [2, 3, 18, 34])])
+
+
 def face_detector_like(S=256, A=896, score_bias=3.0, seed=5):
     """A stand-in with the I/O of the reference's face detector
     (MediaPipeFaceDetector.onnx: image [1,3,S,S] -> box_coords [1,A,16],

@@ -164,6 +164,27 @@ def test_conv_upsample_fusion(ort, precision):
         assert np.array_equal(got[k], again[k])
 
 
+@pytest.mark.parametrize("precision", ["bf16", "f16", "f32"])
+def test_conv_up_into_thin_head(ort, precision):
+    """Resize -> Concat -> 1x1 head of 3 outputs: the thin head launches the
+    pending Resize in front of itself, and matches the oracle with
+    the same operand rounding at the conv_up bound."""
+    data = M.conv_up_thin()
+    rng = np.random.default_rng(12)
+    feeds = {"lo": rng.standard_normal((2, 32, 9, 17)).astype(np.float32),
+             "skip": rng.standard_normal((2, 16, 18, 34)).astype(np.float32)}
+    want = R.run(R.load(data), feeds, conv_operands=None if precision == "f32" else precision)
+    with ort.InferenceSession(data, precision=precision) as s:
+        got = s.run(feeds)
+        names = s.launches()
+    assert sum("k_resize" in n for n in names) == 1, names
+    assert sum("k_conv_thin" in n for n in names) == 1, names
+    for k, w in want.items():
+        err = float(np.abs(got[k] - w).max())
+        print(f"conv_up_thin {precision} {k}: max abs err {err:.3e}")
+        assert err <= 1e-3, (k, err)
+
+
 # MODNet's matte (a sigmoid in [0, 1]) with 16-bit convolution operands, on
 # the graph as exported (InstanceNormalization epsilon 1e-5 everywhere; round 3
 # ran the 16-bit cases at 1e-3).  Every InstanceNorm input channel of the

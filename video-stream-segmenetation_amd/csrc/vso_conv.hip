@@ -545,6 +545,11 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   // wave tiles in f32 than here in any precision (measured: MODNet's 1x1
   // layers 240 us per frame there, 630 here in f32 and 16-bit alike)
   if (ks == 1) return false;
+  // k_conv_tile stages through a buffer descriptor (num_records = C*H*W*4
+  // bytes, 32-bit offsets, out-of-range marker 0x80000000) and its epilogue
+  // offsets are int: an image of 2 GiB or more keeps the 64-bit kernels
+  // (k_conv_gemm / k_conv_small), as pw_kernel and thin_conv_fits do
+  if ((long)c.C * c.H * c.W * 4 >= (1L << 31) || (long)c.M * c.Ho * c.Wo >= (1L << 31)) return false;
   ConvTileShape t{};
   t.up = sh->up;  // (input: the k_conv_tile_up shape is wanted)
   t.prec = prec;

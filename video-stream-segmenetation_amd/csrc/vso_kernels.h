@@ -199,6 +199,11 @@ const char* conv_kernel_name(const ConvParams& p);
 // a depthwise -> 1x1 pair of N images of P pixels into M channels runs fused
 // on k_conv_pw (vso_kernels.hip: where that measured faster)
 bool pw_fused_pays(int N, long P, int M);
+// the same decision with pw_kernel's 32-bit offset limits: a C-channel depthwise
+// over pre_hw input pixels per image into P output pixels, then 1x1 to M
+// channels — what the planner must ask before deferring a depthwise whose
+// channels exceed k_conv_dwpw's LDS tile (kDwPwMaxC)
+bool pw_pair_fits(int N, long C, long pre_hw, long P, int M);
 // false: not a k_conv_tile convolution (grouped, dilated, other kernel sizes)
 bool conv_tile_shape(const ConvParams& p, int prec, ConvTileShape* sh);
 const char* conv_tile_name(const ConvTileShape& t);

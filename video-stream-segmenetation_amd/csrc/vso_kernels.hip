@@ -539,22 +539,26 @@ bool pw_fused_pays(int N, long P, int M) {
   return pw_workgroups(N, P, M, &wm) >= 512;
 }
 
+bool pw_pair_fits(int N, long C, long pre_hw, long P, int M) {
+  if (C * pre_hw >= (1L << 31) || (long)M * P >= (1L << 31)) return false;  // pw_kernel's limits
+  return pw_fused_pays(N, P, M);
+}
+
 // k_conv_pw serves this 1x1 convolution (or dw -> 1x1 pair); WM: waves along
 // the output channels (the rest along pixels)
 static bool pw_kernel(const ConvParams& p, int* wm, int* dwk) {
   const bool one = p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.pt == 0 && p.pl == 0 && p.Ho == p.H &&
                    p.Wo == p.W && p.G == 1;
   if (!one) return false;
-  if ((long)p.C * (p.pre.w ? (long)p.pre.H * p.pre.W : (long)p.Ho * p.Wo) >= (1L << 31) ||
-      (long)p.M * p.Ho * p.Wo >= (1L << 31))
-    return false;  // 32-bit offsets within an image
-  const long P = (long)p.Ho * p.Wo, wgs = pw_workgroups(p.N, P, p.M, wm);
+  const long P = (long)p.Ho * p.Wo;
   *dwk = 0;
   if (p.pre.w) {
     if (p.pre.kh != p.pre.kw || (p.pre.kh != 3 && p.pre.kh != 5)) return false;
     *dwk = p.pre.kh;
-    return pw_fused_pays(p.N, P, p.M);
+    return pw_pair_fits(p.N, p.C, (long)p.pre.H * p.pre.W, P, p.M);
   }
+  if ((long)p.C * P >= (1L << 31) || (long)p.M * P >= (1L << 31)) return false;  // 32-bit offsets within an image
+  const long wgs = pw_workgroups(p.N, P, p.M, wm);
   return wgs >= 256 || p.C <= 192;
 }
 

@@ -1033,13 +1033,13 @@ struct Planner {
     // (k_conv_pw stages the pair's channels in chunks: any count for a 3x3 / 5x5
     // depthwise on enough pixels; k_conv_dwpw, the rest, holds all of them in LDS)
     const int pw_m = consumer_out_channels(out, last);
+    // (pw_pair_fits: pw_kernel's own test, its 32-bit offset limits included —
+    // a pair it declined would fall to k_conv_dwpw, whose LDS holds kDwPwMaxC)
     const bool pw_dw = p.kh == p.kw && (p.kh == 3 || p.kh == 5) && pw_m > 0 &&
-                       pw_fused_pays(p.N, (long)p.Ho * p.Wo, pw_m);
+                       pw_pair_fits(p.N, p.C, (long)p.H * p.W, (long)p.Ho * p.Wo, pw_m);
     if (p.G == p.C && p.G == p.M && !ep.res && ib == ibn.end() && (pw_dw || p.C <= kDwPwMaxC) &&
         feeds_pointwise(out, last, p.M)) {
-      flush_up(nd.in[0]);
-      if (cat_up.count(nd.in[0]))
-        for (const UpRange& u : cat_up[nd.in[0]]) flush_up(u.name);
+      flush_input(nd.in[0]);
       pending_dw[out] = {p.x, DwPre{p.w, p.H, p.W, p.kh, p.kw, p.sh, p.sw, p.dh, p.dw, p.pt, p.pl, ep}};
       return true;  // no launch: its 1x1 consumer computes it (k_conv_pw / k_conv_dwpw)
     }
@@ -1059,7 +1059,7 @@ struct Planner {
         norm = nt->second;
         norm_pending.erase(nt);
       }
-      flush_up(nd.in[0]);
+      flush_input(nd.in[0]);  // (a pending Resize, or a Concat's pending upsampled inputs)
       auto pp = std::make_shared<ConvParams>(p);
       add(conv_thin_name(p.M), [pp, norm](hipStream_t st) { launch_conv_thin(*pp, norm.get(), st); });
       if (cat_direct.count(out)) cat_patch[out].push_back([pp](float* base, int ctot) { retarget(pp.get(), base, ctot); });
@@ -1956,6 +1956,14 @@ struct Planner {
     auto pp = it->second;
     add(resize_kernel_name(*pp), [pp](hipStream_t st) { launch_resize(*pp, st); });
     up_pending.erase(it);
+  }
+  // a consumer that computes no upsample itself: its input's pending Resize and,
+  // when the input is an in-place Concat, every pending upsampled input of it
+  void flush_input(const std::string& name) {
+    flush_up(name);
+    auto cu = cat_up.find(name);
+    if (cu != cat_up.end())
+      for (const UpRange& u : cu->second) flush_up(u.name);
   }
 
   // Resizes whose output feeds one convolution's input, directly or as an

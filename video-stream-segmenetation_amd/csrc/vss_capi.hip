@@ -149,6 +149,7 @@ struct Slot {
                                       // take no ticket and leave it alone)
   bool stem_stored = false;           // the latest forward stored the fused stem (VSS_OPT_KEEP_STEM)
   std::map<GraphKey, std::vector<GraphEntry>> graphs;
+  std::map<GraphKey, unsigned long long> shape_tick;  // per shape: graph_tick of its latest use
   unsigned long long graph_tick = 0;
 #ifdef VSS_TRACE
   std::vector<unsigned long long*> trace;  // per layer, [workgroups][16] stamps of this slot's latest forward
@@ -1066,15 +1067,34 @@ int patch_graph(vss_handle* h, GraphEntry& g, const std::vector<Launch>& ls) {
 // The executable of slot s for this call (see GraphEntry): one bound to the
 // same buffers, else a new one while the shape's set has room, else the least
 // recently used one patched.
+// Bound the cache at kMaxShapes shapes per slot: before a new shape's graphs
+// are added, the least recently used shape's (by shape_tick: its latest
+// prepare or launch) are destroyed.
+constexpr size_t kMaxShapes = 16;
+void make_room_for_shape(Slot& s) {
+  if (s.graphs.size() < kMaxShapes) return;
+  auto victim = s.graphs.begin();
+  unsigned long long oldest = ~0ull;
+  for (auto it = s.graphs.begin(); it != s.graphs.end(); ++it) {
+    const auto t = s.shape_tick.find(it->first);
+    const unsigned long long tick = t == s.shape_tick.end() ? 0ull : t->second;
+    if (tick < oldest) {
+      oldest = tick;
+      victim = it;
+    }
+  }
+  destroy_graph_set(victim->second);
+  s.shape_tick.erase(victim->first);
+  s.graphs.erase(victim);
+}
+
 int pick_graph(vss_handle* h, Slot& s, const GraphKey& key, const std::vector<Launch>& ls, GraphEntry** out) {
   auto it = s.graphs.find(key);
   if (it == s.graphs.end()) {
-    if (s.graphs.size() >= 16) {  // bound the cache (shapes per slot)
-      destroy_graph_set(s.graphs.begin()->second);
-      s.graphs.erase(s.graphs.begin());
-    }
+    make_room_for_shape(s);
     it = s.graphs.emplace(key, std::vector<GraphEntry>()).first;
   }
+  s.shape_tick[key] = s.graph_tick + 1;  // (the launch below takes this tick)
   std::vector<GraphEntry>& v = it->second;
   GraphEntry* lru = nullptr;
   for (GraphEntry& g : v) {
@@ -1134,6 +1154,7 @@ void drop_graphs(vss_handle* h) {
   for (Slot& s : h->slots) {
     for (auto& kv : s.graphs) destroy_graph_set(kv.second);
     s.graphs.clear();
+    s.shape_tick.clear();
   }
 }
 
@@ -2288,11 +2309,11 @@ int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels
   const GraphKey key{n, height, width, channels, row_stride, frame_stride};
   for (size_t k = 0; k < h->slots.size(); ++k) {
     Slot& s = h->slots[k];
-    if (s.graphs.count(key)) continue;
-    if (s.graphs.size() >= 16) {  // the same bound as pick_graph (shapes per slot)
-      destroy_graph_set(s.graphs.begin()->second);
-      s.graphs.erase(s.graphs.begin());
+    if (s.graphs.count(key)) {
+      s.shape_tick[key] = ++s.graph_tick;
+      continue;
     }
+    make_room_for_shape(s);
     std::vector<Launch> ls;
     // null buffers: the first call patches in its own (the slot is idle then)
     forward_launches(h, s, nullptr, n, height, width, channels, row_stride, frame_stride, nullptr, &ls);
@@ -2305,6 +2326,7 @@ int vss_prepare_device(vss_handle* h, int n, int height, int width, int channels
     }
     HIP_TRY(h, hipStreamSynchronize(s.stream));
     s.graphs[key].push_back(std::move(g));
+    s.shape_tick[key] = ++s.graph_tick;
   }
   return VSS_OK;
 }
