@@ -264,13 +264,74 @@ def post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, stream, st
             "composite": composite}
 
 
-def run_steps(sess, streams, n_steps, launch, start=0):
+class Watchdog:
+    """No progress for `limit_s` seconds -> one JSON line (stdout and stderr)
+    naming the rank, the stage, the last step issued, the handle's gather
+    counter and each slot communicator's ncclCommGetAsyncError, then
+    os._exit(3) (never a re-exec).  The main thread beats at every step it
+    issues and after every synchronize, so a collective that never completes
+    (a rank that died, a deadlock between the per-slot communicators) ends
+    the run with a record instead of at the driver's timeout.  Armed only
+    around GPU phases; `status` is a lock-free callable (Session.comm_status)."""
+
+    def __init__(self, limit_s, rank, world):
+        import threading
+        self.limit, self.rank, self.world = limit_s, rank, world
+        self.stage, self.step, self.t = "start", -1, time.monotonic()
+        self.armed, self.status = False, None
+        self._lock = threading.Lock()
+        if limit_s > 0:
+            threading.Thread(target=self._run, daemon=True).start()
+
+    def beat(self, stage=None, step=None):
+        with self._lock:
+            if stage is not None:
+                self.stage = stage
+            if step is not None:
+                self.step = step
+            self.t = time.monotonic()
+
+    def arm(self, stage):
+        self.beat(stage)
+        self.armed = True
+
+    def disarm(self):
+        self.armed = False
+
+    def _run(self):
+        while True:
+            time.sleep(min(1.0, self.limit / 4))
+            with self._lock:
+                idle = time.monotonic() - self.t
+                stage, step = self.stage, self.step
+            if not self.armed or idle < self.limit:
+                continue
+            rec = {"watchdog": "no progress", "rank": self.rank, "world": self.world, "stage": stage,
+                   "last_step_issued": step, "seconds_without_progress": round(idle, 1),
+                   "gather_serial_env": os.environ.get("VSS_GATHER_SERIAL")}
+            try:
+                if self.status is not None:
+                    rec.update(self.status())
+            except Exception as e:  # the record must still go out
+                rec["status_error"] = repr(e)
+            line = json.dumps(rec) + "\n"
+            for fd in (sys.stderr.fileno(), sys.stdout.fileno()):
+                try:
+                    os.write(fd, line.encode())
+                except OSError:
+                    pass
+            os._exit(3)
+
+
+def run_steps(sess, streams, n_steps, launch, start=0, wd=None):
     """Issue n_steps round-robin over the streams (launch(k, stream) per step).
     `start` continues the global step count: step k uses stream, output buffer
     and (the handle's round-robin over device calls) slot k % S, so a slot
     always meets the same buffers and its graph is never patched."""
     for i in range(start, start + n_steps):
         launch(i, streams[i % len(streams)])
+        if wd is not None:
+            wd.beat(step=i)
     return start + n_steps
 
 
@@ -359,6 +420,10 @@ def main():
                     help="rehearse the multi-rank plumbing only (launch_ranks -> torch.distributed.run -> gloo "
                          "-> the clique-id broadcast, with placeholder id bytes) and stop before the first GPU "
                          "call: each rank prints one JSON line; runs on a machine without GPUs")
+    ap.add_argument("--watchdog-s", type=float, default=60.0,
+                    help="no step issued or completed for this long during a GPU phase: print a JSON record "
+                         "(rank, stage, gather counter, communicators' async errors) and exit 3; 0 = off")
+    ap.add_argument("--test-stall-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests: a rank that hangs
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_traffic.json"),
                     help="per-kernel HBM traffic from tools/prof_summary.py (PMC passes)")
     args = ap.parse_args()
@@ -390,15 +455,22 @@ def main():
         # the process group carries only the clique id, barriers and the max-time
         # reduction (CPU tensors); the masks go over the handle's own RCCL clique
         dist.init_process_group("gloo")
+    wd = Watchdog(args.watchdog_s, rank, world)
     if args.dry_run_dist:
         # the same broadcast the GPU run makes (rank 0's clique ids -> every
         # rank), with placeholder bytes of the real size: RCCL's ncclGetUniqueId
         # needs a GPU.  4 slots x sizeof(ncclUniqueId) = 128 B each.
         import hashlib
         ids = [os.urandom(args.inflight * 128) if rank == 0 else None]
+        wd.arm("dry-run: clique-id broadcast")
         if world > 1:
             dist.broadcast_object_list(ids, src=0)
+            if rank == args.test_stall_rank:  # (tests: this rank never reaches the barrier)
+                wd.beat("dry-run: stalled rank")
+                time.sleep(3600)
+            wd.beat("dry-run: barrier")
             dist.barrier()
+        wd.disarm()
         # one write per line: the ranks share the launcher's stdout pipe, and
         # print()'s separate newline write let two ranks' lines interleave
         line = json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local,
@@ -427,6 +499,8 @@ def main():
     if args.no_graph:
         sess.set_option(pkg.VSS_OPT_USE_GRAPH, 0)
     gather = world > 1 or args.gather
+    wd.status = sess.comm_status
+    wd.arm("clique init")
     if world > 1:
         ids = [sess.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
@@ -453,19 +527,26 @@ def main():
     # every slot's graph for this shape is built before the first step, so no
     # build (and, with the buffer pairing of run_steps, no patch) happens in
     # the timed region at any --warmup
+    wd.beat("prepare")
     sess.prepare_device(B, fh, fw, 3, rs, fs)
-    k = run_steps(sess, streams, args.warmup, step)
+    wd.beat("warmup")
+    k = run_steps(sess, streams, args.warmup, step, wd=wd)
     torch.cuda.synchronize(dev)
+    wd.beat("barrier before the timed steps")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     builds0, patches0 = sess.graph_builds, sess.graph_patches
+    wd.beat("timed steps")
     t0 = time.perf_counter()
-    k = run_steps(sess, streams, args.steps, step, start=k)
+    k = run_steps(sess, streams, args.steps, step, start=k, wd=wd)
+    wd.beat("timed steps: synchronize")
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    wd.beat("barrier after the timed steps")
     if world > 1:
         dist.barrier()
+    wd.beat("event pass")
     timed_builds, timed_patches = sess.graph_builds - builds0, sess.graph_patches - patches0
     last = (k - 1) % S
     # per-step completion times (a second pass of the same K steps, events on
@@ -479,8 +560,9 @@ def main():
 
     e0 = torch.cuda.Event(enable_timing=True)
     e0.record(streams[k % S])
-    k = run_steps(sess, streams, args.steps, step_ev, start=k)
+    k = run_steps(sess, streams, args.steps, step_ev, start=k, wd=wd)
     torch.cuda.synchronize(dev)
+    wd.beat("profile pass")
     # completions arrive in bursts (the batches in flight finish close
     # together), so the step interval is taken over S consecutive completions
     done_ms = np.sort(np.array([e0.elapsed_time(e) for e in ends]))
@@ -494,6 +576,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el_max = float(t.item())
+    wd.beat("profile pass")
     value = world * B * args.steps / el_max
 
     # ---- kernel timing pass (events recorded by the launches, one batch at a time) ----
@@ -504,6 +587,7 @@ def main():
     torch.cuda.synchronize(dev)
     sess.set_option(pkg.VSS_OPT_PROFILE, 0)
     ms, cnt = sess.profile_read()
+    wd.disarm()  # (the legs below synchronise per call and run no collective)
 
     blob = open(sess.weights_path, "rb").read()
     sys.path.insert(0, os.path.join(PKG_DIR, "model"))

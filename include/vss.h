@@ -299,6 +299,16 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
                               int channels, size_t row_stride, size_t frame_stride, float* d_gathered,
                               void* stream);
 
+/* Health of the handle's communicators, for a watchdog (takes no handle lock:
+ * safe while another thread is blocked in a call).  async_errors[k] = slot k's
+ * ncclCommGetAsyncError result (0 = ncclSuccess, 7 = ncclInProgress, any other
+ * = an RCCL error code; -1 = the slot has no communicator, -2 = the query
+ * failed) for k < min(cap, *nslots); *gather_calls = vss_segment_gather_device
+ * calls so far (call i runs on slot i % *nslots).  Every gather also checks
+ * its communicator first and fails with VSS_E_RCCL on an asynchronous error.
+ * No reference counterpart (the reference runs on one device). */
+int vss_comm_status(vss_handle* h, int* async_errors, int cap, int* nslots, unsigned long long* gather_calls);
+
 /* Preprocessing alone (frameProcessorTest.ts:79-85): d_out = [n][3][mask_h][mask_w]
  * f32, the exact ORT input tensor. Enqueued on `stream`. */
 int vss_preprocess_device(vss_handle* h, const uint8_t* d_frames, int n, int height, int width,

@@ -43,3 +43,36 @@ def test_gpus_2_dry_run_reaches_the_clique_id_broadcast():
         assert d["world"] == 2 and d["env_world_size"] == "2"
         assert d["ids_len"] == 4 * 128
     assert by_rank[0]["ids_sha256"] == by_rank[1]["ids_sha256"]
+
+
+def test_watchdog_ends_a_stalled_multi_rank_run_with_a_record():
+    """a rank that never reaches the barrier (--test-stall-rank,
+    on the --dry-run-dist path: the same launcher, gloo group and broadcast as
+    the GPU run) must not hang the job.  The waiting rank's watchdog prints one
+    JSON record naming its rank and stage and exits 3 (os._exit, no re-exec);
+    torch.distributed.run then ends the job non-zero, well before any driver
+    timeout."""
+    import json
+    import time
+    t0 = time.monotonic()
+    r = _run(["--gpus", "2", "--dry-run-dist", "--test-stall-rank", "1", "--watchdog-s", "3"])
+    el = time.monotonic() - t0
+    assert r.returncode != 0
+    recs = [json.loads(x) for x in (r.stdout + "\n" + r.stderr).splitlines()
+            if x.startswith("{") and '"watchdog"' in x]
+    assert recs, (r.stdout[-2000:], r.stderr[-2000:])
+    stages = {(d["rank"], d["stage"]) for d in recs}
+    # rank 0 waits in the barrier rank 1 never reaches; rank 1 sits in its stall
+    assert (0, "dry-run: barrier") in stages or (1, "dry-run: stalled rank") in stages, stages
+    for d in recs:
+        assert d["world"] == 2 and d["seconds_without_progress"] >= 3
+    assert el < 120, el
+
+
+def test_watchdog_off_by_zero_and_quiet_on_a_healthy_run():
+    """--watchdog-s 0 starts no thread, and a healthy dry run with the default
+    limit prints no record."""
+    r = _run(["--gpus", "2", "--dry-run-dist"])
+    assert r.returncode == 0 and '"watchdog"' not in r.stdout + r.stderr
+    r = _run(["--gpus", "2", "--dry-run-dist", "--watchdog-s", "0"])
+    assert r.returncode == 0 and '"watchdog"' not in r.stdout + r.stderr

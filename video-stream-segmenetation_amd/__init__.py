@@ -145,6 +145,7 @@ def lib() -> ctypes.CDLL:
                 "vss_comm_unique_id": ([P, P, S, ctypes.POINTER(S)], I),
                 "vss_comm_init_rank": ([P, I, I, P, S], I),
                 "vss_segment_gather_device": ([P, P, I, I, I, I, S, S, P, P], I),
+                "vss_comm_status": ([P, ctypes.POINTER(I), I, ctypes.POINTER(I), ctypes.POINTER(ctypes.c_uint64)], I),
                 "vss_block_lds_bytes": ([I] * 9, I),
                 "vss_preprocess_device": ([P, P, I, I, I, I, S, S, P, P], I),
                 "vss_mask_to_frame_device": ([P, P, I, I, I, P, P], I),
@@ -351,6 +352,17 @@ class Session:
     def comm_init_rank(self, nranks: int, rank: int, ids: bytes):
         buf = ctypes.create_string_buffer(ids, len(ids))
         _check(lib().vss_comm_init_rank(self._h, nranks, rank, buf, len(ids)), self._h)
+
+    def comm_status(self) -> dict:
+        """{'async_errors': per slot (0 ok, 7 in progress, -1 no communicator,
+        else an RCCL error), 'gather_calls': n} — lock-free (vss_comm_status),
+        for a watchdog thread."""
+        errs = (ctypes.c_int * 64)()
+        ns = ctypes.c_int()
+        calls = ctypes.c_uint64()
+        _check(lib().vss_comm_status(self._h, errs, 64, ctypes.byref(ns), ctypes.byref(calls)), self._h)
+        return {"async_errors": list(errs[:min(ns.value, 64)]), "gather_calls": int(calls.value),
+                "slots": ns.value}
 
     def segment_gather_device(self, frames_ptr: int, n: int, h: int, w: int, c: int, row_stride: int,
                               frame_stride: int, gathered_ptr: int, stream: int = 0):

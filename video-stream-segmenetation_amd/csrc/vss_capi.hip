@@ -405,6 +405,23 @@ int fail(vss_handle* h, int code, const std::string& msg) {
       return fail((h), VSS_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));   \
   } while (0)
 
+// A communicator's asynchronous error (ncclCommGetAsyncError): RCCL reports a
+// failed collective — a peer gone, a network or device error — there, not at
+// the enqueue.  Every gather polls it on the communicator it is about to use
+// and fails with VSS_E_RCCL instead of enqueueing behind a broken one (a
+// stuck collective with no error shows up only as no progress: bench.py's
+// watchdog, which reads vss_comm_status).
+int comm_healthy(vss_handle* h, ncclComm_t c, int slot) {
+  if (!c) return VSS_OK;
+  ncclResult_t ae = ncclSuccess;
+  const ncclResult_t q = ncclCommGetAsyncError(c, &ae);
+  if (q != ncclSuccess) return fail(h, VSS_E_RCCL, std::string("ncclCommGetAsyncError: ") + ncclGetErrorString(q));
+  if (ae != ncclSuccess && ae != ncclInProgress)
+    return fail(h, VSS_E_RCCL, "communicator of slot " + std::to_string(slot) + ": asynchronous error " +
+                                   ncclGetErrorString(ae));
+  return VSS_OK;
+}
+
 template <class T>
 int dalloc(vss_handle* h, T** p, size_t bytes) {
   void* q = nullptr;
@@ -1535,6 +1552,8 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   clk.mark(4);
   const float* res = s0.d_masks;
   if (h->rccl) {
+    for (int r = 0; r < R; ++r)
+      if ((rc = comm_healthy(E[r], E[r]->slots[k].comm, k))) return abort_batch(fail(h, rc, E[r]->err));
     // one all-gather of f32 masks per GPU, m frames each (padding rows of the
     // last shards are gathered and dropped): [rank][m][P] = frame order
     ncclResult_t nr_ = ncclGroupStart();
@@ -2093,6 +2112,21 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
   return rc ? rc : rr;
 }
 
+int vss_comm_status(vss_handle* h, int* async_errors, int cap, int* nslots, unsigned long long* gather_calls) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  // no handle lock: a watchdog calls this while another thread may be blocked
+  // inside a call that holds it; the communicators do not change after init
+  const int ns = (int)h->slots.size();
+  if (nslots) *nslots = ns;
+  if (gather_calls) *gather_calls = h->gather_calls;
+  for (int k = 0; k < ns && k < cap && async_errors; ++k) {
+    ncclResult_t ae = ncclSuccess;
+    const ncclComm_t c = h->slots[k].comm;
+    async_errors[k] = !c ? -1 : (ncclCommGetAsyncError(c, &ae) == ncclSuccess ? (int)ae : -2);
+  }
+  return VSS_OK;
+}
+
 int vss_comm_unique_id(vss_handle* h, void* ids, size_t cap, size_t* len) {
   if (!h || !ids) return fail(h, VSS_E_INVALID_ARG, "null handle/ids");
   const size_t need = h->slots.size() * sizeof(ncclUniqueId);
@@ -2142,7 +2176,10 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
   // round-robin over the gather calls alone (a counter of their own), so every
   // rank uses the same slot's communicator for its i-th gather whatever other
   // device calls it interleaves
-  const int k = (int)(h->gather_calls++ % h->slots.size());
+  static const bool serial = getenv("VSS_GATHER_SERIAL") && getenv("VSS_GATHER_SERIAL")[0] == '1';
+  const int k = (int)(h->gather_calls % h->slots.size());
+  if ((rc = comm_healthy(h, h->slots[serial ? 0 : k].comm, serial ? 0 : k))) return rc;
+  h->gather_calls++;
   Slot& sl = h->slots[k];
   if ((rc = claim_slot(h, sl, s))) return rc;
   if ((rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, sl.d_masks, s))) {
@@ -2159,7 +2196,6 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
   // channels (tens of CUs of 256).  VSS_GATHER_SERIAL=1 puts every gather on
   // slot 0's communicator and one stream instead (a total order, for systems
   // where concurrent communicators misbehave).
-  static const bool serial = getenv("VSS_GATHER_SERIAL") && getenv("VSS_GATHER_SERIAL")[0] == '1';
   ncclResult_t nr = ncclSuccess;
   hipError_t he = hipSuccess;
   if (!serial) {
