@@ -323,6 +323,39 @@ class Watchdog:
             os._exit(3)
 
 
+def latency_leg(sess, torch, dev, d_frames, fh, fw, iters):
+    """One call at a time, the way the reference runs its model
+    (runModnetExclusive serialises every processFrame, main.ts:18-22, 66-74;
+    its overlay's `Latency` is session.run's wall time, frameProcessorTest.ts:
+    90-92): the host wall time of vss_segment_device + stream synchronize for
+    1 frame and for a batch of 8, frames already in HBM.  p50 / p99 / min in
+    ms and the serial frames/s (never `value`)."""
+    out = {}
+    st = torch.cuda.Stream(device=dev)
+    P = sess.mask_h * sess.mask_w
+    masks = torch.empty((8, P), dtype=torch.float32, device=dev)
+    for n in (1, 8):
+        sess.prepare_device(n, fh, fw, 3, fw * 3, fh * fw * 3)
+        for _ in range(50):
+            sess.segment_device(d_frames.data_ptr(), n, fh, fw, 3, fw * 3, fh * fw * 3, masks.data_ptr(), st.cuda_stream)
+        st.synchronize()
+        lat = []
+        t1 = time.perf_counter()
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            sess.segment_device(d_frames.data_ptr(), n, fh, fw, 3, fw * 3, fh * fw * 3, masks.data_ptr(), st.cuda_stream)
+            st.synchronize()
+            lat.append((time.perf_counter() - t0) * 1e3)
+        el = time.perf_counter() - t1
+        lat = np.sort(np.array(lat))
+        out[f"batch{n}"] = {"latency_ms_p50": round(float(lat[len(lat) // 2]), 4),
+                            "latency_ms_p99": round(float(lat[min(len(lat) - 1, int(0.99 * len(lat)))]), 4),
+                            "latency_ms_min": round(float(lat[0]), 4), "calls": iters,
+                            "frames_per_s_serial": round(n * iters / el, 1)}
+    out["entry"] = "vss_segment_device + hipStreamSynchronize, one call at a time (frames resident in HBM)"
+    return out
+
+
 def run_steps(sess, streams, n_steps, launch, start=0, wd=None):
     """Issue n_steps round-robin over the streams (launch(k, stream) per step).
     `start` continues the global step count: step k uses stream, output buffer
@@ -414,6 +447,7 @@ def main():
     ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host-buffer legs")
     ap.add_argument("--no-ts", action="store_true", help="skip the TypeScript (Node) leg")
     ap.add_argument("--no-sweep", action="store_true", help="skip the batch sweep")
+    ap.add_argument("--no-latency", action="store_true", help="skip the one-call-at-a-time latency leg")
     ap.add_argument("--gather", action="store_true",
                     help="run the multi-GPU step (RCCL clique all-gather) even at one rank (a rehearsal of N > 1)")
     ap.add_argument("--dry-run-dist", action="store_true",
@@ -612,7 +646,9 @@ def main():
         if tj and tj.get("traffic_bytes"):
             traffic = round(tj["traffic_bytes"] / 1e6, 3)
 
-    post = host = batch_sweep = None
+    post = host = batch_sweep = latency = None
+    if rank == 0 and world == 1 and not args.no_latency:
+        latency = latency_leg(sess, torch, dev, d_frames, fh, fw, max(200, min(args.steps, 1000)))
     if rank == 0 and not args.no_post:
         post = post_leg(pkg, sess, d_frames, d_masks, frames, B, fh, fw, hm, wm, streams[0], args.steps,
                         args.warmup, 0.0 if args.no_cpu else 2.0)
@@ -688,6 +724,7 @@ def main():
             "layer_launches_sum_ms": round(float(sum(ms)), 5),
             "launches_per_forward": sum(1 for n in names if not n.startswith("(fused")),
             "batch_sweep": batch_sweep,
+            "latency": latency,
             "cpu_baseline": cpu,
             "post": post,
             "host_path": host,

@@ -39,6 +39,21 @@ async function main() {
     lat.push(Number(process.hrtime.bigint() - t0) / 1e6);
   }
   lat.sort((a, c) => a - c);
+  // one frame per call, one call at a time: the reference's own usage
+  // (processFrame -> runModnetExclusive, main.ts:18-22, 66-74), whose overlay
+  // shows session.run's wall time as `Latency` (frameProcessorTest.ts:90-92)
+  for (let i = 0; i < 50; i++) await s.segmentFrame(frames[0]);
+  const lat1 = [];
+  const n1 = Math.max(200, it);
+  const t1 = process.hrtime.bigint();
+  for (let i = 0; i < n1; i++) {
+    const t0 = process.hrtime.bigint();
+    await s.segmentFrame(frames[i % b]);
+    lat1.push(Number(process.hrtime.bigint() - t0) / 1e6);
+  }
+  const el1 = Number(process.hrtime.bigint() - t1) / 1e9;
+  lat1.sort((a, c) => a - c);
+  const pct = (a, q) => Math.round(a[Math.min(a.length - 1, Math.floor(q * a.length))] * 1e4) / 1e4;
   // throughput: calls fired ahead of their results (a window of 2 x the queue
   // depth outstanding, so resolved results are dropped as a consumer would)
   const win = 2 * s.queueDepth;
@@ -83,7 +98,12 @@ async function main() {
   console.log(JSON.stringify({ value: Math.round(b * it / el * 10) / 10, unit: 'frames/s',
                                ms_per_batch: Math.round(el * 1e3 / it * 1e4) / 1e4, iters: it,
                                latency_ms_p50: Math.round(lat[lat.length >> 1] * 1e4) / 1e4,
-                               latency_ms_min: Math.round(lat[0] * 1e4) / 1e4, queue_depth: s.queueDepth,
+                               latency_ms_min: Math.round(lat[0] * 1e4) / 1e4, latency_ms_p99: pct(lat, 0.99),
+                               queue_depth: s.queueDepth,
+                               single_frame: { entry: 'Segmenter.segmentFrame, one 640x480 frame per call, one call at a time',
+                                               calls: n1, latency_ms_p50: pct(lat1, 0.5), latency_ms_p99: pct(lat1, 0.99),
+                                               latency_ms_min: Math.round(lat1[0] * 1e4) / 1e4,
+                                               frames_per_s: Math.round(n1 / el1 * 10) / 10 },
                                entry: 'Segmenter.segmentFrames (TS -> N-API -> vss_submit_list / vss_wait)',
                                zero_copy: { value: Math.round(b * it / zel * 10) / 10,
                                             ms_per_batch: Math.round(zel * 1e3 / it * 1e4) / 1e4,

@@ -1,15 +1,15 @@
 #!/bin/bash
 # Build libvss.so from the current sources with extra compile flags into
-# ablib/libvss_<name>.so (a separate tree under /tmp; the in-tree build is
+# abvar/libvss_<name>.so (a separate tree under /tmp; the in-tree build is
 # untouched).  Usage: tools/build_variant.sh NAME "-DVSS_X=1 ..."
 set -e
 NAME=$1; FLAGS=$2
 R=$(cd "$(dirname "$0")/.." && pwd)
 T=/tmp/vssvar_$NAME
-rm -rf "$T"; mkdir -p "$T/video-stream-segmenetation_amd" "$T/ablib"
+rm -rf "$T"; mkdir -p "$T/video-stream-segmenetation_amd" "$R/abvar"
 cp -r "$R/include" "$T/"
 cp -r "$R/video-stream-segmenetation_amd/csrc" "$T/video-stream-segmenetation_amd/"
 mkdir -p "$T/video-stream-segmenetation_amd/lib"
 make -s -j8 -C "$T/video-stream-segmenetation_amd/csrc" HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result -mllvm -amdgpu-mfma-vgpr-form=1 $FLAGS" 2>&1 | grep -E "rror" || true
-cp "$T/video-stream-segmenetation_amd/lib/libvss.so" "$R/ablib/libvss_$NAME.so"
-echo "ablib/libvss_$NAME.so"
+cp "$T/video-stream-segmenetation_amd/lib/libvss.so" "$R/abvar/libvss_$NAME.so"
+echo "abvar/libvss_$NAME.so"

@@ -33,8 +33,30 @@ def r4(v):
     return (v + 3) & ~3
 
 
+SWZ = True  # VSS_SWZ in csrc/vss_kernels.h: the round-5 bank-conflict-free LDS layouts
+
+
+def stem_xwp(iw):
+    """stem_xwp() in csrc/vss_kernels.h: the fused stem's x0 row pitch."""
+    if not SWZ:
+        return 2 * iw + 2
+    x = 2 * iw + 1
+    while (x - (iw + 1)) % 32:
+        x += 1
+    return x
+
+
 def stem_in_lds(ih, iw):
-    return r4(3 * (2 * ih + 1) * (2 * iw + 2)) + 27 * 16 + 16
+    return r4(3 * (2 * ih + 1) * stem_xwp(iw)) + 27 * 16 + 16
+
+
+def dw_run(tw, npb, pw):
+    """dw_run() in csrc/vss_kernels.h: pixels per lane run of the dw stage."""
+    if tw % 4 == 0 and 16 % (tw // 4) == 0 and npb % 4 == 0 and (npb // 4) % pw == 0:
+        return 4
+    if tw % 2 == 0 and 16 % (tw // 2) == 0 and npb % 2 == 0 and (npb // 2) % pw == 0:
+        return 2
+    return 1
 
 
 def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=False):
@@ -52,7 +74,15 @@ def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=False)
     npbw = npb // pw
     nacc = npbw * (cout // 16)
     sr, sc = (th + 1) // 2 + 3, (tw + 1) // 2 + 3
-    f = r4(p_in_pad * (cx + 4))
+    # xt: quad-major planes (direct), swizzled unpadded pixels (expand), or
+    # pixel-major rows padded to 8 mod 16 floats (16-wide decoder tiles)
+    xqm = SWZ and mode == 1
+    xs = (cx + 4) if not SWZ else (4 if xqm else ((cx + (8 if tw == 16 else 4)) if mode == 2 else cx))
+    xt_floats = p_in_pad * cx if xqm else r4(p_in_pad * xs)
+    rs = cout if SWZ else cout + 4
+    xr1 = dw_run(tw, npb, 1) == 1
+    hid = 16 * 4 * (p_in_pad + (1 if stride == 2 else 0)) if (SWZ and xr1) else 4 * p_in_pad * HID_STRIDE
+    f = xt_floats
     f += r4(p_out * cin) if (mode == 0 and stride == 1 and cin == cout) else 0
     f += r4(chid * (cin + 8) // 2) if mode == 0 else 0
     f += r4(cout * (chid + 8) // 2) + r4(9 * chid) + r4(chid) + (r4(chid) if mode == 0 else 0) + r4(cout)
@@ -60,8 +90,8 @@ def block_lds_bytes(mode, stride, th, tw, cin, cskip, chid, cout, stem_in=False)
     f += 4 * p_in_pad if mode == 2 and (th % 2 or tw % 2) else 0  # the decoder's upsample tap records (L.uc; odd tiles)
     # work: expand scratch / slabs / (decoder) the low-res src region; the
     # decoder's slabs go into xt when they fit (its stats scratch then in work)
-    slab_in_xt = mode == 2 and cs * p_out * (cout + 4) <= r4(p_in_pad * (cx + 4))
-    f += max(4 * p_in_pad * HID_STRIDE if mode == 0 else 1024, 0 if slab_in_xt else cs * p_out * (cout + 4),
+    slab_in_xt = mode == 2 and cs * p_out * rs <= xt_floats
+    f += max(hid if mode == 0 else 1024, 0 if slab_in_xt else cs * p_out * rs,
              r4(sr * sc * cin) if mode == 2 else 0, stem_in_lds(ih, iw) if stem_in else 0)
     return f * 4, nacc
 

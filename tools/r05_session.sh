@@ -19,6 +19,11 @@ echo "== smoke"
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1; rc=$?
 tail -1 gpurun_out/${TAG}_smoke.log; fatal $rc
 fi
+if [ -n "${AB_LIBS:-}" ]; then
+  echo "== A/B vs $AB_LIBS"
+  timeout -k 10 600 bash tools/ab_quick.sh ${AB_ROUNDS:-3} $AB_LIBS; fatal $?
+fi
+[ "${NOBENCH:-0}" = 1 ] && exit 0
 echo "== bench (default)"
 timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.log 2>&1; rc=$?; fatal $rc
 tail -1 gpurun_out/${TAG}_bench.log > gpurun_out/${TAG}_bench.json

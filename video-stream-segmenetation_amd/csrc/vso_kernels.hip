@@ -550,7 +550,7 @@ static bool pw_kernel(const ConvParams& p, int* wm, int* dwk) {
   const bool one = p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.pt == 0 && p.pl == 0 && p.Ho == p.H &&
                    p.Wo == p.W && p.G == 1;
   if (!one) return false;
-  const long P = (long)p.Ho * p.Wo;
+  const long P = (long)p.Ho * p.Wo, wgs = pw_workgroups(p.N, P, p.M, wm);  // (sets *wm for the launch)
   *dwk = 0;
   if (p.pre.w) {
     if (p.pre.kh != p.pre.kw || (p.pre.kh != 3 && p.pre.kh != 5)) return false;
@@ -558,7 +558,6 @@ static bool pw_kernel(const ConvParams& p, int* wm, int* dwk) {
     return pw_pair_fits(p.N, p.C, (long)p.pre.H * p.pre.W, P, p.M);
   }
   if ((long)p.C * P >= (1L << 31) || (long)p.M * P >= (1L << 31)) return false;  // 32-bit offsets within an image
-  const long wgs = pw_workgroups(p.N, P, p.M, wm);
   return wgs >= 256 || p.C <= 192;
 }
 

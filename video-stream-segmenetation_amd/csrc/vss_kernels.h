@@ -79,27 +79,94 @@ constexpr int kMaxAcc = 16;         // 16x16 project accumulators per wave
 #endif
 __host__ __device__ constexpr int block_pix(int r) { return VSS_PERM ? (r < 4 ? r : (r < 12 ? r + 4 : r - 8)) : r; }
 // floats per pixel of an expand wave's hidden chunk in LDS (16 channels + pad)
+// (the padded layout, VSS_SWZ=0)
 __host__ __device__ constexpr int hid_stride(int stride) { return stride == 2 ? 20 : VSS_HS1; }
+
+// Bank-conflict-free LDS layouts (round 5, VSS_SWZ=1; tools/lds_sites.py models
+// every access site lane by lane against gfx950's bank rules).  The access
+// pattern that sets them: a ds_read_b128 of a 16-pixel block, lane (r, g) =
+// pixel r, channel quad g, is served in lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31} (+32) over 64 banks (16 bank quads); a pixel stride of
+// 5 or 13 quads — the +4 float pads — is 2-way conflicted, and a plain 16-B
+// write (8 contiguous lanes, 32 banks) wants the opposite of what the reads
+// want from a pad.  Three layouts, no padding:
+//  * quad-major planes ("QM"): quad q of pixel p at q * PLANE + 4 p floats.  A
+//    lane group's 16 pixels are consecutive quads of one or two planes; with
+//    PLANE a multiple of 16 quads the two channel quads of a group fall on
+//    complementary pixel sets, so a run of 16 consecutive pixels is
+//    conflict-free, and so is a write of 8 consecutive pixels of one plane —
+//    at any pixel offset, so the taps keep immediate offsets (no VALU).
+//    Stride-2 taps read every other pixel: their planes are PLANE + 1 quads
+//    apart.  For b1's input tile and every expand layer's hidden chunk;
+//  * XOR-swizzled pixel-major ("SW"): quad q of pixel p at p * CX + 4 (q ^
+//    gray(p) % M), M = the largest power of two dividing the pixel's quads
+//    (<= 16).  For the expand layers' input tile (the MFMA B reads take
+//    pixel cb * 16 + r, whose swizzle is the lane's own for M <= 8), the
+//    epilogue slabs and the residual centre;
+//  * the decoders with 16-wide tiles keep pixel-major rows padded to 8 mod 16
+//    floats (2 mod 4 quads: conflict-free for runs of 16 pixels).
+#ifndef VSS_SWZ
+#define VSS_SWZ 1
+#endif
+__host__ __device__ constexpr int pow2div16(int q) {
+  return q % 16 == 0 ? 16 : (q % 8 == 0 ? 8 : (q % 4 == 0 ? 4 : (q % 2 == 0 ? 2 : 1)));
+}
+__host__ __device__ constexpr int gray_swz(int pix, int m) { return (pix ^ (pix >> 1)) & (m - 1); }
 constexpr int kAccSlots = 4;        // instance-norm accumulator slots per frame and layer
                                     // (spreads the producers' atomics over 16x the cache lines)
 
 __host__ __device__ constexpr int r4(int v) { return (v + 3) & ~3; }
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
+// dw pixel runs: the output pixels of XR consecutive pixel blocks are dealt
+// to lanes in horizontal runs — lane r of a "super-block" evaluates the XR
+// adjacent pixels (row, c0 .. c0 + XR - 1) — so the 3 x 3 taps those pixels
+// share are read from LDS once: per tap row STRIDE * (XR - 1) + 3 reads for
+// XR pixels instead of 3 * XR (stride 1, XR = 4: 18 reads per 4 pixels, not
+// 36).  Element j of the run is pixel block sb * XR + j's column r, so the
+// MFMAs still take one 16-pixel block per call, and every output pixel's
+// arithmetic is unchanged (bitwise the same activations for any XR / tile).
+// XR = the largest of 4, 2, 1 that tiles the TW-wide rows and deals evenly
+// to the PW pixel-block groups of waves.
+__host__ __device__ constexpr int dw_run(int TW, int NPB, int PW) {
+  return (TW % 4 == 0 && 16 % (TW / 4) == 0 && NPB % 4 == 0 && (NPB / 4) % PW == 0)   ? 4
+         : (TW % 2 == 0 && 16 % (TW / 2) == 0 && NPB % 2 == 0 && (NPB / 2) % PW == 0) ? 2
+                                                                                      : 1;
+}
+
 // Geometry + LDS carve (floats) of one k_block instantiation.  Evaluated at
 // compile time in the kernel and at run time by the host planner, so the two
 // can never disagree.  Every region is a multiple of 4 floats (16-B aligned).
 struct BlockLds {
   int IH, IW, P_in, P_in_pad, P_out, CX, XS, LD1, LD2, SR, SC;
+  // layouts (VSS_SWZ): XQM = xt quad-major (plane XPL floats; XS = 4 then),
+  // XSW / RSW / XRW = the xt / slab / residual-centre swizzle modulus (1 = none),
+  // HPL = the hidden chunk's plane (floats; 0 = the padded pixel-major chunk)
+  bool XQM;
+  int XPL, XSW, HPL, RS, RSW, XRW;
   int NCB, NPB, NCHUNK, PW, CS, NPBW, NACC;  // CS = chunk groups, PW = pixel-block groups
   int xt, xr, w1, w2, wdw, bdw, b1, b2, wimg_end, lr, nrm, uc, work, stt, total;  // [w1, wimg_end): the weight image
   int slab_stride;  // floats per wave slab = P_out * (cout + 4)
   int slab;         // the epilogue's accumulator slabs: the work region, or (decoder) the input tile
 };
 
-// LDS the fused stem needs (x0 region [3][2*IH+1][2*IW+2] + stem weights), in the work region
+// Row pitch (floats) of the fused stem's resized region x0 [3][2*IH+1][XWP]:
+// its XW = 2*IW+1 columns are written two per thread, columns lx and lx + HW2
+// (HW2 = (XW+1)/2) of row ly by thread ly*HW2 + lx, so a pitch = HW2 mod 32
+// makes consecutive threads hit consecutive banks (ds_write_b32: 32 banks);
+// being odd it also puts the stem MFMA's paired taps on opposite bank parities
+// (tools/lds_sites.py: 125 -> 19 conflict cycles per b1 wave with the rest of
+// the round-5 layouts).  VSS_SWZ=0: XW + 1.
+__host__ __device__ constexpr int stem_xwp(int IW) {
+  if (!VSS_SWZ) return 2 * IW + 2;
+  const int xw = 2 * IW + 1, hw2 = IW + 1;
+  int x = xw;
+  while ((x - hw2) % 32 != 0) ++x;
+  return x;
+}
+// LDS the fused stem needs (x0 region [3][2*IH+1][stem_xwp(IW)] + stem weights), in the work region
 __host__ __device__ constexpr int stem_in_lds(int IH, int IW) {
-  return r4(3 * (2 * IH + 1) * (2 * IW + 2)) + 27 * 16 + 16;
+  return r4(3 * (2 * IH + 1) * stem_xwp(IW)) + 27 * 16 + 16;
 }
 
 __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, int TW, int cin, int cskip, int chid,
@@ -111,7 +178,14 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   L.P_in_pad = (L.P_in + 15) & ~15;
   L.P_out = TH * TW;
   L.CX = mode == 2 /*MODE_DEC*/ ? cin + cskip : cin;
-  L.XS = L.CX + VSS_XS_PAD;
+  L.XQM = VSS_SWZ && mode == 1;
+  L.XS = !VSS_SWZ ? L.CX + VSS_XS_PAD : (L.XQM ? 4 : (mode == 2 ? L.CX + (TW == 16 ? 8 : VSS_XS_PAD) : L.CX));
+  L.XPL = L.XQM ? 4 * L.P_in_pad : 0;
+  L.XSW = VSS_SWZ && mode == 0 ? pow2div16(L.CX / 4) : 1;
+
+  L.RS = VSS_SWZ ? cout : cout + 4;
+  L.RSW = VSS_SWZ ? pow2div16(cout / 4) : 1;
+  L.XRW = VSS_SWZ ? pow2div16(cin / 4) : 1;
   L.LD1 = cin + 8;   // bf16 elements per W1 row in LDS (16-B aligned rows)
   L.LD2 = chid + 8;  // bf16 elements per W2 row
   L.SR = (TH + 1) / 2 + 3;
@@ -128,9 +202,13 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   L.PW = 4 / L.CS;
   L.NPBW = L.NPB / L.PW;
   L.NACC = L.NPBW * L.NCB;
-  L.slab_stride = L.P_out * (cout + 4);
+  // the hidden chunk quad-major where the dw reads runs of 16 pixels (XR = 1);
+  // the 2- and 4-pixel runs of XR > 1 meet its planes 4-way: they keep HSD
+  L.HPL = VSS_SWZ && mode == 0 && dw_run(TW, L.NPB, 1) == 1 ? 4 * (L.P_in_pad + (stride == 2 ? 1 : 0)) : 0;
+  L.slab_stride = L.P_out * L.RS;
+  const int xt_floats = L.XQM ? L.P_in_pad * L.CX : r4(L.P_in_pad * L.XS);
   int o = 0;
-  L.xt = o;  o += r4(L.P_in_pad * L.XS);
+  L.xt = o;  o += xt_floats;
   // expand blocks keep xt as MFMA operands (bf16 hi/lo pairs in the split
   // mode); the residual-capable shape keeps the exact f32 centre here
   L.xr = o;  o += (mode == 0 && stride == 1 && cin == cout) ? r4(L.P_out * cin) : 0;
@@ -149,11 +227,11 @@ __host__ __device__ constexpr BlockLds block_lds(int mode, int stride, int TH, i
   // epilogue's stats scratch (int64 pairs, 1024 floats); the decoder stages
   // the src's norm slots in xt before the input tile is committed.  (Slabs in
   // xt: d2 50 -> 39 KB of LDS, four workgroups per CU instead of three.)
-  const int xt_floats = r4(L.P_in_pad * L.XS);
   const bool slab_in_xt = mode == 2 && L.CS * L.slab_stride <= xt_floats;
   L.work = o;
   L.lr = o;
-  o += cmax(cmax(cmax(mode == 0 ? 4 * L.P_in_pad * hid_stride(stride) : 1024, slab_in_xt ? 0 : L.CS * L.slab_stride),
+  const int hid_floats = L.HPL ? 4 * 4 * L.HPL : 4 * L.P_in_pad * hid_stride(stride);  // 4 waves
+  o += cmax(cmax(cmax(mode == 0 ? hid_floats : 1024, slab_in_xt ? 0 : L.CS * L.slab_stride),
                  mode == 2 ? r4(L.SR * L.SC * cin) : 0),
             stem_in ? stem_in_lds(L.IH, L.IW) : 0);
   L.nrm = o; o += mode == 2 ? r4(2 * cin) : 0;

@@ -290,6 +290,19 @@ __device__ __forceinline__ f4 stem_mfma(const StemTaps& t, const float* x0, floa
   return acc;
 }
 
+// The same products with the operands swapped (A = the weights, B = the taps):
+// D[channel 4g+i][pixel r], i.e. lane (r, g) gets channels 4g..4g+3 of pixel
+// r — one 16-B store per lane instead of four scalar ones.  Every output is the
+// same sum of the same products over the same k (and the same C), so the
+// activations are bitwise stem_mfma's transposed (test_stem_fusion_bitwise
+// compares the fused stem with k_stem, which keeps stem_mfma).
+__device__ __forceinline__ f4 stem_mfma_t(const StemTaps& t, const float* x0, f4 bias4) {
+  f4 acc = bias4;
+#pragma unroll
+  for (int s = 0; s < 7; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(t.w[s], x0[t.off[s]], acc, 0, 0, 0);
+  return acc;
+}
+
 // ---------------------------------------------------------------------------
 // Stem: output tile 8 x 32 pixels x 16 channels, 16-pixel blocks on the MFMA.
 template <int COUT, bool COH>
@@ -462,21 +475,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// dw pixel runs: the output pixels of XR consecutive pixel blocks are dealt
-// to lanes in horizontal runs — lane r of a "super-block" evaluates the XR
-// adjacent pixels (row, c0 .. c0 + XR - 1) — so the 3 x 3 taps those pixels
-// share are read from LDS once: per tap row STRIDE * (XR - 1) + 3 reads for
-// XR pixels instead of 3 * XR (stride 1, XR = 4: 18 reads per 4 pixels, not
-// 36).  Element j of the run is pixel block sb * XR + j's column r, so the
-// MFMAs still take one 16-pixel block per call, and every output pixel's
-// arithmetic is unchanged (bitwise the same activations for any XR / tile).
-// XR = the largest of 4, 2, 1 that tiles the TW-wide rows and deals evenly
-// to the PW pixel-block groups of waves.
-__host__ __device__ constexpr int dw_run(int TW, int NPB, int PW) {
-  return (TW % 4 == 0 && 16 % (TW / 4) == 0 && NPB % 4 == 0 && (NPB / 4) % PW == 0)   ? 4
-         : (TW % 2 == 0 && 16 % (TW / 2) == 0 && NPB % 2 == 0 && (NPB / 2) % PW == 0) ? 2
-                                                                                      : 1;
-}
 
 // Registers holding one thread's share of a TOTAL-item (16-B items) copy.
 // issue(): every load of the copy in flight (unconditional at clamped indices:
@@ -600,15 +598,16 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   static_assert(SP == 1 || MODE == MODE_DEC, "skip parts: decoder only");
   constexpr int IW = L.IW, P_IN = L.P_in, P_IN_PAD = L.P_in_pad, P_OUT = L.P_out, XS = L.XS;
   constexpr int NCB = L.NCB, NPB = L.NPB, NCHUNK = L.NCHUNK, PW = L.PW, CS = L.CS, NPBW = L.NPBW;
-  constexpr int RS = COUT + 4, SS = L.slab_stride;
+  constexpr int RS = L.RS, SS = L.slab_stride;
   static_assert(L.NACC <= kMaxAcc, "too many accumulators per wave");
   static_assert(CIN % 16 == 0 && CH % 16 == 0 && COUT % 16 == 0 && P_OUT % 16 == 0, "shape");
   static_assert(MODE != MODE_IR_EXPAND || CIN <= 64, "expand cin <= 64");
   static_assert(!RES || (STRIDE == 1 && CIN == COUT && MODE != MODE_DEC), "residual shape");
   static_assert(MODE != MODE_IR_EXPAND || CS == 4, "expand deals its chunks to the 4 waves");
   static_assert(NPB % PW == 0, "pixel blocks must split evenly over the wave groups");
-  static_assert(MODE != MODE_DEC || (r4(P_IN_PAD * XS) >= (NORM_IN ? kAccSlots * 2 * CIN * 2 : 0) &&
-                                     (L.slab == L.xt ? L.stt == L.work : (L.stt == L.xt && r4(P_IN_PAD * XS) >= 1024))),
+  constexpr int XT_FLOATS = L.XQM ? P_IN_PAD * L.CX : r4(P_IN_PAD * XS);
+  static_assert(MODE != MODE_DEC || (XT_FLOATS >= (NORM_IN ? kAccSlots * 2 * CIN * 2 : 0) &&
+                                     (L.slab == L.xt ? L.stt == L.work : (L.stt == L.xt && XT_FLOATS >= 1024))),
                 "decoder: xt holds the src's norm slots (prologue); the stats scratch (epilogue) sits in the "
                 "work region when the slabs take xt, else in xt");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -628,6 +627,15 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   float* work = smem + L.work;
   float* slabs = smem + L.slab;
   float* stt = smem + L.stt;
+  // LDS layouts (vss_kernels.h, VSS_SWZ): float offsets of channel quad q of a
+  // pixel in the input tile xt, an epilogue slab, the residual centre xr and
+  // an expand wave's hidden chunk
+  auto xq = [&](int pix, int q) {
+    if constexpr (L.XQM) return q * L.XPL + 4 * pix;
+    else return pix * XS + 4 * (q ^ gray_swz(pix, L.XSW));
+  };
+  auto sq = [&](int sl, int pix, int q) { return sl * SS + pix * RS + 4 * (q ^ gray_swz(pix, L.RSW)); };
+  auto rq = [&](int pix, int q) { return pix * CIN + 4 * (q ^ (pix & (L.XRW - 1))); };
   VSS_STAMP(0);
 
   // ---- prologue: issue every load, then commit to LDS ----
@@ -651,6 +659,13 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     constexpr int GL = CL / 16, GS = CSKIP / 16;  // 16-channel items per pixel
     Staged16<SR * SC * GL, XP, VSS_STAGE16_DEC> st_lr;
     Staged16<P_IN_PAD * GS, SP, VSS_STAGE16_DEC> st_sk;
+    // The skip commit's 16-B stores go 8 lanes at a time (32 banks) over two
+    // items; with one item per pixel and a pixel stride of 2 mod 4 quads (the
+    // 16-wide decoder tiles' rows) two neighbouring pixels overlap by two bank
+    // quads, pixels two apart do not: items take pixels 0, 2, 1, 3, 4, 6, ...
+    // (a bijection within groups of four; P_IN_PAD is a multiple of 16)
+    constexpr bool SKP = VSS_SWZ && GS == 1 && !L.XQM && VSS_STAGE16_DEC == 0 && (XS / 4) % 4 == 2;
+    auto skip_pix = [&](int it) { return SKP ? (it & ~3) | ((it & 1) << 1) | ((it >> 1) & 1) : it; };
     Staged<WIMG_F4> st_w;
     {
       const float* xb[XP];
@@ -665,7 +680,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
       for (int q = 0; q < SP; ++q) sb[q] = sn + q * p.skip_part_stride;
       st_sk.issue(sb, [&](int i) {
-        const int pix = i / GS, gq = i - pix * GS, py = pix / IW;
+        const int pix = skip_pix(i / GS), gq = i - (i / GS) * GS, py = pix / IW;
         const int yy = min(max(iy0 + py, 0), Ho - 1), xx = min(max(ix0 + pix - py * IW, 0), Wo - 1);
         return (unsigned)((yy * Wo + xx) * CSKIP + 16 * gq);
       });
@@ -733,13 +748,13 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     // loads were clamped to real pixels, and padding pixels are never read)
     const bool sk_interior = iy0 >= 0 && iy0 + L.IH <= Ho && ix0 >= 0 && ix0 + IW <= Wo;
     st_sk.commit_sum([&](int i, int k, f4 v) {
-      const int pix = i / GS, gq = i - pix * GS;
+      const int pix = skip_pix(i / GS), gq = i - (i / GS) * GS;
       if (!sk_interior) {
         const int py = pix / IW, yy = iy0 + py, xx = ix0 + pix - py * IW;
         const bool valid = ((unsigned)yy < (unsigned)Ho) & ((unsigned)xx < (unsigned)Wo);
         v = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
       }
-      *reinterpret_cast<f4*>(xt + pix * XS + CL + 16 * gq + 4 * k) = v;
+      *reinterpret_cast<f4*>(xt + xq(pix, CL / 4 + 4 * gq + k)) = v;
     });
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     VSS_STAMP(4);
@@ -795,11 +810,11 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
             o10 = r1 && x0v ? o10 : z;
             o11 = r1 && x1v ? o11 : z;
           }
-          float* dst = xt + ((2 * qy) * IW + 2 * qx) * XS + 4 * c4;
-          *reinterpret_cast<f4*>(dst) = o00;
-          *reinterpret_cast<f4*>(dst + XS) = o01;
-          *reinterpret_cast<f4*>(dst + IW * XS) = o10;
-          *reinterpret_cast<f4*>(dst + (IW + 1) * XS) = o11;
+          const int p00 = (2 * qy) * IW + 2 * qx;
+          *reinterpret_cast<f4*>(xt + xq(p00, c4)) = o00;
+          *reinterpret_cast<f4*>(xt + xq(p00 + 1, c4)) = o01;
+          *reinterpret_cast<f4*>(xt + xq(p00 + IW, c4)) = o10;
+          *reinterpret_cast<f4*>(xt + xq(p00 + IW + 1, c4)) = o11;
         }
       }
     } else {
@@ -842,7 +857,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
           const f4 bot = __builtin_elementwise_fma(lx1v, t11[k], lx0v * t10[k]);
           v = __builtin_elementwise_fma(ly1v, bot, ly0v * top);
         }
-        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = v;
+        *reinterpret_cast<f4*>(xt + xq(pix, c4)) = v;
       }
     }
     }
@@ -852,7 +867,8 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     // its x0 region -> LDS, then the stem's 3x3 s2 conv + ReLU6 -> xt, in the
     // same operation order as k_stem (bitwise the same activations).
     static_assert(MODE == MODE_IR_DIRECT && STRIDE == 1 && CIN == 16 && XP == 1, "stem fusion shape");
-    constexpr int IH = L.IH, XH = 2 * IH + 1, XW = 2 * IW + 1, XWP = XW + 1;
+    constexpr int IH = L.IH, XH = 2 * IH + 1, XW = 2 * IW + 1, XWP = stem_xwp(IW);
+    static_assert(XWP >= XW, "x0 row pitch");
     const StemParams& sp = p.stem;
     const int H = p.H, W = p.W;  // the stem's output = this block's input
     const uint8_t* fr = sp.frames + (long)n * sp.frame_stride;
@@ -862,9 +878,14 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     float* sbs = sws + 27 * 16;
     Staged<WIMG_F4> st_w;
     st_w.issue([&](int i) { return wsrc[i]; });
+    // the stem weights as [tap][16]: thread i loads w[channel i % 16][tap i / 16]
+    // (sp.w is [c][27]) and stores word i (consecutive banks, no transposing store)
     float wr[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) wr[u] = sp.w[min(tid + 256 * u, 27 * 16 - 1)];
+    for (int u = 0; u < 2; ++u) {
+      const int i = min(tid + 256 * u, 27 * 16 - 1);
+      wr[u] = sp.w[(i % 16) * 27 + i / 16];
+    }
     const float sb = sp.b[min(tid, 15)];
     // Each thread resizes two pixels of one row of the region, columns lx and
     // lx + HW2: the row's source rows, its weight and their byte offsets are
@@ -932,8 +953,8 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int i = tid + 256 * u;  // sp.w is [c][27]
-      if (i < 27 * 16) sws[(i % 27) * 16 + i / 27] = wr[u];
+      const int i = tid + 256 * u;
+      if (i < 27 * 16) sws[i] = wr[u];
     }
     if (tid < 16) sbs[tid] = sb;
     // start of the forward: zero this frame's decoder norm accumulators (the stem's job)
@@ -952,16 +973,27 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     // bitwise k_stem's), zero outside the image
     {
       const StemTaps taps = stem_taps<XH * XWP, XWP>(sws, r, g);
-      const float bias = sbs[r];
       // every pixel of the region first (the pixels past P_IN land in xt's
       // padding, which nothing reads); the stem pixels outside the image are
       // zeroed after, border only, in the tiles that have any (below)
-      for (int blk = wave; blk < P_IN_PAD / 16; blk += 4) {
-        const int pa = min(blk * 16 + r, P_IN - 1), py = pa / IW, px = pa - py * IW;
-        const f4 acc = stem_mfma(taps, x0s + 2 * py * XWP + 2 * px, bias);
-        const int p0 = blk * 16 + 4 * g;
+      if constexpr (VSS_SWZ) {
+        // transposed: lane (r, g) holds channels 4g..4g+3 of pixel r, one
+        // 16-B store into quad g of xt's quad-major planes
+        const f4 bias4 = *reinterpret_cast<const f4*>(sbs + 4 * g);
+        for (int blk = wave; blk < P_IN_PAD / 16; blk += 4) {
+          const int pa = min(blk * 16 + r, P_IN - 1), py = pa / IW, px = pa - py * IW;
+          const f4 acc = stem_mfma_t(taps, x0s + 2 * py * XWP + 2 * px, bias4);
+          *reinterpret_cast<f4*>(xt + xq(blk * 16 + r, g)) = relu6v(acc);
+        }
+      } else {
+        const float bias = sbs[r];
+        for (int blk = wave; blk < P_IN_PAD / 16; blk += 4) {
+          const int pa = min(blk * 16 + r, P_IN - 1), py = pa / IW, px = pa - py * IW;
+          const f4 acc = stem_mfma(taps, x0s + 2 * py * XWP + 2 * px, bias);
+          const int p0 = blk * 16 + 4 * g;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) xt[(p0 + i) * XS + r] = relu6f(acc[i]);  // D[pixel 4g+i][channel r]
+          for (int i = 0; i < 4; ++i) xt[xq(p0 + i, r >> 2) + (r & 3)] = relu6f(acc[i]);  // D[pixel 4g+i][channel r]
+        }
       }
       // a tile at the image's edge: its pixels outside the image (the halo
       // row / column, and a partial tile's columns / rows past the image) are
@@ -971,10 +1003,11 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       if (!interior) {
         __syncthreads();
         for (int i = tid; i < P_IN * 4; i += 256) {
-          const int q = i & 3, e = i >> 2, qy = e / IW, qx = e - qy * IW;
+          // (quad-major: consecutive threads take consecutive pixels of one plane)
+          const int q = L.XQM ? i / P_IN : i & 3, e = L.XQM ? i - q * P_IN : i >> 2, qy = e / IW, qx = e - qy * IW;
           const int yy = iy0 + qy, xx = ix0 + qx;
           if (yy < 0 || yy >= H || xx < 0 || xx >= W)
-            *reinterpret_cast<f4*>(xt + (qy * IW + qx) * XS + 4 * q) = f4{0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<f4*>(xt + xq(qy * IW + qx, q)) = f4{0.f, 0.f, 0.f, 0.f};
         }
       }
     }
@@ -1004,17 +1037,17 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         // no validity test: an expand layer's input pixels outside the image
         // only feed hidden pixels that the expand loop zeroes (its clamp
         // limit is 0 there), and the loads were clamped to real pixels
-        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = to_operand<PREC>(v);
+        *reinterpret_cast<f4*>(xt + xq(pix, c4)) = to_operand<PREC>(v);
         if constexpr (RES) {
           const int py = pix / IW, px = pix - py * IW;
           if (py >= 1 && py <= TH && px >= 1 && px <= TW)
-            *reinterpret_cast<f4*>(smem + L.xr + ((py - 1) * TW + px - 1) * CIN + 4 * c4) = v;
+            *reinterpret_cast<f4*>(smem + L.xr + rq((py - 1) * TW + px - 1, c4)) = v;
         }
       } else {
         const int py = pix / IW, px = pix % IW;
         const int yy = iy0 + py, xx = ix0 + px;
         const bool valid = pix < P_IN && yy >= 0 && yy < H && xx >= 0 && xx < W;
-        *reinterpret_cast<f4*>(xt + pix * XS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(xt + xq(pix, c4)) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
       }
     });
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
@@ -1039,7 +1072,13 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 
   if constexpr (MODE == MODE_IR_EXPAND) {
     constexpr int HSD = hid_stride(STRIDE);
-    float* hid = work + wave * P_IN_PAD * HSD;
+    // the wave's hidden chunk: quad-major planes of L.HPL floats (VSS_SWZ), or
+    // pixel-major with HSD floats per pixel
+    float* hid = work + wave * (L.HPL ? 4 * L.HPL : P_IN_PAD * HSD);
+    auto hq = [&](int pix, int q) {
+      if constexpr (L.HPL != 0) return q * L.HPL + 4 * pix;
+      else return pix * HSD + 4 * q;
+    };
     constexpr int NK = CIN / 16;
     constexpr int NCBI = P_IN_PAD / 16;
     static_assert(NCBI <= 32, "one validity bit per input pixel block");
@@ -1074,8 +1113,8 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         const int pix = cb * 16 + r;
         f4 d = bias;  // the expand's bias enters as the MFMA accumulator
 #pragma unroll
-        for (int s = 0; s < NK; ++s) d = mma16_op<PREC>(d, aw[s], *reinterpret_cast<const f4*>(xt + pix * XS + 16 * s + 4 * g));
-        *reinterpret_cast<f4*>(hid + pix * HSD + 4 * g) = clampv(d, (vmask >> cb) & 1u ? 6.f : 0.f);
+        for (int s = 0; s < NK; ++s) d = mma16_op<PREC>(d, aw[s], *reinterpret_cast<const f4*>(xt + xq(pix, 4 * s + g)));
+        *reinterpret_cast<f4*>(hid + hq(pix, g)) = clampv(d, (vmask >> cb) & 1u ? 6.f : 0.f);
       }
       wave_sync();
       // dw 3x3 computed straight into the project MFMA's B layout: lane (r, g)
@@ -1100,7 +1139,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
             f4 t[NT];
 #pragma unroll
             for (int u = 0; u < NT; ++u)
-              t[u] = *reinterpret_cast<const f4*>(hid + ((STRIDE * ly + ky) * IW + STRIDE * lx0 + u) * HSD + 4 * g);
+              t[u] = *reinterpret_cast<const f4*>(hid + hq((STRIDE * ly + ky) * IW + STRIDE * lx0 + u, g));
 #pragma unroll
             for (int j = 0; j < XR; ++j)
 #pragma unroll
@@ -1152,7 +1191,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
           f4 t[XR + 2];
 #pragma unroll
           for (int u = 0; u < XR + 2; ++u)
-            t[u] = *reinterpret_cast<const f4*>(xt + ((ly + ky) * IW + lx0 + u) * XS + c0 + 4 * g);
+            t[u] = *reinterpret_cast<const f4*>(xt + xq((ly + ky) * IW + lx0 + u, (c0 >> 2) + g));
 #pragma unroll
           for (int j = 0; j < XR; ++j)
 #pragma unroll
@@ -1195,7 +1234,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
           f4 v = acc[(q * XR + j) * NCB + cb] + *reinterpret_cast<const f4*>(b2s + cb * 16 + 4 * g);
-          if constexpr (RES) v = v + *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + cb * 16 + 4 * g);
+          if constexpr (RES) v = v + *reinterpret_cast<const f4*>(xt + xq((ly + 1) * IW + lx + 1, cb * 4 + g));
           if (oy < Ho && ox < Wo) gy.st(((long)oy * Wo + ox) * COUT + cb * 16 + 4 * g, v);
         }
       }
@@ -1203,14 +1242,13 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
   __syncthreads();  // every wave is done with its scratch (reused as slabs)
   VSS_STAMP(2);
   {
-    float* slab = slabs + cw * SS;
 #pragma unroll
     for (int q = 0; q < NPBW / XR; ++q)
 #pragma unroll
       for (int j = 0; j < XR; ++j)
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb)
-          *reinterpret_cast<f4*>(slab + run_pix(pw + q * PW, j) * RS + cb * 16 + 4 * g) = acc[(q * XR + j) * NCB + cb];
+          *reinterpret_cast<f4*>(slabs + sq(cw, run_pix(pw + q * PW, j), cb * 4 + g)) = acc[(q * XR + j) * NCB + cb];
   }
   __syncthreads();
   constexpr int C4O = COUT / 4, NOUT = (P_OUT * C4O + 255) / 256;
@@ -1227,21 +1265,21 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       const int oy = oy0 + ly, ox = ox0 + lx;
       const bool valid = oy < Ho && ox < Wo;
       // slabs of the CS waves that own this pixel block, summed in wave order
-      f4 v = *reinterpret_cast<const f4*>(slabs + pix * RS + 4 * c4);
+      f4 v = *reinterpret_cast<const f4*>(slabs + sq(0, pix, c4));
 #pragma unroll
-      for (int s = 1; s < CS; ++s) v = v + *reinterpret_cast<const f4*>(slabs + s * SS + pix * RS + 4 * c4);
+      for (int s = 1; s < CS; ++s) v = v + *reinterpret_cast<const f4*>(slabs + sq(s, pix, c4));
       if (KS == 1 || ks == 0) {  // bias and residual belong to part 0
         v = v + *reinterpret_cast<const f4*>(b2s + 4 * c4);
         if constexpr (RES) {
           if constexpr (MODE == MODE_IR_EXPAND)
-            v = v + *reinterpret_cast<const f4*>(smem + L.xr + pix * CIN + 4 * c4);
+            v = v + *reinterpret_cast<const f4*>(smem + L.xr + rq(pix, c4));
           else
-            v = v + *reinterpret_cast<const f4*>(xt + ((ly + 1) * IW + lx + 1) * XS + 4 * c4);
+            v = v + *reinterpret_cast<const f4*>(xt + xq((ly + 1) * IW + lx + 1, c4));
         }
       }
       if constexpr (MODE == MODE_DEC) {
         outv[k] = v;
-        *reinterpret_cast<f4*>(slabs + pix * RS + 4 * c4) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(slabs + sq(0, pix, c4)) = valid ? v : f4{0.f, 0.f, 0.f, 0.f};
       } else if (valid) {
         gy.st(((long)oy * Wo + ox) * COUT + 4 * c4, v);
       }
@@ -1274,7 +1312,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 #pragma unroll
       for (int pix = 0; pix < P_OUT; pix += G) {
         if (pix + gg < P_OUT) {
-          const float v = slabs[(pix + gg) * RS + c];
+          const float v = slabs[sq(0, pix + gg, c >> 2) + (c & 3)];
           s += (double)__builtin_rintf(v * 0x1p32f);
           q += (double)__builtin_rintf(v * v * 0x1p24f);
         }
@@ -1288,7 +1326,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         qi = 0;
         for (int pix = 0; pix < P_OUT; pix += G) {
           if (pix + gg < P_OUT) {
-            const float v = slabs[(pix + gg) * RS + c];
+            const float v = slabs[sq(0, pix + gg, c >> 2) + (c & 3)];
             si += (long long)__builtin_rintf(v * 0x1p32f);
             qi += (long long)__builtin_rintf(v * v * 0x1p24f);
           }
@@ -1329,7 +1367,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       const int yy = oy0 + pix / TW, xx = ox0 + pix % TW;
       if (yy < p.H && xx < p.W)
         gst.st(((long)yy * p.W + xx) * 16 + 4 * q,
-               *reinterpret_cast<const f4*>(xt + ((pix / TW + 1) * IW + pix % TW + 1) * XS + 4 * q));
+               *reinterpret_cast<const f4*>(xt + xq((pix / TW + 1) * IW + pix % TW + 1, q)));
     }
   }
   VSS_STAMP(3);

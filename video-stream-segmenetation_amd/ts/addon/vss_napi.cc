@@ -459,11 +459,32 @@ struct QueuedWork {
   vss_ticket ticket = 0;
   size_t out_count = 0;
   int rc = 0;
-  std::string err;
+  std::string err, what = "vss_wait";
+  // segment(): the submit itself (its staging copy of the frames into pinned
+  // memory) runs here on the worker too, not on the JS thread; the frames'
+  // arrays are referenced until the batch is done
+  bool submit = false;
+  std::vector<const uint8_t*> list;
+  const uint8_t* contiguous = nullptr;
+  int n = 0, height = 0, width = 0, channels = 0, out_mode = VSS_OUT_MODEL;
+  size_t rs = 0;
+  float* out = nullptr;
+  std::vector<napi_ref> frame_refs;
 };
 
 void QueuedExecute(napi_env, void* data) {  // libuv worker thread: no JS calls here
   QueuedWork* w = static_cast<QueuedWork*>(data);
+  if (w->submit) {
+    w->rc = !w->list.empty() ? vss_submit_list(w->h, w->list.data(), w->n, w->height, w->width, w->channels, w->rs,
+                                               w->out, w->out_mode, &w->ticket)
+                             : vss_submit(w->h, w->contiguous, w->n, w->height, w->width, w->channels, w->rs, w->out,
+                                          w->out_mode, &w->ticket);
+    if (w->rc != VSS_OK) {
+      w->what = "vss_submit";
+      w->err = vss_last_error(w->h);
+      return;
+    }
+  }
   w->rc = vss_wait(w->h, w->ticket);
   if (w->rc != VSS_OK) w->err = vss_last_error(w->h);
 }
@@ -485,9 +506,10 @@ void QueuedComplete(napi_env env, napi_status, void* data) {
     napi_create_typedarray(env, napi_float32_array, w->out_count, ab, 0, &arr);
     napi_resolve_deferred(env, w->deferred, arr);
   } else {
-    napi_reject_deferred(env, w->deferred, make_error(env, "vss_wait", w->rc, w->err));
+    napi_reject_deferred(env, w->deferred, make_error(env, w->what, w->rc, w->err));
   }
   napi_delete_reference(env, w->out_ref);
+  for (napi_ref r : w->frame_refs) napi_delete_reference(env, r);
   napi_delete_async_work(env, w->work);
   Handle* hd = w->hd;
   delete w;
@@ -686,6 +708,50 @@ napi_value Segment(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
+  // The submit — whose staging copy of the frames into the slot's pinned
+  // memory is most of its cost (3.7 MB per VGA batch of 8) — runs on the
+  // libuv worker with the wait, so the JS thread only enqueues: the frames'
+  // arrays are referenced until the batch is done, and the caller must not
+  // modify them before the promise settles (ts/segment.ts).  Opt-out
+  // VSS_NAPI_SYNC_STAGE=1: staged here, on the JS thread, before this returns
+  // (the round-4 behaviour: frames reusable at once).
+  static const bool sync_stage = [] {
+    const char* e = std::getenv("VSS_NAPI_SYNC_STAGE");
+    return e && e[0] == '1';
+  }();
+  if (!sync_stage) {
+    w->submit = true;
+    w->list = std::move(list);
+    w->contiguous = contiguous;
+    w->n = n;
+    w->height = height;
+    w->width = width;
+    w->channels = channels;
+    w->rs = (size_t)rs;
+    w->out = static_cast<float*>(out);
+    w->out_mode = out_mode;
+    if (is_arr) {
+      for (uint32_t i = 0; i < (uint32_t)n; ++i) {
+        napi_value v;
+        napi_ref r;
+        napi_get_element(env, argv[1], i, &v);
+        NAPI_OK(env, napi_create_reference(env, v, 1, &r));
+        w->frame_refs.push_back(r);
+      }
+    } else {
+      napi_ref r;
+      NAPI_OK(env, napi_create_reference(env, argv[1], 1, &r));
+      w->frame_refs.push_back(r);
+    }
+    napi_create_reference(env, ab, 1, &w->out_ref);
+    napi_value name;
+    napi_create_string_utf8(env, "vss_submit", NAPI_AUTO_LENGTH, &name);
+    NAPI_OK(env, napi_create_async_work(env, nullptr, name, QueuedExecute, QueuedComplete, w, &w->work));
+    NAPI_OK(env, napi_queue_async_work(env, w->work));
+    w->hd = hd;
+    ++hd->pending;
+    return promise;
+  }
   // staged here: the frames may be reused by the caller as soon as this returns
   const int rc = is_arr ? vss_submit_list(hd->h, list.data(), n, height, width, channels, (size_t)rs,
                                           static_cast<float*>(out), out_mode, &w->ticket)
