@@ -113,6 +113,10 @@ int vso_launch_count(const vso_session* s);
 int vso_launch_name(const vso_session* s, int k, char* buf, int cap);
 /* Convolutions planned on the LDS-tiled MFMA kernel (k_conv_tile). */
 int vso_tile_conv_count(const vso_session* s);
+/* Inverted residual blocks (1x1 expand -> Clip -> 3x3 depthwise -> Clip -> 1x1
+ * project [-> + input]) the session runs as one k_ir launch each (MODNet's
+ * MobileNetV2 backbone); VSO_IR=0 plans them as three launches. */
+int vso_ir_block_count(const vso_session* s);
 
 #ifdef __cplusplus
 }

@@ -440,6 +440,39 @@ def conv_up():
                    [(a, [2, 24, 18, 34]), (c, [2, 16, 22, 26]), (d, [2, 70, 22, 26])])
 
 
+def ir_chain():
+    """MobileNetV2 inverted residuals (1x1 expand -> Clip -> 3x3 depthwise ->
+    Clip -> 1x1 project [+ input]) of every k_ir form (vso_ir.hip): stride 1
+    with the residual, stride 2, widening stride-1 blocks, on an odd-sized
+    batch-2 input (edge tiles, a partial last tile row) whose deep blocks have
+    few tiles, so the hidden channels split over workgroups (ks > 1) — and a
+    block whose project output is also a graph output (still fused: the Add's
+    input is kept)."""
+    b = Builder(13)
+    one = lambda: b.const(np.array(0, np.float32))
+    six = lambda: b.const(np.array(6, np.float32))
+
+    def ir(t, cin, cout, stride, e=6):
+        hd = cin * e
+        u = b.op("Clip", [b.conv(t, cin, hd, 1), one(), six()])
+        u = b.op("Clip", [b.conv(u, hd, hd, 3, stride=stride, group=hd), one(), six()])
+        o = b.conv(u, hd, cout, 1)
+        return b.op("Add", [o, t]) if stride == 1 and cin == cout else o
+
+    t = ir("x", 16, 24, 2)          # 38x67 -> 19x34
+    t = ir(t, 24, 24, 1)
+    t = ir(t, 24, 32, 2)            # -> 10x17
+    t = ir(t, 32, 32, 1)
+    t = ir(t, 32, 64, 2)            # -> 5x9
+    t = ir(t, 64, 64, 1)
+    t = ir(t, 64, 96, 1)
+    t = ir(t, 96, 96, 1)
+    t2 = ir(t, 96, 160, 2)          # -> 3x5
+    t3 = ir(t2, 160, 160, 1)
+    t4 = ir(t3, 160, 320, 1)
+    return b.model([("x", [2, 16, 38, 67])], [(t, [2, 96, 5, 9]), (t4, [2, 320, 3, 5])])
+
+
 def conv_up_thin():
     """A pending 2x Resize through an in-place Concat into a thin 1x1 head
     (<= 4 outputs, k_conv_thin: computes no upsample itself), so the planner

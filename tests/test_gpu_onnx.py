@@ -164,6 +164,62 @@ def test_conv_upsample_fusion(ort, precision):
         assert np.array_equal(got[k], again[k])
 
 
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_inverted_residuals_fused(ort, precision):
+    """Every MobileNetV2 inverted residual of ir_chain as one k_ir launch
+    (vso_ir.hip), against the f64 oracle at the f32 bar (1e-4 of the output
+    scale): f32 arithmetic in every session precision (the 1x1 / depthwise
+    convolutions are not k_conv_tile ones, and the oracle rounds none of
+    them); and bitwise the same on a second run (the hidden-channel slices
+    are summed in a fixed order)."""
+    data = M.ir_chain()
+    feeds = {"x": np.random.default_rng(14).standard_normal((2, 16, 38, 67)).astype(np.float32)}
+    want = R.run(R.load(data), feeds, conv_operands=None if precision == "f32" else precision)
+    with ort.InferenceSession(data, precision=precision) as s:
+        got = s.run(feeds)
+        again = s.run(feeds)
+        names = s.launches()
+        assert s.ir_blocks() == 11, names
+    assert sum("k_ir<" in n for n in names) == 11, names
+    assert not any("k_conv_dw" in n or "k_conv_small" in n for n in names), names
+    for k, w in want.items():
+        err = float(np.abs(got[k] - w).max())
+        scale = max(1.0, float(np.abs(w).max()))
+        print(f"ir_chain {precision} {k}: max abs err {err:.3e} (scale {scale:.2f})")
+        assert err <= TOL * scale, (k, err)
+        assert np.array_equal(got[k], again[k])
+
+
+def test_inverted_residuals_unfused_knob(ort):
+    """VSO_IR=0 (read at the first plan of a process) is exercised in a child
+    process: the same graph as three launches per block, equal within the f32
+    bar to the fused plan."""
+    import subprocess
+    import sys
+    code = ("import numpy as np, sys; sys.path.insert(0, 'tests'); import onnx_models as M; "
+            "import importlib.util, os; spec = importlib.util.spec_from_file_location('vss_amd', "
+            "'video-stream-segmenetation_amd/__init__.py', submodule_search_locations=['video-stream-segmenetation_amd']); "
+            "m = importlib.util.module_from_spec(spec); sys.modules['vss_amd'] = m; spec.loader.exec_module(m); "
+            "import vss_amd.ort as o; d = M.ir_chain(); "
+            "x = np.random.default_rng(14).standard_normal((2, 16, 38, 67)).astype(np.float32); "
+            "s = o.InferenceSession(d); r = s.run({'x': x}); "
+            "print(s.ir_blocks(), sum('k_ir<' in n for n in s.launches())); "
+            "np.save('gpurun_out/ir_unfused.npy', np.concatenate([v.ravel() for v in r.values()]))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, VSO_IR="0"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split()[-2:] == ["0", "0"], r.stdout
+    data = M.ir_chain()
+    x = np.random.default_rng(14).standard_normal((2, 16, 38, 67)).astype(np.float32)
+    with ort.InferenceSession(data) as s:
+        fused = np.concatenate([v.ravel() for v in s.run({"x": x}).values()])
+    unfused = np.load(os.path.join(root, "gpurun_out", "ir_unfused.npy"))
+    scale = max(1.0, float(np.abs(unfused).max()))
+    assert float(np.abs(fused - unfused).max()) <= TOL * scale
+
+
 @pytest.mark.parametrize("precision", ["bf16", "f16", "f32"])
 def test_conv_up_into_thin_head(ort, precision):
     """Resize -> Concat -> 1x1 head of 3 outputs: the thin head launches the

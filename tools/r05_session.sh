@@ -19,6 +19,18 @@ echo "== smoke"
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1; rc=$?
 tail -1 gpurun_out/${TAG}_smoke.log; fatal $rc
 fi
+if [ "${ONNX:-0}" = 1 ]; then
+  echo "== ONNX: fused inverted residuals, MODNet parity prints"
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_onnx.py -m gpu -s -q --timeout 200 --timeout-method thread \
+    -k "modnet_topology or inverted or conv_up or synthetic" > gpurun_out/${TAG}_onnx.log 2>&1; rc=$?
+  tail -2 gpurun_out/${TAG}_onnx.log; grep -E "^(FAILED|ERROR)|max abs err|oracle" gpurun_out/${TAG}_onnx.log | cut -c1-200 | head -40; fatal $rc
+  for k in 1 2; do
+    for ir in 1 0; do
+      VSO_IR=$ir timeout -k 10 200 python tools/bench_onnx.py --only-modnet --batch 8 --iters 50 > gpurun_out/${TAG}_modnet_ir$ir.log 2>&1; rc=$?
+      echo "VSO_IR=$ir: $(grep -h '^{' gpurun_out/${TAG}_modnet_ir$ir.log | grep b8_bf16 | cut -c1-160)"; fatal $rc
+    done
+  done
+fi
 if [ -n "${AB_LIBS:-}" ]; then
   echo "== A/B vs $AB_LIBS"
   timeout -k 10 600 bash tools/ab_quick.sh ${AB_ROUNDS:-3} $AB_LIBS; fatal $?

@@ -1,0 +1,299 @@
+// vso_ir.hip — a MobileNetV2 inverted residual block of an ONNX session in ONE
+// launch: 1x1 expand + Clip(ReLU6) -> 3x3 depthwise (stride 1 / 2) + Clip ->
+// 1x1 project (+ the block's input as residual).  MODNet's backbone is eleven
+// of them at /4../32 (tests/onnx_models.py modnet(); the reference runs that
+// topology as model_q4f16.onnx, frameProcessorTest.ts:91, model.ts:12-29).
+// As three launches (k_conv_pw, k_conv_dw_plane, k_conv_small) each block
+// wrote its expanded tensor (6x the channels) to HBM and read it back twice,
+// and the deep /16 - /32 blocks ran as a few dozen latency-bound workgroups:
+// 38-57 us per block at batch 8, 288x512 (profiles/r04q).
+//
+// The seam's fused block (csrc/vss_kernels.hip k_block) on the session's NCHW
+// f32 tensors: a workgroup owns a 4 x 16 output tile, all output channels and
+// a slice of the hidden channels (KS slices per tile when the image has few
+// tiles: the partial tiles meet in the last-arriving workgroup, in slice
+// order — k_conv_tile's split-K protocol, deterministic).  Prologue: the input
+// region (tile + halo) for every input channel, staged in LDS as [c][pixel]
+// (rows 4 mod 8 floats apart: the MFMA B reads of lanes (r, g), rows 4g
+// apart, fall on complementary banks).  Per 16 hidden channels ("chunk"):
+//   expand  — the region's 16-pixel blocks dealt to the 4 waves,
+//             v_mfma_f32_16x16x4_f32 (exact f32 products, as k_conv_pw): D =
+//             W1[chunk][c] x X[c][pixel], bias as the C operand, clip, zero
+//             outside the image (the depthwise's padding), stored as four
+//             quad-major planes (vss_kernels.h: conflict-free 16-B reads of
+//             16-pixel runs; stride 2: planes one quad apart) — double
+//             buffered, one workgroup barrier per chunk;
+//   dw      — wave w computes output row w of the tile: lane (r, g) = pixel r,
+//             channels 4g..4g+3, 9 taps in (ky, kx) order + bias + clip, in
+//             registers in the project MFMA's B layout;
+//   project — 4 MFMAs per 16 output channels (A = W2[out][chunk]), acc in
+//             registers across the chunks.
+// Weights are read from L2 per chunk, the depthwise / project ones in flight
+// during the expand, the next chunk's expand ones during the dw / project.
+// Every operand stays f32 in every session precision (the convolutions here
+// are 1x1 / grouped: onnx_ref.tiled_conv() rounds none of them either).
+#include <hip/hip_runtime.h>
+
+#include "vso_device.h"
+#include "vso_kernels.h"
+
+namespace vso {
+
+template <int S, int TH>
+struct IrGeom {
+  static constexpr int TW = 16;
+  static constexpr int IH = S == 2 ? 2 * TH + 1 : TH + 2, IW = S == 2 ? 2 * TW + 1 : TW + 2;
+  static constexpr int P_IN = IH * IW, NBI = (P_IN + 15) / 16, P_PAD = NBI * 16;
+  static constexpr int HQ = P_PAD + (S == 2 ? 1 : 0);  // quads per hidden plane
+};
+
+template <int NT, int NCB, int S, int TH>
+__global__ __launch_bounds__(256) void k_ir(IrParams p) {
+  using G = IrGeom<S, TH>;
+  constexpr int TW = G::TW, IW = G::IW, P_IN = G::P_IN, NBI = G::NBI, HQ = G::HQ;
+  static_assert(TH <= 4, "one output row per wave");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int CIN = p.CIN, HID = p.HID, COUT = p.COUT, PSTR = p.pstr, H = p.H, W = p.W;
+  float* xs = smem;                   // [CIN][PSTR]
+  float* hbuf = smem + CIN * PSTR;    // 2 x [4 planes][HQ][4]
+  const int t = blockIdx.x, ks = blockIdx.y, n = blockIdx.z;
+  const int ty = t / p.tiles_x, tx = t - ty * p.tiles_x;
+  const int oy0 = ty * TH, ox0 = tx * TW, iy0 = S * oy0 - 1, ix0 = S * ox0 - 1;
+
+  // ---- prologue: the input region, 8 loads in flight per thread ----
+  {
+    const float* xn = p.x + (long)n * CIN * H * W;
+    const int total = CIN * P_IN;
+    constexpr int U = 8;
+    for (int b0 = 0; b0 < total; b0 += 256 * U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(b0 + tid + 256 * u, total - 1);
+        const int c = i / P_IN, q = i - c * P_IN, ly = q / IW, lx = q - ly * IW;
+        const int gy = iy0 + ly, gx = ix0 + lx;
+        const bool in = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+        const float x = xn[c * H * W + (in ? gy * W + gx : 0)];
+        v[u] = in ? x : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = b0 + tid + 256 * u;
+        if (i < total) {
+          const int c = i / P_IN;
+          xs[c * PSTR + i - c * P_IN] = v[u];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  const int nch = HID / 16, c0 = ks * p.cps, c1 = min(c0 + p.cps, nch);
+  const bool outw = wave < TH;
+  // expand A fragments of chunk c: lane (r, g), MFMA 4u + e takes
+  // W1[16c + r][16u + 4g + e] (one float4 per u; zero past CIN)
+  f4 a1[NT];
+  auto load_a1 = [&](int c) {
+    const float* wr = p.w1 + (long)(c * 16 + r) * CIN;
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      const int k = 16 * u + 4 * g;
+      const f4 w = *reinterpret_cast<const f4*>(wr + min(k, CIN - 4));
+      a1[u] = k < CIN ? w : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  f4 acc[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) acc[cb] = f4{0.f, 0.f, 0.f, 0.f};
+  if (c0 < c1) load_a1(c0);
+  for (int c = c0; c < c1; ++c) {
+    float* hid = hbuf + ((c - c0) & 1) * (16 * HQ);
+    const int h0 = c * 16;
+    // this chunk's depthwise and project weights: in flight during the expand
+    const f4 b1v = *reinterpret_cast<const f4*>(p.b1 + h0 + 4 * g);
+    f4 wd[9], bd = f4{0.f, 0.f, 0.f, 0.f}, a2[NCB];
+    if (outw) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) wd[k] = *reinterpret_cast<const f4*>(p.wdw + k * HID + h0 + 4 * g);
+      bd = *reinterpret_cast<const f4*>(p.bdw + h0 + 4 * g);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int m = cb * 16 + r;
+        const f4 w = *reinterpret_cast<const f4*>(p.w2 + (long)min(m, COUT - 1) * HID + h0 + 4 * g);
+        a2[cb] = m < COUT ? w : f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    // expand: D[hidden 4g + i][pixel r] of the region's 16-pixel blocks
+    for (int pb = wave; pb < NBI; pb += 4) {
+      f4 d = b1v;
+      const float* xb = xs + pb * 16 + r;
+#pragma unroll
+      for (int u = 0; u < NT; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = min(16 * u + 4 * g + e, CIN - 1);  // (past CIN: weight 0, a finite value)
+          d = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u][e], xb[k * PSTR], d, 0, 0, 0);
+        }
+      const int pix = pb * 16 + r, ly = pix / IW, lx = pix - ly * IW;
+      const bool in = pix < P_IN && (unsigned)(iy0 + ly) < (unsigned)H && (unsigned)(ix0 + lx) < (unsigned)W;
+      f4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = in ? fminf(fmaxf(d[i], p.lo1), p.hi1) : 0.f;
+      *reinterpret_cast<f4*>(hid + (g * HQ + pix) * 4) = v;
+    }
+    __syncthreads();
+    if (c + 1 < c1) load_a1(c + 1);  // the next chunk's expand fragments, in flight during the dw / project
+    if (outw) {
+      // depthwise at output (oy0 + wave, ox0 + r), channels h0 + 4g .. + 3
+      f4 a = bd;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int rp = (S * wave + ky) * IW + S * r + kx;
+          a = __builtin_elementwise_fma(wd[ky * 3 + kx], *reinterpret_cast<const f4*>(hid + (g * HQ + rp) * 4), a);
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = fminf(fmaxf(a[i], p.lo2), p.hi2);
+      // project: D[out cb*16 + 4g + v][pixel r] += W2[out][h0 + 4g' + j] x dw[h0 + 4g' + j][pixel r]
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[cb][j], a[j], acc[cb], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue ----
+  if (p.ks > 1) {
+    // the partial tile ([blk][slice][wave][cb][lane] as f4), write-through
+    // 8-byte agent-scope stores; the last slice to arrive (any XCD) sums the
+    // slices in order with sc1 loads (k_conv_tile's protocol, vso_conv.hip)
+    const long blk = (long)n * p.tiles + t;
+    if (outw) {
+      uint64_t* part = reinterpret_cast<uint64_t*>(p.part) + ((blk * p.ks + ks) * 4 + wave) * (NCB * 64 * 2);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const uint64_t lo = (uint64_t)__float_as_uint(acc[cb][0]) | ((uint64_t)__float_as_uint(acc[cb][1]) << 32);
+        const uint64_t hi = (uint64_t)__float_as_uint(acc[cb][2]) | ((uint64_t)__float_as_uint(acc[cb][3]) << 32);
+        uint64_t* q = part + (cb * 64 + lane) * 2;
+        __hip_atomic_store(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __shared__ int last;
+    __syncthreads();
+    if (tid == 0) {
+      int* cnt = p.counters + blk;
+      const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == p.ks - 1;
+      if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next run
+    }
+    __syncthreads();
+    if (!last || !outw) return;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint64_t* base = reinterpret_cast<const uint64_t*>(p.part) + (blk * p.ks * 4 + wave) * (NCB * 64 * 2);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < p.ks; k0 += 8) {  // 8 slices' loads in flight, summed in slice order
+        uint64_t lo[8], hi[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (k0 + u < p.ks) {
+            const uint64_t* q = base + ((long)(k0 + u) * 4 * NCB * 64 + cb * 64 + lane) * 2;
+            lo[u] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi[u] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (k0 + u < p.ks)
+            sum += f4{__uint_as_float((uint32_t)lo[u]), __uint_as_float((uint32_t)(lo[u] >> 32)),
+                      __uint_as_float((uint32_t)hi[u]), __uint_as_float((uint32_t)(hi[u] >> 32))};
+      }
+      acc[cb] = sum;
+    }
+  }
+  if (!outw) return;
+  const int oy = oy0 + wave, ox = ox0 + r;
+  if (oy >= p.Ho || ox >= p.Wo) return;
+  const long plane = (long)p.Ho * p.Wo;
+  float* yn = p.y + (long)n * ((long)COUT * plane + p.y_nx) + (long)oy * p.Wo + ox;
+  const int centre = (wave + 1) * IW + r + 1;  // stride 1: the output pixel in the staged region
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int ch = cb * 16 + 4 * g + v;
+      if (ch < COUT) {
+        float o = acc[cb][v] + p.b2[ch];
+        if (p.res) o += xs[ch * PSTR + centre];
+        yn[ch * plane] = o;
+      }
+    }
+}
+
+// ---- host side ----
+namespace {
+struct IrEntry {
+  int nt, ncb, s, th;
+  void (*fn)(IrParams);
+  const char* name;
+};
+#define VSO_IR(NT, NCB, S, TH) {NT, NCB, S, TH, k_ir<NT, NCB, S, TH>, "vso::k_ir<" #NT ", " #NCB ", " #S ", " #TH ">"},
+// MobileNetV2 1.0's blocks (t = 6): input channels / 16 (rounded up), output
+// channels / 16 (rounded up), stride — 16->24 s2, 24->24, 24->32 s2, 32->32,
+// 32->64 s2, 64->64, 64->96, 96->96, 96->160 s2, 160->160, 160->320
+const IrEntry kIr[] = {
+    VSO_IR(1, 2, 2, 4) VSO_IR(2, 2, 1, 4) VSO_IR(2, 2, 2, 4) VSO_IR(2, 4, 2, 4) VSO_IR(4, 4, 1, 4)
+    VSO_IR(4, 6, 1, 4) VSO_IR(6, 6, 1, 4) VSO_IR(6, 10, 2, 4) VSO_IR(10, 10, 1, 4) VSO_IR(10, 20, 1, 4)
+    VSO_IR(4, 4, 2, 4) VSO_IR(6, 6, 2, 4)};
+#undef VSO_IR
+
+const IrEntry* ir_entry(const IrParams& p) {
+  const int nt = (p.CIN + 15) / 16, ncb = (p.COUT + 15) / 16;
+  for (const IrEntry& e : kIr)
+    if (e.nt == nt && e.ncb == ncb && e.s == p.stride && e.th == kIrTH) return &e;
+  return nullptr;
+}
+}  // namespace
+
+int ir_pstr(int stride) {
+  const int pad = stride == 2 ? IrGeom<2, kIrTH>::P_PAD : IrGeom<1, kIrTH>::P_PAD;
+  int v = pad;
+  while (v % 8 != 4) ++v;
+  return v;
+}
+
+size_t ir_lds_bytes(int cin, int stride) {
+  const int hq = stride == 2 ? IrGeom<2, kIrTH>::HQ : IrGeom<1, kIrTH>::HQ;
+  return ((size_t)cin * ir_pstr(stride) + 2 * 16 * (size_t)hq) * 4;
+}
+
+void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles) {
+  *tiles_x = (Wo + 15) / 16;
+  *tiles = *tiles_x * ((Ho + kIrTH - 1) / kIrTH);
+}
+
+bool ir_supported(const IrParams& p) {
+  return p.CIN % 4 == 0 && p.HID % 16 == 0 && (p.stride == 1 || p.stride == 2) && ir_entry(p) != nullptr &&
+         ir_lds_bytes(p.CIN, p.stride) <= 160 * 1024 && (!p.res || (p.stride == 1 && p.CIN == p.COUT));
+}
+
+const char* ir_kernel_name(const IrParams& p) {
+  const IrEntry* e = ir_entry(p);
+  return e ? e->name : "vso::k_ir<?>";
+}
+
+void launch_ir(const IrParams& p, hipStream_t s) {
+  const IrEntry* e = ir_entry(p);
+  if (!e) return;
+  const size_t lds = ir_lds_bytes(p.CIN, p.stride);
+  (void)hipFuncSetAttribute((const void*)e->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(e->fn, dim3(p.tiles, p.ks, p.N), dim3(256), lds, s, p);
+}
+
+}  // namespace vso

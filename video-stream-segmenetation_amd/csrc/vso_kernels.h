@@ -195,6 +195,37 @@ struct GemmParams {  // y[b][m][n] = alpha * sum_k A[b][m][k] B[b][k][n] + beta 
   Epilogue ep;         // act only
 };
 
+// A MobileNetV2 inverted residual block — 1x1 expand + Clip -> 3x3 depthwise
+// (stride 1 / 2) + Clip -> 1x1 project (+ the block input) — in one launch
+// (vso_ir.hip, k_ir): output tiles of kIrTH x 16 pixels, all output channels,
+// a slice of the hidden channels per workgroup (ks slices of cps 16-channel
+// chunks, the partial tiles summed in slice order by the last to arrive).
+constexpr int kIrTH = 4;
+struct IrParams {
+  const float* x;     // [N][CIN][H][W]
+  const float* w1;    // [HID][CIN], b1 [HID]: expand, then clip to [lo1, hi1]
+  const float* b1;
+  const float* wdw;   // [9][HID] (tap-major), bdw [HID]: depthwise, then clip to [lo2, hi2]
+  const float* bdw;
+  const float* w2;    // [COUT][HID], b2 [COUT]: project
+  const float* b2;
+  float* y;           // [N][COUT][Ho][Wo], image n at y + n * (COUT * Ho * Wo + y_nx)
+  long y_nx;
+  int N, CIN, H, W, HID, COUT, Ho, Wo, stride, res;  // res: + x (stride 1, CIN == COUT)
+  float lo1, hi1, lo2, hi2;
+  int pstr;           // floats between the staged input channels' rows in LDS (ir_pstr)
+  int tiles_x, tiles; // output tiles per tile row / per image (ir_tiles)
+  int ks, cps;        // hidden-channel slices per tile, 16-channel chunks per slice
+  float* part;        // ks > 1: partial tiles [N * tiles][ks][4][NCB][64] f4
+  int* counters;      // ks > 1: arrivals per tile [N * tiles], zero between runs
+};
+bool ir_supported(const IrParams& p);
+int ir_pstr(int stride);
+size_t ir_lds_bytes(int cin, int stride);
+void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles);
+const char* ir_kernel_name(const IrParams& p);
+void launch_ir(const IrParams& p, hipStream_t s);
+
 const char* conv_kernel_name(const ConvParams& p);
 // a depthwise -> 1x1 pair of N images of P pixels into M channels runs fused
 // on k_conv_pw (vso_kernels.hip: where that measured faster)

@@ -455,6 +455,7 @@ struct vso_session {
   int device = 0;
   int conv_precision = 0;  // ConvPrec
   int tile_convs = 0;      // convolutions planned on k_conv_tile
+  int ir_blocks = 0;       // inverted residual blocks planned on k_ir
   hipStream_t stream = nullptr;
   std::string err;
   std::vector<std::string> in_names, out_names;
@@ -895,7 +896,142 @@ struct Planner {
   }
 
 
+  // VSO_IR=0: the inverted residual blocks as three launches each (A/B knob)
+  static bool ir_enabled() {
+    static const bool on = [] {
+      const char* e = std::getenv("VSO_IR");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+
+  // A constant conv's geometry: 1x1 / stride 1 / unpadded / undilated, or the
+  // 3x3 depthwise of a MobileNetV2 block (pads 1, stride 1 or 2)
+  bool conv_attrs(const Node& c, int k, int* stride, int* group) {
+    if (c.as("auto_pad", "NOTSET") != "NOTSET") return false;
+    const std::vector<int64_t> st = c.ais("strides"), dl = c.ais("dilations"), pd = c.ais("pads");
+    for (int64_t v : dl) if (v != 1) return false;
+    const int sh = st.size() > 0 ? (int)st[0] : 1, sw = st.size() > 1 ? (int)st[1] : 1;
+    if (sh != sw) return false;
+    for (int64_t v : pd) if (v != (k == 3 ? 1 : 0)) return false;
+    if (k == 3 && pd.size() != 4) return false;
+    *stride = sh;
+    *group = (int)c.ai("group", 1);
+    return true;
+  }
+
+  // The MobileNetV2 inverted residual starting at Conv ni — 1x1 expand ->
+  // Clip -> 3x3 depthwise (stride 1 / 2) -> Clip -> 1x1 project [-> Add of
+  // the block's input] — as one k_ir launch (vso_ir.hip).  1: planned (the
+  // other nodes marked done), 0: not this pattern / no kernel for its shape,
+  // -1: an error.
+  int try_plan_ir(size_t ni) {
+    if (!ir_enabled()) return 0;
+    const Node& ex = g.nodes[ni];
+    if (ibn.count(ni) || ex.in.size() < 2) return 0;
+    Value* x = val(ex.in[0]);
+    Value* w1 = val(ex.in[1]);
+    if (!x || x->is_const || x->shape.size() != 4 || !w1 || !w1->is_const || w1->c.dims.size() != 4) return 0;
+    int s1, g1;
+    if (!conv_attrs(ex, 1, &s1, &g1) || s1 != 1 || g1 != 1 || w1->c.dims[2] != 1 || w1->c.dims[3] != 1) return 0;
+    const int N = (int)x->shape[0], CIN = (int)x->shape[1], H = (int)x->shape[2], W = (int)x->shape[3];
+    const int HID = (int)w1->c.dims[0];
+    if (w1->c.dims[1] != CIN) return 0;
+    // the chain: each value consumed by the next node only
+    const int k1 = sole_consumer(ex.out[0], ni);
+    if (k1 < 0 || g.nodes[k1].op != "Clip") return 0;
+    const int k2 = sole_consumer(g.nodes[k1].out[0], k1);
+    if (k2 < 0 || g.nodes[k2].op != "Conv" || g.nodes[k2].in[0] != g.nodes[k1].out[0]) return 0;
+    const int k3 = sole_consumer(g.nodes[k2].out[0], k2);
+    if (k3 < 0 || g.nodes[k3].op != "Clip") return 0;
+    const int k4 = sole_consumer(g.nodes[k3].out[0], k3);
+    if (k4 < 0 || g.nodes[k4].op != "Conv" || g.nodes[k4].in[0] != g.nodes[k3].out[0]) return 0;
+    const Node &dw = g.nodes[k2], &pj = g.nodes[k4];
+    Value* wd = val(dw.in[1]);
+    Value* w2 = val(pj.in[1]);
+    int sd, gd, s2, g2;
+    if (!wd || !wd->is_const || wd->c.dims.size() != 4 || !conv_attrs(dw, 3, &sd, &gd) || (sd != 1 && sd != 2) ||
+        gd != HID || wd->c.dims[0] != HID || wd->c.dims[1] != 1 || wd->c.dims[2] != 3 || wd->c.dims[3] != 3)
+      return 0;
+    if (!w2 || !w2->is_const || w2->c.dims.size() != 4 || !conv_attrs(pj, 1, &s2, &g2) || s2 != 1 || g2 != 1 ||
+        w2->c.dims[1] != HID || w2->c.dims[2] != 1 || w2->c.dims[3] != 1)
+      return 0;
+    const int COUT = (int)w2->c.dims[0];
+    auto bias_of = [&](const Node& c, int m, std::vector<float>* b) {
+      b->assign(m, 0.f);
+      if (c.in.size() < 3 || c.in[2].empty()) return true;
+      Value* v = val(c.in[2]);
+      if (!v || !v->is_const || v->c.numel() != m) return false;
+      *b = v->c.f;
+      return true;
+    };
+    std::vector<float> b1, bd, b2;
+    if (!bias_of(ex, HID, &b1) || !bias_of(dw, HID, &bd) || !bias_of(pj, COUT, &b2)) return 0;
+    Epilogue c1{}, c2{};
+    if (!act_of(g.nodes[k1], &c1, HID) || !act_of(g.nodes[k3], &c2, HID)) return 0;
+    const int Ho = (H + 2 - 3) / sd + 1, Wo = (W + 2 - 3) / sd + 1;
+    // the residual: an Add of the project's output and the block's input
+    std::string out = pj.out[0];
+    int k5 = sole_consumer(out, k4);
+    bool res = false;
+    if (k5 >= 0 && g.nodes[k5].op == "Add") {
+      const Node& ad = g.nodes[k5];
+      const std::string& other = ad.in[0] == out ? ad.in[1] : ad.in[0];
+      if (other == ex.in[0] && ad.in[0] != ad.in[1] && sd == 1 && CIN == COUT) {
+        res = true;
+        out = ad.out[0];
+      }
+    }
+    if (cat_direct.count(out) || cat_direct.count(pj.out[0])) return 0;  // (written into a Concat: the generic path)
+    IrParams p{};
+    p.N = N; p.CIN = CIN; p.H = H; p.W = W; p.HID = HID; p.COUT = COUT; p.Ho = Ho; p.Wo = Wo;
+    p.stride = sd; p.res = res ? 1 : 0;
+    p.lo1 = c1.a0; p.hi1 = c1.a1; p.lo2 = c2.a0; p.hi2 = c2.a1;
+    if (!ir_supported(p)) return 0;
+    // slices of the hidden channels: about a workgroup per CU (256) over the
+    // tiles and slices, whole 16-channel chunks per slice
+    ir_tiles(Ho, Wo, &p.tiles_x, &p.tiles);
+    const int nch = HID / 16;
+    const long wg0 = (long)N * p.tiles;
+    int ks = (int)std::min<long>(nch, std::max<long>(1, (256 + wg0 / 2) / wg0));
+    p.cps = (nch + ks - 1) / ks;
+    p.ks = (nch + p.cps - 1) / p.cps;
+    p.pstr = ir_pstr(sd);
+    // weights: the expand / project as stored ([out][in]), the depthwise tap-major
+    std::vector<float> wdt((size_t)9 * HID);
+    for (int h = 0; h < HID; ++h)
+      for (int k = 0; k < 9; ++k) wdt[(size_t)k * HID + h] = wd->c.f[(size_t)h * 9 + k];
+    flush_input(ex.in[0]);
+    flush_norm(ex.in[0]);
+    p.x = dptr(*x);
+    p.w1 = upload_vec(w1->c.f);
+    p.b1 = upload_vec(b1);
+    p.wdw = upload_vec(wdt);
+    p.bdw = upload_vec(bd);
+    p.w2 = upload_vec(w2->c.f);
+    p.b2 = upload_vec(b2);
+    if (!p.w1 || !p.b1 || !p.wdw || !p.bdw || !p.w2 || !p.b2) return -1;
+    if (p.ks > 1) {
+      const size_t blocks = (size_t)N * p.tiles;
+      if (!dalloc(&p.part, blocks * p.ks * 4 * ((COUT + 15) / 16) * 64 * 16) || !dalloc(&p.counters, blocks * 4))
+        return -1;
+      if (hipMemset(p.counters, 0, blocks * 4) != hipSuccess) {
+        fail("hipMemset failed");
+        return -1;
+      }
+    }
+    if (!set_runtime(out, {N, COUT, Ho, Wo})) return -1;
+    p.y = dptr(vals[out]);
+    auto pp = std::make_shared<IrParams>(p);
+    add(ir_kernel_name(p), [pp](hipStream_t st) { launch_ir(*pp, st); });
+    for (int k : {k1, k2, k3, k4}) done.insert((size_t)k);
+    if (res) done.insert((size_t)k5);
+    s->ir_blocks++;
+    return 1;
+  }
+
   bool plan_conv(size_t ni) {
+    if (const int rc = try_plan_ir(ni)) return rc > 0;
     const Node& nd = g.nodes[ni];
     Value* x = val(nd.in[0]);
     Value* w = val(nd.in[1]);
@@ -2249,6 +2385,7 @@ int vso_run_device(vso_session* s, const float* const* d_inputs, float* const* d
 int vso_launch_count(const vso_session* s) { return s ? (int)s->launches.size() : VSO_E_INVALID_ARG; }
 
 int vso_tile_conv_count(const vso_session* s) { return s ? s->tile_convs : VSO_E_INVALID_ARG; }
+int vso_ir_block_count(const vso_session* s) { return s ? s->ir_blocks : VSO_E_INVALID_ARG; }
 
 
 int vso_launch_name(const vso_session* s, int k, char* buf, int cap) {

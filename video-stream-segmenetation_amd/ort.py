@@ -47,6 +47,7 @@ def lib():
             "vso_create_ex": ([P, S, I64P, I, I, ctypes.POINTER(Options), ctypes.POINTER(P)], I),
             "vso_options_default": ([ctypes.POINTER(Options)], None),
             "vso_tile_conv_count": ([P], I),
+            "vso_ir_block_count": ([P], I),
             "vso_destroy": ([P], None),
             "vso_last_error": ([P], ctypes.c_char_p),
             "vso_io_count": ([P, ctypes.POINTER(I), ctypes.POINTER(I)], I),
@@ -147,6 +148,10 @@ class InferenceSession:
     def tile_convs(self) -> int:
         """Convolutions planned on the LDS-tiled MFMA kernel (k_conv_tile)."""
         return _check(lib().vso_tile_conv_count(self._h), self._h)
+
+    def ir_blocks(self) -> int:
+        """Inverted residual blocks planned as one fused launch each (k_ir)."""
+        return _check(lib().vso_ir_block_count(self._h), self._h)
 
     def close(self):
         if getattr(self, "_h", None):
