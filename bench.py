@@ -427,7 +427,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     # (2000 steps: a ~75 ms window; 200-step windows (~8.5 ms) read 187-191k
     # against 213-215k on the same box, the pipeline's fill / drain and the
-    # first calls' host costs spread over too few steps — DESIGN.md "Short
+    # first calls' host costs spread over too few steps — profiles/NOTES.md "Short
     # windows"; the per-step work is the same)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=20)
@@ -439,7 +439,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--streams", default="torch", choices=["slot", "torch"],
                     help="step streams: new torch streams (default; measured 184-187k vs 142-147k on plain slot "
-                         "streams, which share the runtime's pooled queues — see DESIGN.md) or the handle's slot "
+                         "streams, which share the runtime's pooled queues — see profiles/NOTES.md) or the handle's slot "
                          "streams (run with VSS_SLOT_QUEUES=cumask for dedicated queues)")
     ap.add_argument("--cpu-budget-s", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")

@@ -70,7 +70,7 @@ enum { VSS_OUT_MODEL = 0, VSS_OUT_FRAME = 1 };
 
 /* Options for vss_set_option.  (Values 3-5 belonged to round-1 experiments —
  * sub-batch graph branches and the persistent k_forward — measured slower and
- * removed; DESIGN.md keeps the numbers.  Setting them fails with
+ * removed; profiles/NOTES.md keeps the numbers.  Setting them fails with
  * VSS_E_UNSUPPORTED.) */
 enum {
   VSS_OPT_USE_GRAPH = 1, /* 1: replay a hipGraph per (slot, shape) (default 1): up to 4 executables

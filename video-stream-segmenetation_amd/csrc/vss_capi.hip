@@ -2276,7 +2276,7 @@ int vss_synchronize(vss_handle* h) {
 int vss_set_option(vss_handle* h, int option, int value) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (option == 3 || option == 4 || option == 5)
-    return fail(h, VSS_E_UNSUPPORTED, "option removed (round-1 experiment measured slower; DESIGN.md)");
+    return fail(h, VSS_E_UNSUPPORTED, "option removed (round-1 experiment measured slower; profiles/NOTES.md)");
   if (option == VSS_OPT_GRAPH_BUILDS || option == VSS_OPT_GRAPH_PATCHES || option == VSS_OPT_COMM_RANKS ||
       option == VSS_OPT_GATHER_CALLS)
     return fail(h, VSS_E_INVALID_ARG, "read-only option (vss_get_option)");

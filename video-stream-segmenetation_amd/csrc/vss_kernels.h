@@ -539,7 +539,7 @@ void launch_post_filter(const PostFilterParams& p, int n, hipStream_t s);
 // past the last full eighth keeps its own index); results do not depend on
 // which workgroup computes which tile (tile-invariant, order-free norm sums).
 // Measured: the post filter and the frame-resolution kernels gain nothing
-// from it, so they keep the natural order.
+// from it (profiles/NOTES.md), so they keep the natural order.
 #ifndef VSS_XCD_REMAP
 #define VSS_XCD_REMAP 1
 #endif
