@@ -39,53 +39,63 @@
 
 namespace vso {
 
+// The input region of a tile: IH x IW pixels, one channel per PSTR floats.
+// PSTR (>= P_IN) is 4 mod 8: the expand's B reads of lanes (r, g) (channels
+// 4g apart) then fall on complementary banks.  The copy into LDS is one
+// contiguous LDS-DMA stream over CIN x PSTR (the PSTR - P_IN gap floats of
+// each channel take any image pixel; nothing reads them as data).
 template <int S, int TH>
 struct IrGeom {
   static constexpr int TW = 16;
   static constexpr int IH = S == 2 ? 2 * TH + 1 : TH + 2, IW = S == 2 ? 2 * TW + 1 : TW + 2;
   static constexpr int P_IN = IH * IW, NBI = (P_IN + 15) / 16, P_PAD = NBI * 16;
+  static constexpr int pstr() {
+    int v = P_IN;
+    while (v % 8 != 4) ++v;
+    return v;
+  }
+  static constexpr int PSTR = pstr();
   static constexpr int HQ = P_PAD + (S == 2 ? 1 : 0);  // quads per hidden plane
 };
+
+// floats of the staged region: CIN rows of PSTR, covering the last channel's
+// reads up to P_PAD, rounded up to whole 256-element DMA blocks (the last
+// block's lanes past the end write into the overhang)
+__host__ __device__ constexpr int ir_xs_floats(int cin, int pstr, int p_pad) {
+  const int f = (cin - 1) * pstr + (p_pad > pstr ? p_pad : pstr);
+  return (f + 255) / 256 * 256;
+}
 
 template <int NT, int NCB, int S, int TH>
 __global__ __launch_bounds__(256) void k_ir(IrParams p) {
   using G = IrGeom<S, TH>;
-  constexpr int TW = G::TW, IW = G::IW, P_IN = G::P_IN, NBI = G::NBI, HQ = G::HQ;
+  constexpr int TW = G::TW, IW = G::IW, P_IN = G::P_IN, NBI = G::NBI, HQ = G::HQ, PSTR = G::PSTR;
   static_assert(TH <= 4, "one output row per wave");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-  const int CIN = p.CIN, HID = p.HID, COUT = p.COUT, PSTR = p.pstr, H = p.H, W = p.W;
-  float* xs = smem;                   // [CIN][PSTR]
-  float* hbuf = smem + CIN * PSTR;    // 2 x [4 planes][HQ][4]
+  const int CIN = p.CIN, HID = p.HID, COUT = p.COUT, H = p.H, W = p.W;
+  float* xs = smem;                                        // [CIN][PSTR] (+ overhang)
+  float* hbuf = smem + ir_xs_floats(CIN, PSTR, G::P_PAD);  // 2 x [4 planes][HQ][4]
   const int t = blockIdx.x, ks = blockIdx.y, n = blockIdx.z;
   const int ty = t / p.tiles_x, tx = t - ty * p.tiles_x;
   const int oy0 = ty * TH, ox0 = tx * TW, iy0 = S * oy0 - 1, ix0 = S * ox0 - 1;
 
-  // ---- prologue: the input region, 8 loads in flight per thread ----
+  // ---- prologue: the input region, global -> LDS by LDS-DMA (no register
+  // stage, every load in flight at once).  Pixels outside the image load the
+  // nearest image pixel: their expand outputs are zeroed below (the
+  // depthwise's padding), so their inputs only need to be finite.
   {
     const float* xn = p.x + (long)n * CIN * H * W;
-    const int total = CIN * P_IN;
-    constexpr int U = 8;
-    for (int b0 = 0; b0 < total; b0 += 256 * U) {
-      float v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = min(b0 + tid + 256 * u, total - 1);
-        const int c = i / P_IN, q = i - c * P_IN, ly = q / IW, lx = q - ly * IW;
-        const int gy = iy0 + ly, gx = ix0 + lx;
-        const bool in = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
-        const float x = xn[c * H * W + (in ? gy * W + gx : 0)];
-        v[u] = in ? x : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = b0 + tid + 256 * u;
-        if (i < total) {
-          const int c = i / P_IN;
-          xs[c * PSTR + i - c * P_IN] = v[u];
-        }
-      }
+    const int total = CIN * PSTR;
+    const int wbase = __builtin_amdgcn_readfirstlane((tid >> 6) << 6);
+    for (int b0 = 0; b0 < total; b0 += 256) {
+      const int i = min(b0 + tid, total - 1);
+      const int c = i / PSTR, q = min(i - c * PSTR, P_IN - 1), ly = q / IW, lx = q - ly * IW;
+      const int gy = min(max(iy0 + ly, 0), H - 1), gx = min(max(ix0 + lx, 0), W - 1);
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(xn + c * H * W + gy * W + gx),
+                                       (__attribute__((address_space(3))) void*)(xs + b0 + wbase), 4, 0, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 
@@ -261,16 +271,12 @@ const IrEntry* ir_entry(const IrParams& p) {
 }
 }  // namespace
 
-int ir_pstr(int stride) {
-  const int pad = stride == 2 ? IrGeom<2, kIrTH>::P_PAD : IrGeom<1, kIrTH>::P_PAD;
-  int v = pad;
-  while (v % 8 != 4) ++v;
-  return v;
-}
+int ir_pstr(int stride) { return stride == 2 ? IrGeom<2, kIrTH>::PSTR : IrGeom<1, kIrTH>::PSTR; }
 
 size_t ir_lds_bytes(int cin, int stride) {
   const int hq = stride == 2 ? IrGeom<2, kIrTH>::HQ : IrGeom<1, kIrTH>::HQ;
-  return ((size_t)cin * ir_pstr(stride) + 2 * 16 * (size_t)hq) * 4;
+  const int pad = stride == 2 ? IrGeom<2, kIrTH>::P_PAD : IrGeom<1, kIrTH>::P_PAD;
+  return ((size_t)ir_xs_floats(cin, ir_pstr(stride), pad) + 2 * 16 * (size_t)hq) * 4;
 }
 
 void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles) {
