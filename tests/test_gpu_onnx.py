@@ -164,14 +164,15 @@ def test_conv_upsample_fusion(ort, precision):
         assert np.array_equal(got[k], again[k])
 
 
-@pytest.mark.parametrize("precision", ["f32", "bf16"])
+@pytest.mark.parametrize("precision", ["f32", "bf16", "f16"])
 def test_inverted_residuals_fused(ort, precision):
-    """Every MobileNetV2 inverted residual of ir_chain as one k_ir launch
-    (vso_ir.hip), against the f64 oracle at the f32 bar (1e-4 of the output
-    scale): f32 arithmetic in every session precision (the 1x1 / depthwise
-    convolutions are not k_conv_tile ones, and the oracle rounds none of
-    them); and bitwise the same on a second run (the hidden-channel slices
-    are summed in a fixed order)."""
+    """Every MobileNetV2 inverted residual of ir_chain as one launch
+    (vso_ir.hip) — k_ir (exact f32 products) in f32 sessions, k_ir_b16 (the
+    1x1 products as hi + lo bf16 splits, ~2^-16 relative) in bf16 / f16 ones —
+    against the f64 oracle at the f32 bar (1e-4 of the output scale): the
+    1x1 / depthwise convolutions are not k_conv_tile ones, and the oracle
+    rounds none of them; and bitwise the same on a second run (the
+    hidden-channel slices are summed in a fixed order)."""
     data = M.ir_chain()
     feeds = {"x": np.random.default_rng(14).standard_normal((2, 16, 38, 67)).astype(np.float32)}
     want = R.run(R.load(data), feeds, conv_operands=None if precision == "f32" else precision)
@@ -180,7 +181,8 @@ def test_inverted_residuals_fused(ort, precision):
         again = s.run(feeds)
         names = s.launches()
         assert s.ir_blocks() == 11, names
-    assert sum("k_ir<" in n for n in names) == 11, names
+    kern = "k_ir<" if precision == "f32" else "k_ir_b16<"
+    assert sum(kern in n for n in names) == 11, names
     assert not any("k_conv_dw" in n or "k_conv_small" in n for n in names), names
     for k, w in want.items():
         err = float(np.abs(got[k] - w).max())

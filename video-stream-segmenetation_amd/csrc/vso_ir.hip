@@ -66,6 +66,83 @@ __host__ __device__ constexpr int ir_xs_floats(int cin, int pstr, int p_pad) {
   return (f + 255) / 256 * 256;
 }
 
+// The epilogue of both forms.  ks > 1: the partial tile ([blk][slice][wave]
+// [cb][lane] as f4), write-through 8-byte agent-scope stores; the last slice
+// to arrive (any XCD) sums the slices in order with sc1 loads (k_conv_tile's
+// protocol, vso_conv.hip).  Then + b2 (+ the residual res(ch) of this lane's
+// output pixel, stride 1) and the store: wave w owns output row w, lane (r, g)
+// pixel r and channels cb * 16 + 4g + v.
+template <int NCB, typename Res>
+__device__ __forceinline__ void ir_finish(const IrParams& p, f4 (&acc)[NCB], bool outw, int t, int ks, int n, int oy0,
+                                          int ox0, Res res) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  if (p.ks > 1) {
+    const long blk = (long)n * p.tiles + t;
+    if (outw) {
+      uint64_t* part = reinterpret_cast<uint64_t*>(p.part) + ((blk * p.ks + ks) * 4 + wave) * (NCB * 64 * 2);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const uint64_t lo = (uint64_t)__float_as_uint(acc[cb][0]) | ((uint64_t)__float_as_uint(acc[cb][1]) << 32);
+        const uint64_t hi = (uint64_t)__float_as_uint(acc[cb][2]) | ((uint64_t)__float_as_uint(acc[cb][3]) << 32);
+        uint64_t* q = part + (cb * 64 + lane) * 2;
+        __hip_atomic_store(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __shared__ int last;
+    __syncthreads();
+    if (tid == 0) {
+      int* cnt = p.counters + blk;
+      const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == p.ks - 1;
+      if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next run
+    }
+    __syncthreads();
+    if (!last || !outw) return;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint64_t* base = reinterpret_cast<const uint64_t*>(p.part) + (blk * p.ks * 4 + wave) * (NCB * 64 * 2);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < p.ks; k0 += 8) {  // 8 slices' loads in flight, summed in slice order
+        uint64_t lo[8], hi[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (k0 + u < p.ks) {
+            const uint64_t* q = base + ((long)(k0 + u) * 4 * NCB * 64 + cb * 64 + lane) * 2;
+            lo[u] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi[u] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (k0 + u < p.ks)
+            sum += f4{__uint_as_float((uint32_t)lo[u]), __uint_as_float((uint32_t)(lo[u] >> 32)),
+                      __uint_as_float((uint32_t)hi[u]), __uint_as_float((uint32_t)(hi[u] >> 32))};
+      }
+      acc[cb] = sum;
+    }
+  }
+  if (!outw) return;
+  const int oy = oy0 + wave, ox = ox0 + r;
+  if (oy >= p.Ho || ox >= p.Wo) return;
+  const long plane = (long)p.Ho * p.Wo;
+  float* yn = p.y + (long)n * ((long)p.COUT * plane + p.y_nx) + (long)oy * p.Wo + ox;
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int ch = cb * 16 + 4 * g + v;
+      if (ch < p.COUT) {
+        float o = acc[cb][v] + p.b2[ch];
+        if (p.res) o += res(ch);
+        yn[ch * plane] = o;
+      }
+    }
+}
+
 template <int NT, int NCB, int S, int TH>
 __global__ __launch_bounds__(256) void k_ir(IrParams p) {
   using G = IrGeom<S, TH>;
@@ -175,75 +252,176 @@ __global__ __launch_bounds__(256) void k_ir(IrParams p) {
   }
 
   // ---- epilogue ----
-  if (p.ks > 1) {
-    // the partial tile ([blk][slice][wave][cb][lane] as f4), write-through
-    // 8-byte agent-scope stores; the last slice to arrive (any XCD) sums the
-    // slices in order with sc1 loads (k_conv_tile's protocol, vso_conv.hip)
-    const long blk = (long)n * p.tiles + t;
-    if (outw) {
-      uint64_t* part = reinterpret_cast<uint64_t*>(p.part) + ((blk * p.ks + ks) * 4 + wave) * (NCB * 64 * 2);
+  ir_finish<NCB>(p, acc, outw, t, ks, n, oy0, ox0, [&](int ch) { return xs[ch * PSTR + (wave + 1) * IW + r + 1]; });
+}
+
+// ---- the bf16x3 form (session precision bf16 / f16) ----
+// The same block with every 1x1 product on v_mfma_f32_16x16x32_bf16 over a
+// hi + lo bf16 split of both operands: w x = wh xh + wh xl + wl xh (+ wl xl,
+// dropped: 2^-16 of the product, as are the splits' own residues) — about f32
+// precision (these convolutions stay unrounded in onnx_ref's bf16 / f16
+// oracle, tiled_conv()) at 3 bf16 MFMAs (48 cycles) per 32 channels where
+// the f32 form takes 8 v_mfma_f32_16x16x4_f32 (256 cycles).
+//   input   — each wave's region blocks loaded straight into registers, split
+//             once: lane (r, g) of block j holds channels 32t + 8g .. + 7 of
+//             pixel r as 8 bf16 hi and 8 lo (the B operands of every chunk);
+//             no staged copy in LDS, which holds the hidden planes only
+//             (14 / 39 KB: up to 4 workgroups per CU);
+//   expand  — A = W1 rows of the chunk, host-split [HID][32 NT2] hi / lo;
+//   project — per PAIR of chunks (32 hidden channels = one MFMA's K): B = the
+//             two chunks' depthwise outputs (lane (r, g): channels 4g..4g+3 of
+//             each, split), A = W2 host-split and permuted to that order
+//             ([COUT pad][pair][g][8]).  Slices hold whole pairs (cps even).
+//   residual — read from x in HBM at the store (exact f32).
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef __bf16 bf4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 mfma_bf(f4 a, f4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a), __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
+}
+
+template <int NT2, int NCB, int S, int TH>
+__global__ __launch_bounds__(256) void k_ir_b16(IrParams p) {
+  using G = IrGeom<S, TH>;
+  constexpr int IW = G::IW, P_IN = G::P_IN, NBI = G::NBI, HQ = G::HQ, NBW = (NBI + 3) / 4;
+  static_assert(TH <= 4, "one output row per wave");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int CIN = p.CIN, HID = p.HID, H = p.H, W = p.W, HW = H * W;
+  float* hbuf = smem;  // 2 x [4 planes][HQ][4]
+  const int t = blockIdx.x, ks = blockIdx.y, n = blockIdx.z;
+  const int ty = t / p.tiles_x, tx = t - ty * p.tiles_x;
+  const int oy0 = ty * TH, ox0 = G::TW * tx, iy0 = S * oy0 - 1, ix0 = S * ox0 - 1;
+
+  // ---- prologue: this wave's region blocks, split into bf16 hi / lo.
+  // Pixels outside the image (and past the region) load the nearest image
+  // pixel: their expand outputs are zeroed below, so they only need to be finite.
+  f4 xh[NBW][NT2], xl[NBW][NT2];
+  {
+    const float* xn = p.x + (long)n * CIN * HW;
 #pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        const uint64_t lo = (uint64_t)__float_as_uint(acc[cb][0]) | ((uint64_t)__float_as_uint(acc[cb][1]) << 32);
-        const uint64_t hi = (uint64_t)__float_as_uint(acc[cb][2]) | ((uint64_t)__float_as_uint(acc[cb][3]) << 32);
-        uint64_t* q = part + (cb * 64 + lane) * 2;
-        __hip_atomic_store(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __shared__ int last;
-    __syncthreads();
-    if (tid == 0) {
-      int* cnt = p.counters + blk;
-      const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = prev == p.ks - 1;
-      if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next run
-    }
-    __syncthreads();
-    if (!last || !outw) return;
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint64_t* base = reinterpret_cast<const uint64_t*>(p.part) + (blk * p.ks * 4 + wave) * (NCB * 64 * 2);
+    for (int j = 0; j < NBW; ++j) {
+      const int pix = min((wave + 4 * j) * 16 + r, P_IN - 1), ly = pix / IW, lx = pix - ly * IW;
+      const int off = min(max(iy0 + ly, 0), H - 1) * W + min(max(ix0 + lx, 0), W - 1);
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      f4 sum = f4{0.f, 0.f, 0.f, 0.f};
-      for (int k0 = 0; k0 < p.ks; k0 += 8) {  // 8 slices' loads in flight, summed in slice order
-        uint64_t lo[8], hi[8];
+      for (int u = 0; u < NT2; ++u) {
+        bf8v h, l;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (k0 + u < p.ks) {
-            const uint64_t* q = base + ((long)(k0 + u) * 4 * NCB * 64 + cb * 64 + lane) * 2;
-            lo[u] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            hi[u] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
+        for (int e = 0; e < 8; ++e) {
+          const int c = 32 * u + 8 * g + e;
+          const float v = xn[min(c, CIN - 1) * HW + off];
+          const float x = c < CIN ? v : 0.f;
+          const __bf16 b = (__bf16)x;
+          h[e] = b;
+          l[e] = (__bf16)(x - (float)b);
         }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (k0 + u < p.ks)
-            sum += f4{__uint_as_float((uint32_t)lo[u]), __uint_as_float((uint32_t)(lo[u] >> 32)),
-                      __uint_as_float((uint32_t)hi[u]), __uint_as_float((uint32_t)(hi[u] >> 32))};
+        xh[j][u] = __builtin_bit_cast(f4, h);
+        xl[j][u] = __builtin_bit_cast(f4, l);
       }
-      acc[cb] = sum;
     }
   }
-  if (!outw) return;
-  const int oy = oy0 + wave, ox = ox0 + r;
-  if (oy >= p.Ho || ox >= p.Wo) return;
-  const long plane = (long)p.Ho * p.Wo;
-  float* yn = p.y + (long)n * ((long)COUT * plane + p.y_nx) + (long)oy * p.Wo + ox;
-  const int centre = (wave + 1) * IW + r + 1;  // stride 1: the output pixel in the staged region
+
+  const int nch = HID / 16, c0 = ks * p.cps, c1 = min(c0 + p.cps, nch);
+  const int cinp = NT2 * 32, npair = (nch + 1) / 2;
+  const bool outw = wave < TH;
+  f4 a1h[NT2], a1l[NT2];
+  auto load_a1 = [&](int c) {
+    const uint16_t* rh = p.w1h + (long)(c * 16 + r) * cinp + 8 * g;
+    const uint16_t* rl = p.w1l + (long)(c * 16 + r) * cinp + 8 * g;
 #pragma unroll
-  for (int cb = 0; cb < NCB; ++cb)
+    for (int u = 0; u < NT2; ++u) {
+      a1h[u] = *reinterpret_cast<const f4*>(rh + 32 * u);
+      a1l[u] = *reinterpret_cast<const f4*>(rl + 32 * u);
+    }
+  };
+  f4 acc[NCB], a2h[NCB], a2l[NCB];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int ch = cb * 16 + 4 * g + v;
-      if (ch < COUT) {
-        float o = acc[cb][v] + p.b2[ch];
-        if (p.res) o += xs[ch * PSTR + centre];
-        yn[ch * plane] = o;
+  for (int cb = 0; cb < NCB; ++cb) acc[cb] = f4{0.f, 0.f, 0.f, 0.f};
+  bf4v dh0 = bf4v{}, dl0 = bf4v{};  // the first chunk of a pair: its depthwise output, split
+  if (c0 < c1) load_a1(c0);
+  for (int c = c0; c < c1; ++c) {
+    const bool first = ((c - c0) & 1) == 0;
+    float* hid = hbuf + ((c - c0) & 1) * (16 * HQ);
+    const int h0 = c * 16;
+    const f4 b1v = *reinterpret_cast<const f4*>(p.b1 + h0 + 4 * g);
+    f4 wd[9], bd = f4{0.f, 0.f, 0.f, 0.f};
+    if (outw) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) wd[k] = *reinterpret_cast<const f4*>(p.wdw + k * HID + h0 + 4 * g);
+      bd = *reinterpret_cast<const f4*>(p.bdw + h0 + 4 * g);
+      if (first) {  // the pair's project weights: in flight during two expands
+        const int pr = c >> 1;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const long o = (((long)(cb * 16 + r) * npair + pr) * 4 + g) * 8;
+          a2h[cb] = *reinterpret_cast<const f4*>(p.w2h + o);
+          a2l[cb] = *reinterpret_cast<const f4*>(p.w2l + o);
+        }
       }
     }
+    // expand: D[hidden 4g + i][pixel r] of this wave's region blocks
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const int pb = wave + 4 * j;
+      if (pb < NBI) {
+        f4 d = b1v;
+#pragma unroll
+        for (int u = 0; u < NT2; ++u) {
+          d = mfma_bf(a1l[u], xh[j][u], d);
+          d = mfma_bf(a1h[u], xl[j][u], d);
+          d = mfma_bf(a1h[u], xh[j][u], d);
+        }
+        const int pix = pb * 16 + r, ly = pix / IW, lx = pix - ly * IW;
+        const bool in = pix < P_IN && (unsigned)(iy0 + ly) < (unsigned)H && (unsigned)(ix0 + lx) < (unsigned)W;
+        f4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = in ? fminf(fmaxf(d[i], p.lo1), p.hi1) : 0.f;
+        *reinterpret_cast<f4*>(hid + (g * HQ + pix) * 4) = v;
+      }
+    }
+    __syncthreads();
+    if (c + 1 < c1) load_a1(c + 1);  // the next chunk's expand fragments, in flight during the dw / project
+    if (outw) {
+      f4 a = bd;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int rp = (S * wave + ky) * IW + S * r + kx;
+          a = __builtin_elementwise_fma(wd[ky * 3 + kx], *reinterpret_cast<const f4*>(hid + (g * HQ + rp) * 4), a);
+        }
+      bf4v dh, dl;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = fminf(fmaxf(a[i], p.lo2), p.hi2);
+        const __bf16 b = (__bf16)v;
+        dh[i] = b;
+        dl[i] = (__bf16)(v - (float)b);
+      }
+      if (first && c + 1 < c1) {
+        dh0 = dh;
+        dl0 = dl;
+      } else {
+        // project the pair: B lane (r, g) = (first chunk's 4g..4g+3, second's)
+        const bf4v z = bf4v{};
+        const bf8v bh = first ? __builtin_shufflevector(dh, z, 0, 1, 2, 3, 4, 5, 6, 7)
+                              : __builtin_shufflevector(dh0, dh, 0, 1, 2, 3, 4, 5, 6, 7);
+        const bf8v bl = first ? __builtin_shufflevector(dl, z, 0, 1, 2, 3, 4, 5, 6, 7)
+                              : __builtin_shufflevector(dl0, dl, 0, 1, 2, 3, 4, 5, 6, 7);
+        const f4 fh = __builtin_bit_cast(f4, bh), fl = __builtin_bit_cast(f4, bl);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          acc[cb] = mfma_bf(a2l[cb], fh, acc[cb]);
+          acc[cb] = mfma_bf(a2h[cb], fl, acc[cb]);
+          acc[cb] = mfma_bf(a2h[cb], fh, acc[cb]);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue ----
+  const float* xres = p.x + (long)n * CIN * HW + (long)(oy0 + wave) * W + ox0 + r;
+  ir_finish<NCB>(p, acc, outw, t, ks, n, oy0, ox0, [&](int ch) { return xres[(long)ch * HW]; });
 }
 
 // ---- host side ----
@@ -254,6 +432,8 @@ struct IrEntry {
   const char* name;
 };
 #define VSO_IR(NT, NCB, S, TH) {NT, NCB, S, TH, k_ir<NT, NCB, S, TH>, "vso::k_ir<" #NT ", " #NCB ", " #S ", " #TH ">"},
+#define VSO_IR16(NT2, NCB, S, TH) \
+  {NT2, NCB, S, TH, k_ir_b16<NT2, NCB, S, TH>, "vso::k_ir_b16<" #NT2 ", " #NCB ", " #S ", " #TH ">"},
 // MobileNetV2 1.0's blocks (t = 6): input channels / 16 (rounded up), output
 // channels / 16 (rounded up), stride — 16->24 s2, 24->24, 24->32 s2, 32->32,
 // 32->64 s2, 64->64, 64->96, 96->96, 96->160 s2, 160->160, 160->320
@@ -261,22 +441,30 @@ const IrEntry kIr[] = {
     VSO_IR(1, 2, 2, 4) VSO_IR(2, 2, 1, 4) VSO_IR(2, 2, 2, 4) VSO_IR(2, 4, 2, 4) VSO_IR(4, 4, 1, 4)
     VSO_IR(4, 6, 1, 4) VSO_IR(6, 6, 1, 4) VSO_IR(6, 10, 2, 4) VSO_IR(10, 10, 1, 4) VSO_IR(10, 20, 1, 4)
     VSO_IR(4, 4, 2, 4) VSO_IR(6, 6, 2, 4)};
+// the same blocks by input channels / 32 (the bf16x3 form's K step)
+const IrEntry kIr16[] = {
+    VSO_IR16(1, 2, 2, 4) VSO_IR16(1, 2, 1, 4) VSO_IR16(1, 4, 2, 4) VSO_IR16(2, 4, 1, 4) VSO_IR16(2, 6, 1, 4)
+    VSO_IR16(3, 6, 1, 4) VSO_IR16(3, 10, 2, 4) VSO_IR16(5, 10, 1, 4) VSO_IR16(5, 20, 1, 4) VSO_IR16(2, 4, 2, 4)
+    VSO_IR16(3, 6, 2, 4)};
 #undef VSO_IR
+#undef VSO_IR16
 
 const IrEntry* ir_entry(const IrParams& p) {
-  const int nt = (p.CIN + 15) / 16, ncb = (p.COUT + 15) / 16;
-  for (const IrEntry& e : kIr)
-    if (e.nt == nt && e.ncb == ncb && e.s == p.stride && e.th == kIrTH) return &e;
+  const int nt = p.b16 ? (p.CIN + 31) / 32 : (p.CIN + 15) / 16, ncb = (p.COUT + 15) / 16;
+  const IrEntry* t = p.b16 ? kIr16 : kIr;
+  const size_t n = p.b16 ? sizeof(kIr16) / sizeof(kIr16[0]) : sizeof(kIr) / sizeof(kIr[0]);
+  for (size_t i = 0; i < n; ++i)
+    if (t[i].nt == nt && t[i].ncb == ncb && t[i].s == p.stride && t[i].th == kIrTH) return &t[i];
   return nullptr;
 }
 }  // namespace
 
 int ir_pstr(int stride) { return stride == 2 ? IrGeom<2, kIrTH>::PSTR : IrGeom<1, kIrTH>::PSTR; }
 
-size_t ir_lds_bytes(int cin, int stride) {
+size_t ir_lds_bytes(int cin, int stride, int b16) {
   const int hq = stride == 2 ? IrGeom<2, kIrTH>::HQ : IrGeom<1, kIrTH>::HQ;
   const int pad = stride == 2 ? IrGeom<2, kIrTH>::P_PAD : IrGeom<1, kIrTH>::P_PAD;
-  return ((size_t)ir_xs_floats(cin, ir_pstr(stride), pad) + 2 * 16 * (size_t)hq) * 4;
+  return ((b16 ? 0 : (size_t)ir_xs_floats(cin, ir_pstr(stride), pad)) + 2 * 16 * (size_t)hq) * 4;
 }
 
 void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles) {
@@ -286,18 +474,18 @@ void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles) {
 
 bool ir_supported(const IrParams& p) {
   return p.CIN % 4 == 0 && p.HID % 16 == 0 && (p.stride == 1 || p.stride == 2) && ir_entry(p) != nullptr &&
-         ir_lds_bytes(p.CIN, p.stride) <= 160 * 1024 && (!p.res || (p.stride == 1 && p.CIN == p.COUT));
+         ir_lds_bytes(p.CIN, p.stride, p.b16) <= 160 * 1024 && (!p.res || (p.stride == 1 && p.CIN == p.COUT));
 }
 
 const char* ir_kernel_name(const IrParams& p) {
   const IrEntry* e = ir_entry(p);
-  return e ? e->name : "vso::k_ir<?>";
+  return e ? e->name : (p.b16 ? "vso::k_ir_b16<?>" : "vso::k_ir<?>");
 }
 
 void launch_ir(const IrParams& p, hipStream_t s) {
   const IrEntry* e = ir_entry(p);
   if (!e) return;
-  const size_t lds = ir_lds_bytes(p.CIN, p.stride);
+  const size_t lds = ir_lds_bytes(p.CIN, p.stride, p.b16);
   (void)hipFuncSetAttribute((const void*)e->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(e->fn, dim3(p.tiles, p.ks, p.N), dim3(256), lds, s, p);
 }

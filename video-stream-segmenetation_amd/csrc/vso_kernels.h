@@ -209,6 +209,12 @@ struct IrParams {
   const float* bdw;
   const float* w2;    // [COUT][HID], b2 [COUT]: project
   const float* b2;
+  // b16 (k_ir_b16, bf16 / f16 sessions): the 1x1 weights split into bf16 hi / lo,
+  // w1h / w1l [HID][32 ceil(CIN / 32)] (zero padded), w2h / w2l [16 NCB][pairs]
+  // [4][8]: row m, hidden pair q (32 channels), lane group g: W2[m][32q + 4g + i]
+  // (i < 4) then W2[m][32q + 16 + 4g + i] (zero past HID / COUT)
+  const uint16_t *w1h, *w1l, *w2h, *w2l;
+  int b16;
   float* y;           // [N][COUT][Ho][Wo], image n at y + n * (COUT * Ho * Wo + y_nx)
   long y_nx;
   int N, CIN, H, W, HID, COUT, Ho, Wo, stride, res;  // res: + x (stride 1, CIN == COUT)
@@ -221,7 +227,7 @@ struct IrParams {
 };
 bool ir_supported(const IrParams& p);
 int ir_pstr(int stride);
-size_t ir_lds_bytes(int cin, int stride);
+size_t ir_lds_bytes(int cin, int stride, int b16);
 void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles);
 const char* ir_kernel_name(const IrParams& p);
 void launch_ir(const IrParams& p, hipStream_t s);
