@@ -240,7 +240,7 @@ def q4f16_like(h=64, w=96):
     return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])], opset=21)
 
 
-def modnet(h=288, w=512, hr=32, q4f16=False, seed=7, in_eps=1e-5):
+def modnet(h=288, w=512, hr=32, q4f16=False, seed=7, in_eps=1e-5, taps=None, export=()):
     """The public MODNet topology (Ke et al., "MODNet: Real-Time Trimap-Free
     Portrait Matting via Objective Decomposition", AAAI 2022; the authors'
     src/models/modnet.py) at inference, the graph an ONNX export of the
@@ -262,7 +262,10 @@ def modnet(h=288, w=512, hr=32, q4f16=False, seed=7, in_eps=1e-5):
     IBNorm = Slice -> BatchNormalization (first half) / InstanceNormalization
     (second half, affine=False) -> Concat.  q4f16=True gives the export's form:
     float16 weights, the input Cast to FLOAT16 and the matte back to FLOAT, the
-    SE's two MatMuls as com.microsoft MatMulNBits (4-bit, block 32)."""
+    SE's two MatMuls as com.microsoft MatMulNBits (4-bit, block 32).
+    taps: a dict filled with {stage name: value name} (enc2x .. fu); export:
+    [(value name, shape)] made graph outputs too (a per-stage diagnostic,
+    tools/modnet_taps.py)."""
     b = Builder(seed)
     rng = b.rng
     x = "input"
@@ -332,6 +335,8 @@ def modnet(h=288, w=512, hr=32, q4f16=False, seed=7, in_eps=1e-5):
         enc[i] = t
     enc2x, enc4x = enc[0], enc[1]
     enc32x = relu6(conv(t, 320, 1280, 1))
+    tap = taps if taps is not None else {}
+    tap.update({"enc2x": enc2x, "enc4x": enc4x, "enc8x": enc[2], "enc16x": enc[4], "enc32x": enc32x})
     # LR branch
     gp = b.op("Flatten", [b.op("GlobalAveragePool", [enc32x])])
     f = b.op("Relu", [matmul(gp, 1280, 320)])
@@ -340,6 +345,7 @@ def modnet(h=288, w=512, hr=32, q4f16=False, seed=7, in_eps=1e-5):
     lr = b.op("Mul", [enc32x, f])
     lr16x = ibn_relu(resize(lr, 2), 1280, 96, 5)
     lr8x = ibn_relu(resize(lr16x, 2), 96, 32, 5)
+    tap.update({"se": lr, "lr16x": lr16x, "lr8x": lr8x})
     # HR branch
     img2x, img4x = resize(img, 0.5), resize(img, 0.25)
     e2 = ibn_relu(enc2x, 16, hr, 1)
@@ -355,14 +361,16 @@ def modnet(h=288, w=512, hr=32, q4f16=False, seed=7, in_eps=1e-5):
     u = ibn_relu(u, 2 * hr, hr, 3)
     u = ibn_relu(u, hr, hr, 3)
     hr2x = ibn_relu(u, hr, hr, 3)
+    tap.update({"e2": e2, "e4": e4, "hr4x": hr4x, "hr2x": hr2x})
     # fusion branch
     l4 = ibn_relu(resize(lr8x, 2), 32, hr, 5)
     f2x = ibn_relu(b.op("Concat", [resize(l4, 2), hr2x], axis=1), 2 * hr, hr, 3)
     fu = ibn_relu(b.op("Concat", [resize(f2x, 2), img], axis=1), hr + 3, hr // 2, 3)
     m = b.op("Sigmoid", [conv(fu, hr // 2, 1, 1)])
+    tap.update({"l4": l4, "f2x": f2x, "fu": fu})
     if q4f16:
         m = b.op("Cast", [m], to=R.DT_FLOAT)
-    return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])], opset=21 if q4f16 else 13)
+    return b.model([(x, [1, 3, h, w])], [(m, [1, 1, h, w])] + list(export), opset=21 if q4f16 else 13)
 
 
 def conv_tiles():

@@ -222,6 +222,38 @@ def test_inverted_residuals_unfused_knob(ort):
     assert float(np.abs(fused - unfused).max()) <= TOL * scale
 
 
+def test_inverted_residuals_b16_knob(ort):
+    """VSO_IR_B16=0 (read at the first plan of a process, in a child process):
+    a bf16 session's blocks on the f32 form (k_ir), equal within the f32 bar
+    to the bf16x3 form (k_ir_b16) of this process."""
+    import subprocess
+    import sys
+    code = ("import numpy as np, sys; sys.path.insert(0, 'tests'); import onnx_models as M; "
+            "import importlib.util, os; spec = importlib.util.spec_from_file_location('vss_amd', "
+            "'video-stream-segmenetation_amd/__init__.py', submodule_search_locations=['video-stream-segmenetation_amd']); "
+            "m = importlib.util.module_from_spec(spec); sys.modules['vss_amd'] = m; spec.loader.exec_module(m); "
+            "import vss_amd.ort as o; d = M.ir_chain(); "
+            "x = np.random.default_rng(14).standard_normal((2, 16, 38, 67)).astype(np.float32); "
+            "s = o.InferenceSession(d, precision='bf16'); r = s.run({'x': x}); "
+            "print(sum('k_ir<' in n for n in s.launches()), sum('k_ir_b16<' in n for n in s.launches())); "
+            "np.save('gpurun_out/ir_f32form.npy', np.concatenate([v.ravel() for v in r.values()]))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, VSO_IR_B16="0"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split()[-2:] == ["11", "0"], r.stdout
+    data = M.ir_chain()
+    x = np.random.default_rng(14).standard_normal((2, 16, 38, 67)).astype(np.float32)
+    with ort.InferenceSession(data, precision="bf16") as s:
+        b16 = np.concatenate([v.ravel() for v in s.run({"x": x}).values()])
+    f32 = np.load(os.path.join(root, "gpurun_out", "ir_f32form.npy"))
+    scale = max(1.0, float(np.abs(f32).max()))
+    err = float(np.abs(b16 - f32).max())
+    print(f"ir_chain bf16x3 vs f32 form: max abs err {err:.3e} (scale {scale:.2f})")
+    assert err <= TOL * scale
+
+
 @pytest.mark.parametrize("precision", ["bf16", "f16", "f32"])
 def test_conv_up_into_thin_head(ort, precision):
     """Resize -> Concat -> 1x1 head of 3 outputs: the thin head launches the

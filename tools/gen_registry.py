@@ -33,7 +33,9 @@ def r4(v):
     return (v + 3) & ~3
 
 
-SWZ = True  # VSS_SWZ in csrc/vss_kernels.h: the round-5 bank-conflict-free LDS layouts
+# VSS_SWZ in csrc/vss_kernels.h: the round-5 bank-conflict-free LDS layouts
+# (env VSS_SWZ=0: round 4's, for a -DVSS_SWZ=0 build: tools/build_variant.sh)
+SWZ = os.environ.get("VSS_SWZ", "1") != "0"
 
 
 def stem_xwp(iw):
@@ -159,7 +161,7 @@ def main():
     for name, key, lds, nacc in entries:
         args = ", ".join(str(v) for v in key)
         lines.append(f"VSS_BLOCK({args})  // {name}: {lds // 1024} KiB LDS, {nacc} acc")
-    csrc = os.path.join(ROOT, "video-stream-segmenetation_amd", "csrc")
+    csrc = os.environ.get("VSS_REGISTRY_DIR") or os.path.join(ROOT, "video-stream-segmenetation_amd", "csrc")
     open(os.path.join(csrc, "vss_registry.inc"), "w").write("\n".join(lines) + "\n")
     # the same lines dealt round-robin to the shard files the Makefile compiles in parallel
     for k in range(SHARDS):

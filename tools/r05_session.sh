@@ -25,9 +25,11 @@ if [ "${ONNX:-0}" = 1 ]; then
     -k "modnet_topology or inverted or conv_up or synthetic" > gpurun_out/${TAG}_onnx.log 2>&1; rc=$?
   tail -2 gpurun_out/${TAG}_onnx.log; grep -E "^(FAILED|ERROR)|max abs err|oracle" gpurun_out/${TAG}_onnx.log | cut -c1-200 | head -40; fatal $rc
   for k in 1 2; do
-    for ir in 1 0; do
-      VSO_IR=$ir timeout -k 10 200 python tools/bench_onnx.py --only-modnet --batch 8 --iters 50 > gpurun_out/${TAG}_modnet_ir$ir.log 2>&1; rc=$?
-      echo "VSO_IR=$ir: $(grep -h '^{' gpurun_out/${TAG}_modnet_ir$ir.log | grep b8_bf16 | cut -c1-160)"; fatal $rc
+    for arm in "1 1" "1 0" "0 1"; do
+      set -- $arm
+      VSO_IR=$1 VSO_IR_B16=$2 timeout -k 10 200 python tools/bench_onnx.py --only-modnet --batch 8 --iters 50 \
+        > gpurun_out/${TAG}_modnet_ir$1$2.log 2>&1; rc=$?
+      echo "VSO_IR=$1 VSO_IR_B16=$2: $(grep -h '^{' gpurun_out/${TAG}_modnet_ir$1$2.log | grep b8_bf16 | cut -c1-160)"; fatal $rc
     done
   done
 fi
