@@ -276,18 +276,28 @@ def test_conv_up_into_thin_head(ort, precision):
 
 
 # MODNet's matte (a sigmoid in [0, 1]) with 16-bit convolution operands, on
-# the graph as exported (InstanceNormalization epsilon 1e-5 everywhere; round 3
-# ran the 16-bit cases at 1e-3).  Every InstanceNorm input channel of the
-# seeded net has a variance far above that epsilon on the test frame (the
-# smallest, 0.018, in the 144x256 one; test_modnet_instance_norm_conditioning
-# checks it), so the norm does not blow up operand rounding.  The q4f16 form
+# the graph as exported (InstanceNormalization epsilon 1e-5 everywhere).  Every
+# InstanceNorm input channel of the seeded net has a variance far above that
+# epsilon on the test frame (test_modnet_instance_norm_conditioning), so the
+# norm does not blow up operand rounding.
+# The same-rounding bar: an oracle run with 16-bit operands is itself chaotic
+# at the 16-bit quantum — any difference before a rounding point (f32 vs f64
+# accumulation, a resize's arithmetic) flips some operands by one ulp, and
+# the flips grow through the 5x5 / 1280-channel LR convolutions and the
+# instance norms.  So each 16-bit case also runs the oracle on the input
+# scaled by (1 + 2^-22) — f32-rounding-sized noise — and the GPU is held to
+# 2x that self-distance ("flip floor", max and mean) from the same-rounding
+# oracle (measured: bf16 1.4e-2 against a floor of 1.0e-2, f16 2.3e-3
+# against 2.2e-3 — per stage, tools/modnet_taps.py: the backbone stays within
+# 6e-5 of the scale, the growth starts at the LR branch).  The q4f16 form
 # (the reference's model_q4f16.onnx arithmetic, main.ts:6, model.ts:12-29)
-# carries f16 weights, so f16 operands round only its activations: the oracle
-# itself moves 0.0018 max between f32 and f16 operands, and the GPU is held to
-# 1e-2 of the same-rounding oracle and of the f32 one.  bf16 operands round
-# the f32-form weights too (8-bit mantissa): 0.089 max in the oracle alone,
-# a measured precision cost, bounded and reported.
-MODNET_TOL = {"f32": TOL, "f16": 1e-2}       # vs the oracle with the same operand rounding
+# carries f16 weights, so f16 operands round only its activations: held to
+# 2e-3 of the f32 oracle too (measured 1.76e-3; the oracle's own f16 cost
+# 1.76e-3).  bf16 operands round the f32-form weights too (8-bit mantissa):
+# 0.089 max from the f32 oracle in the oracle alone, bounded and reported.
+MODNET_TOL = {"f32": TOL, "f16": 2e-3}       # f32: vs the f32 oracle; f16: vs the f32 oracle
+MODNET_FLIP = 2.0                            # 16-bit: x the oracle's flip floor, max and mean
+MODNET_FLIP_EPS = 2.0 ** -22                 # the floor's input perturbation (relative)
 MODNET_BF16_COST = (0.15, 0.02)              # (max, mean) vs the f32 oracle: bf16 rounding, not parity
 MODNET_IN_EPS = {"f32": 1e-5, "f16": 1e-5, "bf16": 1e-5}  # the export's own epsilon
 
@@ -302,6 +312,8 @@ def modnet_cases():
         want = {"f32": R.run(m, {"input": x})}
         if prec != "f32":
             want[prec] = R.run(m, {"input": x}, conv_operands=prec)
+            xp = (x * np.float32(1 + MODNET_FLIP_EPS)).astype(np.float32)
+            want["floor"] = R.run(m, {"input": xp}, conv_operands=prec)
         cases[(q4f16, prec)] = (data, x, want)
     return cases
 
@@ -311,8 +323,9 @@ def test_modnet_topology_288x512(ort, modnet_cases, q4f16, precision):
     """The public MODNet topology at the reference's 288x512
     (onnx_models.modnet; frameProcessorTest.ts:91), f32 and q4f16 forms, on
     k_conv_tile with f32 operands (1e-4 of the f32 oracle), f16 operands (the
-    reference's q4f16 arithmetic: 1e-2 of the same-rounding oracle, and of the
-    f32 one) and bf16 operands (the precision's cost, bounded and reported)."""
+    reference's q4f16 arithmetic: 2e-3 of the f32 oracle) and bf16 operands;
+    both 16-bit forms within 2x the flip floor of the same-rounding oracle
+    (max and mean)."""
     data, x, wants = modnet_cases[(q4f16, precision)]
     label = f"modnet {'q4f16' if q4f16 else 'f32'} {precision}"
     with ort.InferenceSession(data, precision=precision) as s:
@@ -330,17 +343,17 @@ def test_modnet_topology_288x512(ort, modnet_cases, q4f16, precision):
         print(f"{label}: vs the f32 oracle max abs err {err:.3e}, mean {mean:.3e}")
         if precision == "f32":
             assert err <= MODNET_TOL["f32"], (label, err)
-        elif precision == "f16":
-            same = wants["f16"][k]
-            e16 = float(np.abs(got[k] - same).max())
-            print(f"{label}: vs the f16-operand oracle max abs err {e16:.3e}; oracle f16 vs f32 "
-                  f"{float(np.abs(same - w).max()):.3e}")
-            assert e16 <= MODNET_TOL["f16"] and err <= MODNET_TOL["f16"], (label, e16, err)
         else:
-            same = wants["bf16"][k]
-            print(f"{label}: vs the bf16-operand oracle max abs err {float(np.abs(got[k] - same).max()):.3e}; "
-                  f"oracle bf16 vs f32 {float(np.abs(same - w).max()):.3e}")
-            assert err <= MODNET_BF16_COST[0] and mean <= MODNET_BF16_COST[1], (label, err, mean)
+            same, fl = wants[precision][k], wants["floor"][k]
+            es, ms = float(np.abs(got[k] - same).max()), float(np.abs(got[k] - same).mean())
+            fmax, fmean = float(np.abs(fl - same).max()), float(np.abs(fl - same).mean())
+            print(f"{label}: vs the {precision}-operand oracle max abs err {es:.3e}, mean {ms:.3e}; flip floor "
+                  f"max {fmax:.3e}, mean {fmean:.3e}; oracle {precision} vs f32 {float(np.abs(same - w).max()):.3e}")
+            assert es <= MODNET_FLIP * fmax and ms <= MODNET_FLIP * fmean, (label, es, ms, fmax, fmean)
+            if precision == "f16":
+                assert err <= MODNET_TOL["f16"], (label, err)
+            else:
+                assert err <= MODNET_BF16_COST[0] and mean <= MODNET_BF16_COST[1], (label, err, mean)
         assert np.array_equal(got[k], again[k])  # split-K reduction order is fixed
 
 

@@ -61,7 +61,8 @@ def report(launches_path, trace_path):
     grid = [None] * L
     for i, r in enumerate(rows):
         k = i % L
-        assert r["Kernel_Name"].split("(")[0] == names[k].split("(")[0], (k, r["Kernel_Name"], names[k])
+        base = lambda n: n.split("(")[0].replace("void ", "")
+        assert base(r["Kernel_Name"]) == base(names[k]), (k, r["Kernel_Name"], names[k])
         dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
         grid[k] = (r.get("Grid_Size_X") or r.get("Grid_X"), r.get("Grid_Size_Y") or r.get("Grid_Y"),
                    r.get("Grid_Size_Z") or r.get("Grid_Z"))

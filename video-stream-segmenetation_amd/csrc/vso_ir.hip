@@ -34,6 +34,9 @@
 // are 1x1 / grouped: onnx_ref.tiled_conv() rounds none of them either).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstring>
+
 #include "vso_device.h"
 #include "vso_kernels.h"
 
@@ -76,7 +79,7 @@ template <int NCB, typename Res>
 __device__ __forceinline__ void ir_finish(const IrParams& p, f4 (&acc)[NCB], bool outw, int t, int ks, int n, int oy0,
                                           int ox0, Res res) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-  if (p.ks > 1) {
+  if (p.ks > 1 && !(p.probe & 16)) {
     const long blk = (long)n * p.tiles + t;
     if (outw) {
       uint64_t* part = reinterpret_cast<uint64_t*>(p.part) + ((blk * p.ks + ks) * 4 + wave) * (NCB * 64 * 2);
@@ -262,16 +265,20 @@ __global__ __launch_bounds__(256) void k_ir(IrParams p) {
 // precision (these convolutions stay unrounded in onnx_ref's bf16 / f16
 // oracle, tiled_conv()) at 3 bf16 MFMAs (48 cycles) per 32 channels where
 // the f32 form takes 8 v_mfma_f32_16x16x4_f32 (256 cycles).
-//   input   — each wave's region blocks loaded straight into registers, split
-//             once: lane (r, g) of block j holds channels 32t + 8g .. + 7 of
-//             pixel r as 8 bf16 hi and 8 lo (the B operands of every chunk);
-//             no staged copy in LDS, which holds the hidden planes only
-//             (14 / 39 KB: up to 4 workgroups per CU);
-//   expand  — A = W1 rows of the chunk, host-split [HID][32 NT2] hi / lo;
+//   prologue — the slice's whole weight block (ir_slab_build: every operand
+//             pre-split and pre-ordered) copied global -> LDS by 16-byte
+//             LDS-DMA, and each wave's region blocks loaded straight into
+//             registers and split once (lane (r, g) of block j: channels
+//             32t + 8g .. + 7 of pixel r, 8 bf16 hi + 8 lo: the B operands of
+//             every chunk) — one memory round trip per workgroup; the chunk
+//             loop then reads LDS only (a first form read the weights from
+//             L2 per chunk: the compiler's conservative vmcnt(0) waits exposed
+//             three round trips per chunk, 60-80 us for the deep blocks);
+//   expand  — A = the chunk's W1 rows from LDS (rows 2 mod 4 slots apart:
+//             conflict-free ds_read_b128);
 //   project — per PAIR of chunks (32 hidden channels = one MFMA's K): B = the
 //             two chunks' depthwise outputs (lane (r, g): channels 4g..4g+3 of
-//             each, split), A = W2 host-split and permuted to that order
-//             ([COUT pad][pair][g][8]).  Slices hold whole pairs (cps even).
+//             each, split), A = W2 rows from LDS.  Slices hold whole pairs.
 //   residual — read from x in HBM at the store (exact f32).
 typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
 typedef __bf16 bf4v __attribute__((ext_vector_type(4)));
@@ -284,18 +291,26 @@ template <int NT2, int NCB, int S, int TH>
 __global__ __launch_bounds__(256) void k_ir_b16(IrParams p) {
   using G = IrGeom<S, TH>;
   constexpr int IW = G::IW, P_IN = G::P_IN, NBI = G::NBI, HQ = G::HQ, NBW = (NBI + 3) / 4;
-  static_assert(TH <= 4, "one output row per wave");
+  static_assert(TH == 4, "one output row per wave, every wave");
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  unsigned char* lds = reinterpret_cast<unsigned char*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-  const int CIN = p.CIN, HID = p.HID, H = p.H, W = p.W, HW = H * W;
-  float* hbuf = smem;  // 2 x [4 planes][HQ][4]
+  const int CIN = p.CIN, H = p.H, W = p.W, HW = H * W;
+  float* hbuf = reinterpret_cast<float*>(lds + p.o_hid);  // 2 x [4 planes][HQ][4]
   const int t = blockIdx.x, ks = blockIdx.y, n = blockIdx.z;
   const int ty = t / p.tiles_x, tx = t - ty * p.tiles_x;
   const int oy0 = ty * TH, ox0 = G::TW * tx, iy0 = S * oy0 - 1, ix0 = S * ox0 - 1;
 
-  // ---- prologue: this wave's region blocks, split into bf16 hi / lo.
+  // ---- prologue: the slice's weights -> LDS (DMA), the region -> registers.
   // Pixels outside the image (and past the region) load the nearest image
   // pixel: their expand outputs are zeroed below, so they only need to be finite.
+  {
+    const unsigned char* gsl = p.slab + (long)ks * p.sl_bytes;
+    const int wb = __builtin_amdgcn_readfirstlane(wave * 1024);
+    for (int o = wb; o < ((p.probe & 1) ? 0 : p.sl_bytes); o += 4096)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(gsl + o + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(lds + o), 16, 0, 0);
+  }
   f4 xh[NBW][NT2], xl[NBW][NT2];
   {
     const float* xn = p.x + (long)n * CIN * HW;
@@ -303,14 +318,17 @@ __global__ __launch_bounds__(256) void k_ir_b16(IrParams p) {
     for (int j = 0; j < NBW; ++j) {
       const int pix = min((wave + 4 * j) * 16 + r, P_IN - 1), ly = pix / IW, lx = pix - ly * IW;
       const int off = min(max(iy0 + ly, 0), H - 1) * W + min(max(ix0 + lx, 0), W - 1);
+      float v[NT2][8];
+#pragma unroll
+      for (int u = 0; u < NT2; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[u][e] = (p.probe & 2) ? 0.f : xn[min(32 * u + 8 * g + e, CIN - 1) * HW + off];
 #pragma unroll
       for (int u = 0; u < NT2; ++u) {
         bf8v h, l;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const int c = 32 * u + 8 * g + e;
-          const float v = xn[min(c, CIN - 1) * HW + off];
-          const float x = c < CIN ? v : 0.f;
+          const float x = 32 * u + 8 * g + e < CIN ? v[u][e] : 0.f;
           const __bf16 b = (__bf16)x;
           h[e] = b;
           l[e] = (__bf16)(x - (float)b);
@@ -320,56 +338,46 @@ __global__ __launch_bounds__(256) void k_ir_b16(IrParams p) {
       }
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
-  const int nch = HID / 16, c0 = ks * p.cps, c1 = min(c0 + p.cps, nch);
-  const int cinp = NT2 * 32, npair = (nch + 1) / 2;
-  const bool outw = wave < TH;
-  f4 a1h[NT2], a1l[NT2];
-  auto load_a1 = [&](int c) {
-    const uint16_t* rh = p.w1h + (long)(c * 16 + r) * cinp + 8 * g;
-    const uint16_t* rl = p.w1l + (long)(c * 16 + r) * cinp + 8 * g;
-#pragma unroll
-    for (int u = 0; u < NT2; ++u) {
-      a1h[u] = *reinterpret_cast<const f4*>(rh + 32 * u);
-      a1l[u] = *reinterpret_cast<const f4*>(rl + 32 * u);
-    }
-  };
-  f4 acc[NCB], a2h[NCB], a2l[NCB];
+  const int nch = p.HID / 16, c0 = ks * p.cps, c1 = min(c0 + p.cps, nch), c16 = p.cps * 16;
+  const unsigned char* w1h = lds;
+  const unsigned char* w1l = lds + p.o_w1l;
+  const unsigned char* w2h = lds + p.o_w2h;
+  const unsigned char* w2l = lds + p.o_w2l;
+  const float* wds = reinterpret_cast<const float*>(lds + p.o_wd);
+  const float* bds = reinterpret_cast<const float*>(lds + p.o_bd);
+  const float* b1s = reinterpret_cast<const float*>(lds + p.o_b1);
+  f4 acc[NCB];
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) acc[cb] = f4{0.f, 0.f, 0.f, 0.f};
   bf4v dh0 = bf4v{}, dl0 = bf4v{};  // the first chunk of a pair: its depthwise output, split
-  if (c0 < c1) load_a1(c0);
   for (int c = c0; c < c1; ++c) {
-    const bool first = ((c - c0) & 1) == 0;
-    float* hid = hbuf + ((c - c0) & 1) * (16 * HQ);
-    const int h0 = c * 16;
-    const f4 b1v = *reinterpret_cast<const f4*>(p.b1 + h0 + 4 * g);
-    f4 wd[9], bd = f4{0.f, 0.f, 0.f, 0.f};
-    if (outw) {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) wd[k] = *reinterpret_cast<const f4*>(p.wdw + k * HID + h0 + 4 * g);
-      bd = *reinterpret_cast<const f4*>(p.bdw + h0 + 4 * g);
-      if (first) {  // the pair's project weights: in flight during two expands
-        const int pr = c >> 1;
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) {
-          const long o = (((long)(cb * 16 + r) * npair + pr) * 4 + g) * 8;
-          a2h[cb] = *reinterpret_cast<const f4*>(p.w2h + o);
-          a2l[cb] = *reinterpret_cast<const f4*>(p.w2l + o);
-        }
-      }
-    }
+    const int cl = c - c0;
+    const bool first = (cl & 1) == 0;
+    float* hid = hbuf + (cl & 1) * (16 * HQ);
     // expand: D[hidden 4g + i][pixel r] of this wave's region blocks
+    f4 a1h[NT2], a1l[NT2];
+#pragma unroll
+    for (int u = 0; u < NT2; ++u) {
+      const int o = ((cl * 16 + r) * p.s1 + 4 * u + g) * 16;
+      a1h[u] = *reinterpret_cast<const f4*>(w1h + o);
+      a1l[u] = *reinterpret_cast<const f4*>(w1l + o);
+    }
+    const f4 b1v = *reinterpret_cast<const f4*>(b1s + cl * 16 + 4 * g);
 #pragma unroll
     for (int j = 0; j < NBW; ++j) {
       const int pb = wave + 4 * j;
       if (pb < NBI) {
         f4 d = b1v;
+        if (!(p.probe & 4)) {
 #pragma unroll
-        for (int u = 0; u < NT2; ++u) {
-          d = mfma_bf(a1l[u], xh[j][u], d);
-          d = mfma_bf(a1h[u], xl[j][u], d);
-          d = mfma_bf(a1h[u], xh[j][u], d);
+          for (int u = 0; u < NT2; ++u) {
+            d = mfma_bf(a1l[u], xh[j][u], d);
+            d = mfma_bf(a1h[u], xl[j][u], d);
+            d = mfma_bf(a1h[u], xh[j][u], d);
+          }
         }
         const int pix = pb * 16 + r, ly = pix / IW, lx = pix - ly * IW;
         const bool in = pix < P_IN && (unsigned)(iy0 + ly) < (unsigned)H && (unsigned)(ix0 + lx) < (unsigned)W;
@@ -380,48 +388,50 @@ __global__ __launch_bounds__(256) void k_ir_b16(IrParams p) {
       }
     }
     __syncthreads();
-    if (c + 1 < c1) load_a1(c + 1);  // the next chunk's expand fragments, in flight during the dw / project
-    if (outw) {
-      f4 a = bd;
+    // depthwise at output (oy0 + wave, ox0 + r), channels 16c + 4g .. + 3
+    f4 a = *reinterpret_cast<const f4*>(bds + cl * 16 + 4 * g);
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
+    for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int rp = (S * wave + ky) * IW + S * r + kx;
-          a = __builtin_elementwise_fma(wd[ky * 3 + kx], *reinterpret_cast<const f4*>(hid + (g * HQ + rp) * 4), a);
-        }
-      bf4v dh, dl;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float v = fminf(fmaxf(a[i], p.lo2), p.hi2);
-        const __bf16 b = (__bf16)v;
-        dh[i] = b;
-        dl[i] = (__bf16)(v - (float)b);
+      for (int kx = 0; kx < 3; ++kx) {
+        const f4 wk = *reinterpret_cast<const f4*>(wds + (ky * 3 + kx) * c16 + cl * 16 + 4 * g);
+        const int rp = (S * wave + ky) * IW + S * r + kx;
+        a = __builtin_elementwise_fma(wk, *reinterpret_cast<const f4*>(hid + (g * HQ + rp) * 4), a);
       }
-      if (first && c + 1 < c1) {
-        dh0 = dh;
-        dl0 = dl;
-      } else {
-        // project the pair: B lane (r, g) = (first chunk's 4g..4g+3, second's)
-        const bf4v z = bf4v{};
-        const bf8v bh = first ? __builtin_shufflevector(dh, z, 0, 1, 2, 3, 4, 5, 6, 7)
-                              : __builtin_shufflevector(dh0, dh, 0, 1, 2, 3, 4, 5, 6, 7);
-        const bf8v bl = first ? __builtin_shufflevector(dl, z, 0, 1, 2, 3, 4, 5, 6, 7)
-                              : __builtin_shufflevector(dl0, dl, 0, 1, 2, 3, 4, 5, 6, 7);
-        const f4 fh = __builtin_bit_cast(f4, bh), fl = __builtin_bit_cast(f4, bl);
+    bf4v dh, dl;
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) {
-          acc[cb] = mfma_bf(a2l[cb], fh, acc[cb]);
-          acc[cb] = mfma_bf(a2h[cb], fl, acc[cb]);
-          acc[cb] = mfma_bf(a2h[cb], fh, acc[cb]);
-        }
+    for (int i = 0; i < 4; ++i) {
+      const float v = fminf(fmaxf(a[i], p.lo2), p.hi2);
+      const __bf16 b = (__bf16)v;
+      dh[i] = b;
+      dl[i] = (__bf16)(v - (float)b);
+    }
+    if (first && c + 1 < c1) {
+      dh0 = dh;
+      dl0 = dl;
+    } else {
+      // project the pair: B lane (r, g) = (first chunk's 4g..4g+3, second's)
+      const bf4v z = bf4v{};
+      const bf8v bh = first ? __builtin_shufflevector(dh, z, 0, 1, 2, 3, 4, 5, 6, 7)
+                            : __builtin_shufflevector(dh0, dh, 0, 1, 2, 3, 4, 5, 6, 7);
+      const bf8v bl = first ? __builtin_shufflevector(dl, z, 0, 1, 2, 3, 4, 5, 6, 7)
+                            : __builtin_shufflevector(dl0, dl, 0, 1, 2, 3, 4, 5, 6, 7);
+      const f4 fh = __builtin_bit_cast(f4, bh), fl = __builtin_bit_cast(f4, bl);
+      const int qo = (cl >> 1) * 4 + g;
+#pragma unroll
+      for (int cb = 0; cb < ((p.probe & 8) ? 0 : NCB); ++cb) {
+        const int o = ((cb * 16 + r) * p.s2 + qo) * 16;
+        const f4 ah = *reinterpret_cast<const f4*>(w2h + o), al = *reinterpret_cast<const f4*>(w2l + o);
+        acc[cb] = mfma_bf(al, fh, acc[cb]);
+        acc[cb] = mfma_bf(ah, fl, acc[cb]);
+        acc[cb] = mfma_bf(ah, fh, acc[cb]);
       }
     }
   }
 
   // ---- epilogue ----
   const float* xres = p.x + (long)n * CIN * HW + (long)(oy0 + wave) * W + ox0 + r;
-  ir_finish<NCB>(p, acc, outw, t, ks, n, oy0, ox0, [&](int ch) { return xres[(long)ch * HW]; });
+  ir_finish<NCB>(p, acc, true, t, ks, n, oy0, ox0, [&](int ch) { return xres[(long)ch * HW]; });
 }
 
 // ---- host side ----
@@ -431,9 +441,11 @@ struct IrEntry {
   void (*fn)(IrParams);
   const char* name;
 };
-#define VSO_IR(NT, NCB, S, TH) {NT, NCB, S, TH, k_ir<NT, NCB, S, TH>, "vso::k_ir<" #NT ", " #NCB ", " #S ", " #TH ">"},
+// (names as the other launches': the kernel's demangled signature)
+#define VSO_IR(NT, NCB, S, TH) \
+  {NT, NCB, S, TH, k_ir<NT, NCB, S, TH>, "void vso::k_ir<" #NT ", " #NCB ", " #S ", " #TH ">(vso::IrParams)"},
 #define VSO_IR16(NT2, NCB, S, TH) \
-  {NT2, NCB, S, TH, k_ir_b16<NT2, NCB, S, TH>, "vso::k_ir_b16<" #NT2 ", " #NCB ", " #S ", " #TH ">"},
+  {NT2, NCB, S, TH, k_ir_b16<NT2, NCB, S, TH>, "void vso::k_ir_b16<" #NT2 ", " #NCB ", " #S ", " #TH ">(vso::IrParams)"},
 // MobileNetV2 1.0's blocks (t = 6): input channels / 16 (rounded up), output
 // channels / 16 (rounded up), stride — 16->24 s2, 24->24, 24->32 s2, 32->32,
 // 32->64 s2, 64->64, 64->96, 96->96, 96->160 s2, 160->160, 160->320
@@ -461,10 +473,103 @@ const IrEntry* ir_entry(const IrParams& p) {
 
 int ir_pstr(int stride) { return stride == 2 ? IrGeom<2, kIrTH>::PSTR : IrGeom<1, kIrTH>::PSTR; }
 
-size_t ir_lds_bytes(int cin, int stride, int b16) {
-  const int hq = stride == 2 ? IrGeom<2, kIrTH>::HQ : IrGeom<1, kIrTH>::HQ;
-  const int pad = stride == 2 ? IrGeom<2, kIrTH>::P_PAD : IrGeom<1, kIrTH>::P_PAD;
-  return ((b16 ? 0 : (size_t)ir_xs_floats(cin, ir_pstr(stride), pad)) + 2 * 16 * (size_t)hq) * 4;
+static size_t ir_hid_bytes(int stride) {
+  return 2 * 16 * (size_t)(stride == 2 ? IrGeom<2, kIrTH>::HQ : IrGeom<1, kIrTH>::HQ) * 4;
+}
+
+size_t ir_lds_bytes(const IrParams& p) {
+  if (p.b16) return (size_t)p.o_hid + ir_hid_bytes(p.stride);
+  const int pad = p.stride == 2 ? IrGeom<2, kIrTH>::P_PAD : IrGeom<1, kIrTH>::P_PAD;
+  return (size_t)ir_xs_floats(p.CIN, ir_pstr(p.stride), pad) * 4 + ir_hid_bytes(p.stride);
+}
+
+// The b16 slab: per slice, W1 hi / lo planes [cps * 16 rows][s1 slots of 16 B]
+// (slot t of row j: W1[16 c + j][8 t .. 8 t + 7], the expand A operand of lane
+// group t % 4 in K step t / 4), W2 hi / lo planes [16 NCB rows][s2 slots]
+// (slot 4 q + g of row m: W2[m][32 q' + 4g + i] (i < 4) then W2[m][32 q' + 16 +
+// 4g + i], q' the slice's q-th chunk pair: the project A operand of lane group
+// g), the depthwise taps [9][cps * 16], its bias, the expand bias (f32).  Row
+// strides of 2 mod 4 slots: the ds_read_b128 lane groups of an A read (rows
+// r, slots g) hit 16 distinct 16-byte bank groups.  sl_bytes is a whole
+// number of KiB (the prologue's DMA moves 1 KiB per wave instruction).
+static void ir_slab_layout(IrParams* p) {
+  const int nt2 = (p->CIN + 31) / 32, ncb = (p->COUT + 15) / 16, c16 = p->cps * 16;
+  p->s1 = 4 * nt2 + 2;
+  p->s2 = 4 * ((p->cps + 1) / 2) + 2;
+  const int w1 = c16 * p->s1 * 16, w2 = ncb * 16 * p->s2 * 16;
+  p->o_w1l = w1;
+  p->o_w2h = 2 * w1;
+  p->o_w2l = p->o_w2h + w2;
+  p->o_wd = p->o_w2l + w2;
+  p->o_bd = p->o_wd + 9 * c16 * 4;
+  p->o_b1 = p->o_bd + c16 * 4;
+  p->sl_bytes = (p->o_b1 + c16 * 4 + 1023) / 1024 * 1024;
+  p->o_hid = p->sl_bytes;
+}
+
+bool ir_slab_plan(IrParams* p, long wgs) {
+  const int nch = p->HID / 16;
+  const long wg0 = (long)p->N * p->tiles;
+  int ks = (int)std::min<long>(nch, std::max<long>(1, (wgs + wg0 / 2) / wg0));
+  int cps = (nch + ks - 1) / ks;
+  if (cps < nch) cps += cps & 1;  // slices of whole chunk pairs
+  for (;;) {
+    p->cps = cps;
+    ir_slab_layout(p);
+    if (ir_lds_bytes(*p) <= 160 * 1024) break;
+    if (cps <= 2) return false;
+    cps = cps >= nch ? (nch - 1) & ~1 : cps - 2;
+    if (cps < 2) return false;
+  }
+  p->ks = (nch + p->cps - 1) / p->cps;
+  return true;
+}
+
+void ir_slab_build(const IrParams& p, const float* w1, const float* b1, const float* wdt, const float* bd,
+                   const float* w2, std::vector<unsigned char>* out) {
+  const int nch = p.HID / 16, c16 = p.cps * 16, ncb = (p.COUT + 15) / 16;
+  out->assign((size_t)p.ks * p.sl_bytes, 0);
+  auto bf = [](float f) {  // nearest even (f finite)
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+  };
+  auto split = [&](float w, uint16_t* h, uint16_t* l) {
+    *h = bf(w);
+    const uint32_t hb = (uint32_t)*h << 16;
+    float hf;
+    std::memcpy(&hf, &hb, 4);
+    *l = bf(w - hf);
+  };
+  for (int k = 0; k < p.ks; ++k) {
+    unsigned char* b = out->data() + (size_t)k * p.sl_bytes;
+    const int c0 = k * p.cps, cn = std::min(p.cps, nch - c0);
+    for (int cl = 0; cl < cn; ++cl)
+      for (int j = 0; j < 16; ++j) {
+        const int h = 16 * (c0 + cl) + j;
+        for (int c = 0; c < p.CIN; ++c) {
+          const size_t o = ((size_t)(cl * 16 + j) * p.s1 + c / 8) * 16 + (c % 8) * 2;
+          split(w1[(size_t)h * p.CIN + c], reinterpret_cast<uint16_t*>(b + o),
+                reinterpret_cast<uint16_t*>(b + p.o_w1l + o));
+        }
+        for (int t = 0; t < 9; ++t)
+          std::memcpy(b + p.o_wd + ((size_t)t * c16 + cl * 16 + j) * 4, &wdt[(size_t)t * p.HID + h], 4);
+        std::memcpy(b + p.o_bd + (size_t)(cl * 16 + j) * 4, &bd[h], 4);
+        std::memcpy(b + p.o_b1 + (size_t)(cl * 16 + j) * 4, &b1[h], 4);
+      }
+    for (int m = 0; m < p.COUT; ++m)
+      for (int q = 0; q < (cn + 1) / 2; ++q)
+        for (int gg = 0; gg < 4; ++gg)
+          for (int i = 0; i < 8; ++i) {
+            const int h = 16 * c0 + 32 * q + (i < 4 ? 4 * gg + i : 16 + 4 * gg + i - 4);
+            if (h >= std::min(16 * (c0 + cn), p.HID)) continue;
+            const size_t o = ((size_t)m * p.s2 + 4 * q + gg) * 16 + i * 2;
+            split(w2[(size_t)m * p.HID + h], reinterpret_cast<uint16_t*>(b + p.o_w2h + o),
+                  reinterpret_cast<uint16_t*>(b + p.o_w2l + o));
+          }
+    (void)ncb;
+  }
 }
 
 void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles) {
@@ -474,7 +579,7 @@ void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles) {
 
 bool ir_supported(const IrParams& p) {
   return p.CIN % 4 == 0 && p.HID % 16 == 0 && (p.stride == 1 || p.stride == 2) && ir_entry(p) != nullptr &&
-         ir_lds_bytes(p.CIN, p.stride, p.b16) <= 160 * 1024 && (!p.res || (p.stride == 1 && p.CIN == p.COUT));
+         ir_lds_bytes(p) <= 160 * 1024 && (!p.res || (p.stride == 1 && p.CIN == p.COUT));
 }
 
 const char* ir_kernel_name(const IrParams& p) {
@@ -485,7 +590,7 @@ const char* ir_kernel_name(const IrParams& p) {
 void launch_ir(const IrParams& p, hipStream_t s) {
   const IrEntry* e = ir_entry(p);
   if (!e) return;
-  const size_t lds = ir_lds_bytes(p.CIN, p.stride, p.b16);
+  const size_t lds = ir_lds_bytes(p);
   (void)hipFuncSetAttribute((const void*)e->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(e->fn, dim3(p.tiles, p.ks, p.N), dim3(256), lds, s, p);
 }

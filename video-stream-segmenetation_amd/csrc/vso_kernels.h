@@ -3,6 +3,7 @@
 // float32 NCHW tensors; plain structs passed by value.
 #pragma once
 #include <cstdint>
+#include <vector>
 
 #include <hip/hip_runtime.h>
 
@@ -209,12 +210,16 @@ struct IrParams {
   const float* bdw;
   const float* w2;    // [COUT][HID], b2 [COUT]: project
   const float* b2;
-  // b16 (k_ir_b16, bf16 / f16 sessions): the 1x1 weights split into bf16 hi / lo,
-  // w1h / w1l [HID][32 ceil(CIN / 32)] (zero padded), w2h / w2l [16 NCB][pairs]
-  // [4][8]: row m, hidden pair q (32 channels), lane group g: W2[m][32q + 4g + i]
-  // (i < 4) then W2[m][32q + 16 + 4g + i] (zero past HID / COUT)
-  const uint16_t *w1h, *w1l, *w2h, *w2l;
-  int b16;
+  // b16 (k_ir_b16, bf16 / f16 sessions): each hidden-channel slice's weights
+  // as one contiguous block of sl_bytes (ir_slab_build: the 1x1 weights split
+  // into bf16 hi / lo planes in the MFMA operand order, rows padded for
+  // conflict-free LDS reads, then the depthwise taps and biases in f32),
+  // copied into LDS by the workgroup's prologue; o_*: byte offsets of the
+  // parts, s1 / s2: 16-byte slots per W1 / W2 row, o_hid: the hidden planes
+  const unsigned char* slab;
+  int b16, sl_bytes, o_w1l, o_w2h, o_w2l, o_wd, o_bd, o_b1, o_hid, s1, s2;
+  int probe;  // timing probes (VSO_IR_PROBE, results invalid): 1 no slab DMA, 2 no x loads,
+              // 4 no expand MFMAs, 8 no project MFMAs, 16 no split-K exchange
   float* y;           // [N][COUT][Ho][Wo], image n at y + n * (COUT * Ho * Wo + y_nx)
   long y_nx;
   int N, CIN, H, W, HID, COUT, Ho, Wo, stride, res;  // res: + x (stride 1, CIN == COUT)
@@ -227,7 +232,14 @@ struct IrParams {
 };
 bool ir_supported(const IrParams& p);
 int ir_pstr(int stride);
-size_t ir_lds_bytes(int cin, int stride, int b16);
+size_t ir_lds_bytes(const IrParams& p);
+// b16: choose the slices (p->cps / ks, LDS budget and ~wgs workgroups) and the
+// slab's layout (p->sl_bytes, offsets); then ir_slab_build writes every
+// slice's block: w1 [HID][CIN], b1 [HID], wdt [9][HID] (tap-major), bd [HID],
+// w2 [COUT][HID]
+bool ir_slab_plan(IrParams* p, long wgs);
+void ir_slab_build(const IrParams& p, const float* w1, const float* b1, const float* wdt, const float* bd,
+                   const float* w2, std::vector<unsigned char>* out);
 void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles);
 const char* ir_kernel_name(const IrParams& p);
 void launch_ir(const IrParams& p, hipStream_t s);

@@ -542,16 +542,6 @@ struct Planner {
     dev_consts[&c] = d;
     return d;
   }
-  const uint16_t* upload_u16(const std::vector<uint16_t>& v) {
-    uint16_t* d = nullptr;
-    if (!dalloc(&d, v.size() * 2)) return nullptr;
-    if (!v.empty() && hipMemcpy(d, v.data(), v.size() * 2, hipMemcpyHostToDevice) != hipSuccess) {
-      fail("constant upload failed");
-      return nullptr;
-    }
-    return d;
-  }
-
   const float* upload_vec(const std::vector<float>& v) {
     float* d = nullptr;
     if (!dalloc(&d, v.size() * 4)) return nullptr;
@@ -1006,16 +996,28 @@ struct Planner {
     p.stride = sd; p.res = res ? 1 : 0;
     p.lo1 = c1.a0; p.hi1 = c1.a1; p.lo2 = c2.a0; p.hi2 = c2.a1;
     p.b16 = s->conv_precision != PREC_F32 && ir_b16_enabled() ? 1 : 0;
-    if (!ir_supported(p)) return 0;
-    // slices of the hidden channels: about a workgroup per CU (256) over the
-    // tiles and slices, whole 16-channel chunks per slice
     ir_tiles(Ho, Wo, &p.tiles_x, &p.tiles);
+    // slices of the hidden channels: about a workgroup per CU (256; VSO_IR_WGS)
+    // over the tiles and slices, whole 16-channel chunks per slice (b16: whole
+    // chunk pairs, and the slice's weights within the LDS budget)
+    static const long wgs = [] {
+      const char* e = std::getenv("VSO_IR_WGS");
+      return e ? std::max(1L, std::atol(e)) : 256L;
+    }();
+    static const int probe = [] {
+      const char* e = std::getenv("VSO_IR_PROBE");
+      return e ? std::atoi(e) : 0;
+    }();
+    p.probe = probe;
     const int nch = HID / 16;
-    const long wg0 = (long)N * p.tiles;
-    int ks = (int)std::min<long>(nch, std::max<long>(1, (256 + wg0 / 2) / wg0));
-    p.cps = (nch + ks - 1) / ks;
-    if (p.b16 && p.cps < nch) p.cps += p.cps & 1;  // the bf16x3 form projects whole chunk pairs
-    p.ks = (nch + p.cps - 1) / p.cps;
+    if (p.b16 && (HID % 16 != 0 || !ir_slab_plan(&p, wgs))) return 0;
+    if (!ir_supported(p)) return 0;
+    if (!p.b16) {
+      const long wg0 = (long)N * p.tiles;
+      int ks = (int)std::min<long>(nch, std::max<long>(1, (wgs + wg0 / 2) / wg0));
+      p.cps = (nch + ks - 1) / ks;
+      p.ks = (nch + p.cps - 1) / p.cps;
+    }
     p.pstr = ir_pstr(sd);
     // weights: the expand / project as stored ([out][in]), the depthwise tap-major
     std::vector<float> wdt((size_t)9 * HID);
@@ -1032,34 +1034,14 @@ struct Planner {
     p.b2 = upload_vec(b2);
     if (!p.w1 || !p.b1 || !p.wdw || !p.bdw || !p.w2 || !p.b2) return -1;
     if (p.b16) {
-      // hi = bf16(w) (nearest even), lo = bf16(w - hi): vso_kernels.h IrParams
-      auto split = [](float w, uint16_t* h, uint16_t* l) {
-        *h = float_to_bf16(w);
-        const uint32_t hb = (uint32_t)*h << 16;
-        float hf;
-        std::memcpy(&hf, &hb, 4);
-        *l = float_to_bf16(w - hf);
-      };
-      const int cinp = (CIN + 31) / 32 * 32, np = (HID / 16 + 1) / 2, mp = (COUT + 15) / 16 * 16;
-      std::vector<uint16_t> w1h((size_t)HID * cinp, 0), w1l(w1h.size(), 0), w2h((size_t)mp * np * 32, 0),
-          w2l(w2h.size(), 0);
-      for (int h = 0; h < HID; ++h)
-        for (int c = 0; c < CIN; ++c)
-          split(w1->c.f[(size_t)h * CIN + c], &w1h[(size_t)h * cinp + c], &w1l[(size_t)h * cinp + c]);
-      for (int m = 0; m < COUT; ++m)
-        for (int q = 0; q < np; ++q)
-          for (int gg = 0; gg < 4; ++gg)
-            for (int i = 0; i < 8; ++i) {
-              const int h = 32 * q + (i < 4 ? 4 * gg + i : 16 + 4 * gg + i - 4);
-              if (h >= HID) continue;
-              const size_t o = (((size_t)m * np + q) * 4 + gg) * 8 + i;
-              split(w2->c.f[(size_t)m * HID + h], &w2h[o], &w2l[o]);
-            }
-      p.w1h = upload_u16(w1h);
-      p.w1l = upload_u16(w1l);
-      p.w2h = upload_u16(w2h);
-      p.w2l = upload_u16(w2l);
-      if (!p.w1h || !p.w1l || !p.w2h || !p.w2l) return -1;
+      std::vector<unsigned char> slab;
+      ir_slab_build(p, w1->c.f.data(), b1.data(), wdt.data(), bd.data(), w2->c.f.data(), &slab);
+      unsigned char* d = nullptr;
+      if (!dalloc(&d, slab.size()) || hipMemcpy(d, slab.data(), slab.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        fail("constant upload failed");
+        return -1;
+      }
+      p.slab = d;
     }
     if (p.ks > 1) {
       const size_t blocks = (size_t)N * p.tiles;
