@@ -69,69 +69,35 @@ __host__ __device__ constexpr int ir_xs_floats(int cin, int pstr, int p_pad) {
   return (f + 255) / 256 * 256;
 }
 
-// The epilogue of both forms.  ks > 1: the partial tile ([blk][slice][wave]
-// [cb][lane] as f4), write-through 8-byte agent-scope stores; the last slice
-// to arrive (any XCD) sums the slices in order with sc1 loads (k_conv_tile's
-// protocol, vso_conv.hip).  Then + b2 (+ the residual res(ch) of this lane's
-// output pixel, stride 1) and the store: wave w owns output row w, lane (r, g)
-// pixel r and channels cb * 16 + 4g + v.
+// The epilogue of both forms: wave w owns output row w, lane (r, g) pixel r
+// and channels cb * 16 + 4g + v.  ks == 1: + b2 (+ the residual res(ch) of
+// this lane's output pixel, stride 1) and the store.  ks > 1: the slice's
+// partial sums, plain stores into part [ks][N][COUT][Ho * Wo]; k_ir_reduce
+// (the next launch) adds the slices in order, then b2 and the residual — the
+// same operations in the same order as one workgroup summing them, spread
+// over the whole chip.  (An in-kernel exchange — partials written through to
+// L2, an arrival counter, the last workgroup of a tile reading every slice —
+// cost 25-80 us per deep block at batch 8: one CU reading 0.4-2.4 MB.)
 template <int NCB, typename Res>
 __device__ __forceinline__ void ir_finish(const IrParams& p, f4 (&acc)[NCB], bool outw, int t, int ks, int n, int oy0,
                                           int ox0, Res res) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-  if (p.ks > 1 && !(p.probe & 16)) {
-    const long blk = (long)n * p.tiles + t;
-    if (outw) {
-      uint64_t* part = reinterpret_cast<uint64_t*>(p.part) + ((blk * p.ks + ks) * 4 + wave) * (NCB * 64 * 2);
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        const uint64_t lo = (uint64_t)__float_as_uint(acc[cb][0]) | ((uint64_t)__float_as_uint(acc[cb][1]) << 32);
-        const uint64_t hi = (uint64_t)__float_as_uint(acc[cb][2]) | ((uint64_t)__float_as_uint(acc[cb][3]) << 32);
-        uint64_t* q = part + (cb * 64 + lane) * 2;
-        __hip_atomic_store(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __shared__ int last;
-    __syncthreads();
-    if (tid == 0) {
-      int* cnt = p.counters + blk;
-      const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = prev == p.ks - 1;
-      if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next run
-    }
-    __syncthreads();
-    if (!last || !outw) return;
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint64_t* base = reinterpret_cast<const uint64_t*>(p.part) + (blk * p.ks * 4 + wave) * (NCB * 64 * 2);
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      f4 sum = f4{0.f, 0.f, 0.f, 0.f};
-      for (int k0 = 0; k0 < p.ks; k0 += 8) {  // 8 slices' loads in flight, summed in slice order
-        uint64_t lo[8], hi[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (k0 + u < p.ks) {
-            const uint64_t* q = base + ((long)(k0 + u) * 4 * NCB * 64 + cb * 64 + lane) * 2;
-            lo[u] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            hi[u] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (k0 + u < p.ks)
-            sum += f4{__uint_as_float((uint32_t)lo[u]), __uint_as_float((uint32_t)(lo[u] >> 32)),
-                      __uint_as_float((uint32_t)hi[u]), __uint_as_float((uint32_t)(hi[u] >> 32))};
-      }
-      acc[cb] = sum;
-    }
-  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  (void)t;
   if (!outw) return;
   const int oy = oy0 + wave, ox = ox0 + r;
   if (oy >= p.Ho || ox >= p.Wo) return;
   const long plane = (long)p.Ho * p.Wo;
+  if (p.ks > 1 && !(p.probe & 16)) {
+    float* pn = p.part + (((long)ks * p.N + n) * p.COUT) * plane + (long)oy * p.Wo + ox;
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int ch = cb * 16 + 4 * g + v;
+        if (ch < p.COUT) pn[ch * plane] = acc[cb][v];
+      }
+    return;
+  }
   float* yn = p.y + (long)n * ((long)p.COUT * plane + p.y_nx) + (long)oy * p.Wo + ox;
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb)
@@ -144,6 +110,30 @@ __device__ __forceinline__ void ir_finish(const IrParams& p, f4 (&acc)[NCB], boo
         yn[ch * plane] = o;
       }
     }
+}
+
+// y = sum over the ks slices of part (in slice order) + b2 (+ x): one output
+// element per thread, the ks loads in flight together
+__global__ __launch_bounds__(256) void k_ir_reduce(IrParams p) {
+  const long plane = (long)p.Ho * p.Wo, per = (long)p.COUT * plane, total = (long)p.N * per;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int n = (int)(i / per);
+  const long rem = i - (long)n * per;
+  const int ch = (int)(rem / plane);
+  const long px = rem - (long)ch * plane;
+  float s = 0.f;
+  for (int k0 = 0; k0 < p.ks; k0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = k0 + u < p.ks ? p.part[(long)(k0 + u) * total + i] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (k0 + u < p.ks) s += v[u];
+  }
+  s += p.b2[ch];
+  if (p.res) s += p.x[((long)n * p.CIN + ch) * plane + px];  // stride 1: the same plane
+  p.y[(long)n * (per + p.y_nx) + rem] = s;
 }
 
 template <int NT, int NCB, int S, int TH>
@@ -585,6 +575,11 @@ bool ir_supported(const IrParams& p) {
 const char* ir_kernel_name(const IrParams& p) {
   const IrEntry* e = ir_entry(p);
   return e ? e->name : (p.b16 ? "vso::k_ir_b16<?>" : "vso::k_ir<?>");
+}
+
+void launch_ir_reduce(const IrParams& p, hipStream_t s) {
+  const long total = (long)p.N * p.COUT * p.Ho * p.Wo;
+  hipLaunchKernelGGL(k_ir_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
 }
 
 void launch_ir(const IrParams& p, hipStream_t s) {

@@ -227,8 +227,7 @@ struct IrParams {
   int pstr;           // floats between the staged input channels' rows in LDS (ir_pstr)
   int tiles_x, tiles; // output tiles per tile row / per image (ir_tiles)
   int ks, cps;        // hidden-channel slices per tile, 16-channel chunks per slice
-  float* part;        // ks > 1: partial tiles [N * tiles][ks][4][NCB][64] f4
-  int* counters;      // ks > 1: arrivals per tile [N * tiles], zero between runs
+  float* part;        // ks > 1: the slices' partial sums [ks][N][COUT][Ho][Wo] (k_ir_reduce adds them)
 };
 bool ir_supported(const IrParams& p);
 int ir_pstr(int stride);
@@ -243,6 +242,7 @@ void ir_slab_build(const IrParams& p, const float* w1, const float* b1, const fl
 void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles);
 const char* ir_kernel_name(const IrParams& p);
 void launch_ir(const IrParams& p, hipStream_t s);
+void launch_ir_reduce(const IrParams& p, hipStream_t s);  // ks > 1: the launch after launch_ir
 
 const char* conv_kernel_name(const ConvParams& p);
 // a depthwise -> 1x1 pair of N images of P pixels into M channels runs fused

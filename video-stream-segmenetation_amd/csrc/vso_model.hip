@@ -997,12 +997,13 @@ struct Planner {
     p.lo1 = c1.a0; p.hi1 = c1.a1; p.lo2 = c2.a0; p.hi2 = c2.a1;
     p.b16 = s->conv_precision != PREC_F32 && ir_b16_enabled() ? 1 : 0;
     ir_tiles(Ho, Wo, &p.tiles_x, &p.tiles);
-    // slices of the hidden channels: about a workgroup per CU (256; VSO_IR_WGS)
+    // slices of the hidden channels: about two workgroups per CU (512; VSO_IR_WGS:
+    // 256 measured 1.445 against 1.424 ms on MODNet batch 8 bf16, profiles/r05f)
     // over the tiles and slices, whole 16-channel chunks per slice (b16: whole
     // chunk pairs, and the slice's weights within the LDS budget)
     static const long wgs = [] {
       const char* e = std::getenv("VSO_IR_WGS");
-      return e ? std::max(1L, std::atol(e)) : 256L;
+      return e ? std::max(1L, std::atol(e)) : 512L;
     }();
     static const int probe = [] {
       const char* e = std::getenv("VSO_IR_PROBE");
@@ -1043,19 +1044,12 @@ struct Planner {
       }
       p.slab = d;
     }
-    if (p.ks > 1) {
-      const size_t blocks = (size_t)N * p.tiles;
-      if (!dalloc(&p.part, blocks * p.ks * 4 * ((COUT + 15) / 16) * 64 * 16) || !dalloc(&p.counters, blocks * 4))
-        return -1;
-      if (hipMemset(p.counters, 0, blocks * 4) != hipSuccess) {
-        fail("hipMemset failed");
-        return -1;
-      }
-    }
+    if (p.ks > 1 && !dalloc(&p.part, (size_t)p.ks * N * COUT * Ho * Wo * 4)) return -1;
     if (!set_runtime(out, {N, COUT, Ho, Wo})) return -1;
     p.y = dptr(vals[out]);
     auto pp = std::make_shared<IrParams>(p);
     add(ir_kernel_name(p), [pp](hipStream_t st) { launch_ir(*pp, st); });
+    if (p.ks > 1) add("void vso::k_ir_reduce(vso::IrParams)", [pp](hipStream_t st) { launch_ir_reduce(*pp, st); });
     for (int k : {k1, k2, k3, k4}) done.insert((size_t)k);
     if (res) done.insert((size_t)k5);
     s->ir_blocks++;
