@@ -168,7 +168,9 @@ def test_conv_upsample_fusion(ort, precision):
 def test_inverted_residuals_fused(ort, precision):
     """Every MobileNetV2 inverted residual of ir_chain as one launch
     (vso_ir.hip) — k_ir (exact f32 products) in f32 sessions, k_ir_b16 (the
-    1x1 products as hi + lo bf16 splits, ~2^-16 relative) in bf16 / f16 ones —
+    1x1 products as hi + lo bf16 splits, ~2^-16 relative; k_ir_b16w, its
+    wave-private form, for the 7 blocks of <= 64 input channels) in bf16 /
+    f16 ones —
     against the f64 oracle at the f32 bar (1e-4 of the output scale): the
     1x1 / depthwise convolutions are not k_conv_tile ones, and the oracle
     rounds none of them; and bitwise the same on a second run (the
@@ -181,8 +183,11 @@ def test_inverted_residuals_fused(ort, precision):
         again = s.run(feeds)
         names = s.launches()
         assert s.ir_blocks() == 11, names
-    kern = "k_ir<" if precision == "f32" else "k_ir_b16<"
-    assert sum(kern in n for n in names) == 11, names
+    if precision == "f32":
+        assert sum("k_ir<" in n for n in names) == 11, names
+    else:
+        assert sum("k_ir_b16<" in n for n in names) == 4, names
+        assert sum("k_ir_b16w<" in n for n in names) == 7, names
     assert not any("k_conv_dw" in n or "k_conv_small" in n for n in names), names
     for k, w in want.items():
         err = float(np.abs(got[k] - w).max())
@@ -222,10 +227,14 @@ def test_inverted_residuals_unfused_knob(ort):
     assert float(np.abs(fused - unfused).max()) <= TOL * scale
 
 
-def test_inverted_residuals_b16_knob(ort):
-    """VSO_IR_B16=0 (read at the first plan of a process, in a child process):
-    a bf16 session's blocks on the f32 form (k_ir), equal within the f32 bar
-    to the bf16x3 form (k_ir_b16) of this process."""
+@pytest.mark.parametrize("knob", ["VSO_IR_B16", "VSO_IR_WAVE"])
+def test_inverted_residuals_16bit_knobs(ort, knob):
+    """The 16-bit forms' knobs (read at the first plan of a process, so in a
+    child process), on a bf16 session of ir_chain: VSO_IR_B16=0 runs every
+    block on the f32 form (k_ir), equal within the f32 bar to the bf16x3 form
+    of this process; VSO_IR_WAVE=0 runs the small blocks on the shared form
+    (k_ir_b16) — the same operands, products and sums as the wave-private
+    one, so bitwise equal."""
     import subprocess
     import sys
     code = ("import numpy as np, sys; sys.path.insert(0, 'tests'); import onnx_models as M; "
@@ -234,24 +243,28 @@ def test_inverted_residuals_b16_knob(ort):
             "m = importlib.util.module_from_spec(spec); sys.modules['vss_amd'] = m; spec.loader.exec_module(m); "
             "import vss_amd.ort as o; d = M.ir_chain(); "
             "x = np.random.default_rng(14).standard_normal((2, 16, 38, 67)).astype(np.float32); "
-            "s = o.InferenceSession(d, precision='bf16'); r = s.run({'x': x}); "
-            "print(sum('k_ir<' in n for n in s.launches()), sum('k_ir_b16<' in n for n in s.launches())); "
-            "np.save('gpurun_out/ir_f32form.npy', np.concatenate([v.ravel() for v in r.values()]))")
+            "s = o.InferenceSession(d, precision='bf16'); r = s.run({'x': x}); L = s.launches(); "
+            "print(sum('k_ir<' in n for n in L), sum('k_ir_b16<' in n for n in L), sum('k_ir_b16w<' in n for n in L)); "
+            f"np.save('gpurun_out/ir_{knob}.npy', np.concatenate([v.ravel() for v in r.values()]))")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
-    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, VSO_IR_B16="0"),
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, **{knob: "0"}),
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
-    assert r.stdout.split()[-2:] == ["11", "0"], r.stdout
+    want_counts = ["11", "0", "0"] if knob == "VSO_IR_B16" else ["0", "11", "0"]
+    assert r.stdout.split()[-3:] == want_counts, r.stdout
     data = M.ir_chain()
     x = np.random.default_rng(14).standard_normal((2, 16, 38, 67)).astype(np.float32)
     with ort.InferenceSession(data, precision="bf16") as s:
-        b16 = np.concatenate([v.ravel() for v in s.run({"x": x}).values()])
-    f32 = np.load(os.path.join(root, "gpurun_out", "ir_f32form.npy"))
-    scale = max(1.0, float(np.abs(f32).max()))
-    err = float(np.abs(b16 - f32).max())
-    print(f"ir_chain bf16x3 vs f32 form: max abs err {err:.3e} (scale {scale:.2f})")
-    assert err <= TOL * scale
+        here = np.concatenate([v.ravel() for v in s.run({"x": x}).values()])
+    other = np.load(os.path.join(root, "gpurun_out", f"ir_{knob}.npy"))
+    scale = max(1.0, float(np.abs(other).max()))
+    err = float(np.abs(here - other).max())
+    print(f"ir_chain bf16 default vs {knob}=0: max abs err {err:.3e} (scale {scale:.2f})")
+    if knob == "VSO_IR_B16":
+        assert err <= TOL * scale
+    else:
+        assert np.array_equal(here, other)
 
 
 @pytest.mark.parametrize("precision", ["bf16", "f16", "f32"])

@@ -424,6 +424,163 @@ __global__ __launch_bounds__(256) void k_ir_b16(IrParams p) {
   ir_finish<NCB>(p, acc, true, t, ks, n, oy0, ox0, [&](int ch) { return xres[(long)ch * HW]; });
 }
 
+// ---- the bf16x3 form, wave-private (small input channel counts) ----
+// k_ir_b16 with no workgroup barrier in the chunk loop: wave w expands the
+// three region rows its own output row reads (S w .. S w + 2; the rows
+// between two waves' outputs are expanded by both — 2x the expand MFMAs at
+// stride 1, 1.33x at stride 2) into its own hidden planes, so the waves only
+// meet once, after the prologue's DMA.  For the wide, shallow blocks (MODNet
+// at /2 - /8: 16-64 input channels, 6-9 chunks, ~1000 workgroups) whose
+// chunks carry little MFMA work: there the per-chunk barrier and its LDS
+// round trips set the pace.  Same slab, operands, rounding and sums as
+// k_ir_b16 (bitwise the same outputs).
+template <int S>
+struct IrWaveGeom {
+  static constexpr int IW = IrGeom<S, 4>::IW, PW = 3 * IW, NB = (PW + 15) / 16;
+  static constexpr int HQ = NB * 16 + (S == 2 ? 1 : 0);  // quads per hidden plane
+};
+
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int NT2, int NCB, int S>
+__global__ __launch_bounds__(256) void k_ir_b16w(IrParams p) {
+  using WG = IrWaveGeom<S>;
+  constexpr int IW = WG::IW, PW = WG::PW, NB = WG::NB, HQ = WG::HQ, TW = 16, TH = 4;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  unsigned char* lds = reinterpret_cast<unsigned char*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int CIN = p.CIN, H = p.H, W = p.W, HW = H * W;
+  float* hid = reinterpret_cast<float*>(lds + p.o_hid) + wave * (16 * HQ);  // this wave's [4 planes][HQ][4]
+  const int t = blockIdx.x, ks = blockIdx.y, n = blockIdx.z;
+  const int ty = t / p.tiles_x, tx = t - ty * p.tiles_x;
+  const int oy0 = ty * TH, ox0 = TW * tx;
+  const int ry0 = S * (oy0 + wave) - 1, ix0 = S * ox0 - 1;  // this wave's region: rows ry0 .. ry0 + 2
+  {
+    const unsigned char* gsl = p.slab + (long)ks * p.sl_bytes;
+    const int wb = __builtin_amdgcn_readfirstlane(wave * 1024);
+    for (int o = wb; o < ((p.probe & 1) ? 0 : p.sl_bytes); o += 4096)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(gsl + o + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(lds + o), 16, 0, 0);
+  }
+  f4 xh[NB][NT2], xl[NB][NT2];
+  {
+    const float* xn = p.x + (long)n * CIN * HW;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int pix = min(j * 16 + r, PW - 1), ly = pix / IW, lx = pix - ly * IW;
+      const int off = min(max(ry0 + ly, 0), H - 1) * W + min(max(ix0 + lx, 0), W - 1);
+      float v[NT2][8];
+#pragma unroll
+      for (int u = 0; u < NT2; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[u][e] = (p.probe & 2) ? 0.f : xn[min(32 * u + 8 * g + e, CIN - 1) * HW + off];
+#pragma unroll
+      for (int u = 0; u < NT2; ++u) {
+        bf8v h, l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = 32 * u + 8 * g + e < CIN ? v[u][e] : 0.f;
+          const __bf16 b = (__bf16)x;
+          h[e] = b;
+          l[e] = (__bf16)(x - (float)b);
+        }
+        xh[j][u] = __builtin_bit_cast(f4, h);
+        xl[j][u] = __builtin_bit_cast(f4, l);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int nch = p.HID / 16, c0 = ks * p.cps, c1 = min(c0 + p.cps, nch), c16 = p.cps * 16;
+  const unsigned char* w1h = lds;
+  const unsigned char* w1l = lds + p.o_w1l;
+  const unsigned char* w2h = lds + p.o_w2h;
+  const unsigned char* w2l = lds + p.o_w2l;
+  const float* wds = reinterpret_cast<const float*>(lds + p.o_wd);
+  const float* bds = reinterpret_cast<const float*>(lds + p.o_bd);
+  const float* b1s = reinterpret_cast<const float*>(lds + p.o_b1);
+  f4 acc[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) acc[cb] = f4{0.f, 0.f, 0.f, 0.f};
+  bf4v dh0 = bf4v{}, dl0 = bf4v{};
+  for (int c = c0; c < c1; ++c) {
+    const int cl = c - c0;
+    const bool first = (cl & 1) == 0;
+    f4 a1h[NT2], a1l[NT2];
+#pragma unroll
+    for (int u = 0; u < NT2; ++u) {
+      const int o = ((cl * 16 + r) * p.s1 + 4 * u + g) * 16;
+      a1h[u] = *reinterpret_cast<const f4*>(w1h + o);
+      a1l[u] = *reinterpret_cast<const f4*>(w1l + o);
+    }
+    const f4 b1v = *reinterpret_cast<const f4*>(b1s + cl * 16 + 4 * g);
+    wave_fence();  // the previous chunk's depthwise reads of hid are done
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      f4 d = b1v;
+      if (!(p.probe & 4)) {
+#pragma unroll
+        for (int u = 0; u < NT2; ++u) {
+          d = mfma_bf(a1l[u], xh[j][u], d);
+          d = mfma_bf(a1h[u], xl[j][u], d);
+          d = mfma_bf(a1h[u], xh[j][u], d);
+        }
+      }
+      const int pix = j * 16 + r, ly = pix / IW, lx = pix - ly * IW;
+      const bool in = pix < PW && (unsigned)(ry0 + ly) < (unsigned)H && (unsigned)(ix0 + lx) < (unsigned)W;
+      f4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = in ? fminf(fmaxf(d[i], p.lo1), p.hi1) : 0.f;
+      *reinterpret_cast<f4*>(hid + (g * HQ + pix) * 4) = v;
+    }
+    wave_fence();
+    f4 a = *reinterpret_cast<const f4*>(bds + cl * 16 + 4 * g);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const f4 wk = *reinterpret_cast<const f4*>(wds + (ky * 3 + kx) * c16 + cl * 16 + 4 * g);
+        const int rp = ky * IW + S * r + kx;
+        a = __builtin_elementwise_fma(wk, *reinterpret_cast<const f4*>(hid + (g * HQ + rp) * 4), a);
+      }
+    bf4v dh, dl;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v = fminf(fmaxf(a[i], p.lo2), p.hi2);
+      const __bf16 b = (__bf16)v;
+      dh[i] = b;
+      dl[i] = (__bf16)(v - (float)b);
+    }
+    if (first && c + 1 < c1) {
+      dh0 = dh;
+      dl0 = dl;
+    } else {
+      const bf4v z = bf4v{};
+      const bf8v bh = first ? __builtin_shufflevector(dh, z, 0, 1, 2, 3, 4, 5, 6, 7)
+                            : __builtin_shufflevector(dh0, dh, 0, 1, 2, 3, 4, 5, 6, 7);
+      const bf8v bl = first ? __builtin_shufflevector(dl, z, 0, 1, 2, 3, 4, 5, 6, 7)
+                            : __builtin_shufflevector(dl0, dl, 0, 1, 2, 3, 4, 5, 6, 7);
+      const f4 fh = __builtin_bit_cast(f4, bh), fl = __builtin_bit_cast(f4, bl);
+      const int qo = (cl >> 1) * 4 + g;
+#pragma unroll
+      for (int cb = 0; cb < ((p.probe & 8) ? 0 : NCB); ++cb) {
+        const int o = ((cb * 16 + r) * p.s2 + qo) * 16;
+        const f4 ah = *reinterpret_cast<const f4*>(w2h + o), al = *reinterpret_cast<const f4*>(w2l + o);
+        acc[cb] = mfma_bf(al, fh, acc[cb]);
+        acc[cb] = mfma_bf(ah, fl, acc[cb]);
+        acc[cb] = mfma_bf(ah, fh, acc[cb]);
+      }
+    }
+  }
+  const float* xres = p.x + (long)n * CIN * HW + (long)(oy0 + wave) * W + ox0 + r;
+  ir_finish<NCB>(p, acc, true, t, ks, n, oy0, ox0, [&](int ch) { return xres[(long)ch * HW]; });
+}
+
 // ---- host side ----
 namespace {
 struct IrEntry {
@@ -448,13 +605,20 @@ const IrEntry kIr16[] = {
     VSO_IR16(1, 2, 2, 4) VSO_IR16(1, 2, 1, 4) VSO_IR16(1, 4, 2, 4) VSO_IR16(2, 4, 1, 4) VSO_IR16(2, 6, 1, 4)
     VSO_IR16(3, 6, 1, 4) VSO_IR16(3, 10, 2, 4) VSO_IR16(5, 10, 1, 4) VSO_IR16(5, 20, 1, 4) VSO_IR16(2, 4, 2, 4)
     VSO_IR16(3, 6, 2, 4)};
+// the wave-private form (k_ir_b16w) for <= 64 input channels
+#define VSO_IR16W(NT2, NCB, S) \
+  {NT2, NCB, S, 4, k_ir_b16w<NT2, NCB, S>, "void vso::k_ir_b16w<" #NT2 ", " #NCB ", " #S ">(vso::IrParams)"},
+const IrEntry kIr16w[] = {VSO_IR16W(1, 2, 2) VSO_IR16W(1, 2, 1) VSO_IR16W(1, 4, 2) VSO_IR16W(2, 4, 1)
+                              VSO_IR16W(2, 6, 1) VSO_IR16W(2, 4, 2)};
 #undef VSO_IR
 #undef VSO_IR16
+#undef VSO_IR16W
 
 const IrEntry* ir_entry(const IrParams& p) {
   const int nt = p.b16 ? (p.CIN + 31) / 32 : (p.CIN + 15) / 16, ncb = (p.COUT + 15) / 16;
-  const IrEntry* t = p.b16 ? kIr16 : kIr;
-  const size_t n = p.b16 ? sizeof(kIr16) / sizeof(kIr16[0]) : sizeof(kIr) / sizeof(kIr[0]);
+  const IrEntry* t = p.wv ? kIr16w : p.b16 ? kIr16 : kIr;
+  const size_t n = p.wv ? sizeof(kIr16w) / sizeof(kIr16w[0])
+                        : p.b16 ? sizeof(kIr16) / sizeof(kIr16[0]) : sizeof(kIr) / sizeof(kIr[0]);
   for (size_t i = 0; i < n; ++i)
     if (t[i].nt == nt && t[i].ncb == ncb && t[i].s == p.stride && t[i].th == kIrTH) return &t[i];
   return nullptr;
@@ -468,6 +632,8 @@ static size_t ir_hid_bytes(int stride) {
 }
 
 size_t ir_lds_bytes(const IrParams& p) {
+  if (p.wv)
+    return (size_t)p.o_hid + 4 * 16 * (size_t)(p.stride == 2 ? IrWaveGeom<2>::HQ : IrWaveGeom<1>::HQ) * 4;
   if (p.b16) return (size_t)p.o_hid + ir_hid_bytes(p.stride);
   const int pad = p.stride == 2 ? IrGeom<2, kIrTH>::P_PAD : IrGeom<1, kIrTH>::P_PAD;
   return (size_t)ir_xs_floats(p.CIN, ir_pstr(p.stride), pad) * 4 + ir_hid_bytes(p.stride);
@@ -574,7 +740,7 @@ bool ir_supported(const IrParams& p) {
 
 const char* ir_kernel_name(const IrParams& p) {
   const IrEntry* e = ir_entry(p);
-  return e ? e->name : (p.b16 ? "vso::k_ir_b16<?>" : "vso::k_ir<?>");
+  return e ? e->name : (p.wv ? "vso::k_ir_b16w<?>" : p.b16 ? "vso::k_ir_b16<?>" : "vso::k_ir<?>");
 }
 
 void launch_ir_reduce(const IrParams& p, hipStream_t s) {

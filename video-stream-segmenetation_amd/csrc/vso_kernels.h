@@ -218,6 +218,7 @@ struct IrParams {
   // parts, s1 / s2: 16-byte slots per W1 / W2 row, o_hid: the hidden planes
   const unsigned char* slab;
   int b16, sl_bytes, o_w1l, o_w2h, o_w2l, o_wd, o_bd, o_b1, o_hid, s1, s2;
+  int wv;     // b16 with CIN <= 64: the wave-private form (k_ir_b16w, VSO_IR_WAVE=0: off)
   int probe;  // timing probes (VSO_IR_PROBE, results invalid): 1 no slab DMA, 2 no x loads,
               // 4 no expand MFMAs, 8 no project MFMAs, 16 no split-K exchange
   float* y;           // [N][COUT][Ho][Wo], image n at y + n * (COUT * Ho * Wo + y_nx)

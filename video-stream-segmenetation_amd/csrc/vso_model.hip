@@ -1010,6 +1010,11 @@ struct Planner {
       return e ? std::atoi(e) : 0;
     }();
     p.probe = probe;
+    static const bool wave_form = [] {
+      const char* e = std::getenv("VSO_IR_WAVE");
+      return !(e && e[0] == '0');
+    }();
+    p.wv = p.b16 && wave_form && CIN <= 64 ? 1 : 0;
     const int nch = HID / 16;
     if (p.b16 && (HID % 16 != 0 || !ir_slab_plan(&p, wgs))) return 0;
     if (!ir_supported(p)) return 0;
