@@ -168,9 +168,7 @@ def test_conv_upsample_fusion(ort, precision):
 def test_inverted_residuals_fused(ort, precision):
     """Every MobileNetV2 inverted residual of ir_chain as one launch
     (vso_ir.hip) — k_ir (exact f32 products) in f32 sessions, k_ir_b16 (the
-    1x1 products as hi + lo bf16 splits, ~2^-16 relative; k_ir_b16w, its
-    wave-private form, for the 7 blocks of <= 64 input channels) in bf16 /
-    f16 ones —
+    1x1 products as hi + lo bf16 splits, ~2^-16 relative) in bf16 / f16 ones —
     against the f64 oracle at the f32 bar (1e-4 of the output scale): the
     1x1 / depthwise convolutions are not k_conv_tile ones, and the oracle
     rounds none of them; and bitwise the same on a second run (the
@@ -186,8 +184,7 @@ def test_inverted_residuals_fused(ort, precision):
     if precision == "f32":
         assert sum("k_ir<" in n for n in names) == 11, names
     else:
-        assert sum("k_ir_b16<" in n for n in names) == 4, names
-        assert sum("k_ir_b16w<" in n for n in names) == 7, names
+        assert sum("k_ir_b16<" in n for n in names) == 11, names
     assert not any("k_conv_dw" in n or "k_conv_small" in n for n in names), names
     for k, w in want.items():
         err = float(np.abs(got[k] - w).max())
@@ -227,14 +224,14 @@ def test_inverted_residuals_unfused_knob(ort):
     assert float(np.abs(fused - unfused).max()) <= TOL * scale
 
 
-@pytest.mark.parametrize("knob", ["VSO_IR_B16", "VSO_IR_WAVE"])
-def test_inverted_residuals_16bit_knobs(ort, knob):
+@pytest.mark.parametrize("knob,value", [("VSO_IR_B16", "0"), ("VSO_IR_WAVE", "1")])
+def test_inverted_residuals_16bit_knobs(ort, knob, value):
     """The 16-bit forms' knobs (read at the first plan of a process, so in a
     child process), on a bf16 session of ir_chain: VSO_IR_B16=0 runs every
     block on the f32 form (k_ir), equal within the f32 bar to the bf16x3 form
-    of this process; VSO_IR_WAVE=0 runs the small blocks on the shared form
-    (k_ir_b16) — the same operands, products and sums as the wave-private
-    one, so bitwise equal."""
+    of this process; VSO_IR_WAVE=1 runs the 7 blocks of <= 64 input channels
+    on the wave-private form (k_ir_b16w, measured slower on MODNet: opt-in) —
+    the same operands, products and sums as k_ir_b16, so bitwise equal."""
     import subprocess
     import sys
     code = ("import numpy as np, sys; sys.path.insert(0, 'tests'); import onnx_models as M; "
@@ -248,10 +245,10 @@ def test_inverted_residuals_16bit_knobs(ort, knob):
             f"np.save('gpurun_out/ir_{knob}.npy', np.concatenate([v.ravel() for v in r.values()]))")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
-    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, **{knob: "0"}),
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, **{knob: value}),
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
-    want_counts = ["11", "0", "0"] if knob == "VSO_IR_B16" else ["0", "11", "0"]
+    want_counts = ["11", "0", "0"] if knob == "VSO_IR_B16" else ["0", "4", "7"]
     assert r.stdout.split()[-3:] == want_counts, r.stdout
     data = M.ir_chain()
     x = np.random.default_rng(14).standard_normal((2, 16, 38, 67)).astype(np.float32)
@@ -260,7 +257,7 @@ def test_inverted_residuals_16bit_knobs(ort, knob):
     other = np.load(os.path.join(root, "gpurun_out", f"ir_{knob}.npy"))
     scale = max(1.0, float(np.abs(other).max()))
     err = float(np.abs(here - other).max())
-    print(f"ir_chain bf16 default vs {knob}=0: max abs err {err:.3e} (scale {scale:.2f})")
+    print(f"ir_chain bf16 default vs {knob}={value}: max abs err {err:.3e} (scale {scale:.2f})")
     if knob == "VSO_IR_B16":
         assert err <= TOL * scale
     else:

@@ -663,10 +663,15 @@ static void ir_slab_layout(IrParams* p) {
   p->o_hid = p->sl_bytes;
 }
 
-bool ir_slab_plan(IrParams* p, long wgs) {
+bool ir_slab_plan(IrParams* p, long wgs, int cps_target) {
   const int nch = p->HID / 16;
   const long wg0 = (long)p->N * p->tiles;
   int ks = (int)std::min<long>(nch, std::max<long>(1, (wgs + wg0 / 2) / wg0));
+  if (cps_target > 0) {  // about cps_target chunks per slice, at least one chip's worth of workgroups
+    ks = (nch + cps_target - 1) / cps_target;
+    if (wg0 * ks < 256) ks = (int)std::min<long>(nch, (256 + wg0 - 1) / wg0);
+    if (wg0 >= 1024) ks = 1;
+  }
   int cps = (nch + ks - 1) / ks;
   if (cps < nch) cps += cps & 1;  // slices of whole chunk pairs
   for (;;) {

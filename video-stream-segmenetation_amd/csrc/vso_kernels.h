@@ -218,7 +218,7 @@ struct IrParams {
   // parts, s1 / s2: 16-byte slots per W1 / W2 row, o_hid: the hidden planes
   const unsigned char* slab;
   int b16, sl_bytes, o_w1l, o_w2h, o_w2l, o_wd, o_bd, o_b1, o_hid, s1, s2;
-  int wv;     // b16 with CIN <= 64: the wave-private form (k_ir_b16w, VSO_IR_WAVE=0: off)
+  int wv;     // b16 with CIN <= 64: the wave-private form (k_ir_b16w; opt-in, VSO_IR_WAVE=1)
   int probe;  // timing probes (VSO_IR_PROBE, results invalid): 1 no slab DMA, 2 no x loads,
               // 4 no expand MFMAs, 8 no project MFMAs, 16 no split-K exchange
   float* y;           // [N][COUT][Ho][Wo], image n at y + n * (COUT * Ho * Wo + y_nx)
@@ -237,7 +237,7 @@ size_t ir_lds_bytes(const IrParams& p);
 // slab's layout (p->sl_bytes, offsets); then ir_slab_build writes every
 // slice's block: w1 [HID][CIN], b1 [HID], wdt [9][HID] (tap-major), bd [HID],
 // w2 [COUT][HID]
-bool ir_slab_plan(IrParams* p, long wgs);
+bool ir_slab_plan(IrParams* p, long wgs, int cps_target);
 void ir_slab_build(const IrParams& p, const float* w1, const float* b1, const float* wdt, const float* bd,
                    const float* w2, std::vector<unsigned char>* out);
 void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles);

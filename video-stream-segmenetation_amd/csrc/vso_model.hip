@@ -1012,11 +1012,19 @@ struct Planner {
     p.probe = probe;
     static const bool wave_form = [] {
       const char* e = std::getenv("VSO_IR_WAVE");
-      return !(e && e[0] == '0');
+      return e && e[0] == '1';
     }();
     p.wv = p.b16 && wave_form && CIN <= 64 ? 1 : 0;
     const int nch = HID / 16;
-    if (p.b16 && (HID % 16 != 0 || !ir_slab_plan(&p, wgs))) return 0;
+    // b16: about 6 chunks per slice, at least 256 workgroups (VSO_IR_CPS; 0:
+    // the VSO_IR_WGS target alone) — MODNet batch 8 bf16 1407.5 us of kernel
+    // time against 1411 (4), 1415 (8), 1421 (the 512-workgroup target),
+    // profiles/r05i
+    static const int cps_target = [] {
+      const char* e = std::getenv("VSO_IR_CPS");
+      return e ? std::atoi(e) : 6;
+    }();
+    if (p.b16 && (HID % 16 != 0 || !ir_slab_plan(&p, wgs, cps_target))) return 0;
     if (!ir_supported(p)) return 0;
     if (!p.b16) {
       const long wg0 = (long)N * p.tiles;
