@@ -14,6 +14,7 @@ IFS=';' read -ra arms <<< "${ARMS:-VSO_IR_WAVE=1}"
 k=0
 for a in "${arms[@]}"; do
   k=$((k + 1))
+  a=${a//VSS_LIBRARY=/VSS_LIBRARY=$R/}  # (the profiled run starts in /tmp)
   cd /tmp
   env $a timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/${TAG}_a$k" -o run -- \
     python3 "$R/tools/onnx_layers.py" run "$KEY" "$R/gpurun_out/${TAG}_a$k/launches.json" > "$R/gpurun_out/${TAG}_a$k.log" 2>&1

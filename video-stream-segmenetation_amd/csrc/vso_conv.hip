@@ -110,9 +110,6 @@ template <> __device__ __forceinline__ f4 mma32<PREC_F16>(const u4* a, const u4*
 #ifndef VSO_CONV_WPE
 #define VSO_CONV_WPE 0
 #endif
-#ifndef VSO_CONV_PROBE
-#define VSO_CONV_PROBE 0
-#endif
 template <int PREC, int KS, int S, int TH, int TW, int BM>
 constexpr int conv_tile_wpe() {
   if (!VSO_CONV_WPE) return 1;
@@ -335,11 +332,7 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           if (WL) {
-#if VSO_CONV_PROBE
-            a[i][0] = u4{(unsigned)tap, (unsigned)i, 0u, 0u};  // timing probe: no weight reads (results invalid)
-#else
             a[i][0] = wsm[(tap * BM + 16 * i + r) * QW + g];
-#endif
           } else {
             const u4* row = wq + ((long)tap * p.Mp + m0 + 16 * i + r) * cq + wc;
 #pragma unroll
