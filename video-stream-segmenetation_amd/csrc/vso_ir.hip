@@ -739,6 +739,8 @@ void ir_tiles(int Ho, int Wo, int* tiles_x, int* tiles) {
 }
 
 bool ir_supported(const IrParams& p) {
+  // the kernels index an image's input planes with 32-bit offsets
+  if ((long)p.CIN * p.H * p.W >= (1L << 31)) return false;
   return p.CIN % 4 == 0 && p.HID % 16 == 0 && (p.stride == 1 || p.stride == 2) && ir_entry(p) != nullptr &&
          ir_lds_bytes(p) <= 160 * 1024 && (!p.res || (p.stride == 1 && p.CIN == p.COUT));
 }
