@@ -114,8 +114,13 @@ int vso_launch_name(const vso_session* s, int k, char* buf, int cap);
 /* Convolutions planned on the LDS-tiled MFMA kernel (k_conv_tile). */
 int vso_tile_conv_count(const vso_session* s);
 /* Inverted residual blocks (1x1 expand -> Clip -> 3x3 depthwise -> Clip -> 1x1
- * project [-> + input]) the session runs as one k_ir launch each (MODNet's
- * MobileNetV2 backbone); VSO_IR=0 plans them as three launches. */
+ * project [-> + input]) the session runs as one fused launch each (MODNet's
+ * MobileNetV2 backbone): k_ir in f32 sessions, k_ir_b16 (bf16 hi / lo splits
+ * of both 1x1 operands, ~f32 precision) in bf16 / f16 ones, plus a
+ * k_ir_reduce launch when the hidden channels are split over workgroups.
+ * Planning knobs, read once per process: VSO_IR=0 plans them as three
+ * launches; VSO_IR_B16=0 keeps the f32 form in 16-bit sessions; VSO_IR_CPS
+ * (default 6) hidden 16-channel chunks per slice of a 16-bit block. */
 int vso_ir_block_count(const vso_session* s);
 
 #ifdef __cplusplus

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "vso_device.h"
@@ -670,7 +671,11 @@ bool ir_slab_plan(IrParams* p, long wgs, int cps_target) {
   if (cps_target > 0) {  // about cps_target chunks per slice, at least one chip's worth of workgroups
     ks = (nch + cps_target - 1) / cps_target;
     if (wg0 * ks < 256) ks = (int)std::min<long>(nch, (256 + wg0 - 1) / wg0);
-    if (wg0 >= 1024) ks = 1;
+    static const long one_slice = [] {  // tiles x images from which a block is not split (VSO_IR_KS1)
+      const char* e = std::getenv("VSO_IR_KS1");
+      return e ? std::atol(e) : 1024L;
+    }();
+    if (wg0 >= one_slice) ks = 1;
   }
   int cps = (nch + ks - 1) / ks;
   if (cps < nch) cps += cps & 1;  // slices of whole chunk pairs
