@@ -122,6 +122,13 @@ int vso_tile_conv_count(const vso_session* s);
  * launches; VSO_IR_B16=0 keeps the f32 form in 16-bit sessions; VSO_IR_CPS
  * (default 6) hidden 16-channel chunks per slice of a 16-bit block. */
 int vso_ir_block_count(const vso_session* s);
+/* Lanes of the captured graph (0 before the first run): launches that share no
+ * activation buffer run on two capture streams, so independent branches of
+ * the model (MODNet's HR branch beside its backbone) execute concurrently —
+ * for sessions whose input 0 holds >= 2^21 elements; smaller ones capture one
+ * stream (the cross-lane event edges cost more than the overlap there).
+ * VSO_LANES=1 / 2 (read once per process) forces either. */
+int vso_lane_count(const vso_session* s);
 
 #ifdef __cplusplus
 }

@@ -264,6 +264,38 @@ def test_inverted_residuals_16bit_knobs(ort, knob, value):
         assert np.array_equal(here, other)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
+def test_modnet_two_lanes_bitwise(ort, precision):
+    """The captured graph's two lanes (vso_lane_count; launches that share no
+    activation buffer on two capture streams — by default for inputs of
+    >= 2^21 elements, forced here by VSO_LANES, read once per process, so in
+    child processes): MODNet's graph uses both, and its outputs are bitwise
+    those of a one-lane capture — the schedule orders every pair of launches
+    that touch a common buffer."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    outs = {}
+    for lanes in ("2", "1"):
+        code = ("import numpy as np, sys; sys.path.insert(0, 'tests'); import onnx_models as M; "
+                "import importlib.util, os; spec = importlib.util.spec_from_file_location('vss_amd', "
+                "'video-stream-segmenetation_amd/__init__.py', submodule_search_locations=['video-stream-segmenetation_amd']); "
+                "m = importlib.util.module_from_spec(spec); sys.modules['vss_amd'] = m; spec.loader.exec_module(m); "
+                "import vss_amd.ort as o; d = M.modnet(144, 256); "
+                "x = np.random.default_rng(23).random((2, 3, 144, 256), dtype=np.float32); "
+                f"s = o.InferenceSession(d, input_shape=(2, 3, 144, 256), precision='{precision}'); "
+                "a = s.run({'input': x}); b = s.run({'input': x}); print(s.lanes()); "
+                "assert all(np.array_equal(a[k], b[k]) for k in a); "
+                f"np.save('gpurun_out/modnet_lanes{lanes}_{precision}.npy', np.concatenate([v.ravel() for v in a.values()]))")
+        r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, VSO_LANES=lanes),
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert r.stdout.split()[-1] == lanes, r.stdout
+        outs[lanes] = np.load(os.path.join(root, "gpurun_out", f"modnet_lanes{lanes}_{precision}.npy"))
+    assert np.array_equal(outs["2"], outs["1"])
+
+
 @pytest.mark.parametrize("precision", ["bf16", "f16", "f32"])
 def test_conv_up_into_thin_head(ort, precision):
     """Resize -> Concat -> 1x1 head of 3 outputs: the thin head launches the

@@ -59,13 +59,19 @@ def report(launches_path, trace_path):
     assert len(rows) == meta["iters"] * L, (len(rows), L)
     dur = [[] for _ in range(L)]
     grid = [None] * L
-    for i, r in enumerate(rows):
-        k = i % L
-        base = lambda n: n.split("(")[0].replace("void ", "")
-        assert base(r["Kernel_Name"]) == base(names[k]), (k, r["Kernel_Name"], names[k])
-        dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
-        grid[k] = (r.get("Grid_Size_X") or r.get("Grid_X"), r.get("Grid_Size_Y") or r.get("Grid_Y"),
-                   r.get("Grid_Size_Z") or r.get("Grid_Z"))
+    base = lambda n: n.split("(")[0].replace("void ", "")
+    # per iteration, each dispatch (in start order) goes to the first launch of
+    # its name not yet matched: with two capture lanes (vso_lane_count) the
+    # lanes' dispatches interleave, each lane in launch order
+    for it in range(meta["iters"]):
+        free = list(range(L))
+        for r in rows[it * L:(it + 1) * L]:
+            k = next((j for j in free if base(names[j]) == base(r["Kernel_Name"])), None)
+            assert k is not None, (it, r["Kernel_Name"])
+            free.remove(k)
+            dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
+            grid[k] = (r.get("Grid_Size_X") or r.get("Grid_X"), r.get("Grid_Size_Y") or r.get("Grid_Y"),
+                       r.get("Grid_Size_Z") or r.get("Grid_Z"))
     starts = [int(r["Start_Timestamp"]) for r in rows]
     ends = [int(r["End_Timestamp"]) for r in rows]
     span = [(ends[(i + 1) * L - 1] - starts[i * L]) / 1000.0 for i in range(meta["iters"])]
@@ -73,7 +79,7 @@ def report(launches_path, trace_path):
     busy = sum(avg)
     wall = sum(span) / len(span)
     print(f"{meta['key']}: {L} launches, kernel time {busy:.1f} us, first-to-last {wall:.1f} us "
-          f"(gaps {wall - busy:.1f} us)")
+          f"(gaps {wall - busy:.1f} us; negative: launches overlapping on the capture lanes)")
     order = sorted(range(L), key=lambda k: -avg[k])
     for k in order[:25]:
         print(f"  #{k:3d} {avg[k]:7.2f} us  grid {grid[k]}  {names[k].split('(')[0]}")

@@ -446,9 +446,25 @@ struct Value {
   }
 };
 
+// A host region holding a launch's parameters: at capture, every aligned
+// 8-byte word of it that points into one of the session's device
+// allocations marks that allocation as used by the launch (read or written:
+// the lane schedule treats every use as a conflict).
+struct Region {
+  std::shared_ptr<const void> keep;
+  const void* p;
+  size_t n;
+};
+
 struct Launch {
   std::string name;
   std::function<void(hipStream_t)> fn;
+  std::vector<Region> io;
+};
+
+struct DevRange {
+  uintptr_t lo, hi;
+  bool ro;  // constants: never written by a kernel (no dependency through them)
 };
 
 struct vso_session {
@@ -465,6 +481,10 @@ struct vso_session {
   std::vector<int> in_bufs, out_bufs;
   std::vector<void*> allocs;
   std::vector<Launch> launches;
+  std::vector<DevRange> ranges;   // every device allocation of the session
+  hipStream_t side = nullptr;     // the second capture lane
+  std::vector<hipEvent_t> events; // cross-lane edges of the captured graph
+  int lanes_used = 1;             // lanes of the captured schedule (vso_lane_count)
   hipGraphExec_t graph = nullptr;
   std::atomic<int> busy{0};
 };
@@ -515,10 +535,21 @@ struct Planner {
   template <class T>
   bool dalloc(T** p, size_t bytes) {
     void* q = nullptr;
-    if (hipMalloc(&q, std::max<size_t>(bytes, 16)) != hipSuccess) return fail("hipMalloc failed");
+    const size_t n = std::max<size_t>(bytes, 16);
+    if (hipMalloc(&q, n) != hipSuccess) return fail("hipMalloc failed");
     s->allocs.push_back(q);
+    s->ranges.push_back(DevRange{(uintptr_t)q, (uintptr_t)q + n, false});
     *p = static_cast<T*>(q);
     return true;
+  }
+  // a constant's allocation (weights, biases, tables): kernels only read it
+  void mark_ro(const void* q) {
+    for (DevRange& r : s->ranges)
+      if ((uintptr_t)q >= r.lo && (uintptr_t)q < r.hi) r.ro = true;
+  }
+  template <class T>
+  static Region reg(const std::shared_ptr<T>& sp) {
+    return Region{std::static_pointer_cast<const void>(sp), sp.get(), sizeof(T)};
   }
 
   int new_buf(int64_t elems) {
@@ -540,6 +571,7 @@ struct Planner {
       return nullptr;
     }
     dev_consts[&c] = d;
+    mark_ro(d);
     return d;
   }
   const float* upload_vec(const std::vector<float>& v) {
@@ -549,6 +581,7 @@ struct Planner {
       fail("constant upload failed");
       return nullptr;
     }
+    mark_ro(d);
     return d;
   }
 
@@ -577,7 +610,9 @@ struct Planner {
     vals[name] = v;
   }
 
-  void add(const char* name, std::function<void(hipStream_t)> fn) { s->launches.push_back(Launch{name, fn}); }
+  void add(const char* name, std::function<void(hipStream_t)> fn, std::vector<Region> io) {
+    s->launches.push_back(Launch{name, fn, std::move(io)});
+  }
 
   // ---- constant folding (host) ---------------------------------------------
   bool fold(const Node& nd, std::vector<Value*>& in) {
@@ -1056,13 +1091,15 @@ struct Planner {
         return -1;
       }
       p.slab = d;
+      mark_ro(d);
     }
     if (p.ks > 1 && !dalloc(&p.part, (size_t)p.ks * N * COUT * Ho * Wo * 4)) return -1;
     if (!set_runtime(out, {N, COUT, Ho, Wo})) return -1;
     p.y = dptr(vals[out]);
     auto pp = std::make_shared<IrParams>(p);
-    add(ir_kernel_name(p), [pp](hipStream_t st) { launch_ir(*pp, st); });
-    if (p.ks > 1) add("void vso::k_ir_reduce(vso::IrParams)", [pp](hipStream_t st) { launch_ir_reduce(*pp, st); });
+    add(ir_kernel_name(p), [pp](hipStream_t st) { launch_ir(*pp, st); }, {reg(pp)});
+    if (p.ks > 1)
+      add("void vso::k_ir_reduce(vso::IrParams)", [pp](hipStream_t st) { launch_ir_reduce(*pp, st); }, {reg(pp)});
     for (int k : {k1, k2, k3, k4}) done.insert((size_t)k);
     if (res) done.insert((size_t)k5);
     s->ir_blocks++;
@@ -1236,7 +1273,9 @@ struct Planner {
       }
       flush_input(nd.in[0]);  // (a pending Resize, or a Concat's pending upsampled inputs)
       auto pp = std::make_shared<ConvParams>(p);
-      add(conv_thin_name(p.M), [pp, norm](hipStream_t st) { launch_conv_thin(*pp, norm.get(), st); });
+      std::vector<Region> io{reg(pp)};
+      if (norm) io.push_back(reg(norm));
+      add(conv_thin_name(p.M), [pp, norm](hipStream_t st) { launch_conv_thin(*pp, norm.get(), st); }, io);
       if (cat_direct.count(out)) cat_patch[out].push_back([pp](float* base, int ctot) { retarget(pp.get(), base, ctot); });
       return true;
     }
@@ -1271,7 +1310,7 @@ struct Planner {
       if (up) up_pending.erase(ups[0].name);
     } else {
       auto pp = std::make_shared<ConvParams>(p);
-      add(conv_kernel_name(p), [pp](hipStream_t st) { launch_conv(*pp, st, nullptr); });
+      add(conv_kernel_name(p), [pp](hipStream_t st) { launch_conv(*pp, st, nullptr); }, {reg(pp)});
       if (direct) cat_patch[out].push_back([pp](float* base, int ctot) { retarget(pp.get(), base, ctot); });
     }
     if (ib != ibn.end()) {
@@ -1344,6 +1383,7 @@ struct Planner {
         return fail("conv weight upload failed");
     }
     tp.wp = d;
+    mark_ro(d);
     if (ts.ksplit > 1) {
       const size_t blocks = (size_t)p.N * (ts.Mp / ts.bm) * ts.tiles;
       // partial tiles in accumulator order: per output block and split, 256 threads x bm/16 x th*tw/64 f4
@@ -1353,7 +1393,7 @@ struct Planner {
       if (hipMemset(tp.counters, 0, blocks * 4) != hipSuccess) return fail("hipMemset failed");
     }
     auto tpp = std::make_shared<ConvTileParams>(tp);
-    add(conv_tile_name(ts), [tpp, ts](hipStream_t st) { launch_conv_tile(*tpp, ts, st); });
+    add(conv_tile_name(ts), [tpp, ts](hipStream_t st) { launch_conv_tile(*tpp, ts, st); }, {reg(tpp)});
     if (direct) cat_patch[*direct].push_back([tpp](float* base, int ctot) { retarget(&tpp->c, base, ctot); });
     s->tile_convs++;
     return true;
@@ -1415,7 +1455,8 @@ struct Planner {
     if (!set_runtime(nd.out[0], os)) return false;
     p.y = dptr(vals[nd.out[0]]);
     p.n = vals[nd.out[0]].numel();
-    add("vso::k_binary(vso::BinParams)", [p](hipStream_t st) { launch_binary(p, st); });
+    auto bp = std::make_shared<BinParams>(p);
+    add("vso::k_binary(vso::BinParams)", [bp](hipStream_t st) { launch_binary(*bp, st); }, {reg(bp)});
     return true;
   }
 
@@ -1474,11 +1515,13 @@ struct Planner {
         for (size_t k = 0; k < rk; ++k) sb += src_start[k] * sst[k];
         q.src_base = sb;
         q.dst_base = base;
-        add(row_copy_name(q), [q](hipStream_t st) { launch_copy_rows(q, st); });
+        auto qp = std::make_shared<decltype(q)>(q);
+        add(row_copy_name(q), [qp](hipStream_t st) { launch_copy_rows(*qp, st); }, {reg(qp)});
         return true;
       }
     }
-    add("vso::k_copy(vso::CopyParams)", [p](hipStream_t st) { launch_copy(p, st); });
+    auto cp = std::make_shared<CopyParams>(p);
+    add("vso::k_copy(vso::CopyParams)", [cp](hipStream_t st) { launch_copy(*cp, st); }, {reg(cp)});
     return true;
   }
 
@@ -1514,7 +1557,8 @@ struct Planner {
       if (!set_runtime(nd.out[0], xs)) return false;
       p.y = dptr(vals[nd.out[0]]);
       p.n = vals[nd.out[0]].numel();
-      add("vso::k_unary(vso::UnaryParams)", [p](hipStream_t st) { launch_unary(p, st); });
+      auto up = std::make_shared<UnaryParams>(p);
+      add("vso::k_unary(vso::UnaryParams)", [up](hipStream_t st) { launch_unary(*up, st); }, {reg(up)});
       return true;
     }
     if (op == "Identity" || op == "Dropout" || op == "Cast") {
@@ -1531,7 +1575,8 @@ struct Planner {
       if (!set_runtime(nd.out[0], xs)) return false;
       p.y = dptr(vals[nd.out[0]]);
       p.n = vals[nd.out[0]].numel();
-      add("vso::k_unary(vso::UnaryParams)", [p](hipStream_t st) { launch_unary(p, st); });
+      auto up = std::make_shared<UnaryParams>(p);
+      add("vso::k_unary(vso::UnaryParams)", [up](hipStream_t st) { launch_unary(*up, st); }, {reg(up)});
       return true;
     }
     if (op == "Add" || op == "Sub" || op == "Mul" || op == "Div")
@@ -1574,7 +1619,8 @@ struct Planner {
       p.x = dptr(*x);
       if (!set_runtime(nd.out[0], {xs[0], xs[1], p.Ho, p.Wo})) return false;
       p.y = dptr(vals[nd.out[0]]);
-      add("vso::k_pool(vso::PoolParams)", [p](hipStream_t st) { launch_pool(p, st); });
+      auto pp = std::make_shared<PoolParams>(p);
+      add("vso::k_pool(vso::PoolParams)", [pp](hipStream_t st) { launch_pool(*pp, st); }, {reg(pp)});
       return true;
     }
     if (op == "GlobalAveragePool") {
@@ -1587,7 +1633,8 @@ struct Planner {
       for (size_t d = 2; d < xs.size(); ++d) os.push_back(1);
       if (!set_runtime(nd.out[0], os)) return false;
       p.y = dptr(vals[nd.out[0]]);
-      add("vso::k_gap(vso::RowParams)", [p](hipStream_t st) { launch_gap(p, st); });
+      auto rp = std::make_shared<RowParams>(p);
+      add("vso::k_gap(vso::RowParams)", [rp](hipStream_t st) { launch_gap(*rp, st); }, {reg(rp)});
       return true;
     }
     if (op == "InstanceNormalization") {
@@ -1620,7 +1667,8 @@ struct Planner {
       if (!set_runtime(nd.out[0], xs)) return false;
       p.y = dptr(vals[nd.out[0]]);
       p.n = vals[nd.out[0]].numel();
-      add("vso::k_affine(vso::AffineParams)", [p](hipStream_t st) { launch_affine(p, st); });
+      auto ap = std::make_shared<AffineParams>(p);
+      add("vso::k_affine(vso::AffineParams)", [ap](hipStream_t st) { launch_affine(*ap, st); }, {reg(ap)});
       return true;
     }
     if (op == "Softmax") {
@@ -1633,7 +1681,8 @@ struct Planner {
       p.rows = x->numel() / std::max<int64_t>(p.inner, 1);
       if (!set_runtime(nd.out[0], xs)) return false;
       p.y = dptr(vals[nd.out[0]]);
-      add("vso::k_softmax(vso::RowParams)", [p](hipStream_t st) { launch_softmax(p, st); });
+      auto rp = std::make_shared<RowParams>(p);
+      add("vso::k_softmax(vso::RowParams)", [rp](hipStream_t st) { launch_softmax(*rp, st); }, {reg(rp)});
       return true;
     }
     if (op == "Transpose") {
@@ -1804,7 +1853,7 @@ struct Planner {
           p.Ho == 2 * p.H && p.Wo == 2 * p.W && p.C % 32 == 0 && s->conv_precision != PREC_F32)
         up_pending[nd.out[0]] = pp;  // its consumer convolution computes it (or flush_up launches it)
       else
-        add(resize_kernel_name(p), [pp](hipStream_t st) { launch_resize(*pp, st); });
+        add(resize_kernel_name(p), [pp](hipStream_t st) { launch_resize(*pp, st); }, {reg(pp)});
       if (cat_direct.count(nd.out[0]))
         cat_patch[nd.out[0]].push_back([pp](float* base, int ctot) {
           pp->y = base;
@@ -1871,7 +1920,8 @@ struct Planner {
       if (!p.a || !p.b) return false;
       if (!set_runtime(nd.out[0], os)) return false;
       p.y = dptr(vals[nd.out[0]]);
-      add(gemm_kernel_name(p), [p](hipStream_t st) { launch_gemm(p, st); });
+      auto gp = std::make_shared<decltype(p)>(p);
+      add(gemm_kernel_name(p), [gp](hipStream_t st) { launch_gemm(*gp, st); }, {reg(gp)});
       return true;
     }
     if (op == "MatMulNBits") return plan_matmul_nbits(nd, in);
@@ -1929,7 +1979,8 @@ struct Planner {
     os.push_back(N);
     if (!set_runtime(nd.out[0], os)) return false;
     p.y = dptr(vals[nd.out[0]]);
-    add(gemm_kernel_name(p), [p](hipStream_t st) { launch_gemm(p, st); });
+    auto gp = std::make_shared<decltype(p)>(p);
+    add(gemm_kernel_name(p), [gp](hipStream_t st) { launch_gemm(*gp, st); }, {reg(gp)});
     return true;
   }
 
@@ -1959,14 +2010,14 @@ struct Planner {
     if (inner == 0 || N * C == 0) return true;
     auto pp = std::make_shared<NormParams>(p);
     if (!defer && norm_plane_fits(inner) && norm_plane_enabled()) {
-      add(norm_plane_name(inner), [pp](hipStream_t st) { launch_norm_plane(*pp, st); });
+      add(norm_plane_name(inner), [pp](hipStream_t st) { launch_norm_plane(*pp, st); }, {reg(pp)});
     } else {
-      add("vso::k_norm_stats(vso::NormParams)", [pp](hipStream_t st) { launch_norm_stats(*pp, st); });
+      add("vso::k_norm_stats(vso::NormParams)", [pp](hipStream_t st) { launch_norm_stats(*pp, st); }, {reg(pp)});
       if (defer) {  // the apply step runs in the consumer (k_conv_thin) or, failing that, flush_up
         norm_pending[*defer] = pp;
         return true;
       }
-      add("vso::k_norm_apply(vso::NormParams)", [pp](hipStream_t st) { launch_norm_apply(*pp, st); });
+      add("vso::k_norm_apply(vso::NormParams)", [pp](hipStream_t st) { launch_norm_apply(*pp, st); }, {reg(pp)});
     }
     if (direct)  // in place on the conv's output, wherever that now lies
       cat_patch[*direct].push_back([pp](float* base, int ctot) { pp->x = pp->y = base; pp->ctot = ctot; });
@@ -2121,7 +2172,7 @@ struct Planner {
     auto nt = norm_pending.find(name);
     if (nt == norm_pending.end()) return;
     auto pp = nt->second;
-    add("vso::k_norm_apply(vso::NormParams)", [pp](hipStream_t st) { launch_norm_apply(*pp, st); });
+    add("vso::k_norm_apply(vso::NormParams)", [pp](hipStream_t st) { launch_norm_apply(*pp, st); }, {reg(pp)});
     norm_pending.erase(nt);
   }
   void flush_up(const std::string& name) {
@@ -2129,7 +2180,7 @@ struct Planner {
     auto it = up_pending.find(name);
     if (it == up_pending.end()) return;
     auto pp = it->second;
-    add(resize_kernel_name(*pp), [pp](hipStream_t st) { launch_resize(*pp, st); });
+    add(resize_kernel_name(*pp), [pp](hipStream_t st) { launch_resize(*pp, st); }, {reg(pp)});
     up_pending.erase(it);
   }
   // a consumer that computes no upsample itself: its input's pending Resize and,
@@ -2255,14 +2306,139 @@ int64_t numel(const std::vector<int64_t>& v) {
   return n;
 }
 
+// Two capture lanes (VSO_LANES=1: one).  Launch i uses the device allocations
+// its parameter regions point into (constants excepted); it depends on the
+// last earlier launch that used each of them (every use counts as a write, so
+// the users of an allocation form one chain).  List scheduling in launch
+// order, unit costs: a launch starts on the lane where it can start first
+// (ties: the lane of its latest dependency, then lane 0); a dependency on the
+// other lane becomes an event edge.  MODNet: the HR branch's entry (the
+// image resizes, e2 / e4, the first HR convolutions) runs on lane 1 beside
+// the backbone's latency-bound blocks (tools/micro/graph_branches.hip:
+// independent branches of one captured graph run concurrently).
+struct LaneSchedule {
+  std::vector<int> lane, wait_on;  // wait_on: the other lane's launch to wait for, or -1
+  std::vector<char> record;        // an event is recorded after this launch
+  int used = 1;
+};
+
+static LaneSchedule schedule_lanes(const vso_session* s, int lanes) {
+  const size_t n = s->launches.size();
+  LaneSchedule ls;
+  ls.lane.assign(n, 0);
+  ls.wait_on.assign(n, -1);
+  ls.record.assign(n, 0);
+  if (lanes < 2 || n < 2) return ls;
+  std::vector<DevRange> rs = s->ranges;
+  std::sort(rs.begin(), rs.end(), [](const DevRange& a, const DevRange& b) { return a.lo < b.lo; });
+  auto find = [&](uintptr_t v) -> int {
+    size_t lo = 0, hi = rs.size();
+    while (lo < hi) {  // the last range with lo <= v
+      const size_t mid = (lo + hi) / 2;
+      if (rs[mid].lo <= v) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo == 0) return -1;
+    const DevRange& r = rs[lo - 1];
+    return v < r.hi && !r.ro ? (int)(lo - 1) : -1;
+  };
+  std::vector<int> last(rs.size(), -1), fin(n, 0);
+  int ready_at[2] = {0, 0};
+  for (size_t i = 0; i < n; ++i) {
+    std::set<int> deps;
+    std::set<int> used;
+    for (const Region& rg : s->launches[i].io)
+      for (size_t o = 0; o + 8 <= rg.n; o += 8) {
+        uint64_t v;
+        std::memcpy(&v, static_cast<const char*>(rg.p) + o, 8);
+        const int k = find((uintptr_t)v);
+        if (k >= 0) used.insert(k);
+      }
+    for (int k : used)
+      if (last[k] >= 0) deps.insert(last[k]);
+    int ready = 0, latest = -1;
+    for (int d : deps) {
+      ready = std::max(ready, fin[d]);
+      if (latest < 0 || fin[d] > fin[latest]) latest = d;
+    }
+    int best = 0, best_start = std::max(ready, ready_at[0]);
+    const int s1 = std::max(ready, ready_at[1]);
+    if (s1 < best_start || (s1 == best_start && latest >= 0 && ls.lane[latest] == 1)) {
+      best = 1;
+      best_start = s1;
+    }
+    ls.lane[i] = best;
+    fin[i] = best_start + 1;
+    ready_at[best] = fin[i];
+    int w = -1;
+    for (int d : deps)
+      if (ls.lane[d] != best) w = std::max(w, d);
+    if (w >= 0) {
+      ls.wait_on[i] = w;
+      ls.record[w] = 1;
+    }
+    for (int k : used) last[k] = (int)i;
+    if (best == 1) ls.used = 2;
+  }
+  return ls;
+}
+
+// Two lanes for sessions of >= 2^21 input elements (MODNet batch 8 at
+// 288x512: 1.41 -> 1.35 ms bf16, 3.88 -> 3.72 f32), one below: at batch 1 and
+// on the MediaPipe nets the cross-lane edges cost more than the overlap gives
+// (MODNet batch 1 0.594 -> 0.62 ms, the face detector 0.405 -> 0.447 ms;
+// profiles/r05u).  VSO_LANES=1 / 2 forces either.
+static int lanes_wanted(const vso_session* s) {
+  static const int forced = [] {
+    const char* e = std::getenv("VSO_LANES");
+    return e ? std::max(1, std::min(2, std::atoi(e))) : 0;
+  }();
+  if (forced) return forced;
+  return !s->in_shapes.empty() && numel(s->in_shapes[0]) >= (int64_t{1} << 21) ? 2 : 1;
+}
+
 int run_graph(vso_session* s, hipStream_t st) {
   if (!s->graph) {  // capture the launch list once (buffers are the session's own)
     hipGraph_t g = nullptr;
     hipStream_t cs = s->stream;
+    const LaneSchedule ls = schedule_lanes(s, lanes_wanted(s));
+    if (ls.used > 1 && !s->side && hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess)
+      return fail_s(s, VSO_E_HIP, "hipStreamCreate failed");
+    const size_t n = s->launches.size();
+    std::vector<hipEvent_t> ev(n, nullptr);
+    hipEvent_t fork = nullptr, join = nullptr;
+    if (ls.used > 1) {
+      for (size_t i = 0; i < n; ++i)
+        if (ls.record[i]) {
+          if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
+            return fail_s(s, VSO_E_HIP, "hipEventCreate failed");
+          s->events.push_back(ev[i]);
+        }
+      if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&join, hipEventDisableTiming) != hipSuccess)
+        return fail_s(s, VSO_E_HIP, "hipEventCreate failed");
+      s->events.push_back(fork);
+      s->events.push_back(join);
+    }
     if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess)
       return fail_s(s, VSO_E_HIP, "hipStreamBeginCapture failed");
-    for (const Launch& l : s->launches) l.fn(cs);
+    bool ok = true;
+    if (ls.used > 1)  // the side lane joins the capture
+      ok = hipEventRecord(fork, cs) == hipSuccess && hipStreamWaitEvent(s->side, fork, 0) == hipSuccess;
+    for (size_t i = 0; i < n && ok; ++i) {
+      hipStream_t ls_st = ls.lane[i] ? s->side : cs;
+      if (ls.wait_on[i] >= 0) ok = hipStreamWaitEvent(ls_st, ev[ls.wait_on[i]], 0) == hipSuccess;
+      s->launches[i].fn(ls_st);
+      if (ok && ls.record[i]) ok = hipEventRecord(ev[i], ls_st) == hipSuccess;
+    }
+    if (ok && ls.used > 1)  // and rejoins it at the end
+      ok = hipEventRecord(join, s->side) == hipSuccess && hipStreamWaitEvent(cs, join, 0) == hipSuccess;
     const hipError_t e = hipStreamEndCapture(cs, &g);
+    if (!ok) {
+      if (g) (void)hipGraphDestroy(g);
+      return fail_s(s, VSO_E_HIP, "capturing the lane schedule failed");
+    }
+    s->lanes_used = ls.used;
     if (e != hipSuccess || !g) return fail_s(s, VSO_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
     const hipError_t e2 = hipGraphInstantiate(&s->graph, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
@@ -2345,7 +2521,9 @@ void vso_destroy(vso_session* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   if (s->graph) (void)hipGraphExecDestroy(s->graph);
+  for (hipEvent_t e : s->events) (void)hipEventDestroy(e);
   for (void* p : s->allocs) (void)hipFree(p);
+  if (s->side) (void)hipStreamDestroy(s->side);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -2425,6 +2603,7 @@ int vso_launch_count(const vso_session* s) { return s ? (int)s->launches.size() 
 
 int vso_tile_conv_count(const vso_session* s) { return s ? s->tile_convs : VSO_E_INVALID_ARG; }
 int vso_ir_block_count(const vso_session* s) { return s ? s->ir_blocks : VSO_E_INVALID_ARG; }
+int vso_lane_count(const vso_session* s) { return s ? (s->graph ? s->lanes_used : 0) : VSO_E_INVALID_ARG; }
 
 
 int vso_launch_name(const vso_session* s, int k, char* buf, int cap) {

@@ -48,6 +48,7 @@ def lib():
             "vso_options_default": ([ctypes.POINTER(Options)], None),
             "vso_tile_conv_count": ([P], I),
             "vso_ir_block_count": ([P], I),
+            "vso_lane_count": ([P], I),
             "vso_destroy": ([P], None),
             "vso_last_error": ([P], ctypes.c_char_p),
             "vso_io_count": ([P, ctypes.POINTER(I), ctypes.POINTER(I)], I),
@@ -152,6 +153,10 @@ class InferenceSession:
     def ir_blocks(self) -> int:
         """Inverted residual blocks planned as one fused launch each (k_ir)."""
         return _check(lib().vso_ir_block_count(self._h), self._h)
+
+    def lanes(self) -> int:
+        """Capture lanes of the session's graph (0 before its first run)."""
+        return _check(lib().vso_lane_count(self._h), self._h)
 
     def close(self):
         if getattr(self, "_h", None):
