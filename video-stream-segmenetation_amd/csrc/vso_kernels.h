@@ -78,6 +78,7 @@ struct ConvTileParams {
   // are the 2x linear (half-pixel) upsample of up ([N][up_c1 - up_c0][up_H][up_W])
   const float* up;
   int up_c0, up_c1, up_H, up_W;
+  int items;           // work items (pixel tile x M tile x image x split); set by launch_conv_tile
 };
 
 constexpr int kDwPwMaxC = 256;  // channels a fused depthwise -> 1x1 pair may have
