@@ -566,6 +566,39 @@ struct Staged16 {
   }
 };
 
+// The layer's weight image global -> LDS by LDS-DMA (VSS_WDMA, default on):
+// 16 B per lane, 1 KiB per wave instruction, written straight into LDS — no
+// register staging (Staged<WIMG_F4> held up to ~19 float4s per lane) and no
+// commit stores; the prologue's closing barrier waits for it (dma_wait).
+// Used by the decoders and the blocks whose image is >= 40 KiB (block_wdma):
+// measured per layer against register staging (profiles/r05ac, isolated
+// event pass, 3 interleaved runs): b7 6.70 -> 6.14 us, b6 6.43 -> 6.23,
+// b5 5.88 -> 5.75, d1 5.06 -> 4.95, d2 6.48 -> 6.22, but b2 6.50 -> 6.85 and
+// b4 5.40 -> 5.56 (small images: register staging kept there).
+#ifndef VSS_WDMA
+#define VSS_WDMA 1
+#endif
+constexpr bool block_wdma(int mode, int wimg_f4) { return VSS_WDMA && (mode == 2 || wimg_f4 >= 2560); }
+template <int N>
+__device__ __forceinline__ void dma_f4(const f4* src, f4* dst) {
+  const int lane = (int)threadIdx.x & 63;
+  const int wb = __builtin_amdgcn_readfirstlane(((int)threadIdx.x >> 6) * 64);
+  for (int o = wb; o < N; o += 256)
+    if (N % 64 == 0 || o + lane < N)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + o + lane),
+                                       (__attribute__((address_space(3))) void*)(dst + o), 16, 0, 0);
+}
+struct NoStaged {  // Staged's interface for the DMA'd copy
+  template <class Load>
+  __device__ __forceinline__ void issue(Load) {}
+  template <class Store>
+  __device__ __forceinline__ void commit(Store) const {}
+};
+template <bool ON>
+__device__ __forceinline__ void dma_wait() {
+  if constexpr (ON) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <bool B>
 struct ChunkTag {
   static constexpr bool value = B;
@@ -640,6 +673,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
 
   // ---- prologue: issue every load, then commit to LDS ----
   constexpr int WIMG_F4 = (L.wimg_end - L.w1) / 4;
+  constexpr bool WDMA = block_wdma(MODE, WIMG_F4);
   const f4* wsrc = reinterpret_cast<const f4*>(p.wimg + ks * p.wimg_stride);
   f4* wdst = reinterpret_cast<f4*>(smem + L.w1);
   if constexpr (MODE == MODE_DEC) {
@@ -666,7 +700,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     // (a bijection within groups of four; P_IN_PAD is a multiple of 16)
     constexpr bool SKP = VSS_SWZ && GS == 1 && !L.XQM && VSS_STAGE16_DEC == 0 && (XS / 4) % 4 == 2;
     auto skip_pix = [&](int it) { return SKP ? (it & ~3) | ((it & 1) << 1) | ((it >> 1) & 1) : it; };
-    Staged<WIMG_F4> st_w;
+    std::conditional_t<WDMA, NoStaged, Staged<WIMG_F4>> st_w;
     {
       const float* xb[XP];
 #pragma unroll
@@ -685,6 +719,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         return (unsigned)((yy * Wo + xx) * CSKIP + 16 * gq);
       });
     }
+    if constexpr (WDMA) dma_f4<WIMG_F4>(wsrc, reinterpret_cast<f4*>(smem + L.w1));
     st_w.issue([&](int i) { return wsrc[i]; });
     VSS_STAMP(6);  // every load issued
     // the upsample's tap records, one per input-tile pixel, while the loads
@@ -758,6 +793,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     });
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     VSS_STAMP(4);
+    dma_wait<WDMA>();
     __syncthreads();
     // upsampled channels: PyTorch upsample_bilinear2d(scale 2, align_corners=False)
     // of relu(src * scale + shift) (the src's instance norm, applied per tap)
@@ -876,7 +912,8 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     float* x0s = work;                            // [3][XH][XWP]
     float* sws = work + r4(3 * XH * XWP);          // [tap][16]
     float* sbs = sws + 27 * 16;
-    Staged<WIMG_F4> st_w;
+    std::conditional_t<WDMA, NoStaged, Staged<WIMG_F4>> st_w;
+    if constexpr (WDMA) dma_f4<WIMG_F4>(wsrc, reinterpret_cast<f4*>(smem + L.w1));
     st_w.issue([&](int i) { return wsrc[i]; });
     // the stem weights as [tap][16]: thread i loads w[channel i % 16][tap i / 16]
     // (sp.w is [c][27]) and stores word i (consecutive banks, no transposing store)
@@ -967,6 +1004,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
       }
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     VSS_STAMP(4);
+    dma_wait<WDMA>();
     __syncthreads();
     VSS_STAMP(5);  // resized region in LDS: the stem conv starts
     // stem outputs of the region, 16-pixel blocks on the MFMA (stem_mfma,
@@ -1018,7 +1056,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     static_assert(CIN % 16 == 0, "16-channel staging items");
     constexpr int GI = CIN / 16;  // 16-channel items per pixel
     Staged16<P_IN_PAD * GI, XP, VSS_STAGE16> st_x;
-    Staged<WIMG_F4> st_w;
+    std::conditional_t<WDMA, NoStaged, Staged<WIMG_F4>> st_w;
     {
       const float* xb[XP];
 #pragma unroll
@@ -1029,6 +1067,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         return (unsigned)((yy * W + xx) * CIN + 16 * gq);
       });
     }
+    if constexpr (WDMA) dma_f4<WIMG_F4>(wsrc, reinterpret_cast<f4*>(smem + L.w1));
     st_w.issue([&](int i) { return wsrc[i]; });
     VSS_STAMP(6);  // every load issued
     st_x.commit_sum([&](int i, int k, f4 v) {
@@ -1053,6 +1092,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     st_w.commit([&](int i, f4 v) { wdst[i] = v; });
     VSS_STAMP(4);
   }
+  dma_wait<WDMA>();
   __syncthreads();
   VSS_STAMP(1);
 
