@@ -184,6 +184,7 @@ struct ResizeParams {
   long y_nx;     // as ConvParams::y_nx (C * Ho * Wo + y_nx elements per image)
 };
 
+constexpr long kGapWaveMax = 1024;  // k_gap_wave: planes of at most this many elements
 struct GemmParams {  // y[b][m][n] = alpha * sum_k A[b][m][k] B[b][k][n] + beta * c
   const float* a;
   const float* b;
@@ -293,6 +294,8 @@ const char* resize_kernel_name(const ResizeParams& p);  // the kernel launch_res
 void launch_resize(const ResizeParams& p, hipStream_t s);
 void launch_gemm(const GemmParams& p, hipStream_t s);
 bool gemm_vec(const GemmParams& p);
+const char* binary_kernel_name(const BinParams& p);
+const char* gap_kernel_name(const RowParams& p);
 const char* gemm_kernel_name(const GemmParams& p);
 
 }  // namespace vso

@@ -832,6 +832,46 @@ void launch_conv(const ConvParams& p, hipStream_t s, const char** name) {
 
 // ---------------------------------------------------------------------------
 
+__device__ __forceinline__ float bin_op(int op, float a, float b) {
+  switch (op) {
+    case BIN_ADD: return a + b;
+    case BIN_SUB: return a - b;
+    case BIN_MUL: return a * b;
+    case BIN_DIV: return a / b;
+    default: return a < 0.f ? a * b : a;  // PRELU
+  }
+}
+
+// a 4-D contiguous a (op) b of one value per (n, c) plane (the SE blocks'
+// channel gate, MODNet 288x512: 8 x 1280 planes of 144): float4s of a, b's
+// value per plane, y contiguous — the general form's per-element unravel ran
+// this at 0.8 TB/s (15 us)
+__global__ __launch_bounds__(256) void k_binary_planes(BinParams p) {
+  const long inner = (long)p.dims[2] * p.dims[3];
+  const long n4 = p.n / 4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const long plane = (4 * i) / inner;
+    const long nn = plane / p.dims[1], cc = plane - nn * p.dims[1];
+    const float bv = p.b[nn * p.sb[0] + cc * p.sb[1]];
+    const f4 av = reinterpret_cast<const f4*>(p.a)[i];
+    reinterpret_cast<f4*>(p.y)[i] = f4{bin_op(p.op, av.x, bv), bin_op(p.op, av.y, bv), bin_op(p.op, av.z, bv),
+                                       bin_op(p.op, av.w, bv)};
+  }
+}
+bool binary_planes(const BinParams& p) {
+  static const bool on = [] {
+    const char* e = std::getenv("VSO_BIN_PLANES");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (!on) return false;
+  const auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (p.nd != 4 || p.sb[2] != 0 || p.sb[3] != 0 || ((long)p.dims[2] * p.dims[3]) % 4 != 0) return false;
+  if (p.sa[3] != 1 || p.sa[2] != p.dims[3] || p.sa[1] != (long)p.dims[2] * p.dims[3] ||
+      (p.dims[0] > 1 && p.sa[0] != (long)p.dims[1] * p.sa[1]))
+    return false;
+  return al(p.a) && al(p.y);
+}
+
 template <typename I>
 __device__ __forceinline__ void binary_body(const BinParams& p) {
   for (I i = (I)blockIdx.x * 256 + (I)threadIdx.x; i < (I)p.n; i += (I)gridDim.x * 256) {
@@ -983,6 +1023,22 @@ __global__ __launch_bounds__(256) void k_gap(RowParams p) {
   for (long i = threadIdx.x; i < p.inner; i += 256) s += x[i];
   s = block_sum(s, sh);
   if (threadIdx.x == 0) p.y[blockIdx.x] = s / (float)p.inner;
+}
+
+// Short planes (inner <= kGapWaveMax): a wave per plane, four per workgroup —
+// MODNet's SE pool (8 x 1280 planes of 9 x 16 at 288x512): 14.1 -> 8.3 us
+// against 10240 workgroups of 256 threads summing 144 elements each (r05ag).
+// (A wave per output column for the SE's few-row GEMMs measured slower than
+// k_gemm's 16 x 16 MFMA tiles: 20 against 13 us each.)
+__global__ __launch_bounds__(256) void k_gap_wave(RowParams p) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.rows) return;  // (whole waves)
+  const float* x = p.x + row * p.inner;
+  float s = 0.f;
+  for (long i = lane; i < p.inner; i += 64) s += x[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) p.y[row] = s / (float)p.inner;
 }
 
 // Planes whose length is a multiple of 4 (and 16-B aligned tensors) move
@@ -1486,8 +1542,15 @@ bool gemm_vec(const GemmParams& p) {
          p.sbb % 4 == 0 && al(p.a) && al(p.b);
 }
 
+
+const char* binary_kernel_name(const BinParams& p) {
+  return binary_planes(p) ? "void vso::k_binary_planes(vso::BinParams)" : "vso::k_binary(vso::BinParams)";
+}
 void launch_binary(const BinParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_binary, dim3(grid_for(p.n)), dim3(256), 0, s, p);
+  if (binary_planes(p))
+    hipLaunchKernelGGL(k_binary_planes, dim3(grid_for(p.n / 4)), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(k_binary, dim3(grid_for(p.n)), dim3(256), 0, s, p);
 }
 void launch_unary(const UnaryParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_unary, dim3(grid_for(p.n)), dim3(256), 0, s, p);
@@ -1498,8 +1561,21 @@ void launch_copy(const CopyParams& p, hipStream_t s) {
 void launch_pool(const PoolParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_pool, dim3(grid_for((long)p.N * p.C * p.Ho * p.Wo)), dim3(256), 0, s, p);
 }
+static bool gap_wave(const RowParams& p) {
+  static const bool on = [] {
+    const char* e = std::getenv("VSO_GAP_WAVE");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on && p.inner <= kGapWaveMax;
+}
+const char* gap_kernel_name(const RowParams& p) {
+  return gap_wave(p) ? "void vso::k_gap_wave(vso::RowParams)" : "void vso::k_gap(vso::RowParams)";
+}
 void launch_gap(const RowParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_gap, dim3((unsigned)p.rows), dim3(256), 0, s, p);
+  if (gap_wave(p))
+    hipLaunchKernelGGL(k_gap_wave, dim3((unsigned)((p.rows + 3) / 4)), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(k_gap, dim3((unsigned)p.rows), dim3(256), 0, s, p);
 }
 void launch_norm_stats(const NormParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_norm_stats, dim3((unsigned)p.chunks, (unsigned)(p.N * p.C)), dim3(256), 0, s, p);

@@ -931,6 +931,15 @@ struct Planner {
   }
 
 
+  // VSO_GEMM_ACT=0: a Gemm / MatMul's activation as its own launch (A/B knob)
+  static bool gemm_act_enabled() {
+    static const bool on = [] {
+      const char* e = std::getenv("VSO_GEMM_ACT");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+
   // VSO_IR=0: the inverted residual blocks as three launches each (A/B knob)
   static bool ir_enabled() {
     static const bool on = [] {
@@ -1456,7 +1465,7 @@ struct Planner {
     p.y = dptr(vals[nd.out[0]]);
     p.n = vals[nd.out[0]].numel();
     auto bp = std::make_shared<BinParams>(p);
-    add("vso::k_binary(vso::BinParams)", [bp](hipStream_t st) { launch_binary(*bp, st); }, {reg(bp)});
+    add(binary_kernel_name(*bp), [bp](hipStream_t st) { launch_binary(*bp, st); }, {reg(bp)});
     return true;
   }
 
@@ -1634,7 +1643,7 @@ struct Planner {
       if (!set_runtime(nd.out[0], os)) return false;
       p.y = dptr(vals[nd.out[0]]);
       auto rp = std::make_shared<RowParams>(p);
-      add("vso::k_gap(vso::RowParams)", [rp](hipStream_t st) { launch_gap(*rp, st); }, {reg(rp)});
+      add(gap_kernel_name(*rp), [rp](hipStream_t st) { launch_gap(*rp, st); }, {reg(rp)});
       return true;
     }
     if (op == "InstanceNormalization") {
@@ -1918,8 +1927,16 @@ struct Planner {
         p.b = operand(*b);
       }
       if (!p.a || !p.b) return false;
-      if (!set_runtime(nd.out[0], os)) return false;
-      p.y = dptr(vals[nd.out[0]]);
+      // a following elementwise activation (the SE blocks' Relu / Sigmoid) in
+      // the epilogue (PRelu not: its slope's axis is ambiguous on [M, N])
+      std::string out = nd.out[0];
+      const int c1 = gemm_act_enabled() ? sole_consumer(out, ni) : -1;
+      if (c1 >= 0 && is_act(g.nodes[c1].op) && g.nodes[c1].op != "PRelu" && act_of(g.nodes[c1], &p.ep, p.N)) {
+        done.insert((size_t)c1);
+        out = g.nodes[c1].out[0];
+      }
+      if (!set_runtime(out, os)) return false;
+      p.y = dptr(vals[out]);
       auto gp = std::make_shared<decltype(p)>(p);
       add(gemm_kernel_name(p), [gp](hipStream_t st) { launch_gemm(*gp, st); }, {reg(gp)});
       return true;
