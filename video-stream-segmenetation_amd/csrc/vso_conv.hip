@@ -249,12 +249,22 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
       return;
     }
     const unsigned cofs = (unsigned)(ch * CK) * plane4;  // the chunk's first plane
+    // quads with no channel below C (a partial last chunk: MODNet's 35 -> 16
+    // fusion layer stages 3 real channels of 32) skip their loads — one
+    // branch per item; the zeros are those the range check would return
+    const int qv = p.qskip ? min(NQ, (c.C - ch * CK + CG - 1) / CG) : NQ;
+    const int uend = (qv * NPIX + 255) / 256;  // items u >= uend hold only such quads (uniform)
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const unsigned o = soff[u] + cofs;  // out-of-range items stay out of range (no wrap: < 2 GiB added)
+      if (u < uend) {
 #pragma unroll
-      for (int e = 0; e < CG; ++e)
-        st[u][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(o + e * plane4), 0, 0));
+        for (int e = 0; e < CG; ++e)
+          st[u][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(o + e * plane4), 0, 0));
+      } else {
+#pragma unroll
+        for (int e = 0; e < CG; ++e) st[u][e] = 0.f;
+      }
     }
   };
   const u4* wq = static_cast<const u4*>(p.wp);  // [tap][Mp][Cp] in quads of T
@@ -640,12 +650,22 @@ __device__ __forceinline__ void conv_tile_body_persist(const ConvTileParams& p) 
       return;
     }
     const unsigned cofs = (unsigned)(ch * CK) * plane4;  // the chunk's first plane
+    // quads with no channel below C (a partial last chunk: MODNet's 35 -> 16
+    // fusion layer stages 3 real channels of 32) skip their loads — one
+    // branch per item; the zeros are those the range check would return
+    const int qv = p.qskip ? min(NQ, (c.C - ch * CK + CG - 1) / CG) : NQ;
+    const int uend = (qv * NPIX + 255) / 256;  // items u >= uend hold only such quads (uniform)
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const unsigned o = soff[u] + cofs;  // out-of-range items stay out of range (no wrap: < 2 GiB added)
+      if (u < uend) {
 #pragma unroll
-      for (int e = 0; e < CG; ++e)
-        st[u][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(o + e * plane4), 0, 0));
+        for (int e = 0; e < CG; ++e)
+          st[u][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(o + e * plane4), 0, 0));
+      } else {
+#pragma unroll
+        for (int e = 0; e < CG; ++e) st[u][e] = 0.f;
+      }
     }
   };
   const u4* wq = static_cast<const u4*>(p.wp);  // [tap][Mp][Cp] in quads of T

@@ -79,6 +79,7 @@ struct ConvTileParams {
   const float* up;
   int up_c0, up_c1, up_H, up_W;
   int items;           // work items (pixel tile x M tile x image x split); set by launch_conv_tile
+  int qskip;           // skip the loads of quads past C in a partial last chunk (VSO_CONV_QSKIP=0: off)
 };
 
 constexpr int kDwPwMaxC = 256;  // channels a fused depthwise -> 1x1 pair may have

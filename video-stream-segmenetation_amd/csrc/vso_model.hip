@@ -1366,6 +1366,11 @@ struct Planner {
     ConvTileParams tp{};
     tp.c = p;
     tp.Mp = ts.Mp; tp.Cp = ts.Cp; tp.tiles_x = ts.tiles_x; tp.ksplit = ts.ksplit; tp.cps = ts.cps;
+    static const int qskip = [] {
+      const char* e = std::getenv("VSO_CONV_QSKIP");
+      return e ? std::atoi(e) : 1;
+    }();
+    tp.qskip = qskip;
     tp.tiles = ts.tiles; tp.mtiles = ts.Mp / ts.bm;
     if (up) {
       tp.up = up->x;
