@@ -414,6 +414,28 @@ def norm_planes():
                    outs)
 
 
+def se_forms():
+    """The SE chain's kernel forms (vso_kernels.hip): GlobalAveragePool on
+    short planes (k_gap_wave: 24 and 35 elements) and a long one (k_gap:
+    1600), Gemm + Relu / Sigmoid / LeakyRelu in the GEMM epilogue, Gemm +
+    PRelu left as its own launch, and the channel gate Mul on the float4
+    per-plane form (inner 24) and the general broadcast (inner 35)."""
+    b = Builder(21)
+    outs = []
+    for name, shape in (("a", [2, 6, 4, 6]), ("c", [2, 6, 5, 7])):
+        C = shape[1]
+        gp = b.op("Flatten", [b.op("GlobalAveragePool", [name])])
+        f = b.op("Relu", [b.op("Gemm", [gp, b.w(4, C), b.w(4, scale=0.1)], transB=1)])
+        f = b.op("Sigmoid", [b.op("Gemm", [f, b.w(C, 4), b.w(C, scale=0.1)], transB=1)])
+        f = b.op("Reshape", [f, b.const(np.array([shape[0], C, 1, 1], np.int64))])
+        outs.append((b.op("Mul", [name, f]), shape))
+    gl = b.op("Flatten", [b.op("GlobalAveragePool", ["l"])])
+    outs.append((b.op("LeakyRelu", [b.op("Gemm", [gl, b.w(5, 3), b.w(5, scale=0.1)], transB=1)], alpha=0.2), [2, 5]))
+    outs.append((b.op("PRelu", [b.op("Gemm", [gl, b.w(5, 3)], transB=1),
+                                b.const((b.rng.random(5) * 0.3).astype(np.float32))]), [2, 5]))
+    return b.model([("a", [2, 6, 4, 6]), ("c", [2, 6, 5, 7]), ("l", [2, 3, 40, 40])], outs)
+
+
 def conv_thin():
     """1x1 heads of <= 4 outputs on k_conv_thin (vso_kernels.h): 3 outputs
     with a Sigmoid on a 37x70 plane (scalar pixel path), 4 outputs with a

@@ -118,6 +118,26 @@ def test_conv_thin(ort):
     _check(got, want, "conv_thin")
 
 
+def test_se_forms(ort):
+    """The SE chain's kernel forms against the oracle (f32: 1e-4 of the output
+    scale): the wave-per-plane and per-workgroup pools, Gemm activations in
+    the epilogue (PRelu not), the per-plane and general broadcast Mul."""
+    data = M.se_forms()
+    rng = np.random.default_rng(29)
+    feeds = {"a": rng.standard_normal((2, 6, 4, 6)).astype(np.float32),
+             "c": rng.standard_normal((2, 6, 5, 7)).astype(np.float32),
+             "l": rng.standard_normal((2, 3, 40, 40)).astype(np.float32)}
+    want = R.run(R.load(data), feeds)
+    with ort.InferenceSession(data) as s:
+        got = s.run(feeds)
+        names = [n.split("(")[0] for n in s.launches()]
+    print(names)
+    assert names.count("void vso::k_gap_wave") == 2 and names.count("void vso::k_gap") == 1, names
+    assert names.count("void vso::k_binary_planes") == 1 and names.count("vso::k_binary") >= 1, names
+    assert sum("k_unary" in n for n in names) == 0, names  # Relu / Sigmoid / LeakyRelu in the GEMM epilogues
+    _check(got, want, "se_forms")
+
+
 def test_norm_planes(ort):
     """k_norm_plane's three forms and the two-launch path beyond it against the
     oracle (f32: 1e-4 of the output scale)."""
