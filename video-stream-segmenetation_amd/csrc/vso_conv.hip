@@ -205,6 +205,10 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
   // branch and an exec-mask swap per element (~5k instructions per chunk).
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(uniform_ptr(xn)), 0, (int)((long)c.C * plane * 4), 0x00020000);
+  // (the chunks from p.x2_c0 on: the Concat's last input, its own tensor)
+  const __amdgpu_buffer_rsrc_t xr2 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(uniform_ptr(p.x2 ? p.x2 + (long)n * p.x2_C * plane : xn)), 0,
+      (int)((long)(p.x2 ? p.x2_C : c.C) * plane * 4), 0x00020000);
   const unsigned plane4 = (unsigned)plane * 4u;
   unsigned soff[PER];  // per item: the byte offset of (channel q * CG, pixel) in the chunk, or out of range
 #pragma unroll
@@ -248,11 +252,14 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
       load_region(ch);
       return;
     }
-    const unsigned cofs = (unsigned)(ch * CK) * plane4;  // the chunk's first plane
+    const bool sec = p.x2 && ch * CK >= p.x2_c0;  // (uniform) from the Concat's last input
+    const __amdgpu_buffer_rsrc_t r = sec ? xr2 : xr;
+    const unsigned cofs = (unsigned)(sec ? ch * CK - p.x2_c0 : ch * CK) * plane4;  // the chunk's first plane
     // quads with no channel below C (a partial last chunk: MODNet's 35 -> 16
     // fusion layer stages 3 real channels of 32) skip their loads — one
     // branch per item; the zeros are those the range check would return
-    const int qv = p.qskip ? min(NQ, (c.C - ch * CK + CG - 1) / CG) : NQ;
+    const int cend_ch = sec ? p.x2_c0 + p.x2_C : (p.x2 ? p.x2_c0 : c.C);
+    const int qv = p.qskip ? min(NQ, (cend_ch - ch * CK + CG - 1) / CG) : NQ;
     const int uend = (qv * NPIX + 255) / 256;  // items u >= uend hold only such quads (uniform)
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -260,7 +267,7 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
       if (u < uend) {
 #pragma unroll
         for (int e = 0; e < CG; ++e)
-          st[u][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(o + e * plane4), 0, 0));
+          st[u][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(o + e * plane4), 0, 0));
       } else {
 #pragma unroll
         for (int e = 0; e < CG; ++e) st[u][e] = 0.f;
@@ -601,12 +608,16 @@ __device__ __forceinline__ void conv_tile_body_persist(const ConvTileParams& p) 
   // (the state below is the loading item's: set by set_load_item)
   __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(uniform_ptr(c.x)), 0, (int)((long)c.C * plane * 4), 0x00020000);
+  __amdgpu_buffer_rsrc_t xr2 = xr;  // (the Concat's last input: conv_tile_body)
   const unsigned plane4 = (unsigned)plane * 4u;
   unsigned soff[PER];  // per item: the byte offset of (channel q * CG, pixel) in the chunk, or out of range
   auto set_soff = [&](const Item& it) {
     const float* xn = c.x + (long)it.n * c.C * c.H * c.W;
     xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(xn)), 0, (int)((long)c.C * plane * 4),
                                            0x00020000);
+    xr2 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(uniform_ptr(p.x2 ? p.x2 + (long)it.n * p.x2_C * plane : xn)), 0,
+        (int)((long)(p.x2 ? p.x2_C : c.C) * plane * 4), 0x00020000);
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int idx = tid + 256 * u;
@@ -649,11 +660,14 @@ __device__ __forceinline__ void conv_tile_body_persist(const ConvTileParams& p) 
       load_region(ch);
       return;
     }
-    const unsigned cofs = (unsigned)(ch * CK) * plane4;  // the chunk's first plane
+    const bool sec = p.x2 && ch * CK >= p.x2_c0;  // (uniform) from the Concat's last input
+    const __amdgpu_buffer_rsrc_t r = sec ? xr2 : xr;
+    const unsigned cofs = (unsigned)(sec ? ch * CK - p.x2_c0 : ch * CK) * plane4;  // the chunk's first plane
     // quads with no channel below C (a partial last chunk: MODNet's 35 -> 16
     // fusion layer stages 3 real channels of 32) skip their loads — one
     // branch per item; the zeros are those the range check would return
-    const int qv = p.qskip ? min(NQ, (c.C - ch * CK + CG - 1) / CG) : NQ;
+    const int cend_ch = sec ? p.x2_c0 + p.x2_C : (p.x2 ? p.x2_c0 : c.C);
+    const int qv = p.qskip ? min(NQ, (cend_ch - ch * CK + CG - 1) / CG) : NQ;
     const int uend = (qv * NPIX + 255) / 256;  // items u >= uend hold only such quads (uniform)
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -661,7 +675,7 @@ __device__ __forceinline__ void conv_tile_body_persist(const ConvTileParams& p) 
       if (u < uend) {
 #pragma unroll
         for (int e = 0; e < CG; ++e)
-          st[u][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(o + e * plane4), 0, 0));
+          st[u][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(o + e * plane4), 0, 0));
       } else {
 #pragma unroll
         for (int e = 0; e < CG; ++e) st[u][e] = 0.f;
@@ -971,8 +985,22 @@ void k_conv_tile(ConvTileParams p) {
     conv_tile_body<PREC, KS, S, TH, TW, BM, false>(p);
 }
 
+// The upsample tiles whose LDS (pixel tile, weights, source region) leaves two
+// workgroups per CU are held to 256 VGPRs (two waves per SIMD): the 8 x 32 x
+// 32 tile sits at 253-258 by the compiler's choice, and one VGPR past 256
+// halves its occupancy (49 -> 69 us, profiles/r05x r05y).
 template <int PREC, int KS, int S, int TH, int TW, int BM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv_tile_wpe<PREC, KS, S, TH, TW, BM>(), 8)))
+constexpr int conv_tile_up_wpe() {
+  constexpr int NQ = CK * (PREC == PREC_F32 ? 4 : 2) / 16, IH = (TH - 1) * S + KS, IW = (TW - 1) * S + KS;
+  constexpr bool WL = PREC != PREC_F32 && (KS <= 3 || BM <= 32);
+  constexpr int SRC = (IH / 2 + 2) * (IW / 2 + 2), PR = (SRC * CK + 255) / 256;
+  constexpr int lds = IH * IW * conv_qs<PREC, S>() * 16 + (WL ? KS * KS * BM * NQ * 16 : 16) + PR * 256 * 4;
+  // (3x3, <= 32 output channels: the planner's upsample tiles; the larger
+  // ones spill under the cap)
+  return KS == 3 && BM <= 32 && 163840 / lds >= 2 ? 2 : 1;
+}
+template <int PREC, int KS, int S, int TH, int TW, int BM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv_tile_up_wpe<PREC, KS, S, TH, TW, BM>(), 8)))
 void k_conv_tile_up(ConvTileParams p) {
   conv_tile_body<PREC, KS, S, TH, TW, BM, true>(p);
 }

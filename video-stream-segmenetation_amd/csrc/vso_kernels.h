@@ -78,6 +78,11 @@ struct ConvTileParams {
   // are the 2x linear (half-pixel) upsample of up ([N][up_c1 - up_c0][up_H][up_W])
   const float* up;
   int up_c0, up_c1, up_H, up_W;
+  // a Concat's last input read from its own tensor instead of copied into the
+  // concatenation: channels [x2_c0, x2_c0 + x2_C) ([N][x2_C][H][W]; x2_c0 a
+  // multiple of 32), or x2 = null
+  const float* x2;
+  int x2_c0, x2_C;
   int items;           // work items (pixel tile x M tile x image x split); set by launch_conv_tile
   int qskip;           // skip the loads of quads past C in a partial last chunk (VSO_CONV_QSKIP=0: off)
 };

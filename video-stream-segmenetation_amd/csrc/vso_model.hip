@@ -525,6 +525,17 @@ struct Planner {
   struct UpRange { std::string name; int c0, c1; };
   std::map<std::string, std::vector<UpRange>> cat_up;
   std::map<std::string, std::vector<std::function<void(float*, int)>>> cat_patch;
+  // A Concat's last input (whole 32-channel chunks on) left in its own tensor
+  // instead of copied in: its sole consumer, a convolution on k_conv_tile,
+  // reads those chunks from there (ConvTileParams::x2); any other plan runs
+  // the copy just before itself (flush_tail).  MODNet: 3 copies of 8 x 3 /
+  // 32 x H x W planes (52 us of k_copy_rows at batch 8).
+  struct CatTail {
+    const float* x;
+    int c0, C;
+    std::function<bool()> copy;
+  };
+  std::map<std::string, CatTail> cat_tail;
   std::string err;
 
   bool fail(const std::string& m) {
@@ -931,6 +942,15 @@ struct Planner {
   }
 
 
+  // VSO_CAT_TAIL=0: every Concat input not written in place is copied (A/B knob)
+  static bool cat_tail_enabled() {
+    static const bool on = [] {
+      const char* e = std::getenv("VSO_CAT_TAIL");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+
   // VSO_GEMM_ACT=0: a Gemm / MatMul's activation as its own launch (A/B knob)
   static bool gemm_act_enabled() {
     static const bool on = [] {
@@ -1116,6 +1136,17 @@ struct Planner {
   }
 
   bool plan_conv(size_t ni) {
+    {  // a deferred Concat copy into this Conv's input: only a dense 3x3 / 5x5
+       // convolution (the k_conv_tile branch below, or its fallback, which
+       // flushes) may take it; every other plan reads the whole concatenation
+      const Node& cn = g.nodes[ni];
+      if (cat_tail.count(cn.in[0])) {
+        Value* w = cn.in.size() > 1 ? val(cn.in[1]) : nullptr;
+        const bool dense = w && w->shape.size() == 4 && cn.ai("group", 1) == 1 && w->shape[2] == w->shape[3] &&
+                           (w->shape[2] == 3 || w->shape[2] == 5);
+        if (!dense && !flush_tail(cn.in[0])) return false;
+      }
+    }
     if (const int rc = try_plan_ir(ni)) return rc > 0;
     const Node& nd = g.nodes[ni];
     Value* x = val(nd.in[0]);
@@ -1315,9 +1346,18 @@ struct Planner {
     for (const UpRange& u : ups)
       if (!up || u.name != ups[0].name) flush_up(u.name);
     if (tile) {
-      if (!plan_conv_tile(p, ts, wf, direct, up, up ? ups[0].c0 : 0, up ? ups[0].c1 : 0)) return false;
+      const CatTail* tail = nullptr;
+      auto ct = cat_tail.find(nd.in[0]);
+      if (ct != cat_tail.end() && ct->second.c0 + ct->second.C == p.C && ct->second.c0 % 32 == 0 &&
+          (!up || ct->second.c0 >= ups[0].c1))
+        tail = &ct->second;
+      else if (!flush_tail(nd.in[0]))
+        return false;
+      if (!plan_conv_tile(p, ts, wf, direct, up, up ? ups[0].c0 : 0, up ? ups[0].c1 : 0, tail)) return false;
+      if (tail) cat_tail.erase(nd.in[0]);
       if (up) up_pending.erase(ups[0].name);
     } else {
+      if (!flush_tail(nd.in[0])) return false;
       auto pp = std::make_shared<ConvParams>(p);
       add(conv_kernel_name(p), [pp](hipStream_t st) { launch_conv(*pp, st, nullptr); }, {reg(pp)});
       if (direct) cat_patch[out].push_back([pp](float* base, int ctot) { retarget(pp.get(), base, ctot); });
@@ -1360,7 +1400,8 @@ struct Planner {
   // partial-sum buffer when the channel chunks are split over workgroups.
   static constexpr double kTileMinMacs = 8e6;  // f32: smaller convs keep k_conv_small / k_conv_gemm
   bool plan_conv_tile(const ConvParams& p, const ConvTileShape& ts, const std::vector<float>& wf,
-                      const std::string* direct, const ResizeParams* up = nullptr, int up_c0 = 0, int up_c1 = 0) {
+                      const std::string* direct, const ResizeParams* up = nullptr, int up_c0 = 0, int up_c1 = 0,
+                      const CatTail* tail = nullptr) {
     const int taps = p.kh * p.kw;
     const size_t n = (size_t)taps * ts.Mp * ts.Cp;
     ConvTileParams tp{};
@@ -1371,6 +1412,11 @@ struct Planner {
       return e ? std::atoi(e) : 1;
     }();
     tp.qskip = qskip;
+    if (tail) {
+      tp.x2 = tail->x;
+      tp.x2_c0 = tail->c0;
+      tp.x2_C = tail->C;
+    }
     tp.tiles = ts.tiles; tp.mtiles = ts.Mp / ts.bm;
     if (up) {
       tp.up = up->x;
@@ -1764,6 +1810,20 @@ struct Planner {
           continue;
         }
         flush_up(nd.in[q]);
+        if (q + 1 == in.size() && rk == 4 && ax == 1 && doff[1] % 32 == 0 && doff[1] > 0 && cat_tail_enabled()) {
+          const int c = sole_consumer(nd.out[0], ni);
+          if (c >= 0 && g.nodes[c].op == "Conv" && g.nodes[c].in[0] == nd.out[0]) {
+            const float* src = operand(*v);
+            if (!src) return false;
+            const std::vector<int64_t> vs = v->shape;
+            float* dst = dptr(vals[nd.out[0]]);
+            cat_tail[nd.out[0]] = {src, (int)doff[1], (int)v->shape[1], [this, src, vs, dst, os, doff, rk]() {
+                                     return plan_copy_into(src, vs, dst, os, vs, doff, std::vector<int64_t>(rk, 0),
+                                                           std::vector<int64_t>(rk, 1), {}, 0.f);
+                                   }};
+            continue;
+          }
+        }
         if (!plan_copy_into(operand(*v), v->shape, dptr(vals[nd.out[0]]), os, v->shape, doff,
                             std::vector<int64_t>(rk, 0), std::vector<int64_t>(rk, 1), {}, 0.f))
           return false;
@@ -2207,7 +2267,15 @@ struct Planner {
   }
   // a consumer that computes no upsample itself: its input's pending Resize and,
   // when the input is an in-place Concat, every pending upsampled input of it
+  bool flush_tail(const std::string& name) {
+    auto t = cat_tail.find(name);
+    if (t == cat_tail.end()) return true;
+    std::function<bool()> copy = std::move(t->second.copy);
+    cat_tail.erase(t);
+    return copy();
+  }
   void flush_input(const std::string& name) {
+    flush_tail(name);
     flush_up(name);
     auto cu = cat_up.find(name);
     if (cu != cat_up.end())
@@ -2295,6 +2363,7 @@ struct Planner {
       if (!plan_node(k)) return false;
     }
     if (!up_pending.empty()) return fail("internal: Resize '" + up_pending.begin()->first + "' never launched");
+    if (!cat_tail.empty()) return fail("internal: Concat input copy into '" + cat_tail.begin()->first + "' never launched");
     if (!norm_pending.empty()) return fail("internal: InstanceNorm of '" + norm_pending.begin()->first + "' never applied");
     for (const IO& o : g.outputs) {
       Value* v = val(o.name);
