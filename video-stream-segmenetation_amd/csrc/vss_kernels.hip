@@ -578,7 +578,15 @@ struct Staged16 {
 #ifndef VSS_WDMA
 #define VSS_WDMA 1
 #endif
-constexpr bool block_wdma(int mode, int wimg_f4) { return VSS_WDMA && (mode == 2 || wimg_f4 >= 2560); }
+#ifndef VSS_WDMA_ALL
+#define VSS_WDMA_ALL 0  // (A/B knob: every layer)
+#endif
+#ifndef VSS_WDMA_FIRST
+#define VSS_WDMA_FIRST 0  // (A/B knob: the DMA issued before the input tile's loads)
+#endif
+constexpr bool block_wdma(int mode, int wimg_f4) {
+  return VSS_WDMA && (VSS_WDMA_ALL || mode == 2 || wimg_f4 >= 2560);
+}
 template <int N>
 __device__ __forceinline__ void dma_f4(const f4* src, f4* dst) {
   const int lane = (int)threadIdx.x & 63;
@@ -1057,6 +1065,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
     constexpr int GI = CIN / 16;  // 16-channel items per pixel
     Staged16<P_IN_PAD * GI, XP, VSS_STAGE16> st_x;
     std::conditional_t<WDMA, NoStaged, Staged<WIMG_F4>> st_w;
+    if constexpr (WDMA && VSS_WDMA_FIRST) dma_f4<WIMG_F4>(wsrc, reinterpret_cast<f4*>(smem + L.w1));
     {
       const float* xb[XP];
 #pragma unroll
@@ -1067,7 +1076,7 @@ __device__ __forceinline__ void block_body(const BlockParams& p, int bx, int by,
         return (unsigned)((yy * W + xx) * CIN + 16 * gq);
       });
     }
-    if constexpr (WDMA) dma_f4<WIMG_F4>(wsrc, reinterpret_cast<f4*>(smem + L.w1));
+    if constexpr (WDMA && !VSS_WDMA_FIRST) dma_f4<WIMG_F4>(wsrc, reinterpret_cast<f4*>(smem + L.w1));
     st_w.issue([&](int i) { return wsrc[i]; });
     VSS_STAMP(6);  // every load issued
     st_x.commit_sum([&](int i, int k, f4 v) {
