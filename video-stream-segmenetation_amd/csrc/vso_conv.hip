@@ -1130,7 +1130,10 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   // k_conv_tile_up keeps the uncapped choice: a taller tile interpolates each
   // staged source region for more pixels (MODNet's 35 -> 16 layer at 288x512:
   // 146 us at 2 x 32, 113 at 8 x 32; the 64 -> 32 at 144x256: 59.7 -> 49.1)
-  const int max_th = t.up ? 0 : max_th_env >= 0 ? max_th_env : (prec == PREC_F32 ? 0 : 2);
+  // (64-channel upsample tiles, VSO_UP_BM64: capped like the plain 16-bit
+  // ones — 8 x 32 x 64 ran at 319 VGPRs, one wave per SIMD: 99 us against the
+  // 2 x 32 x 64 tile's 50, profiles/r05x r05ao)
+  const int max_th = (t.up && t.bm <= 32) ? 0 : max_th_env >= 0 ? max_th_env : (prec == PREC_F32 ? 0 : 2);
   long wgs = 0;
   for (int k = 0; k < nc; ++k) {
     if (max_th > 0 && cand[k][0] > max_th && k + 1 < nc) continue;

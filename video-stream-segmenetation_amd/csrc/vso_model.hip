@@ -1333,8 +1333,12 @@ struct Planner {
     // (one output-channel tile of at most 32 only: each tile would interpolate
     // the whole input again, and at 64 output channels the interpolation
     // measured slower than the Resize's own launch, MODNet 288x512 b8 bf16)
+    static const bool up_bm64 = [] {  // (A/B knob: 64-channel upsample tiles)
+      const char* e = std::getenv("VSO_UP_BM64");
+      return e && e[0] == '1';
+    }();
     if (tile && ups.size() == 1 && ts.s == 1 && (ts.ks == 3 || ts.ks == 5) && ts.Mp == ts.bm &&
-        ts.bm <= 32 &&
+        (ts.bm <= 32 || up_bm64) &&
         ts.prec != PREC_F32 && ups[0].c0 % 32 == 0 && ups[0].c1 % 32 == 0 && up_fuse_enabled()) {
       ConvTileShape tu{};
       tu.up = 1;
