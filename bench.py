@@ -279,6 +279,7 @@ class Watchdog:
         self.limit, self.rank, self.world = limit_s, rank, world
         self.stage, self.step, self.t = "start", -1, time.monotonic()
         self.armed, self.status = False, None
+        self.gather_form = None  # the all-gather form the ranks run (VSS_OPT_GATHER_FORM)
         self._lock = threading.Lock()
         if limit_s > 0:
             threading.Thread(target=self._run, daemon=True).start()
@@ -308,7 +309,7 @@ class Watchdog:
                 continue
             rec = {"watchdog": "no progress", "rank": self.rank, "world": self.world, "stage": stage,
                    "last_step_issued": step, "seconds_without_progress": round(idle, 1),
-                   "gather_serial_env": os.environ.get("VSS_GATHER_SERIAL")}
+                   "gather_form": self.gather_form}
             try:
                 if self.status is not None:
                     rec.update(self.status())
@@ -450,6 +451,11 @@ def main():
     ap.add_argument("--no-latency", action="store_true", help="skip the one-call-at-a-time latency leg")
     ap.add_argument("--gather", action="store_true",
                     help="run the multi-GPU step (RCCL clique all-gather) even at one rank (a rehearsal of N > 1)")
+    ap.add_argument("--gather-form", default="ordered", choices=["ordered", "concurrent"],
+                    help="how the N > 1 all-gathers are issued (VSS_OPT_GATHER_FORM, DESIGN.md §6): 'ordered' "
+                         "(default: one communicator and one gather stream per rank, a total order of "
+                         "collectives) or 'concurrent' (one communicator per slot; opt-in until an 8-GPU "
+                         "record exists)")
     ap.add_argument("--dry-run-dist", action="store_true",
                     help="rehearse the multi-rank plumbing only (launch_ranks -> torch.distributed.run -> gloo "
                          "-> the clique-id broadcast, with placeholder id bytes) and stop before the first GPU "
@@ -490,6 +496,8 @@ def main():
         # reduction (CPU tensors); the masks go over the handle's own RCCL clique
         dist.init_process_group("gloo")
     wd = Watchdog(args.watchdog_s, rank, world)
+    gather = world > 1 or args.gather
+    wd.gather_form = args.gather_form if gather else None
     if args.dry_run_dist:
         # the same broadcast the GPU run makes (rank 0's clique ids -> every
         # rank), with placeholder bytes of the real size: RCCL's ncclGetUniqueId
@@ -509,7 +517,8 @@ def main():
         # print()'s separate newline write let two ranks' lines interleave
         line = json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local,
                            "env_world_size": os.environ.get("WORLD_SIZE"), "ids_len": len(ids[0]),
-                           "ids_sha256": hashlib.sha256(ids[0]).hexdigest()})
+                           "ids_sha256": hashlib.sha256(ids[0]).hexdigest(),
+                           "gather_form": wd.gather_form})
         os.write(sys.stdout.fileno(), (line + "\n").encode())
         if world > 1:
             dist.destroy_process_group()
@@ -532,8 +541,8 @@ def main():
                        max_frame_h=fh, max_frame_w=fw, queue_depth=S)
     if args.no_graph:
         sess.set_option(pkg.VSS_OPT_USE_GRAPH, 0)
-    gather = world > 1 or args.gather
-    wd.status = sess.comm_status
+    if gather:
+        sess.gather_form = args.gather_form  # (fixed by comm_init_rank)
     wd.arm("clique init")
     if world > 1:
         ids = [sess.comm_unique_id() if rank == 0 else None]
@@ -541,6 +550,10 @@ def main():
         sess.comm_init_rank(world, rank, ids[0])
     elif gather:
         sess.comm_init_rank(1, 0, sess.comm_unique_id())
+    # the communicators' health only once they exist (the record names the stage before)
+    wd.status = sess.comm_status
+    if gather:
+        wd.gather_form = sess.gather_form
     d_frames = torch.from_numpy(frames).to(dev)
     P = hm * wm
     # one output buffer per stream: step i writes buffer i % S on stream i % S
@@ -702,6 +715,7 @@ def main():
                 "graph": not args.no_graph,
                 "inflight": S,
                 "parallelism": f"dp{world}",
+                "gather_form": sess.gather_form if gather else None,
             },
             "mask_max_abs_err": err,
             "roofline": {

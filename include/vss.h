@@ -97,11 +97,24 @@ enum {
   VSS_OPT_GRAPH_PATCHES = 9, /* graph replays that patched their buffers' kernel parameters */
   VSS_OPT_COMM_RANKS = 10,   /* ranks of the handle's RCCL clique (ncclCommCount; the GPUs of a
                                 multi-GPU handle; 1 without a clique)                        */
-  VSS_OPT_GATHER_CALLS = 11  /* vss_segment_gather_device calls so far: call i runs on slot (and
-                                that slot's communicator) i % queue_depth, counted apart from the
-                                other device calls, so ranks that interleave different
-                                vss_segment_device calls still agree on every collective's
-                                communicator */
+  VSS_OPT_GATHER_CALLS = 11, /* vss_segment_gather_device calls so far: call i runs on slot i %
+                                queue_depth, counted apart from the other device calls, so ranks
+                                that interleave different vss_segment_device calls still agree on
+                                every collective (read-only) */
+  VSS_OPT_GATHER_FORM = 12   /* how vss_segment_gather_device issues its all-gathers (VSS_GATHER_*);
+                                settable until vss_comm_init_rank, fixed after it.  Default
+                                VSS_GATHER_ORDERED (environment VSS_GATHER_SERIAL=0 at vss_create:
+                                VSS_GATHER_CONCURRENT) */
+};
+
+/* VSS_OPT_GATHER_FORM values. */
+enum {
+  VSS_GATHER_ORDERED = 0,    /* one communicator (slot 0's, the only one created) and one gather
+                                stream: every rank issues one total order of collectives (its call
+                                order), which no stream -> hardware-queue mapping can reorder; the
+                                forwards of the batches in flight still overlap the gathers */
+  VSS_GATHER_CONCURRENT = 1  /* one communicator per slot, each gather on its slot's stream: the
+                                gathers of the batches in flight overlap each other too */
 };
 
 typedef struct vss_handle vss_handle;
@@ -163,7 +176,10 @@ int vss_create(const vss_config* cfg, vss_handle** out);
 /* Replaces InferenceSession.release. */
 void vss_destroy(vss_handle* h);
 
-/* Replaces _OrtGetLastError (ort-wasm-simd-threaded.mjs:50). */
+/* Replaces _OrtGetLastError (ort-wasm-simd-threaded.mjs:50).  Thread-safe: the
+ * handle's last message is copied into a buffer of the calling thread, valid
+ * until that thread's next vss_last_error call (NULL handle: the calling
+ * thread's last failure without a handle, e.g. vss_create's). */
 const char* vss_last_error(const vss_handle* h);
 
 int vss_get_info(const vss_handle* h, vss_info* info);
@@ -203,6 +219,17 @@ int vss_submit(vss_handle* h, const uint8_t* frames, int n, int height, int widt
  * into the pinned staging (no packing copy on the caller's side). */
 int vss_submit_list(vss_handle* h, const uint8_t* const* frames, int n, int height, int width, int channels,
                     size_t row_stride, float* masks_out, int out_mode, vss_ticket* ticket);
+
+/* vss_submit_list with a completion callback instead of a wait, for a host
+ * that must not block a thread per batch (the N-API addon's one submit thread
+ * per handle: its calls are queued in call order, and cb resolves the batch's
+ * promise): waits for a free slot instead of returning VSS_E_BUSY (from a
+ * completion callback, where that wait could not end: VSS_E_BUSY).  cb fires
+ * on the handle's completion thread once masks_out is filled or the batch
+ * failed, in submission order; *ticket (may be NULL) as vss_submit's. */
+int vss_submit_list_async(vss_handle* h, const uint8_t* const* frames, int n, int height, int width, int channels,
+                          size_t row_stride, float* masks_out, int out_mode, vss_callback cb, void* user,
+                          vss_ticket* ticket);
 
 /* Block until batch `ticket` is done (its masks_out filled); returns that
  * batch's status.  vss_query: 1 done, 0 still running, < 0 an error. */

@@ -503,6 +503,26 @@ def ir_chain():
     return b.model([("x", [2, 16, 38, 67])], [(t, [2, 96, 5, 9]), (t4, [2, 320, 3, 5])])
 
 
+def dw_separable_chain():
+    """MobileNetV1-style depthwise-separable blocks with ReLU6 (dw 3x3 -> Clip
+    -> 1x1 -> Clip, twice, then a stride-2 pair): the first 1x1's input is a
+    depthwise output that the planner leaves to its 1x1 consumer (no launch of
+    its own), and the 1x1 -> Clip -> dw -> Clip -> 1x1 after it has the shape of
+    an inverted residual, which must not take the fused k_ir form over an input
+    nothing wrote."""
+    b = Builder(21)
+    zero = lambda: b.const(np.array(0, np.float32))
+    six = lambda: b.const(np.array(6, np.float32))
+    clip = lambda t: b.op("Clip", [t, zero(), six()])
+    t = clip(b.conv("x", 32, 32, 3, group=32))
+    t = clip(b.conv(t, 32, 64, 1))
+    t = clip(b.conv(t, 64, 64, 3, group=64))
+    t = clip(b.conv(t, 64, 64, 1))
+    t = clip(b.conv(t, 64, 64, 3, stride=2, group=64))
+    t = b.conv(t, 64, 48, 1)
+    return b.model([("x", [2, 32, 30, 44])], [(t, [2, 48, 15, 22])])
+
+
 def conv_up_thin():
     """A pending 2x Resize through an in-place Concat into a thin 1x1 head
     (<= 4 outputs, k_conv_thin: computes no upsample itself), so the planner

@@ -45,6 +45,21 @@ def test_gpus_2_dry_run_reaches_the_clique_id_broadcast():
     assert by_rank[0]["ids_sha256"] == by_rank[1]["ids_sha256"]
 
 
+def test_gpus_2_selects_the_ordered_gather_form():
+    """the first R > 1 run must not be able to deadlock, so the
+    N > 1 bench defaults to the ordered all-gather (one communicator and one
+    gather stream per rank: one total order of collectives); the
+    concurrent per-slot communicators are opt-in (--gather-form concurrent).
+    Every rank reports the form it would run."""
+    import json
+    for extra, want in (([], "ordered"), (["--gather-form", "concurrent"], "concurrent")):
+        r = _run(["--gpus", "2", "--dry-run-dist"] + extra)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{") and '"dry_run"' in x]
+        assert sorted(d["rank"] for d in lines) == [0, 1], r.stdout
+        assert all(d["gather_form"] == want for d in lines), (extra, lines)
+
+
 def test_watchdog_ends_a_stalled_multi_rank_run_with_a_record():
     """a rank that never reaches the barrier (--test-stall-rank,
     on the --dry-run-dist path: the same launcher, gloo group and broadcast as
@@ -66,6 +81,7 @@ def test_watchdog_ends_a_stalled_multi_rank_run_with_a_record():
     assert (0, "dry-run: barrier") in stages or (1, "dry-run: stalled rank") in stages, stages
     for d in recs:
         assert d["world"] == 2 and d["seconds_without_progress"] >= 3
+        assert d["gather_form"] == "ordered", d  # the record names the form the ranks run
     assert el < 120, el
 
 

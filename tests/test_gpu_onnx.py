@@ -284,6 +284,67 @@ def test_inverted_residuals_16bit_knobs(ort, knob, value):
         assert np.array_equal(here, other)
 
 
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_depthwise_separable_chain(ort, precision):
+    """dw -> Clip -> 1x1 -> Clip -> dw -> Clip -> 1x1 (MobileNetV1 blocks): the
+    first depthwise is computed inside its 1x1 consumer (no launch writes its
+    output), so the 1x1 -> dw -> 1x1 after it — an inverted residual's shape —
+    must not be planned as a fused k_ir over that unwritten input.
+    The depthwise / 1x1 forms are unrounded in the 16-bit oracle as well: both
+    precisions at the f32 bar."""
+    data = M.dw_separable_chain()
+    feeds = {"x": np.random.default_rng(31).standard_normal((2, 32, 30, 44)).astype(np.float32)}
+    want = R.run(R.load(data), feeds, conv_operands=None if precision == "f32" else precision)
+    with ort.InferenceSession(data, precision=precision) as s:
+        got = s.run(feeds)
+        names = s.launches()
+        assert s.ir_blocks() == 0, names
+    print(precision, names)
+    _check(got, want, f"dw_separable {precision}")
+
+
+def test_small_graphs_two_lanes_bitwise(ort):
+    """The two-lane schedule on small graphs (forced by VSO_LANES,
+    read once per process, so one child process per setting runs every case):
+    a Concat tail into a dense conv, fused Resize -> conv, a pending
+    InstanceNorm, k_ir blocks and a depthwise computed in its 1x1 consumer —
+    bitwise equal to the one-lane capture, bf16 and f32 sessions."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    cases = [("modnet_like", "M.modnet_like()", "{'input': r.random((1, 3, 64, 96), dtype=np.float32)}"),
+             ("ir_chain", "M.ir_chain()", "{'x': r.standard_normal((2, 16, 38, 67)).astype(np.float32)}"),
+             ("conv_up", "M.conv_up()", "{'lo': r.standard_normal((2, 64, 9, 17)).astype(np.float32), "
+              "'skip': r.standard_normal((2, 5, 18, 34)).astype(np.float32), "
+              "'lo2': r.standard_normal((2, 32, 11, 13)).astype(np.float32)}"),
+             ("dw_sep", "M.dw_separable_chain()", "{'x': r.standard_normal((2, 32, 30, 44)).astype(np.float32)}")]
+    outs = {}
+    for lanes in ("2", "1"):
+        body = "; ".join(
+            f"r = np.random.default_rng(3); s = o.InferenceSession({mk}, precision=pr); a = s.run({fd}); "
+            f"res['{nm}_' + pr] = (np.concatenate([v.ravel() for v in a.values()]), s.lanes()); s.close()"
+            for nm, mk, fd in cases)
+        code = ("import numpy as np, sys; sys.path.insert(0, 'tests'); import onnx_models as M; "
+                "import importlib.util, os; spec = importlib.util.spec_from_file_location('vss_amd', "
+                "'video-stream-segmenetation_amd/__init__.py', submodule_search_locations=['video-stream-segmenetation_amd']); "
+                "m = importlib.util.module_from_spec(spec); sys.modules['vss_amd'] = m; spec.loader.exec_module(m); "
+                "import vss_amd.ort as o; res = {}\n"
+                f"for pr in ('bf16', 'f32'):\n    {body}\n"
+                f"np.savez('gpurun_out/small_lanes{lanes}.npz', **{{k: v[0] for k, v in res.items()}}); "
+                "print(' '.join(f'{k}:{v[1]}' for k, v in res.items()))")
+        r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, VSO_LANES=lanes),
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        print(lanes, r.stdout.strip())
+        used = dict(kv.split(":") for kv in r.stdout.split())
+        if lanes == "2":  # the graphs with independent branches put some on the side lane
+            assert any(v == "2" for v in used.values()), used
+        outs[lanes] = dict(np.load(os.path.join(root, "gpurun_out", f"small_lanes{lanes}.npz")))
+    for k in outs["1"]:
+        assert np.array_equal(outs["2"][k], outs["1"][k]), k
+
+
 @pytest.mark.parametrize("precision", ["bf16", "f32"])
 def test_modnet_two_lanes_bitwise(ort, precision):
     """The captured graph's two lanes (vso_lane_count; launches that share no

@@ -57,16 +57,30 @@ def test_device_ids_rejected(pkg, torch_cuda):
     assert e.value.code == pkg.VSS_E_INVALID_ARG
 
 
-def test_clique_one_rank_gather_bitwise(pkg, synthetic, torch_cuda):
+@pytest.mark.parametrize("form", ["ordered", "concurrent"])
+def test_clique_one_rank_gather_bitwise(pkg, synthetic, torch_cuda, form):
+    """Both all-gather forms (VSS_OPT_GATHER_FORM) at one rank:
+    bitwise the plain handle's masks; the ordered form (the default) creates
+    slot 0's communicator alone, and the form is fixed once the clique exists;
+    vss_comm_status reports every slot -1 until then."""
     torch = torch_cuda
     f = _frames(synthetic, 8, start=60)
     with pkg.Session(dtype="bf16x2", max_batch=8, max_frame_h=480, max_frame_w=640, queue_depth=2) as s:
         ref, _, _ = s.segment_frames(f)
+        assert s.gather_form == "ordered"
+        assert s.comm_status()["async_errors"] == [-1, -1]
+        s.gather_form = form
         ids = s.comm_unique_id()
         assert len(ids) == 2 * 128
         with pytest.raises(pkg.VssError):
             s.comm_init_rank(1, 0, ids[:128])  # one id per slot is required
         s.comm_init_rank(1, 0, ids)
+        assert s.gather_form == form
+        other = "concurrent" if form == "ordered" else "ordered"
+        with pytest.raises(pkg.VssError):
+            s.gather_form = other  # fixed by comm_init_rank
+        st = s.comm_status()["async_errors"]
+        assert st[0] in (0, 7) and (st[1] == -1 if form == "ordered" else st[1] in (0, 7)), st
         d = torch.from_numpy(f).cuda()
         outs = [torch.zeros((8, 144 * 256), dtype=torch.float32, device="cuda") for _ in range(3)]
         streams = [torch.cuda.Stream() for _ in range(2)]

@@ -41,6 +41,9 @@ VSS_OK, VSS_E_INVALID_ARG, VSS_E_HIP, VSS_E_RCCL, VSS_E_BUSY, VSS_E_OOM, VSS_E_I
 DTYPES = {"f32": 0, "bf16x2": 1}
 VSS_OPT_USE_GRAPH, VSS_OPT_PROFILE, VSS_OPT_KEEP_STEM, VSS_OPT_ROW_FETCH = 1, 2, 6, 7
 VSS_OPT_GRAPH_BUILDS, VSS_OPT_GRAPH_PATCHES, VSS_OPT_COMM_RANKS, VSS_OPT_GATHER_CALLS = 8, 9, 10, 11  # read-only
+VSS_OPT_GATHER_FORM = 12  # settable until comm_init_rank
+VSS_GATHER_ORDERED, VSS_GATHER_CONCURRENT = 0, 1
+GATHER_FORMS = {"ordered": VSS_GATHER_ORDERED, "concurrent": VSS_GATHER_CONCURRENT}
 VSS_CREATE_NO_AUTOTUNE = 1
 VSS_OUT_MODEL, VSS_OUT_FRAME = 0, 1
 
@@ -395,6 +398,18 @@ class Session:
     def graph_patches(self) -> int:
         """Replays that patched a graph's buffer pointers (callers rotating buffers)."""
         return self.get_option(VSS_OPT_GRAPH_PATCHES)
+
+    @property
+    def gather_form(self) -> str:
+        """How segment_gather_device issues its all-gathers: "ordered" (one
+        communicator and one gather stream: one total order of collectives per
+        rank, the default) or "concurrent" (one communicator per slot)."""
+        v = self.get_option(VSS_OPT_GATHER_FORM)
+        return next(k for k, f in GATHER_FORMS.items() if f == v)
+
+    @gather_form.setter
+    def gather_form(self, form: str):
+        self.set_option(VSS_OPT_GATHER_FORM, GATHER_FORMS[form])
 
     @property
     def comm_ranks(self) -> int:

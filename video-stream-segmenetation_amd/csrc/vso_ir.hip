@@ -11,11 +11,12 @@
 // The seam's fused block (csrc/vss_kernels.hip k_block) on the session's NCHW
 // f32 tensors: a workgroup owns a 4 x 16 output tile, all output channels and
 // a slice of the hidden channels (KS slices per tile when the image has few
-// tiles: the partial tiles meet in the last-arriving workgroup, in slice
-// order — k_conv_tile's split-K protocol, deterministic).  Prologue: the input
-// region (tile + halo) for every input channel, staged in LDS as [c][pixel]
-// (rows 4 mod 8 floats apart: the MFMA B reads of lanes (r, g), rows 4g
-// apart, fall on complementary banks).  Per 16 hidden channels ("chunk"):
+// tiles: each slice stores its plain partial sums and k_ir_reduce adds them in
+// slice order — deterministic).  Prologue: the input region (tile + halo) for
+// every input channel, staged in LDS as [c][pixel] (rows 4 mod 8 floats apart:
+// the MFMA B reads of lanes (r, g), rows 4g apart, fall on complementary
+// banks).  Two forms, the same chunk structure:
+//  * k_ir (f32 sessions), per 16 hidden channels ("chunk"):
 //   expand  — the region's 16-pixel blocks dealt to the 4 waves,
 //             v_mfma_f32_16x16x4_f32 (exact f32 products, as k_conv_pw): D =
 //             W1[chunk][c] x X[c][pixel], bias as the C operand, clip, zero
@@ -28,10 +29,17 @@
 //             registers in the project MFMA's B layout;
 //   project — 4 MFMAs per 16 output channels (A = W2[out][chunk]), acc in
 //             registers across the chunks.
-// Weights are read from L2 per chunk, the depthwise / project ones in flight
-// during the expand, the next chunk's expand ones during the dw / project.
-// Every operand stays f32 in every session precision (the convolutions here
-// are 1x1 / grouped: onnx_ref.tiled_conv() rounds none of them either).
+//   Its weights are read from L2 per chunk, the depthwise / project ones in
+//   flight during the expand, the next chunk's expand ones during the dw /
+//   project; every operand stays f32.
+//  * k_ir_b16 (bf16 / f16 sessions): every 1x1 product on
+//   v_mfma_f32_16x16x32_bf16 over hi + lo bf16 splits of both operands (w x =
+//   wh xh + wh xl + wl xh, ~2^-16 relative: about f32 precision — the
+//   convolutions here are 1x1 / grouped, which onnx_ref.tiled_conv() rounds in
+//   no session precision); the slice's weights pre-split and pre-ordered on
+//   the host into one slab that the prologue copies to LDS by 16-byte LDS-DMA
+//   (not read from L2 per chunk), the input region split once into registers,
+//   projects per pair of chunks (32 hidden channels = one MFMA's K).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -1001,6 +1001,9 @@ struct Planner {
     if (!ir_enabled()) return 0;
     const Node& ex = g.nodes[ni];
     if (ibn.count(ni) || ex.in.size() < 2) return 0;
+    // an input that is a depthwise output left to its 1x1 consumer (pending_dw:
+    // no launch writes it) is computed by plan_conv's fused form, not here
+    if (pending_dw.count(ex.in[0])) return 0;
     Value* x = val(ex.in[0]);
     Value* w1 = val(ex.in[1]);
     if (!x || x->is_const || x->shape.size() != 4 || !w1 || !w1->is_const || w1->c.dims.size() != 4) return 0;
@@ -1301,6 +1304,7 @@ struct Planner {
         return fail("Conv '" + nd.name + "': internal: fused depthwise producer");
       p.x = pre->second.first;
       p.pre = pre->second.second;
+      pending_dw.erase(pre);  // (its sole consumer: taken)
     }
     if (ib == ibn.end() && thin_conv_fits(p) && p.C <= kThinMaxC && thin_enabled()) {
       // (a matte / logit head: memory bound, on the VALU; its input's
@@ -2369,6 +2373,7 @@ struct Planner {
     if (!up_pending.empty()) return fail("internal: Resize '" + up_pending.begin()->first + "' never launched");
     if (!cat_tail.empty()) return fail("internal: Concat input copy into '" + cat_tail.begin()->first + "' never launched");
     if (!norm_pending.empty()) return fail("internal: InstanceNorm of '" + norm_pending.begin()->first + "' never applied");
+    if (!pending_dw.empty()) return fail("internal: depthwise Conv into '" + pending_dw.begin()->first + "' never computed");
     for (const IO& o : g.outputs) {
       Value* v = val(o.name);
       if (!v) return fail("graph output '" + o.name + "' is never produced");
@@ -2442,6 +2447,10 @@ static LaneSchedule schedule_lanes(const vso_session* s, int lanes) {
   for (size_t i = 0; i < n; ++i) {
     std::set<int> deps;
     std::set<int> used;
+    // a launch that registered no parameter block: unknown buffers, so it
+    // conflicts with every buffer (ordered after and before everything)
+    if (s->launches[i].io.empty())
+      for (int k = 0; k < (int)rs.size(); ++k) used.insert(k);
     for (const Region& rg : s->launches[i].io)
       for (size_t o = 0; o + 8 <= rg.n; o += 8) {
         uint64_t v;
@@ -2523,14 +2532,21 @@ int run_graph(vso_session* s, hipStream_t st) {
     for (size_t i = 0; i < n && ok; ++i) {
       hipStream_t ls_st = ls.lane[i] ? s->side : cs;
       if (ls.wait_on[i] >= 0) ok = hipStreamWaitEvent(ls_st, ev[ls.wait_on[i]], 0) == hipSuccess;
+      if (!ok) break;  // (never captured without its cross-lane dependency)
       s->launches[i].fn(ls_st);
-      if (ok && ls.record[i]) ok = hipEventRecord(ev[i], ls_st) == hipSuccess;
+      if (ls.record[i]) ok = hipEventRecord(ev[i], ls_st) == hipSuccess;
     }
-    if (ok && ls.used > 1)  // and rejoins it at the end
-      ok = hipEventRecord(join, s->side) == hipSuccess && hipStreamWaitEvent(cs, join, 0) == hipSuccess;
+    if (ls.used > 1) {  // the side lane rejoins the capture, also after a failure (so it can end)
+      const bool joined = hipEventRecord(join, s->side) == hipSuccess && hipStreamWaitEvent(cs, join, 0) == hipSuccess;
+      ok = ok && joined;
+    }
     const hipError_t e = hipStreamEndCapture(cs, &g);
     if (!ok) {
       if (g) (void)hipGraphDestroy(g);
+      if (s->side) {  // whatever capture state it was left in: a fresh side stream next time
+        (void)hipStreamDestroy(s->side);
+        s->side = nullptr;
+      }
       return fail_s(s, VSO_E_HIP, "capturing the lane schedule failed");
     }
     s->lanes_used = ls.used;

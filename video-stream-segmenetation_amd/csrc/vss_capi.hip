@@ -298,7 +298,11 @@ constexpr size_t kKsplitWeightBytes = 40 * 1024;
 struct vss_handle {
   vss_config cfg{};            // this engine's config (max_batch = its share of the handle's)
   std::string weights_path;
+  // the last error: written by any thread that fails a call (several may
+  // submit at once) and by the completion thread; read by vss_last_error,
+  // which copies it under err_mu into the caller's thread-local buffer
   std::string err;
+  mutable std::mutex err_mu;
   int device = 0;
   hipStream_t stream = nullptr;          // NULL-stream device calls, post / composite, autotune
   std::vector<Rec> recs;
@@ -347,10 +351,16 @@ struct vss_handle {
   int user_max_batch = 0;          // the handle's max_batch (all GPUs)
   bool rccl = false;               // host calls all-gather over RCCL (device_ids given)
   int nranks = 1, rank = 0;        // vss_comm_init_rank clique (one GPU per process)
-  bool clique = false;
-  // VSS_GATHER_SERIAL=1: the clique's all-gathers on one communicator (slot
-  // 0's) and one stream, events ordering each gather after its forward and
-  // the caller's stream after the gather (vss_segment_gather_device)
+  // set (release) once every communicator of the clique exists: the lock-free
+  // vss_comm_status reads the communicators only after seeing it (acquire)
+  std::atomic<bool> clique{false};
+  // VSS_OPT_GATHER_FORM, fixed at vss_comm_init_rank.  VSS_GATHER_ORDERED (the
+  // default): the clique's all-gathers on one communicator (slot 0's, the only
+  // one created) and one stream, events ordering each gather after its forward
+  // and the caller's stream after the gather — one total order of collectives
+  // per rank.  VSS_GATHER_CONCURRENT: each slot's own communicator on the
+  // slot's stream (vss_segment_gather_device)
+  int gather_form = VSS_GATHER_ORDERED;
   hipStream_t gather_stream = nullptr;
   std::vector<hipEvent_t> gather_ev;  // per slot: [2k] forward done, [2k+1] gather done
   // Submissions (slot choice, staging, enqueue) are serialised by mu; no
@@ -360,7 +370,8 @@ struct vss_handle {
   std::mutex post_mu;              // the synchronous post / composite calls share scratch
   vss_ticket next_ticket = 0;      // host batches (vss_submit*, vss_segment*)
   unsigned long long device_calls = 0;  // vss_segment_device: slot = count % depth
-  unsigned long long gather_calls = 0;  // vss_segment_gather_device: slot (and communicator) = count % depth
+  std::atomic<unsigned long long> gather_calls{0};  // vss_segment_gather_device: slot = count % depth
+                                                   // (atomic: vss_comm_status reads it lock-free)
   long graph_builds = 0, graph_patches = 0;  // VSS_OPT_GRAPH_BUILDS / _PATCHES
   CopyPool* pool = nullptr;
   // The completion thread (started on the first host batch that needs one):
@@ -384,8 +395,13 @@ struct vss_handle {
 
 namespace {
 
+void set_err(vss_handle* h, const std::string& msg) {
+  std::lock_guard<std::mutex> lk(h->err_mu);
+  h->err = msg;
+}
+
 int fail(vss_handle* h, int code, const std::string& msg) {
-  if (h) h->err = msg;
+  if (h) set_err(h, msg);
   else g_tls_error = msg;
   return code;
 }
@@ -1348,7 +1364,7 @@ void completion_loop(vss_handle* h) {
     (void)hipSetDevice(h->device);
     {
       std::lock_guard<std::mutex> lk(h->mu);
-      if (st != VSS_OK) h->err = std::string("batch failed: ") + hipGetErrorString(e);
+      if (st != VSS_OK) set_err(h, std::string("batch failed: ") + hipGetErrorString(e));
       s.status = st;
       s.host_busy = false;
     }
@@ -1784,6 +1800,9 @@ int create_engine(const vss_config* cfg, int device, int max_batch, int user_max
   if (const char* ev = std::getenv("VSS_KSPLIT_PIXELS")) h->ksplit_pixels = std::atol(ev);
   if (const char* ev = std::getenv("VSS_KSPLIT")) h->ksplit_on = std::atoi(ev) != 0;
   if (const char* ev = std::getenv("VSS_FUSE_STEM")) h->fuse_stem = std::atoi(ev) != 0;
+  // (the round-5 knob: VSS_GATHER_SERIAL=0 selects the concurrent form, =1 the ordered one)
+  if (const char* ev = std::getenv("VSS_GATHER_SERIAL"))
+    h->gather_form = ev[0] == '0' ? VSS_GATHER_CONCURRENT : VSS_GATHER_ORDERED;
   int rc = load_weights(h);
   if (!rc) rc = plan(h);
   if (!rc) rc = upload(h);
@@ -1852,7 +1871,16 @@ extern "C" {
 
 int vss_version(void) { return VSS_VERSION; }
 
-const char* vss_last_error(const vss_handle* h) { return h ? h->err.c_str() : g_tls_error.c_str(); }
+const char* vss_last_error(const vss_handle* h) {
+  // a handle's message is copied under its lock into this thread's buffer:
+  // the pointer stays valid until this thread's next vss_last_error or failing
+  // call, whatever other threads' calls on the handle write meanwhile
+  if (!h) return g_tls_error.c_str();
+  thread_local std::string copy;
+  std::lock_guard<std::mutex> lk(h->err_mu);
+  copy = h->err;
+  return copy.c_str();
+}
 
 int vss_create(const vss_config* cfg, vss_handle** out) {
   if (!cfg || !out) return fail(nullptr, VSS_E_INVALID_ARG, "null cfg/out");
@@ -1993,6 +2021,15 @@ int vss_submit_list(vss_handle* h, const uint8_t* const* frames, int n, int heig
                      nullptr, nullptr, ticket);
 }
 
+int vss_submit_list_async(vss_handle* h, const uint8_t* const* frames, int n, int height, int width, int channels,
+                          size_t row_stride, float* masks_out, int out_mode, vss_callback cb, void* user,
+                          vss_ticket* ticket) {
+  if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
+  if (!frames || !cb) return fail(h, VSS_E_INVALID_ARG, "null frames/callback");
+  return submit_host(h, nullptr, frames, n, height, width, channels, row_stride, masks_out, out_mode, true, false, cb,
+                     user, ticket);
+}
+
 // The slot holding host ticket t, or -1 when no slot does any more: a slot
 // takes a new host batch only once it is free (its previous batch done and
 // completed), so a ticket no slot holds is done.  mu held.
@@ -2115,13 +2152,16 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
 int vss_comm_status(vss_handle* h, int* async_errors, int cap, int* nslots, unsigned long long* gather_calls) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   // no handle lock: a watchdog calls this while another thread may be blocked
-  // inside a call that holds it; the communicators do not change after init
+  // inside a call that holds it.  The communicators are read only once the
+  // clique is published (vss_comm_init_rank's release store; they do not
+  // change after it); before that every slot reports -1
   const int ns = (int)h->slots.size();
   if (nslots) *nslots = ns;
-  if (gather_calls) *gather_calls = h->gather_calls;
+  if (gather_calls) *gather_calls = h->gather_calls.load(std::memory_order_relaxed);
+  const bool ready = h->clique.load(std::memory_order_acquire) || h->rccl;
   for (int k = 0; k < ns && k < cap && async_errors; ++k) {
     ncclResult_t ae = ncclSuccess;
-    const ncclComm_t c = h->slots[k].comm;
+    const ncclComm_t c = ready ? h->slots[k].comm : nullptr;
     async_errors[k] = !c ? -1 : (ncclCommGetAsyncError(c, &ae) == ncclSuccess ? (int)ae : -2);
   }
   return VSS_OK;
@@ -2149,7 +2189,9 @@ int vss_comm_init_rank(vss_handle* h, int nranks, int rank, const void* ids, siz
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipDeviceSynchronize());
-  for (size_t k = 0; k < h->slots.size(); ++k) {
+  // the ordered form uses slot 0's communicator alone: only it is created
+  const size_t ncomm = h->gather_form == VSS_GATHER_ORDERED ? 1 : h->slots.size();
+  for (size_t k = 0; k < ncomm; ++k) {
     ncclUniqueId id;
     std::memcpy(&id, static_cast<const char*>(ids) + k * sizeof(ncclUniqueId), sizeof(id));
     NCCL_TRY(h, ncclCommInitRank(&h->slots[k].comm, nranks, id, rank));
@@ -2159,7 +2201,7 @@ int vss_comm_init_rank(vss_handle* h, int nranks, int rank, const void* ids, siz
   for (hipEvent_t& e : h->gather_ev) HIP_TRY(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   h->nranks = nranks;
   h->rank = rank;
-  h->clique = true;
+  h->clique.store(true, std::memory_order_release);
   return VSS_OK;
 }
 
@@ -2176,10 +2218,10 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
   // round-robin over the gather calls alone (a counter of their own), so every
   // rank uses the same slot's communicator for its i-th gather whatever other
   // device calls it interleaves
-  static const bool serial = getenv("VSS_GATHER_SERIAL") && getenv("VSS_GATHER_SERIAL")[0] == '1';
-  const int k = (int)(h->gather_calls % h->slots.size());
+  const bool serial = h->gather_form == VSS_GATHER_ORDERED;
+  const int k = (int)(h->gather_calls.load(std::memory_order_relaxed) % h->slots.size());
   if ((rc = comm_healthy(h, h->slots[serial ? 0 : k].comm, serial ? 0 : k))) return rc;
-  h->gather_calls++;
+  h->gather_calls.fetch_add(1, std::memory_order_relaxed);
   Slot& sl = h->slots[k];
   if ((rc = claim_slot(h, sl, s))) return rc;
   if ((rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, sl.d_masks, s))) {
@@ -2187,15 +2229,15 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
     return rc;
   }
   const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
-  // Default: each slot's own communicator on the slot's stream, so the
-  // gathers of the batches in flight overlap (at one rank 170k frames/s vs
-  // 123k with every gather on one stream).  Every rank uses slot k for its
-  // i-th call (round-robin), so each communicator sees its collectives in the
-  // same order on every rank, which is what RCCL requires; the kernels of
-  // several communicators need to co-run only to the extent of their
-  // channels (tens of CUs of 256).  VSS_GATHER_SERIAL=1 puts every gather on
-  // slot 0's communicator and one stream instead (a total order, for systems
-  // where concurrent communicators misbehave).
+  // VSS_GATHER_ORDERED (default): every gather on slot 0's
+  // communicator and one stream — one total order of collectives per rank, the
+  // same on every rank (call order), whatever the runtime's stream -> hardware
+  // queue mapping; the forwards of the batches in flight still overlap the
+  // gathers.  VSS_GATHER_CONCURRENT (opt-in until an 8-GPU record exists):
+  // each slot's own communicator on the slot's stream, so the gathers of the
+  // batches in flight overlap too (at one rank 170k frames/s vs 123k); every
+  // rank uses slot k for its i-th call, so each communicator sees its
+  // collectives in the same order on every rank.
   ncclResult_t nr = ncclSuccess;
   hipError_t he = hipSuccess;
   if (!serial) {
@@ -2281,9 +2323,17 @@ int vss_set_option(vss_handle* h, int option, int value) {
       option == VSS_OPT_GATHER_CALLS)
     return fail(h, VSS_E_INVALID_ARG, "read-only option (vss_get_option)");
   if (option != VSS_OPT_KEEP_STEM && option != VSS_OPT_USE_GRAPH && option != VSS_OPT_PROFILE &&
-      option != VSS_OPT_ROW_FETCH)
+      option != VSS_OPT_ROW_FETCH && option != VSS_OPT_GATHER_FORM)
     return fail(h, VSS_E_INVALID_ARG, "unknown option");
   std::lock_guard<std::mutex> lk(h->mu);
+  if (option == VSS_OPT_GATHER_FORM) {
+    if (value != VSS_GATHER_ORDERED && value != VSS_GATHER_CONCURRENT)
+      return fail(h, VSS_E_INVALID_ARG, "gather form: VSS_GATHER_ORDERED or VSS_GATHER_CONCURRENT");
+    if (h->clique && value != h->gather_form)
+      return fail(h, VSS_E_INVALID_ARG, "the gather form is fixed at vss_comm_init_rank");
+    h->gather_form = value;
+    return VSS_OK;
+  }
   for (vss_handle* e : engines(h)) {
     if (option == VSS_OPT_KEEP_STEM) {
       if ((value ? 1 : 0) != e->keep_stem) drop_graphs(e);  // the graphs hold the stem pointer
@@ -2316,8 +2366,9 @@ int vss_get_option(vss_handle* h, int option, int* value) {
       return VSS_OK;
     }
     case VSS_OPT_GATHER_CALLS:
-      *value = (int)(h->gather_calls & 0x7FFFFFFF);
+      *value = (int)(h->gather_calls.load() & 0x7FFFFFFF);
       return VSS_OK;
+    case VSS_OPT_GATHER_FORM: *value = h->gather_form; return VSS_OK;
     case VSS_OPT_COMM_RANKS: {
       if (h->rccl) {
         *value = 1 + (int)h->peers.size();
@@ -2530,7 +2581,7 @@ constexpr int kRangeTab = 3 * 255 * 255 + 1;
 
 int post_fail(vss_post_state* st, int code, const std::string& msg) {
   st->err = msg;
-  if (st->h) st->h->err = msg;
+  if (st->h) set_err(st->h, msg);
   return code;
 }
 

@@ -12,10 +12,11 @@
 //   segment(handle, frames: Uint8Array | Uint8Array[], n, height, width, channels, rowStride, outMode?)
 //       -> Promise<Float32Array>      (n * maskH * maskW masks, or n * height * width with
 //                                      outMode 1 = VSS_OUT_FRAME; rejects with Error(vss_last_error)).
-//       Queued (vss_submit / vss_submit_list on the calling thread, vss_wait on a libuv
-//       worker): returns once the frames are staged, up to queueDepth batches in flight
-//       (beyond that it rejects with code -4 = VSS_E_BUSY; segment.ts keeps within it).
-//       An array of frames is copied frame by frame into the pinned staging (no packing).
+//       Queued: returns at once; the handle's submit thread submits the batches in call
+//       order (vss_submit_list_async: the frames copied frame by frame into the pinned
+//       staging, no packing) and the completion callback settles the promise through a
+//       thread-safe function (no thread waits per batch).  segment.ts keeps at most
+//       queueDepth batches in flight (beyond that the submit waits for a free slot).
 //   stagingAcquire(handle) -> {slot, data: Uint8Array}   zero-copy input: a free slot's pinned
 //       staging buffer (valid until the handle is destroyed; waits for a free slot)
 //   segmentStaged(handle, slot, n, height, width, channels, rowStride, outMode?) -> Promise<Float32Array>
@@ -46,8 +47,8 @@
 //       -> Promise<{affine: number[6] | null, box: number[4] | null, videoW, videoH}[]>
 //       (the postSetFaces form, one entry per frame)
 //   faceReset(tracker), faceDestroy(tracker)
-// segment waits for its batch on a libuv worker thread (napi_create_async_work),
-// so the event loop is not blocked — as `await session.run` does not block.
+//   traceDump() -> Float64Array   VSS_NAPI_TRACE=1: per-batch phase stamps (see TracePoint)
+// Nothing blocks the event loop while a batch runs — as `await session.run` does not block.
 #include <node_api.h>
 
 #include <execinfo.h>
@@ -56,12 +57,16 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <deque>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../../include/vsf.h"
@@ -78,7 +83,12 @@ namespace {
     }                                                                        \
   } while (0)
 
+// Set by the environment's cleanup hook: finalizers that run during teardown
+// make no more N-API calls (the env is going away).
+std::atomic<bool> g_env_closing{false};
+
 struct Post;
+struct Submitter;
 
 struct Handle {
   vss_handle* h = nullptr;
@@ -90,7 +100,10 @@ struct Handle {
   int pending = 0;
   bool closing = false;    // destroy() / finalizer ran: no new work; release when pending == 0
   bool finalized = false;  // the JS external is gone: the last completion deletes this
+  Submitter* sub = nullptr;  // segment()'s submit thread + result delivery (created on first use)
 };
+
+void stop_submitter(Handle* hd);  // (pending == 0: joins the thread, releases the delivery)
 
 struct Post {
   Handle* hd = nullptr;
@@ -106,6 +119,7 @@ void release_handle(Handle* hd) {
     p->hd = nullptr;
   }
   hd->posts.clear();
+  stop_submitter(hd);
   if (hd->h) vss_destroy(hd->h);
   hd->h = nullptr;
 }
@@ -449,45 +463,72 @@ napi_value PostDestroy(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
-// ---- queued segment: submit on the JS thread, wait on a libuv worker -------
+// ---- queued segment ----------------------------------------------------------
+// segment(): the JS thread validates the call, takes a result block and
+// queues the batch on the handle's submit thread (Submitter), then returns
+// its promise.  That one thread submits the batches in call order
+// (vss_submit_list_async: the staging copy of the frames into the slot's
+// pinned memory, on the handle's staging_threads pool, then H2D -> forward ->
+// D2H enqueued), so ticket order is call order and no two threads submit on a
+// handle at once (several libuv workers submitted concurrently).
+// The batch's completion callback, on the library's completion thread, hands
+// the batch to the JS thread through a thread-safe function that settles the
+// promise — no libuv worker is blocked in vss_wait per batch in flight.
+// VSS_NAPI_SYNC_STAGE=1 (the round-4 form): the submit (staging copy) runs
+// inside the call and a libuv worker waits for the batch.
+// VSS_NAPI_TRACE=1: per batch, CLOCK_MONOTONIC stamps (ns) of each phase for
+// traceDump() (tools/ts_prof.js: the phase table of profiles/r06*/).
+enum TracePoint : int {
+  TP_CALL = 0,      // segment() entered (JS thread)
+  TP_QUEUED,        // segment() returns: the batch is queued for the submit thread
+  TP_SUBMIT,        // the submit thread starts vss_submit_list_async
+  TP_SUBMITTED,     // it returned: frames staged, H2D / forward / D2H enqueued
+  TP_DONE,          // completion callback (the library's completion thread)
+  TP_JS,            // the JS thread runs the delivery
+  TP_RESOLVED,      // the promise is resolved
+  TP_COUNT
+};
+const bool g_trace = [] {
+  const char* e = std::getenv("VSS_NAPI_TRACE");
+  return e && e[0] == '1';
+}();
+std::mutex& g_trace_mu = *new std::mutex;
+std::vector<double>& g_trace_rows = *new std::vector<double>;  // [batch][TP_COUNT + 1] (+ frames)
+
+double now_ns() {
+  return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct QueuedWork {
-  napi_async_work work = nullptr;
+  napi_async_work work = nullptr;  // (the synchronous-stage form only)
   napi_deferred deferred = nullptr;
   napi_ref out_ref = nullptr;
-  Handle* hd = nullptr;  // pending counted until QueuedComplete
+  Handle* hd = nullptr;  // pending counted until the promise is settled
   vss_handle* h = nullptr;
   vss_ticket ticket = 0;
   size_t out_count = 0;
   int rc = 0;
   std::string err, what = "vss_wait";
-  // segment(): the submit itself (its staging copy of the frames into pinned
-  // memory) runs here on the worker too, not on the JS thread; the frames'
-  // arrays are referenced until the batch is done
-  bool submit = false;
+  // the submit thread's inputs; the frames' arrays are referenced until the batch is done
   std::vector<const uint8_t*> list;
-  const uint8_t* contiguous = nullptr;
+  int slot = -1;  // segmentStaged: the leased slot whose pinned staging holds the frames
   int n = 0, height = 0, width = 0, channels = 0, out_mode = VSS_OUT_MODEL;
   size_t rs = 0;
   float* out = nullptr;
   std::vector<napi_ref> frame_refs;
+  double t[TP_COUNT] = {};
 };
 
-void QueuedExecute(napi_env, void* data) {  // libuv worker thread: no JS calls here
-  QueuedWork* w = static_cast<QueuedWork*>(data);
-  if (w->submit) {
-    w->rc = !w->list.empty() ? vss_submit_list(w->h, w->list.data(), w->n, w->height, w->width, w->channels, w->rs,
-                                               w->out, w->out_mode, &w->ticket)
-                             : vss_submit(w->h, w->contiguous, w->n, w->height, w->width, w->channels, w->rs, w->out,
-                                          w->out_mode, &w->ticket);
-    if (w->rc != VSS_OK) {
-      w->what = "vss_submit";
-      w->err = vss_last_error(w->h);
-      return;
-    }
-  }
-  w->rc = vss_wait(w->h, w->ticket);
-  if (w->rc != VSS_OK) w->err = vss_last_error(w->h);
-}
+struct Submitter {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<QueuedWork*> q;
+  bool stop = false;
+  napi_threadsafe_function tsfn = nullptr;
+  int owed = 0;  // (JS thread) batches whose delivery is still due: the tsfn keeps the loop alive while > 0
+};
 
 napi_value make_error(napi_env env, const std::string& what, int rc, const std::string& err) {
   napi_value msg, code, e;
@@ -498,8 +539,8 @@ napi_value make_error(napi_env env, const std::string& what, int rc, const std::
   return e;
 }
 
-void QueuedComplete(napi_env env, napi_status, void* data) {
-  QueuedWork* w = static_cast<QueuedWork*>(data);
+// Settle a batch's promise and drop its references (JS thread).
+void settle(napi_env env, QueuedWork* w) {
   if (w->rc == VSS_OK) {
     napi_value ab = nullptr, arr;
     napi_get_reference_value(env, w->out_ref, &ab);
@@ -510,10 +551,138 @@ void QueuedComplete(napi_env env, napi_status, void* data) {
   }
   napi_delete_reference(env, w->out_ref);
   for (napi_ref r : w->frame_refs) napi_delete_reference(env, r);
-  napi_delete_async_work(env, w->work);
+  if (g_trace) {
+    w->t[TP_RESOLVED] = now_ns();
+    std::lock_guard<std::mutex> lk(g_trace_mu);
+    g_trace_rows.insert(g_trace_rows.end(), w->t, w->t + TP_COUNT);
+    g_trace_rows.push_back((double)w->n);
+  }
   Handle* hd = w->hd;
   delete w;
   work_done(hd);
+}
+
+// The submit thread's delivery of a batch to the JS thread.
+void deliver_js(napi_env env, napi_value, void* context, void* data) {
+  QueuedWork* w = static_cast<QueuedWork*>(data);
+  if (!env) {  // the environment is being torn down: nothing to settle
+    delete w;
+    return;
+  }
+  if (g_trace) w->t[TP_JS] = now_ns();
+  Submitter* sub = static_cast<Submitter*>(context);
+  if (--sub->owed == 0) napi_unref_threadsafe_function(env, sub->tsfn);
+  settle(env, w);
+}
+
+// vss_callback: the batch is done (library completion thread).
+void batch_done(void* user, int status) {
+  QueuedWork* w = static_cast<QueuedWork*>(user);
+  if (g_trace) w->t[TP_DONE] = now_ns();
+  w->rc = status;
+  if (status != VSS_OK) w->err = vss_last_error(w->h);
+  napi_call_threadsafe_function(w->hd->sub->tsfn, w, napi_tsfn_nonblocking);
+}
+
+void submit_loop(Submitter* sub) {
+  for (;;) {
+    QueuedWork* w = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(sub->mu);
+      sub->cv.wait(lk, [&] { return sub->stop || !sub->q.empty(); });
+      if (sub->q.empty()) return;
+      w = sub->q.front();
+      sub->q.pop_front();
+    }
+    if (g_trace) w->t[TP_SUBMIT] = now_ns();
+    const int rc = w->slot >= 0 ? vss_submit_staged(w->h, w->slot, w->n, w->height, w->width, w->channels, w->rs,
+                                                    w->out, w->out_mode, batch_done, w, &w->ticket)
+                                : vss_submit_list_async(w->h, w->list.data(), w->n, w->height, w->width, w->channels,
+                                                        w->rs, w->out, w->out_mode, batch_done, w, &w->ticket);
+    if (g_trace) w->t[TP_SUBMITTED] = now_ns();
+    if (rc != VSS_OK) {  // never queued: no callback will come
+      w->rc = rc;
+      w->what = w->slot >= 0 ? "vss_submit_staged" : "vss_submit";
+      w->err = vss_last_error(w->h);
+      napi_call_threadsafe_function(sub->tsfn, w, napi_tsfn_blocking);
+    }
+  }
+}
+
+Submitter* submitter(napi_env env, Handle* hd) {
+  if (hd->sub) return hd->sub;
+  Submitter* sub = new Submitter();
+  napi_value name;
+  napi_create_string_utf8(env, "vss_segment", NAPI_AUTO_LENGTH, &name);
+  if (napi_create_threadsafe_function(env, nullptr, nullptr, name, 0, 1, nullptr, nullptr, sub, deliver_js,
+                                      &sub->tsfn) != napi_ok) {
+    delete sub;
+    return nullptr;
+  }
+  napi_unref_threadsafe_function(env, sub->tsfn);  // referenced only while deliveries are owed
+  sub->th = std::thread(submit_loop, sub);
+  hd->sub = sub;
+  return sub;
+}
+
+// Queue a batch on the submit thread (JS thread).
+void enqueue(napi_env env, Handle* hd, QueuedWork* w) {
+  Submitter* sub = hd->sub;
+  if (sub->owed++ == 0) napi_ref_threadsafe_function(env, sub->tsfn);
+  w->hd = hd;
+  ++hd->pending;
+  if (g_trace) w->t[TP_QUEUED] = now_ns();
+  {
+    std::lock_guard<std::mutex> lk(sub->mu);
+    sub->q.push_back(w);
+  }
+  sub->cv.notify_one();
+}
+
+void stop_submitter(Handle* hd) {
+  Submitter* sub = hd->sub;
+  if (!sub) return;
+  {
+    std::lock_guard<std::mutex> lk(sub->mu);
+    sub->stop = true;
+  }
+  sub->cv.notify_one();
+  if (sub->th.joinable()) sub->th.join();
+  // (at environment teardown Node finalizes the thread-safe function itself)
+  if (!g_env_closing.load()) napi_release_threadsafe_function(sub->tsfn, napi_tsfn_release);
+  delete sub;
+  hd->sub = nullptr;
+}
+
+// The synchronous-stage form: a libuv worker waits for the batch.
+void QueuedExecute(napi_env, void* data) {  // libuv worker thread: no JS calls here
+  QueuedWork* w = static_cast<QueuedWork*>(data);
+  w->rc = vss_wait(w->h, w->ticket);
+  if (w->rc != VSS_OK) w->err = vss_last_error(w->h);
+  if (g_trace) w->t[TP_DONE] = now_ns();
+}
+
+void QueuedComplete(napi_env env, napi_status, void* data) {
+  QueuedWork* w = static_cast<QueuedWork*>(data);
+  if (g_trace) w->t[TP_JS] = now_ns();
+  napi_delete_async_work(env, w->work);
+  settle(env, w);
+}
+
+// traceDump() -> Float64Array [batch][8]: the TracePoint stamps (ns, CLOCK_MONOTONIC
+// — process.hrtime's clock) and the batch's frame count; clears the record.
+napi_value TraceDump(napi_env env, napi_callback_info) {
+  std::vector<double> rows;
+  {
+    std::lock_guard<std::mutex> lk(g_trace_mu);
+    rows.swap(g_trace_rows);
+  }
+  napi_value ab, arr;
+  void* d = nullptr;
+  NAPI_OK(env, napi_create_arraybuffer(env, rows.size() * sizeof(double), &d, &ab));
+  if (!rows.empty()) std::memcpy(d, rows.data(), rows.size() * sizeof(double));
+  NAPI_OK(env, napi_create_typedarray(env, napi_float64_array, rows.size(), ab, 0, &arr));
+  return arr;
 }
 
 // The masks' ArrayBuffer: a pinned block (vss_host_alloc), so the batch's D2H
@@ -540,9 +709,6 @@ struct MaskBlock {
 std::mutex& g_pool_mu = *new std::mutex;
 std::multimap<size_t, void*>& g_pool = *new std::multimap<size_t, void*>;  // free pinned blocks by size
 size_t g_pinned_bytes = 0;             // every pinned block, free or live
-// Set by the environment's cleanup hook: finalizers that run during teardown
-// make no more N-API calls (the env is going away).
-std::atomic<bool> g_env_closing{false};
 constexpr size_t kPinnedCap = size_t(1) << 30;
 
 // VSS_NAPI_PINNED=0: malloc'd results (the completion copies), for A/B runs
@@ -697,7 +863,17 @@ napi_value Segment(napi_env env, napi_callback_info info) {
       return nullptr;
     }
   }
+  const double t_call = g_trace ? now_ns() : 0.0;
+  static const bool sync_stage = [] {
+    const char* e = std::getenv("VSS_NAPI_SYNC_STAGE");
+    return e && e[0] == '1';
+  }();
+  if (!sync_stage && !submitter(env, hd)) {
+    napi_throw_error(env, nullptr, "segment: cannot create the result delivery");
+    return nullptr;
+  }
   QueuedWork* w = new QueuedWork();
+  w->t[TP_CALL] = t_call;
   w->h = hd->h;
   w->out_count = out_mode == VSS_OUT_FRAME ? (size_t)n * height * width : (size_t)n * hd->mask_h * hd->mask_w;
   napi_value ab, promise;
@@ -708,21 +884,14 @@ napi_value Segment(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
-  // The submit — whose staging copy of the frames into the slot's pinned
-  // memory is most of its cost (3.7 MB per VGA batch of 8) — runs on the
-  // libuv worker with the wait, so the JS thread only enqueues: the frames'
-  // arrays are referenced until the batch is done, and the caller must not
-  // modify them before the promise settles (ts/segment.ts).  Opt-out
-  // VSS_NAPI_SYNC_STAGE=1: staged here, on the JS thread, before this returns
-  // (the round-4 behaviour: frames reusable at once).
-  static const bool sync_stage = [] {
-    const char* e = std::getenv("VSS_NAPI_SYNC_STAGE");
-    return e && e[0] == '1';
-  }();
+  if (!is_arr)
+    for (int i = 0; i < n; ++i) list.push_back(contiguous + (size_t)i * fbytes);
   if (!sync_stage) {
-    w->submit = true;
+    // the submit thread stages the frames (the submit's cost: 3.7 MB per VGA
+    // batch of 8 copied into pinned memory), so the JS thread only enqueues;
+    // the frames' arrays are referenced until the batch is done, and the
+    // caller must not modify them before the promise settles (ts/segment.ts)
     w->list = std::move(list);
-    w->contiguous = contiguous;
     w->n = n;
     w->height = height;
     w->width = width;
@@ -744,19 +913,16 @@ napi_value Segment(napi_env env, napi_callback_info info) {
       w->frame_refs.push_back(r);
     }
     napi_create_reference(env, ab, 1, &w->out_ref);
-    napi_value name;
-    napi_create_string_utf8(env, "vss_submit", NAPI_AUTO_LENGTH, &name);
-    NAPI_OK(env, napi_create_async_work(env, nullptr, name, QueuedExecute, QueuedComplete, w, &w->work));
-    NAPI_OK(env, napi_queue_async_work(env, w->work));
-    w->hd = hd;
-    ++hd->pending;
+    w->n = n;
+    enqueue(env, hd, w);
     return promise;
   }
   // staged here: the frames may be reused by the caller as soon as this returns
-  const int rc = is_arr ? vss_submit_list(hd->h, list.data(), n, height, width, channels, (size_t)rs,
-                                          static_cast<float*>(out), out_mode, &w->ticket)
-                        : vss_submit(hd->h, contiguous, n, height, width, channels, (size_t)rs,
-                                     static_cast<float*>(out), out_mode, &w->ticket);
+  w->n = n;
+  if (g_trace) w->t[TP_QUEUED] = w->t[TP_SUBMIT] = now_ns();
+  const int rc = vss_submit_list(hd->h, list.data(), n, height, width, channels, (size_t)rs, static_cast<float*>(out),
+                                 out_mode, &w->ticket);
+  if (g_trace) w->t[TP_SUBMITTED] = now_ns();
   if (rc != VSS_OK) {
     napi_reject_deferred(env, w->deferred, make_error(env, "vss_submit", rc, vss_last_error(hd->h)));
     delete w;
@@ -834,7 +1000,13 @@ napi_value SegmentStaged(napi_env env, napi_callback_info info) {
     napi_throw_range_error(env, nullptr, "segmentStaged: n, height, width and rowStride must be >= 1");
     return nullptr;
   }
+  const double t_call = g_trace ? now_ns() : 0.0;
+  if (!submitter(env, hd)) {
+    napi_throw_error(env, nullptr, "segmentStaged: cannot create the result delivery");
+    return nullptr;
+  }
   QueuedWork* w = new QueuedWork();
+  w->t[TP_CALL] = t_call;
   w->h = hd->h;
   w->out_count = out_mode == VSS_OUT_FRAME ? (size_t)n * height * width : (size_t)n * hd->mask_h * hd->mask_w;
   napi_value ab, promise;
@@ -845,20 +1017,18 @@ napi_value SegmentStaged(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   NAPI_OK(env, napi_create_promise(env, &w->deferred, &promise));
-  const int rc = vss_submit_staged(hd->h, slot, n, height, width, channels, (size_t)rs, static_cast<float*>(out),
-                                   out_mode, nullptr, nullptr, &w->ticket);
-  if (rc != VSS_OK) {
-    napi_reject_deferred(env, w->deferred, make_error(env, "vss_submit_staged", rc, vss_last_error(hd->h)));
-    delete w;
-    return promise;
-  }
+  // submitted by the submit thread, after every earlier call's batch (call
+  // order is ticket order); nothing to stage: the frames are in the slot
+  w->slot = slot;
+  w->n = n;
+  w->height = height;
+  w->width = width;
+  w->channels = channels;
+  w->rs = (size_t)rs;
+  w->out = static_cast<float*>(out);
+  w->out_mode = out_mode;
   napi_create_reference(env, ab, 1, &w->out_ref);
-  napi_value name;
-  napi_create_string_utf8(env, "vss_wait", NAPI_AUTO_LENGTH, &name);
-  NAPI_OK(env, napi_create_async_work(env, nullptr, name, QueuedExecute, QueuedComplete, w, &w->work));
-  NAPI_OK(env, napi_queue_async_work(env, w->work));
-  w->hd = hd;
-  ++hd->pending;
+  enqueue(env, hd, w);
   return promise;
 }
 
@@ -1526,6 +1696,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"stagingAcquire", nullptr, StagingAcquire, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"stagingRelease", nullptr, StagingRelease, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"segmentStaged", nullptr, SegmentStaged, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"traceDump", nullptr, TraceDump, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"destroy", nullptr, Destroy, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"postCreate", nullptr, PostCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"postSetConfig", nullptr, PostSetConfig, nullptr, nullptr, nullptr, napi_default, nullptr},
