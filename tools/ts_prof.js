@@ -41,7 +41,7 @@ function table(js) {
     for (let k = 0; k < PH.length; k++) ph[k].push((pts[k + 1] - pts[k]) / 1e3);
     total.push((j1 - j0) / 1e3);
   }
-  const out = { calls: n, total_us: stats(total) };
+  const out = { calls: n, total_us: stats(total), pool: addon.poolStats() };
   PH.forEach((p, k) => { out[p + '_us'] = stats(ph[k]); });
   return out;
 }

@@ -31,6 +31,7 @@
 #include <deque>
 #include <fstream>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -231,58 +232,70 @@ class CopyPool {
     const void* src;
     size_t len;
   };
-  // Copies every job; returns when all bytes are in place and every worker
-  // has left this generation (so no worker ever touches a later one's pieces
-  // with a stale index).
+  // Copies every job; returns as soon as every piece is in place.  A copy's
+  // pieces live in a generation object that the workers share (shared_ptr), so
+  // a worker that wakes after the copy is done finds no piece left and touches
+  // nothing: the caller never waits for a sleeping worker's wake-up (round 5
+  // waited for every worker to leave the generation — for one VGA frame, ~144
+  // row runs of 3.8 KB, the slowest wake-up of 7 threads set the call's time,
+  // 36 us at p50 where the caller alone copies it in ~14; tools/ts_prof.js).
   void run(const std::vector<Job>& jobs) {
     constexpr size_t kPiece = size_t(256) << 10;
-    std::vector<Job> pieces;
+    auto g = std::make_shared<Gen>();
     for (const Job& j : jobs)
       for (size_t off = 0; off < j.len; off += kPiece)
-        pieces.push_back({static_cast<char*>(j.dst) + off, static_cast<const char*>(j.src) + off,
-                          std::min(kPiece, j.len - off)});
-    if (pieces.size() <= 1 || workers_.empty()) {
-      for (const Job& p : pieces) staging_copy(p.dst, p.src, p.len);
+        g->pieces.push_back({static_cast<char*>(j.dst) + off, static_cast<const char*>(j.src) + off,
+                             std::min(kPiece, j.len - off)});
+    const size_t n = g->pieces.size();
+    if (n <= 1 || workers_.empty()) {
+      for (const Job& p : g->pieces) staging_copy(p.dst, p.src, p.len);
       return;
     }
-    std::unique_lock<std::mutex> lk(mu_);
-    pieces_ = &pieces;
-    next_.store(0);
-    active_ = workers_.size();
-    ++gen_;
-    lk.unlock();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      cur_ = g;
+      ++gen_;
+    }
     cv_.notify_all();
-    work(&pieces);
-    lk.lock();
-    done_cv_.wait(lk, [&] { return active_ == 0; });
-    pieces_ = nullptr;
+    work(*g);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return g->done.load() == n; });
+    if (cur_ == g) cur_.reset();
   }
 
  private:
-  void work(const std::vector<Job>* ps) {
-    for (size_t i = next_.fetch_add(1); i < ps->size(); i = next_.fetch_add(1))
-      staging_copy((*ps)[i].dst, (*ps)[i].src, (*ps)[i].len);
+  struct Gen {
+    std::vector<Job> pieces;
+    std::atomic<size_t> next{0}, done{0};
+  };
+  void work(Gen& g) {
+    const size_t n = g.pieces.size();
+    for (size_t i = g.next.fetch_add(1); i < n; i = g.next.fetch_add(1)) {
+      staging_copy(g.pieces[i].dst, g.pieces[i].src, g.pieces[i].len);
+      if (g.done.fetch_add(1) + 1 == n) {  // the last piece: wake the caller (under mu_: no lost wake-up)
+        std::lock_guard<std::mutex> lk(mu_);
+        done_cv_.notify_all();
+      }
+    }
   }
   void loop() {
     unsigned long seen = 0;
     for (;;) {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-      if (stop_) return;
-      seen = gen_;
-      const std::vector<Job>* ps = pieces_;
-      lk.unlock();
-      work(ps);
-      lk.lock();
-      if (--active_ == 0) done_cv_.notify_all();
+      std::shared_ptr<Gen> g;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        g = cur_;
+      }
+      if (g) work(*g);
     }
   }
   std::vector<std::thread> workers_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
-  const std::vector<Job>* pieces_ = nullptr;
-  std::atomic<size_t> next_{0};
-  size_t active_ = 0;
+  std::shared_ptr<Gen> cur_;
   unsigned long gen_ = 0;
   bool stop_ = false;
 };
@@ -1664,6 +1677,13 @@ int autotune(vss_handle* h) {
   if (int rc = ensure_staging(h, s)) return rc;  // the stem reads the staging buffer as frames
   static const char* mode_env = std::getenv("VSS_AUTOTUNE");
   const bool concurrent = h->slots.size() > 1 && mode_env && !std::strcmp(mode_env, "throughput");
+  // VSS_AUTOTUNE=lds: the latency timings, but the pick minimises the layer's
+  // LDS x lifetime (workgroups x allocated LDS x latency / rounds of
+  // workgroups: what one batch costs the LDS-full chip at 4 batches in flight,
+  // tools/lds_time.py) instead of its latency.  VSS_AUTOTUNE_DUMP=1: every
+  // candidate's numbers on stderr.
+  const bool lds_obj = mode_env && !std::strcmp(mode_env, "lds");
+  static const bool dump = std::getenv("VSS_AUTOTUNE_DUMP") != nullptr;
   const int S = concurrent ? (int)h->slots.size() : 1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   HIP_TRY(h, hipEventCreate(&e0));
@@ -1729,12 +1749,33 @@ int autotune(vss_handle* h) {
       }
     }
     const BlockEntry* best = l.entry;
-    float best_ms = 1e30f;
-    for (size_t c = 0; c < cands.size(); ++c)
-      if (usable[c] && best_of[c] < best_ms * 0.98f) {  // ties keep the earlier (planner-preferred) shape
-        best_ms = best_of[c];
+    double best_obj = 1e30;
+    for (size_t c = 0; c < cands.size(); ++c) {
+      if (!usable[c]) continue;
+      double obj = best_of[c];
+      if (lds_obj || dump) {
+        set_tile(l, cands[c]);
+        int occ = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)cands[c]->fn[pi], cands[c]->threads,
+                                                            (int)l.lds);
+        occ = std::max(1, std::min(occ, lds_wg_per_cu((int)l.lds)));
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+        const long wgs = (long)l.tiles_x * l.tiles_y * N * l.ks;
+        const long rounds = (wgs + (long)cus * occ - 1) / ((long)cus * occ);
+        const double alloc = (double)((l.lds + kLdsGranule - 1) / kLdsGranule * kLdsGranule);
+        const double lt = (double)wgs * alloc * (best_of[c] / 8.0 * 1e3) / (double)rounds / 1e6;  // MB x us
+        if (dump)
+          std::fprintf(stderr, "autotune layer %zu cand %zu %dx%d var %d: %.2f us/launch, %ld WGs, %d/CU, %zu B LDS, "
+                       "%ld rounds, LDS x life %.1f MB*us\n", li, c, cands[c]->TH, cands[c]->TW, cands[c]->variant,
+                       best_of[c] / 8.0 * 1e3, wgs, occ, (size_t)l.lds, rounds, lt);
+        if (lds_obj) obj = lt;
+      }
+      if (obj < best_obj * 0.98) {  // ties keep the earlier (planner-preferred) shape
+        best_obj = obj;
         best = cands[c];
       }
+    }
     set_tile(l, best);
     if (rc) break;
   }

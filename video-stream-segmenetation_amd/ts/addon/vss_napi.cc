@@ -48,6 +48,7 @@
 //       (the postSetFaces form, one entry per frame)
 //   faceReset(tracker), faceDestroy(tracker)
 //   traceDump() -> Float64Array   VSS_NAPI_TRACE=1: per-batch phase stamps (see TracePoint)
+//   poolStats() -> {hits, carves, slabs, fallbacks, pinnedBytes}   the result blocks' allocator
 // Nothing blocks the event loop while a batch runs — as `await session.run` does not block.
 #include <node_api.h>
 
@@ -685,21 +686,26 @@ napi_value TraceDump(napi_env env, napi_callback_info) {
   return arr;
 }
 
-// The masks' ArrayBuffer: a pinned block (vss_host_alloc), so the batch's D2H
-// lands in it directly and the completion copies nothing — before, the masks
-// were copied out of the slot's pinned buffer into fresh malloc'd pages on the
-// HIP completion thread, one batch after another.  Pinning (and unpinning:
-// hipHostFree waits for the device) is far too slow for the per-call path, so
-// blocks are recycled: the finalizer V8 runs when a result is collected puts
-// its block on a free list by size, and blocks are never unpinned while the
+// The masks' ArrayBuffer: a pinned block, so the batch's D2H lands in it
+// directly and the completion copies nothing — before, the masks were copied
+// out of the slot's pinned buffer into fresh malloc'd pages on the HIP
+// completion thread, one batch after another.  Pinning (and unpinning:
+// hipHostFree waits for the device) is far too slow for the per-call path:
+// blocks are carved from 64 MiB pinned slabs (vss_host_alloc; the library's
+// direct-D2H check accepts any range inside one) in 64 KiB size classes and
+// recycled — the finalizer V8 runs when a result is collected puts its block
+// on the free list of its class, and slabs are never unpinned while the
 // process runs.  In steady state the live blocks are the results V8 has not
 // collected yet (its external-memory pressure — napi_adjust_external_memory —
-// sets the pace); past kPinnedCap bytes of pinned blocks, results fall back
-// to malloc'd memory (then the completion copies).  Not zero-filled (Node 12's
+// sets the pace); past kPinnedCap bytes of slabs, results fall back to
+// malloc'd memory (then the completion copies).  Round 5 pinned one block per
+// size as it was first needed: a one-frame call (147 KB of masks) whose size
+// had no free block paid a hipHostMalloc, 41 us at p50 of segment()'s 42
+// (tools/ts_prof.js, profiles/r06a).  Not zero-filled (Node 12's
 // napi_create_arraybuffer spent ~0.19 ms clearing 1.2 MB on the JS thread per
 // call).
 struct MaskBlock {
-  size_t bytes;
+  size_t bytes;  // the size class
   bool pinned;
 };
 
@@ -707,9 +713,16 @@ struct MaskBlock {
 // exits (V8 tearing the environment down), after static destructors of this
 // module could otherwise have run.
 std::mutex& g_pool_mu = *new std::mutex;
-std::multimap<size_t, void*>& g_pool = *new std::multimap<size_t, void*>;  // free pinned blocks by size
-size_t g_pinned_bytes = 0;             // every pinned block, free or live
-constexpr size_t kPinnedCap = size_t(1) << 30;
+std::multimap<size_t, void*>& g_pool = *new std::multimap<size_t, void*>;  // free pinned blocks by size class
+char* g_slab = nullptr;                // the slab being carved
+size_t g_slab_left = 0;
+size_t g_pinned_bytes = 0;             // every slab
+struct PoolStats {
+  unsigned long long hits = 0, carves = 0, slabs = 0, fallbacks = 0;
+};
+PoolStats g_pool_stats;
+constexpr size_t kPinnedCap = size_t(2) << 30;
+constexpr size_t kSlab = size_t(64) << 20, kClass = size_t(64) << 10;
 
 // VSS_NAPI_PINNED=0: malloc'd results (the completion copies), for A/B runs
 const bool g_use_pinned = [] {
@@ -717,42 +730,64 @@ const bool g_use_pinned = [] {
   return !(e && e[0] == '0');
 }();
 
-void* pool_get(size_t bytes, bool* pinned) {
-  if (!g_use_pinned) {
-    *pinned = false;
-    return std::malloc(bytes);
-  }
-  {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    auto it = g_pool.find(bytes);
-    if (it != g_pool.end()) {
-      void* p = it->second;
-      g_pool.erase(it);
-      *pinned = true;
-      return p;
-    }
-    if (g_pinned_bytes + bytes > kPinnedCap) {
-      *pinned = false;
-      return std::malloc(bytes);
-    }
-    g_pinned_bytes += bytes;
-  }
-  void* p = nullptr;
-  if (vss_host_alloc(bytes, &p) == VSS_OK) {
+size_t size_class(size_t bytes) { return (bytes + kClass - 1) / kClass * kClass; }
+
+void* pool_get(size_t cls, bool* pinned) {
+  *pinned = false;
+  if (!g_use_pinned) return std::malloc(cls);
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  auto it = g_pool.find(cls);
+  if (it != g_pool.end()) {
+    void* p = it->second;
+    g_pool.erase(it);
     *pinned = true;
+    ++g_pool_stats.hits;
     return p;
   }
-  {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pinned_bytes -= bytes;
+  if (g_slab_left < cls) {  // a new slab (the rest of the old one stays unused)
+    const size_t sz = std::max(kSlab, cls);
+    void* p = nullptr;
+    if (g_pinned_bytes + sz > kPinnedCap || vss_host_alloc(sz, &p) != VSS_OK) {
+      ++g_pool_stats.fallbacks;
+      return std::malloc(cls);
+    }
+    g_pinned_bytes += sz;
+    ++g_pool_stats.slabs;
+    g_slab = static_cast<char*>(p);
+    g_slab_left = sz;
   }
-  *pinned = false;
-  return std::malloc(bytes);
+  void* p = g_slab;
+  g_slab += cls;
+  g_slab_left -= cls;
+  ++g_pool_stats.carves;
+  *pinned = true;
+  return p;
 }
 
-void pool_put(void* p, size_t bytes) {
+void pool_put(void* p, size_t cls) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool.emplace(bytes, p);
+  g_pool.emplace(cls, p);
+}
+
+// poolStats() -> {hits, carves, slabs, fallbacks, pinnedBytes}: the result blocks' allocator
+napi_value PoolStatsJs(napi_env env, napi_callback_info) {
+  PoolStats st;
+  size_t pinned = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    st = g_pool_stats;
+    pinned = g_pinned_bytes;
+  }
+  napi_value o, v;
+  NAPI_OK(env, napi_create_object(env, &o));
+  const std::pair<const char*, double> kv[] = {{"hits", (double)st.hits}, {"carves", (double)st.carves},
+                                               {"slabs", (double)st.slabs}, {"fallbacks", (double)st.fallbacks},
+                                               {"pinnedBytes", (double)pinned}};
+  for (const auto& e : kv) {
+    napi_create_double(env, e.second, &v);
+    napi_set_named_property(env, o, e.first, v);
+  }
+  return o;
 }
 
 void free_masks(napi_env env, void* data, void* hint) {
@@ -769,7 +804,7 @@ void free_masks(napi_env env, void* data, void* hint) {
 }
 
 bool masks_buffer(napi_env env, size_t bytes, void** data, napi_value* ab) {
-  MaskBlock* b = new MaskBlock{std::max<size_t>(bytes, 16), false};
+  MaskBlock* b = new MaskBlock{size_class(std::max<size_t>(bytes, 16)), false};
   void* p = pool_get(b->bytes, &b->pinned);
   if (!p) {
     delete b;
@@ -1697,6 +1732,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"stagingRelease", nullptr, StagingRelease, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"segmentStaged", nullptr, SegmentStaged, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"traceDump", nullptr, TraceDump, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"poolStats", nullptr, PoolStatsJs, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"destroy", nullptr, Destroy, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"postCreate", nullptr, PostCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"postSetConfig", nullptr, PostSetConfig, nullptr, nullptr, nullptr, napi_default, nullptr},
