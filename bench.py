@@ -482,7 +482,10 @@ def main():
 
     ts = None
     if rank == 0 and world == 1 and not args.no_ts and not args.dry_run_dist:
-        ts = ts_leg(B, fh, fw, max(100, min(args.steps, 400)), args.inflight)  # before this process touches the GPU
+        # (a fixed 600 batches per timed loop, whatever --steps: at the driver's
+        # --steps 20 the legs ran 100 batches, ~15 ms windows that read 36-57k
+        # on one box, profiles/r06c)
+        ts = ts_leg(B, fh, fw, 600, args.inflight)  # before this process touches the GPU
         # the Node process's GPU context is torn down after it exits; one full
         # bench (r03i) timed its headline 9 % under its own median step right
         # after this leg, so the headline starts on a settled device
@@ -667,9 +670,9 @@ def main():
                         args.warmup, 0.0 if args.no_cpu else 2.0)
     if rank == 0 and world == 1 and not args.no_host:
         ref = d_masks.cpu().numpy()
-        host = {"vga": host_leg(pkg, frames, B, fh, fw, S, max(50, min(args.steps, 400)), ref)}
+        host = {"vga": host_leg(pkg, frames, B, fh, fw, S, 600, ref)}
         big = syn.make_batch(B, 1080, 1920, 3)
-        host["1080p"] = host_leg(pkg, big, B, 1080, 1920, S, max(30, min(args.steps // 2, 200)))
+        host["1080p"] = host_leg(pkg, big, B, 1080, 1920, S, 200)
     if rank == 0 and world == 1 and not args.no_sweep:
         batch_sweep = sweep(pkg, torch, dev, fh, fw, args.dtype, S, args.steps)
 

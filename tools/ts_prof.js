@@ -50,7 +50,8 @@ async function main() {
   const args = process.argv.slice(2);
   const it = Number(args.find((a) => /^\d+$/.test(a)) || 400);
   const b = 8, h = 480, w = 640;
-  const s = new seg.Segmenter({ maxBatch: b, maxFrameWidth: w, maxFrameHeight: h, queueDepth: 4 });
+  const st = Number(process.env.TS_PROF_STAGING_THREADS || 0);  // 0: the library's default (8)
+  const s = new seg.Segmenter({ maxBatch: b, maxFrameWidth: w, maxFrameHeight: h, queueDepth: 4, stagingThreads: st });
   const frames = [];
   for (let i = 0; i < b; i++) frames.push({ data: new Uint8Array(h * w * 3).fill(i * 20), width: w, height: h, channels: 3 });
   for (let i = 0; i < 150; i++) await s.segmentFrames(frames);

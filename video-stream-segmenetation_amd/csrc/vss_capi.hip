@@ -73,6 +73,7 @@ struct LayerPlan {
   long wimg_stride = 0;        // floats between the slices' weight images
   size_t lds = 0;
   const BlockEntry* entry = nullptr;  // compiled shape (registry)
+  const BlockEntry* small = nullptr;  // the autotuner's batch-1 pick, for forwards of <= small_tile_n frames
   bool fused = false;          // computed inside its only consumer's prologue (no launch of its own)
   int acc_off = -1;            // DEC: offset of its [kAccSlots][2][C] norm accumulator in a frame's row
   const float* wimg = nullptr;  // LDS weight image (block_lds regions w1..b2)
@@ -247,7 +248,15 @@ class CopyPool {
         g->pieces.push_back({static_cast<char*>(j.dst) + off, static_cast<const char*>(j.src) + off,
                              std::min(kPiece, j.len - off)});
     const size_t n = g->pieces.size();
-    if (n <= 1 || workers_.empty()) {
+    // a small copy (one VGA frame's rows: ~0.55 MB) on the calling thread
+    // alone: waking the workers costs more than they save (VSS_COPY_INLINE_BYTES)
+    static const size_t inline_bytes = [] {
+      const char* e = std::getenv("VSS_COPY_INLINE_BYTES");
+      return e ? (size_t)std::atoll(e) : (size_t(1) << 20);
+    }();
+    size_t total = 0;
+    for (const Job& j : jobs) total += j.len;
+    if (n <= 1 || workers_.empty() || total < inline_bytes) {
       for (const Job& p : g->pieces) staging_copy(p.dst, p.src, p.len);
       return;
     }
@@ -258,15 +267,18 @@ class CopyPool {
     }
     cv_.notify_all();
     work(*g);
+    // (VSS_COPY_WAIT_ALL=1, an A/B knob: also wait for every worker to have
+    // taken and left this copy, round 5's protocol)
+    static const bool wait_all = std::getenv("VSS_COPY_WAIT_ALL") && std::getenv("VSS_COPY_WAIT_ALL")[0] == '1';
     std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return g->done.load() == n; });
+    done_cv_.wait(lk, [&] { return g->done.load() == n && (!wait_all || g->left.load() == workers_.size()); });
     if (cur_ == g) cur_.reset();
   }
 
  private:
   struct Gen {
     std::vector<Job> pieces;
-    std::atomic<size_t> next{0}, done{0};
+    std::atomic<size_t> next{0}, done{0}, left{0};
   };
   void work(Gen& g) {
     const size_t n = g.pieces.size();
@@ -289,7 +301,13 @@ class CopyPool {
         seen = gen_;
         g = cur_;
       }
-      if (g) work(*g);
+      if (g) {
+        work(*g);
+        if (g->left.fetch_add(1) + 1 == workers_.size()) {
+          std::lock_guard<std::mutex> lk(mu_);
+          done_cv_.notify_all();
+        }
+      }
     }
   }
   std::vector<std::thread> workers_;
@@ -383,6 +401,7 @@ struct vss_handle {
   std::mutex post_mu;              // the synchronous post / composite calls share scratch
   vss_ticket next_ticket = 0;      // host batches (vss_submit*, vss_segment*)
   unsigned long long device_calls = 0;  // vss_segment_device: slot = count % depth
+  int small_tile_n = 0;            // forwards of at most this many frames use LayerPlan::small
   std::atomic<unsigned long long> gather_calls{0};  // vss_segment_gather_device: slot = count % depth
                                                    // (atomic: vss_comm_status reads it lock-free)
   long graph_builds = 0, graph_patches = 0;  // VSS_OPT_GRAPH_BUILDS / _PATCHES
@@ -884,8 +903,8 @@ StemParams stem_params(const vss_handle* h, const Slot& s, int li, const uint8_t
 }
 
 // Kernel parameters of block layer li for the call's n frames.
-BlockParams block_params(const vss_handle* h, const Slot& s, int li, int n) {
-  const LayerPlan& l = h->L[li];
+BlockParams block_params(const vss_handle* h, const Slot& s, int li, int n, const LayerPlan* lp = nullptr) {
+  const LayerPlan& l = lp ? *lp : h->L[li];
   const Rec& r = l.rec;
   const LayerPlan& src = h->L[r.src];
   BlockParams p{};
@@ -953,19 +972,27 @@ void forward_launches(vss_handle* h, Slot& s, const uint8_t* frames, int n, int 
       L.lds = kStemLds * 4;
       L.prm.stem = p;
     } else if (r.kind == K_IR || r.kind == K_DEC) {
-      BlockParams p = block_params(h, s, i, n);
+      // a small batch on the batch-1 tile (autotune): bitwise the same results
+      LayerPlan small_plan;
+      const bool use_small = l.small && n <= h->small_tile_n;
+      if (use_small) {
+        small_plan = l;
+        set_tile(small_plan, l.small);
+      }
+      const LayerPlan& lt = use_small ? small_plan : l;
+      BlockParams p = block_params(h, s, i, n, &lt);
       if (flags_stem_in(l.flags)) {
         p.stem = stem_params(h, s, (int)r.src, frames, rs, fs, fh, fw, fc);
         if (!h->keep_stem) p.stem.y = nullptr;  // no layer reads it (vss_read_layer(0) only)
       }
 #ifdef VSS_TRACE
       p.trace = s.trace[i];
-      h->trace_wgs[i] = l.tiles_x * l.tiles_y * n * l.ks;
+      h->trace_wgs[i] = lt.tiles_x * lt.tiles_y * n * lt.ks;
 #endif
-      L.fn = (const void*)l.entry->fn[prec == PREC_F32 ? 0 : 1];
-      L.grid = dim3(l.tiles_x, l.tiles_y, n * l.ks);
-      L.threads = l.entry->threads;
-      L.lds = l.lds;
+      L.fn = (const void*)lt.entry->fn[prec == PREC_F32 ? 0 : 1];
+      L.grid = dim3(lt.tiles_x, lt.tiles_y, n * lt.ks);
+      L.threads = lt.entry->threads;
+      L.lds = lt.lds;
       L.prm.block = p;
     } else if (r.kind == K_HEAD) {
       const LayerPlan& src = h->L[r.src];
@@ -1164,6 +1191,41 @@ int pick_graph(vss_handle* h, Slot& s, const GraphKey& key, const std::vector<La
   return VSS_OK;
 }
 
+// VSS_TIME_DEVICE=1: host-clock stamps of each phase of vss_segment_device
+// (entry, lock, claim, launch list, pick_graph, hipGraphLaunch, event,
+// release), the last 256 calls printed to stderr when the handle is destroyed
+// (tools/window_trace.py: where the short window's first call goes).
+struct DeviceClock {
+  static constexpr int kPts = 8, kRing = 256;
+  bool on = std::getenv("VSS_TIME_DEVICE") != nullptr;
+  double t[kRing][kPts] = {};
+  long calls = 0;
+  double* cur = nullptr;
+  static double now() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  void begin() {
+    if (!on) return;
+    cur = t[calls++ % kRing];
+    cur[0] = now();
+  }
+  void mark(int k) {
+    if (on && cur) cur[k] = now();
+  }
+  void dump() {
+    if (!on || !calls) return;
+    const long n = std::min<long>(calls, kRing);
+    std::fprintf(stderr, "vss device calls (us from entry: lock claim list pick launch event release):\n");
+    for (long i = calls - n; i < calls; ++i) {
+      const double* c = t[i % kRing];
+      std::fprintf(stderr, "  call %ld at %.1f:", i, c[0]);
+      for (int k = 1; k < kPts; ++k) std::fprintf(stderr, " %.1f", c[k] - c[0]);
+      std::fprintf(stderr, "\n");
+    }
+  }
+};
+DeviceClock g_device_clock;
+
 // The forward of n frames with slot `si`'s buffers, on stream st: one of the
 // slot's executable graphs for this shape replayed (pick_graph), or eager
 // launches.
@@ -1175,6 +1237,7 @@ int forward(vss_handle* h, int si, const uint8_t* frames, int n, int fh, int fw,
   s.stem_stored = !has_fused_stem(h) || h->keep_stem;
   std::vector<Launch> ls;
   forward_launches(h, s, frames, n, fh, fw, fc, rs, fs, masks, &ls);
+  g_device_clock.mark(3);
   if (h->profile) {
     const int ring = h->prof_next;
     h->prof_next = (h->prof_next + 1) % vss_handle::kProfRing;
@@ -1189,8 +1252,11 @@ int forward(vss_handle* h, int si, const uint8_t* frames, int n, int fh, int fw,
   if (!h->use_graph) return launch_eager(h, ls, st, -1);
   GraphEntry* g = nullptr;
   if (int rc = pick_graph(h, s, GraphKey{n, fh, fw, fc, rs, fs}, ls, &g)) return rc;
+  g_device_clock.mark(4);
   HIP_TRY(h, hipGraphLaunch(g->exec, st));
+  g_device_clock.mark(5);
   HIP_TRY(h, hipEventRecord(g->last, st));
+  g_device_clock.mark(6);
   g->launched = true;
   g->tick = ++s.graph_tick;
   return VSS_OK;
@@ -1670,8 +1736,9 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
 // tools/trace_inflight.py).  Measured (round 3, 2 x 2 interleaved runs):
 // 179.6k / 193.6k frames/s throughput-tuned against 192.5k / 188.9k — its
 // picks vary between runs, so latency stays the default.
-int autotune(vss_handle* h) {
-  const int N = h->cfg.max_batch;
+//   small: time the candidates at batch N (1) and keep the pick as the layer's
+// small-batch tile (LayerPlan::small), the layer's own tile restored.
+int autotune_at(vss_handle* h, int N, bool small) {
   const int pi = h->cfg.dtype == VSS_DTYPE_F32 ? 0 : 1;
   Slot& s = h->slots[0];
   if (int rc = ensure_staging(h, s)) return rc;  // the stem reads the staging buffer as frames
@@ -1696,6 +1763,7 @@ int autotune(vss_handle* h) {
     if (l.mode < 0) continue;
     const std::vector<const BlockEntry*> cands = tile_candidates(l);
     if (cands.size() < 2) continue;
+    const BlockEntry* own = l.entry;
     // three rounds over the candidates, each candidate's best round kept: one
     // timing per candidate let clock / cache noise pick a different tile per
     // run (a +-2% spread of the whole forward between runs)
@@ -1766,8 +1834,8 @@ int autotune(vss_handle* h) {
         const double alloc = (double)((l.lds + kLdsGranule - 1) / kLdsGranule * kLdsGranule);
         const double lt = (double)wgs * alloc * (best_of[c] / 8.0 * 1e3) / (double)rounds / 1e6;  // MB x us
         if (dump)
-          std::fprintf(stderr, "autotune layer %zu cand %zu %dx%d var %d: %.2f us/launch, %ld WGs, %d/CU, %zu B LDS, "
-                       "%ld rounds, LDS x life %.1f MB*us\n", li, c, cands[c]->TH, cands[c]->TW, cands[c]->variant,
+          std::fprintf(stderr, "autotune batch %d layer %zu cand %zu %dx%d var %d: %.2f us/launch, %ld WGs, %d/CU, %zu B LDS, "
+                       "%ld rounds, LDS x life %.1f MB*us\n", N, li, c, cands[c]->TH, cands[c]->TW, cands[c]->variant,
                        best_of[c] / 8.0 * 1e3, wgs, occ, (size_t)l.lds, rounds, lt);
         if (lds_obj) obj = lt;
       }
@@ -1776,13 +1844,34 @@ int autotune(vss_handle* h) {
         best = cands[c];
       }
     }
-    set_tile(l, best);
+    if (small) {
+      l.small = best != own ? best : nullptr;
+      set_tile(l, own);
+    } else {
+      set_tile(l, best);
+    }
     if (rc) break;
   }
   for (auto e : ends) (void)hipEventDestroy(e);
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return rc;
+}
+
+// Tiles for max_batch, then (max_batch >= 4) a second pick at batch 1 that
+// the forwards of at most max_batch / 4 frames use (small_tile_n): one batch
+// of 8 and one frame want different tiles — at batch 1 the batch-8 tiles leave
+// most CUs idle (b1's 4x16 tile: 144 workgroups).  Results do not depend on
+// the tile (block_lds), so a forward's masks are bitwise the same either way.
+// VSS_SMALL_TILES=0: the max_batch tiles for every batch size.
+int autotune(vss_handle* h) {
+  if (int rc = autotune_at(h, h->cfg.max_batch, false)) return rc;
+  static const bool small_on = !(std::getenv("VSS_SMALL_TILES") && std::getenv("VSS_SMALL_TILES")[0] == '0');
+  if (small_on && h->cfg.max_batch >= 4) {
+    if (int rc = autotune_at(h, 1, true)) return rc;
+    h->small_tile_n = h->cfg.max_batch / 4;
+  }
+  return VSS_OK;
 }
 
 // Pin layers to given compiled tiles (after the planner and the autotuner):
@@ -2009,6 +2098,7 @@ int vss_create(const vss_config* cfg, vss_handle** out) {
 
 void vss_destroy(vss_handle* h) {
   if (!h) return;
+  g_device_clock.dump();
   // drain the completion thread first: it reads h->peers and waits on the
   // peers' slot events, so every queued batch completes (and its callback
   // fires) while the peers still exist (use-after-free otherwise)
@@ -2174,10 +2264,12 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
                        size_t row_stride, size_t frame_stride, float* d_masks, void* stream) {
   if (!h) return fail(nullptr, VSS_E_INVALID_ARG, "null handle");
   if (!d_frames || !d_masks) return fail(h, VSS_E_INVALID_ARG, "null device pointer");
+  g_device_clock.begin();
   int rc = check_frames(h, n, height, width, channels, row_stride, frame_stride, h->cfg.max_batch);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(h, hipSetDevice(h->device));
+  g_device_clock.mark(1);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
   // round-robin slots, ordered on the device (no host wait): consecutive
   // calls on different streams run concurrently.  Device calls take no
@@ -2185,8 +2277,10 @@ int vss_segment_device(vss_handle* h, const uint8_t* d_frames, int n, int height
   const int k = (int)(h->device_calls++ % h->slots.size());
   Slot& sl = h->slots[k];
   if ((rc = claim_slot(h, sl, s))) return rc;
+  g_device_clock.mark(2);
   rc = forward(h, k, d_frames, n, height, width, channels, row_stride, frame_stride, d_masks, s);
   const int rr = release_slot(h, sl, s);  // also after a failed enqueue: the next user orders after it
+  g_device_clock.mark(7);
   return rc ? rc : rr;
 }
 
