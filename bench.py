@@ -460,6 +460,15 @@ def main():
                     help="rehearse the multi-rank plumbing only (launch_ranks -> torch.distributed.run -> gloo "
                          "-> the clique-id broadcast, with placeholder id bytes) and stop before the first GPU "
                          "call: each rank prints one JSON line; runs on a machine without GPUs")
+    # (the HIP runtime retires the warm-up's commands on its own threads for a
+    # few hundred us after a synchronize; step calls made meanwhile took 25-70
+    # us instead of 12-16 and the GPU started the window with 1-2 batches in
+    # flight: the driver's 20-step window read 129-193k (mean 162.5k) with no
+    # pause against 167-184k (mean 174.4k) after 5 ms, median steps alike —
+    # profiles/NOTES.md "The short window's first calls", profiles/r06j)
+    ap.add_argument("--settle-ms", type=float, default=5.0,
+                    help="untimed pause between the warm-up's synchronize and the timed window's barrier + "
+                         "synchronize (the device idle throughout; no GPU work)")
     ap.add_argument("--watchdog-s", type=float, default=60.0,
                     help="no step issued or completed for this long during a GPU phase: print a JSON record "
                          "(rank, stage, gather counter, communicators' async errors) and exit 3; 0 = off")
@@ -582,6 +591,8 @@ def main():
     wd.beat("warmup")
     k = run_steps(sess, streams, args.warmup, step, wd=wd)
     torch.cuda.synchronize(dev)
+    if args.settle_ms > 0:
+        time.sleep(args.settle_ms / 1e3)
     wd.beat("barrier before the timed steps")
     if world > 1:
         dist.barrier()
@@ -699,6 +710,7 @@ def main():
             "median_step_ms": round(median_step_ms, 5) if median_step_ms else None,
             "value_at_median_step": round(world * B / (median_step_ms * 1e-3), 1) if median_step_ms else None,
             "graph_builds_in_timed_region": timed_builds,
+            "settle_ms_before_window": args.settle_ms,
             "graph_patches_in_timed_region": timed_patches,
             "higher_is_better": True,
             "scaling": "weak",

@@ -52,6 +52,12 @@ def run(K=20, W=5, pre="sleep"):
             torch.cuda.synchronize()
         elif pre == "sleep1ms":
             time.sleep(0.001)
+        elif pre in ("spin1ms", "sleep_spin"):  # the host thread busy right up to the window
+            if pre == "sleep_spin":
+                time.sleep(0.05)
+            t_end = time.perf_counter() + (0.001 if pre == "spin1ms" else 0.0003)
+            while time.perf_counter() < t_end:
+                pass
         calls, durs = [], []
         t0 = time.perf_counter()
         for i in range(W, W + K):

@@ -1300,6 +1300,10 @@ std::vector<vss_handle*> engines(vss_handle* h) {
 // which a destroyed-and-recreated stream or two threads' hipStreamPerThread
 // could fool; caller streams now always wait.
 int claim_slot(vss_handle* e, Slot& s, hipStream_t st) {
+  // (VSS_TEST_NO_CLAIM=1: no wait at all — a diagnostic for callers that keep
+  // one stream per slot, tools/window_trace.py; never set in the product)
+  static const bool no_claim = std::getenv("VSS_TEST_NO_CLAIM") && std::getenv("VSS_TEST_NO_CLAIM")[0] == '1';
+  if (no_claim) return VSS_OK;
   if (s.used && !(st == s.stream && s.done_stream == s.stream)) HIP_TRY(e, hipStreamWaitEvent(st, s.done, 0));
   return VSS_OK;
 }
