@@ -1478,20 +1478,29 @@ void stop_completions(vss_handle* h) {
 // VSS_TIME_SUBMIT=1: host time of each phase of the queued submit, summed over
 // the calls and printed when the handle is destroyed (where the calling
 // thread's time goes; tools/ts_prof.js showed the N-API call dominating).
+// Every call's phases are kept too (up to 8192 calls) and printed as per-phase
+// medians by batch size.
 struct SubmitClock {
   static constexpr int kPhases = 8;
   bool on = std::getenv("VSS_TIME_SUBMIT") != nullptr;
   double ns[kPhases] = {};
   long calls = 0;
   std::chrono::steady_clock::time_point t;
+  std::vector<std::pair<int, std::vector<double>>> rows;  // (frames, per-phase ns)
   void start() {
     if (on) t = std::chrono::steady_clock::now();
   }
   void mark(int k) {
     if (!on) return;
     const auto n = std::chrono::steady_clock::now();
-    ns[k] += std::chrono::duration<double, std::nano>(n - t).count();
+    const double d = std::chrono::duration<double, std::nano>(n - t).count();
+    ns[k] += d;
+    if (k == 0 && rows.size() < 8192) rows.push_back({0, std::vector<double>(kPhases, 0.0)});
+    if (!rows.empty()) rows.back().second[k] = d;
     t = n;
+  }
+  void frames(int n) {
+    if (on && !rows.empty()) rows.back().first = n;
   }
 };
 SubmitClock g_submit_clock;
@@ -1546,6 +1555,7 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
   SubmitClock& clk = g_submit_clock;
   clk.start();
+  const int clk_n = n;
   std::unique_lock<std::mutex> lk(h->mu);
   clk.mark(0);
   // a free slot: its previous batch is done on every GPU, so its staging may be rewritten
@@ -1724,6 +1734,7 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
     push_completion(h, {t, k, direct ? nullptr : masks_out, src, bytes, cb, user});
   }
   clk.mark(7);
+  clk.frames(clk_n);
   clk.calls += clk.on ? 1 : 0;
   if (ticket) *ticket = t;
   return VSS_OK;
@@ -1973,6 +1984,18 @@ void destroy_engine(vss_handle* h) {
     for (int k = 0; k < SubmitClock::kPhases; ++k)
       std::fprintf(stderr, " %s %.1f", names[k], g_submit_clock.ns[k] / 1e3 / g_submit_clock.calls);
     std::fprintf(stderr, "\n");
+    std::map<int, std::vector<std::vector<double>>> by_n;
+    for (const auto& r : g_submit_clock.rows) by_n[r.first].push_back(r.second);
+    for (auto& kv : by_n) {
+      std::fprintf(stderr, "vss submit phases, %d-frame calls (%zu), median us:", kv.first, kv.second.size());
+      for (int k = 0; k < SubmitClock::kPhases; ++k) {
+        std::vector<double> v;
+        for (const auto& r : kv.second) v.push_back(r[k]);
+        std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+        std::fprintf(stderr, " %s %.1f", names[k], v[v.size() / 2] / 1e3);
+      }
+      std::fprintf(stderr, "\n");
+    }
     g_submit_clock = SubmitClock();
     g_submit_clock.on = true;
   }
