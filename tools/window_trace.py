@@ -35,15 +35,25 @@ def run(K=20, W=5, pre="sleep"):
             s.segment_device(d.data_ptr(), B, fh, fw, 3, fw * 3, fh * fw * 3, outs[i % S].data_ptr(),
                              sts[i % S].cuda_stream)
 
+        extra = []
+        if pre == "sleep_xs":  # 24 more streams, each used once: does the post-sync cost grow with them?
+            extra = [torch.cuda.Stream() for _ in range(24)]
+            for st in extra:
+                torch.cuda.Event().record(st)
         for i in range(W):
             step(i)
         torch.cuda.synchronize()
-        if pre in ("sleep", "sleep_event"):
+        if pre == "sleep_ss":  # the pause, then each step stream synchronized (no device-wide synchronize)
+            time.sleep(0.05)
+            for st in sts:
+                st.synchronize()
+        elif pre in ("sleep", "sleep_event", "sleep_xs"):
             time.sleep(0.05)  # a gap that marks the timed window in the trace
         if pre in ("event", "sleep_event"):  # one event record on every step stream (no kernel)
             for st in sts:
                 torch.cuda.Event().record(st)
-        torch.cuda.synchronize()
+        if pre != "sleep_ss":
+            torch.cuda.synchronize()
         if pre == "q_event":  # one host-side HIP query after the sync (no GPU work)
             torch.cuda.Event().query()
         elif pre == "q_stream":
@@ -58,18 +68,24 @@ def run(K=20, W=5, pre="sleep"):
             t_end = time.perf_counter() + (0.001 if pre == "spin1ms" else 0.0003)
             while time.perf_counter() < t_end:
                 pass
-        calls, durs = [], []
+        import resource
+        calls, durs, faults, csw = [], [], [], []
         t0 = time.perf_counter()
         for i in range(W, W + K):
+            r0 = resource.getrusage(resource.RUSAGE_THREAD) if i < W + 4 else None
             c0 = time.perf_counter()
             step(i)
             calls.append((c0 - t0) * 1e6)
             durs.append((time.perf_counter() - c0) * 1e6)
+            if r0 is not None:  # minor faults and context switches of this thread during the call
+                r1 = resource.getrusage(resource.RUSAGE_THREAD)
+                faults.append(r1.ru_minflt - r0.ru_minflt)
+                csw.append((r1.ru_nvcsw - r0.ru_nvcsw, r1.ru_nivcsw - r0.ru_nivcsw))
         t_issued = (time.perf_counter() - t0) * 1e6
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) * 1e6
     print(json.dumps({"pre": pre, "window_us": round(el, 1), "issued_us": round(t_issued, 1),
-                      "call_us": [round(c, 1) for c in durs],
+                      "call_us": [round(c, 1) for c in durs], "minor_faults": faults, "ctx_switches": csw,
                       "call_start_us": [round(c, 1) for c in calls], "frames_per_s": round(B * K / el * 1e6, 1)}))
 
 
