@@ -184,8 +184,19 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
   // 1-D grid, split index fastest: workgroups b and b + 8 share an XCD
   // (round-robin dispatch), so with ksplit a multiple of 8 each XCD's L2 holds
   // the weights of its own splits only (MODNet's 5x5 1280 -> 96 layer: 6 MB
-  // of bf16 weights, re-read per pixel tile, no longer from HBM)
-  const int L = blockIdx.x;
+  // of bf16 weights, re-read per pixel tile, no longer from HBM).
+  // Without a split (p.xcd) the items are dealt to the XCDs in contiguous
+  // runs instead: XCD x = b % 8 runs items [x q + min(x, r), ...) of the
+  // grid's q = G / 8, r = G % 8 split, in raster order, so the halo rows a
+  // tile shares with the tiles above and below it and the 128-B lines its
+  // 34-pixel rows straddle are read once into that XCD's L2 rather than
+  // once per XCD (3x3 64 -> 64 at 72x128, batch 8: ~2.4x the input's bytes
+  // fetched past L2 in round-robin order).  A bijection on [0, G).
+  int L = blockIdx.x;
+  if (p.xcd && p.ksplit == 1) {
+    const int G = gridDim.x, q = G >> 3, r = G & 7, x = L & 7;
+    L = x * q + min(x, r) + (L >> 3);
+  }
   const int kz = L % p.ksplit;
   const int rest = L / p.ksplit;
   const int t = rest % p.tiles, mt = (rest / p.tiles) % p.mtiles, n = rest / (p.tiles * p.mtiles);

@@ -85,6 +85,7 @@ struct ConvTileParams {
   int x2_c0, x2_C;
   int items;           // work items (pixel tile x M tile x image x split); set by launch_conv_tile
   int qskip;           // skip the loads of quads past C in a partial last chunk (VSO_CONV_QSKIP=0: off)
+  int xcd;             // XCD-contiguous item order (k_conv_tile, ksplit 1; VSO_CONV_XCD=0: off)
 };
 
 constexpr int kDwPwMaxC = 256;  // channels a fused depthwise -> 1x1 pair may have

@@ -1420,6 +1420,11 @@ struct Planner {
       return e ? std::atoi(e) : 1;
     }();
     tp.qskip = qskip;
+    static const int xcd = [] {
+      const char* e = std::getenv("VSO_CONV_XCD");
+      return e ? std::atoi(e) : 1;
+    }();
+    tp.xcd = xcd;
     if (tail) {
       tp.x2 = tail->x;
       tp.x2_c0 = tail->c0;
