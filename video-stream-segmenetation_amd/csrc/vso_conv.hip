@@ -193,10 +193,7 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
   // once per XCD (3x3 64 -> 64 at 72x128, batch 8: ~2.4x the input's bytes
   // fetched past L2 in round-robin order).  A bijection on [0, G).
   int L = blockIdx.x;
-  if (p.xcd && p.ksplit == 1) {
-    const int G = gridDim.x, q = G >> 3, r = G & 7, x = L & 7;
-    L = x * q + min(x, r) + (L >> 3);
-  }
+  if (p.xcd && p.ksplit == 1) L = xcd_item(L, gridDim.x);
   const int kz = L % p.ksplit;
   const int rest = L / p.ksplit;
   const int t = rest % p.tiles, mt = (rest / p.tiles) % p.mtiles, n = rest / (p.tiles * p.mtiles);

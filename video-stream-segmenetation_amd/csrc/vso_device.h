@@ -21,6 +21,20 @@ __device__ __forceinline__ const void* uniform_ptr(const void* p) {
   return reinterpret_cast<const void*>(((unsigned long long)hi << 32) | lo);
 }
 
+// XCD-contiguous work items.  The dispatcher deals linear workgroup b to
+// XCD b % 8; xcd_item(b, G) gives XCD x the contiguous items
+// [x q + min(x, r), ...) of q = G / 8, r = G % 8, so neighbouring tiles — the
+// halo rows they share, the 128-B lines their rows straddle — sit on one L2
+// instead of eight (MODNet's k_conv_tile 3x3 at 72x128: 4.8x -> 1.0x the
+// input's bytes fetched past L2).  A bijection on [0, G): the same items and
+// arithmetic, placed differently.  (Measured and not kept on k_ir_b16 and the
+// fused depthwise -> 1x1 k_conv_pw: fetched bytes 1.3-3x lower, no faster —
+// latency-bound there — and MODNet b8 0.5 % slower, profiles/r06/r06u.)
+__device__ __forceinline__ int xcd_item(int b, int G) {
+  const int q = G >> 3, r = G & 7, x = b & 7;
+  return x * q + min(x, r) + (b >> 3);
+}
+
 __device__ __forceinline__ float act_apply(float v, int act, float a0, float a1, const float* slope, int ch,
                                            int slope_stride) {
   switch (act) {
