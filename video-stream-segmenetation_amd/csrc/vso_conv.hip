@@ -241,17 +241,21 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
   const float* upn = UP ? p.up + (long)n * (p.up_c1 - p.up_c0) * up_plane : xn;
   // is chunk ch an upsampled one (uniform: the range is whole chunks)
   auto up_chunk = [&](int ch) { return UP && ch * CK >= p.up_c0 && ch * CK < p.up_c1; };
+  // (the chunk's CK planes as a buffer: 32-bit byte offsets, no 64-bit
+  // address arithmetic per element — it was ~25 VALU per element, as many
+  // as the interpolation's)
   auto load_region = [&](int ch) {
     const int c0 = ch * CK - p.up_c0;
     const int wbase = __builtin_amdgcn_readfirstlane((tid >> 6) << 6);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(uniform_ptr(upn + (long)c0 * up_plane)), 0, CK * up_plane * 4, 0x00020000);
 #pragma unroll
     for (int u = 0; u < PR; ++u) {
       const int idx = min(tid + 256 * u, RITEMS - 1);
       const int cc = idx / SRC, rem = idx - cc * SRC, a = rem / SC, b = rem - a * SC;
       const int yy = min(ry0 + a, p.up_H - 1), xx = min(rx0 + b, p.up_W - 1);
-      __builtin_amdgcn_global_load_lds(
-          (__attribute__((address_space(1))) void*)(upn + (c0 + cc) * up_plane + yy * p.up_W + xx),
-          (__attribute__((address_space(3))) void*)(lrs + 256 * u + wbase), 4, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (__attribute__((address_space(3))) void*)(lrs + 256 * u + wbase), 4,
+                                               (cc * up_plane + yy * p.up_W + xx) * 4, 0, 0, 0);
     }
   };
   float st[PER][CG];
@@ -343,15 +347,24 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
             const int t00 = a0 * SC + b0, t01 = a0 * SC + b1, t10 = a1 * SC + b0, t11 = a1 * SC + b1;
             const float* l = lrs + q * CG * SRC;
             // every tap read unconditionally (the clamped taps lie in the
-            // region), all 4 x CG in flight at once, the halo's zero selected
-            // after: a conditional read per channel compiled to a branch and
-            // an LDS round trip per channel (8 exposed latencies per item)
+            // region), all 4 x CG in flight at once, the halo's zero applied
+            // after as a product with 0 / 1 (finite values: the same as the
+            // select): with `in ? interp : 0` the compiler sank the reads
+            // into a branch per channel, an exposed LDS round trip each (8
+            // per item, 48 per thread and chunk at 8 x 32 tiles)
+            float t0[CG], t1[CG], t2[CG], t3[CG];
+#pragma unroll
+            for (int e = 0; e < CG; ++e) {
+              t0[e] = l[e * SRC + t00];
+              t1[e] = l[e * SRC + t01];
+              t2[e] = l[e * SRC + t10];
+              t3[e] = l[e * SRC + t11];
+            }
+            const float keep = in ? 1.f : 0.f;
             float v[CG];
 #pragma unroll
             for (int e = 0; e < CG; ++e)
-              v[e] = in ? (1.f - ly) * ((1.f - lx) * l[e * SRC + t00] + lx * l[e * SRC + t01]) +
-                              ly * ((1.f - lx) * l[e * SRC + t10] + lx * l[e * SRC + t11])
-                        : 0.f;
+              v[e] = keep * ((1.f - ly) * ((1.f - lx) * t0[e] + lx * t1[e]) + ly * ((1.f - lx) * t2[e] + lx * t3[e]));
             xs[pix * QS + q] = pack_quad<PREC>(v);
           }
         }
