@@ -321,9 +321,18 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
     const int ty = b / (TW / 16), tx = (b % (TW / 16)) * 16 + r;
     bpix[j] = ty * S * IW + tx * S;
   }
+  // UP: a plain chunk right after the upsampled one (staged by DMA, no
+  // registers) loads into its registers from the start, in flight with the
+  // source region instead of after the interpolation (MODNet's 35 -> 16
+  // fusion layer: the image's 3 channels behind the 32 upsampled ones)
+  bool ahead = false;
   if (cbeg < cend) {
     load(cbeg);
     load_w(cbeg);
+    if (UP && up_chunk(cbeg) && cbeg + 1 < cend && !up_chunk(cbeg + 1)) {
+      load(cbeg + 1);
+      ahead = true;
+    }
   }
   for (int ch = cbeg; ch < cend; ++ch) {
     __syncthreads();  // the previous chunk's fragment reads are done
@@ -389,7 +398,7 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
     }
     __syncthreads();
     if (ch + 1 < cend) {  // in flight during this chunk's MFMAs
-      load(ch + 1);
+      if (!(ahead && ch == cbeg)) load(ch + 1);
       load_w(ch + 1);
     }
     const int wc = ch * (CK / CG);    // this chunk's first quad in a weight row
