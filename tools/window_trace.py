@@ -52,6 +52,13 @@ def run(K=20, W=5, pre="sleep"):
         if pre in ("event", "sleep_event"):  # one event record on every step stream (no kernel)
             for st in sts:
                 torch.cuda.Event().record(st)
+        if pre in ("sleep_busy", "sleep_busy_step"):  # the pause, then the device busy ~50 us right up to the sync
+            time.sleep(0.05)
+            if pre == "sleep_busy":
+                torch.cuda._sleep(120000)
+            else:  # or one untimed step on every slot
+                for i in range(S):
+                    step(i)
         if pre != "sleep_ss":
             torch.cuda.synchronize()
         if pre == "q_event":  # one host-side HIP query after the sync (no GPU work)
