@@ -1163,7 +1163,11 @@ bool conv_tile_shape(const ConvParams& c, int prec, ConvTileShape* sh) {
   // (64-channel upsample tiles, VSO_UP_BM64: capped like the plain 16-bit
   // ones — 8 x 32 x 64 ran at 319 VGPRs, one wave per SIMD: 99 us against the
   // 2 x 32 x 64 tile's 50, profiles/r05x r05ao)
-  const int max_th = (t.up && t.bm <= 32) ? 0 : max_th_env >= 0 ? max_th_env : (prec == PREC_F32 ? 0 : 2);
+  static const int up_max_th = [] {  // (A/B knob: a height cap for the upsample tiles too)
+    const char* e = std::getenv("VSO_UP_MAX_TH");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int max_th = (t.up && t.bm <= 32) ? up_max_th : max_th_env >= 0 ? max_th_env : (prec == PREC_F32 ? 0 : 2);
   long wgs = 0;
   for (int k = 0; k < nc; ++k) {
     if (max_th > 0 && cand[k][0] > max_th && k + 1 < nc) continue;
