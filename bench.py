@@ -465,10 +465,13 @@ def main():
     # us instead of 12-16 and the GPU started the window with 1-2 batches in
     # flight: the driver's 20-step window read 129-193k (mean 162.5k) with no
     # pause against 167-184k (mean 174.4k) after 5 ms, median steps alike —
-    # profiles/NOTES.md "The short window's first calls", profiles/r06j)
+    # profiles/NOTES.md "The short window's first calls", profiles/r06j.  The
+    # first step call after the pause still paid 36-190 us unless the slots
+    # had each run a step since: the warm-up's last S steps therefore run after
+    # the pause — W warm-up steps in all — profiles/r06z)
     ap.add_argument("--settle-ms", type=float, default=5.0,
-                    help="untimed pause between the warm-up's synchronize and the timed window's barrier + "
-                         "synchronize (the device idle throughout; no GPU work)")
+                    help="untimed pause inside the warm-up: after its first W - S steps and their synchronize, "
+                         "before its last S steps (one per slot) and the timed window's barrier + synchronize")
     ap.add_argument("--watchdog-s", type=float, default=60.0,
                     help="no step issued or completed for this long during a GPU phase: print a JSON record "
                          "(rank, stage, gather counter, communicators' async errors) and exit 3; 0 = off")
@@ -589,10 +592,14 @@ def main():
     wd.beat("prepare")
     sess.prepare_device(B, fh, fw, 3, rs, fs)
     wd.beat("warmup")
-    k = run_steps(sess, streams, args.warmup, step, wd=wd)
+    # W warm-up steps: W - S of them, a synchronize and the settle pause, then
+    # the last S (one per slot, the window's first S slots warm again)
+    tail = min(args.warmup, S) if args.settle_ms > 0 else 0
+    k = run_steps(sess, streams, args.warmup - tail, step, wd=wd)
     torch.cuda.synchronize(dev)
     if args.settle_ms > 0:
         time.sleep(args.settle_ms / 1e3)
+        k = run_steps(sess, streams, tail, step, start=k, wd=wd)
     wd.beat("barrier before the timed steps")
     if world > 1:
         dist.barrier()
@@ -711,6 +718,7 @@ def main():
             "value_at_median_step": round(world * B / (median_step_ms * 1e-3), 1) if median_step_ms else None,
             "graph_builds_in_timed_region": timed_builds,
             "settle_ms_before_window": args.settle_ms,
+            "warmup_steps_after_settle": tail,
             "graph_patches_in_timed_region": timed_patches,
             "higher_is_better": True,
             "scaling": "weak",
