@@ -284,6 +284,45 @@ def test_inverted_residuals_16bit_knobs(ort, knob, value):
         assert np.array_equal(here, other)
 
 
+@pytest.mark.parametrize("model", ["conv_tiles", "conv_up"])
+def test_conv_tile_xcd_order_bitwise(ort, model):
+    """k_conv_tile's XCD-contiguous item order (xcd_item, vso_device.h) is a
+    bijection on the grid: every tile computed by some workgroup with the same
+    arithmetic.  Every k_conv_tile form of conv_tiles (3x3 / 5x5, stride 2,
+    the K split that keeps the dispatcher's order, partial chunks) and the
+    fused-upsample forms of conv_up, f16, in a child process with the order
+    off (VSO_CONV_XCD=0, read at the first plan of a process) and in this
+    process with it on: bitwise equal."""
+    import subprocess
+    import sys
+    feeds = {"conv_tiles": ("{'x': r.standard_normal((2, 40, 37, 70)).astype(np.float32), "
+                            "'x2': r.standard_normal((2, 200, 9, 16)).astype(np.float32)}"),
+             "conv_up": ("{'lo': r.standard_normal((2, 64, 9, 17)).astype(np.float32), "
+                         "'skip': r.standard_normal((2, 5, 18, 34)).astype(np.float32), "
+                         "'lo2': r.standard_normal((2, 32, 11, 13)).astype(np.float32)}")}[model]
+    code = ("import numpy as np, sys; sys.path.insert(0, 'tests'); import onnx_models as M; "
+            "import importlib.util, os; spec = importlib.util.spec_from_file_location('vss_amd', "
+            "'video-stream-segmenetation_amd/__init__.py', submodule_search_locations=['video-stream-segmenetation_amd']); "
+            "m = importlib.util.module_from_spec(spec); sys.modules['vss_amd'] = m; spec.loader.exec_module(m); "
+            f"import vss_amd.ort as o; d = M.{model}(); r = np.random.default_rng(5); f = {feeds}; "
+            "s = o.InferenceSession(d, precision='f16'); g = s.run(f); "
+            f"np.savez('gpurun_out/xcd0_{model}.npz', **g)")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, VSO_CONV_XCD="0"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rng = np.random.default_rng(5)
+    f = eval(feeds, {"np": np, "r": rng})
+    with ort.InferenceSession(getattr(M, model)(), precision="f16") as s:
+        here = s.run(f)
+        names = s.launches()
+    assert any("k_conv_tile" in n for n in names), names
+    other = np.load(os.path.join(root, "gpurun_out", f"xcd0_{model}.npz"))
+    for k, v in here.items():
+        assert np.array_equal(v, other[k]), (model, k, float(np.abs(v - other[k]).max()))
+
+
 @pytest.mark.parametrize("precision", ["f32", "bf16"])
 def test_depthwise_separable_chain(ort, precision):
     """dw -> Clip -> 1x1 -> Clip -> dw -> Clip -> 1x1 (MobileNetV1 blocks): the
