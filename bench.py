@@ -453,8 +453,8 @@ def main():
                     help="run the multi-GPU step (RCCL clique all-gather) even at one rank (a rehearsal of N > 1)")
     ap.add_argument("--gather-form", default="ordered", choices=["ordered", "concurrent"],
                     help="how the N > 1 all-gathers are issued (VSS_OPT_GATHER_FORM, DESIGN.md §6): 'ordered' "
-                         "(default: one communicator and one gather stream per rank, a total order of "
-                         "collectives) or 'concurrent' (one communicator per slot; opt-in until an 8-GPU "
+                         "(default: one communicator per rank, its collectives one at a time in call order by an "
+                         "event chain) or 'concurrent' (one communicator per slot; opt-in until an 8-GPU "
                          "record exists)")
     ap.add_argument("--dry-run-dist", action="store_true",
                     help="rehearse the multi-rank plumbing only (launch_ranks -> torch.distributed.run -> gloo "

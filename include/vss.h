@@ -109,10 +109,12 @@ enum {
 
 /* VSS_OPT_GATHER_FORM values. */
 enum {
-  VSS_GATHER_ORDERED = 0,    /* one communicator (slot 0's, the only one created) and one gather
-                                stream: every rank issues one total order of collectives (its call
-                                order), which no stream -> hardware-queue mapping can reorder; the
-                                forwards of the batches in flight still overlap the gathers */
+  VSS_GATHER_ORDERED = 0,    /* one communicator (slot 0's, the only one created); each gather on
+                                the caller's stream behind its forward, after the previous call's
+                                gather has completed (an event chain): every rank runs one
+                                collective at a time in its call order, which no stream ->
+                                hardware-queue mapping can reorder; the forwards of the batches in
+                                flight still overlap the gathers */
   VSS_GATHER_CONCURRENT = 1  /* one communicator per slot, each gather on its slot's stream: the
                                 gathers of the batches in flight overlap each other too */
 };

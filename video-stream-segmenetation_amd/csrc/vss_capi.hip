@@ -392,8 +392,7 @@ struct vss_handle {
   // per rank.  VSS_GATHER_CONCURRENT: each slot's own communicator on the
   // slot's stream (vss_segment_gather_device)
   int gather_form = VSS_GATHER_ORDERED;
-  hipStream_t gather_stream = nullptr;
-  std::vector<hipEvent_t> gather_ev;  // per slot: [2k] forward done, [2k+1] gather done
+  std::vector<hipEvent_t> gather_ev;  // the ordered form's gather-done events, a ring of 2 x depth (call % size)
   // Submissions (slot choice, staging, enqueue) are serialised by mu; no
   // thread holds it while it waits for the GPU (waiters drop it first).
   std::mutex mu;
@@ -2013,7 +2012,6 @@ void destroy_engine(vss_handle* h) {
     if (e) (void)hipEventDestroy(e);
   for (auto e : h->gather_ev)
     if (e) (void)hipEventDestroy(e);
-  if (h->gather_stream) (void)hipStreamDestroy(h->gather_stream);
   for (void* p : h->dev_allocs) (void)hipFree(p);
   for (void* p : h->host_allocs) (void)hipHostFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -2358,7 +2356,6 @@ int vss_comm_init_rank(vss_handle* h, int nranks, int rank, const void* ids, siz
     std::memcpy(&id, static_cast<const char*>(ids) + k * sizeof(ncclUniqueId), sizeof(id));
     NCCL_TRY(h, ncclCommInitRank(&h->slots[k].comm, nranks, id, rank));
   }
-  HIP_TRY(h, hipStreamCreateWithFlags(&h->gather_stream, hipStreamNonBlocking));
   h->gather_ev.assign(2 * h->slots.size(), nullptr);
   for (hipEvent_t& e : h->gather_ev) HIP_TRY(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   h->nranks = nranks;
@@ -2381,7 +2378,8 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
   // rank uses the same slot's communicator for its i-th gather whatever other
   // device calls it interleaves
   const bool serial = h->gather_form == VSS_GATHER_ORDERED;
-  const int k = (int)(h->gather_calls.load(std::memory_order_relaxed) % h->slots.size());
+  const unsigned long long call = h->gather_calls.load(std::memory_order_relaxed);
+  const int k = (int)(call % h->slots.size());
   if ((rc = comm_healthy(h, h->slots[serial ? 0 : k].comm, serial ? 0 : k))) return rc;
   h->gather_calls.fetch_add(1, std::memory_order_relaxed);
   Slot& sl = h->slots[k];
@@ -2392,27 +2390,28 @@ int vss_segment_gather_device(vss_handle* h, const uint8_t* d_frames, int n, int
   }
   const size_t P = (size_t)h->cfg.model_h * h->cfg.model_w;
   // VSS_GATHER_ORDERED (default): every gather on slot 0's
-  // communicator and one stream — one total order of collectives per rank, the
-  // same on every rank (call order), whatever the runtime's stream -> hardware
-  // queue mapping; the forwards of the batches in flight still overlap the
-  // gathers.  VSS_GATHER_CONCURRENT (opt-in until an 8-GPU record exists):
-  // each slot's own communicator on the slot's stream, so the gathers of the
-  // batches in flight overlap too (at one rank 170k frames/s vs 123k); every
-  // rank uses slot k for its i-th call, so each communicator sees its
-  // collectives in the same order on every rank.
+  // communicator, one at a time in call order — one total order of
+  // collectives per rank, the same on every rank, whatever the runtime's
+  // stream -> hardware queue mapping.  Each gather runs on the caller's
+  // stream right behind its forward and first waits for the previous call's
+  // gather (an event chain), so no two collectives of a rank are ever in
+  // flight together; the forwards of the batches in flight still overlap
+  // the gathers.  (Round 6 ran them on a gather stream of their own, two
+  // cross-stream hops per call: each collective then held that stream ~57 us
+  // at one rank, 141-145k frames/s against 198-205k, profiles/r06/r06ak.)
+  // VSS_GATHER_CONCURRENT (opt-in until an 8-GPU record exists): each slot's
+  // own communicator on the slot's stream, so the gathers of the batches in
+  // flight overlap too; every rank uses slot k for its i-th call, so each
+  // communicator sees its collectives in the same order on every rank.
   ncclResult_t nr = ncclSuccess;
   hipError_t he = hipSuccess;
   if (!serial) {
     nr = ncclAllGather(sl.d_masks, d_gathered, (size_t)n * P, ncclFloat32, sl.comm, s);
   } else {
-    hipEvent_t fwd = h->gather_ev[2 * k], gat = h->gather_ev[2 * k + 1];
-    he = hipEventRecord(fwd, s);
-    if (he == hipSuccess) he = hipStreamWaitEvent(h->gather_stream, fwd, 0);
-    if (he == hipSuccess) nr = ncclAllGather(sl.d_masks, d_gathered, (size_t)n * P, ncclFloat32, h->slots[0].comm,
-                                             h->gather_stream);
-    if (he == hipSuccess && nr == ncclSuccess) he = hipEventRecord(gat, h->gather_stream);
-    // the caller's stream (and the slot's release) after the gather
-    if (he == hipSuccess && nr == ncclSuccess) he = hipStreamWaitEvent(s, gat, 0);
+    const size_t ne = h->gather_ev.size();
+    if (call > 0) he = hipStreamWaitEvent(s, h->gather_ev[(call - 1) % ne], 0);  // the previous gather, done
+    if (he == hipSuccess) nr = ncclAllGather(sl.d_masks, d_gathered, (size_t)n * P, ncclFloat32, h->slots[0].comm, s);
+    if (he == hipSuccess && nr == ncclSuccess) he = hipEventRecord(h->gather_ev[call % ne], s);
   }
   const int rr = release_slot(h, sl, s);
   if (nr != ncclSuccess) return fail(h, VSS_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
