@@ -1581,13 +1581,22 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   // copied into the staging (the other rows of the staged frames are never
   // read: the fused stem, k_prep and the post chain's guide all sample the
   // same rows): at 640x480 that halves the host memcpy of the copy path.
+  // A one-frame batch moves its rows with k_fetch_rows whatever their share:
+  // there the kernel's reads of pinned memory beat one DMA of the whole frame
+  // (640x480: the TS segmentFrame device phase 104-111 -> 91-99 us, p50
+  // 0.155-0.198 -> 0.146-0.152 ms, profiles/r06/r06an); batches keep the
+  // DMA (VSS_FETCH_SINGLE=k: batches of at most k frames; 0: off)
+  static const int fetch_single = [] {
+    const char* e = std::getenv("VSS_FETCH_SINGLE");
+    return e ? std::atoi(e) : 1;
+  }();
   std::vector<const RowPlan*> plans(R, nullptr);  // the rows (row_fetch on)
   std::vector<bool> fetch(R, false);              // move them with k_fetch_rows (else one DMA)
   for (int r = 0; r < R; ++r) {
     HIP_TRY(E[r], hipSetDevice(E[r]->device));
     if (!h->row_fetch) continue;
     if ((rc = row_plan(E[r], fh, &plans[r]))) return fail(h, rc, E[r]->err);
-    fetch[r] = plans[r]->rows.size() * 5 <= (size_t)fh * 2;
+    fetch[r] = plans[r]->rows.size() * 5 <= (size_t)fh * 2 || (n <= fetch_single && n >= 1);
   }
   // stage every GPU's shard (zero-copy when the caller wrote into this slot's buffer)
   std::vector<CopyPool::Job> jobs;
