@@ -1581,14 +1581,15 @@ int submit_host(vss_handle* h, const uint8_t* frames, const uint8_t* const* list
   // copied into the staging (the other rows of the staged frames are never
   // read: the fused stem, k_prep and the post chain's guide all sample the
   // same rows): at 640x480 that halves the host memcpy of the copy path.
-  // A one-frame batch moves its rows with k_fetch_rows whatever their share:
-  // there the kernel's reads of pinned memory beat one DMA of the whole frame
-  // (640x480: the TS segmentFrame device phase 104-111 -> 91-99 us, p50
-  // 0.155-0.198 -> 0.146-0.152 ms, profiles/r06/r06an); batches keep the
-  // DMA (VSS_FETCH_SINGLE=k: batches of at most k frames; 0: off)
+  // (VSS_FETCH_SINGLE=k, an A/B knob, default 0: batches of at most k
+  // frames move their rows with k_fetch_rows whatever their share.  For one
+  // 640x480 frame it depends on the box: the TS segmentFrame p50 0.146-0.152
+  // against 0.155-0.198 ms on one (profiles/r06/r06an), 0.182-0.185 against
+  // 0.155-0.191 on another (r06aq) — the kernel's reads of pinned host
+  // memory are slower on some hosts than one DMA of the whole frame)
   static const int fetch_single = [] {
     const char* e = std::getenv("VSS_FETCH_SINGLE");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 0;
   }();
   std::vector<const RowPlan*> plans(R, nullptr);  // the rows (row_fetch on)
   std::vector<bool> fetch(R, false);              // move them with k_fetch_rows (else one DMA)
