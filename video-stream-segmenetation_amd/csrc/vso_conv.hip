@@ -338,11 +338,16 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
     __syncthreads();  // the previous chunk's fragment reads are done
     if (up_chunk(ch)) {
       if constexpr (UP) {
+        // items of one pixel and QI quads (QI x CG channels): the pixel's
+        // source coordinates and taps worked out once per item rather than
+        // once per quad (the coordinate and address arithmetic was most of
+        // this loop's VALU: ~150 per 8-channel item, 36 of them the lerps)
+        constexpr int QI = NQ % 2 == 0 ? 2 : 1, NIT = NPIX * (NQ / QI), PERI = (NIT + 255) / 256;
 #pragma unroll 1
-        for (int u = 0; u < PER; ++u) {
+        for (int u = 0; u < PERI; ++u) {
           const int idx = tid + 256 * u;
-          if (idx < ITEMS) {
-            const int q = idx / NPIX, pix = idx - q * NPIX;
+          if (idx < NIT) {
+            const int qh = idx / NPIX, pix = idx - qh * NPIX;
             const int iy = pix / IW, ix = pix - iy * IW;
             const int gy = iy0 + iy, gx = ix0 + ix;
             const bool in = (unsigned)gy < (unsigned)c.H && (unsigned)gx < (unsigned)c.W;
@@ -354,27 +359,30 @@ __device__ __forceinline__ void conv_tile_body(const ConvTileParams& p) {
             const int a0 = min(max(y0 - ry0, 0), SR - 1), a1 = min(max(min(y0 + 1, p.up_H - 1) - ry0, 0), SR - 1);
             const int b0 = min(max(x0 - rx0, 0), SC - 1), b1 = min(max(min(x0 + 1, p.up_W - 1) - rx0, 0), SC - 1);
             const int t00 = a0 * SC + b0, t01 = a0 * SC + b1, t10 = a1 * SC + b0, t11 = a1 * SC + b1;
-            const float* l = lrs + q * CG * SRC;
-            // every tap read unconditionally (the clamped taps lie in the
-            // region), all 4 x CG in flight at once, the halo's zero applied
-            // after as a product with 0 / 1 (finite values: the same as the
-            // select): with `in ? interp : 0` the compiler sank the reads
-            // into a branch per channel, an exposed LDS round trip each (8
-            // per item, 48 per thread and chunk at 8 x 32 tiles)
-            float t0[CG], t1[CG], t2[CG], t3[CG];
-#pragma unroll
-            for (int e = 0; e < CG; ++e) {
-              t0[e] = l[e * SRC + t00];
-              t1[e] = l[e * SRC + t01];
-              t2[e] = l[e * SRC + t10];
-              t3[e] = l[e * SRC + t11];
-            }
             const float keep = in ? 1.f : 0.f;
-            float v[CG];
+#pragma unroll 1
+            for (int qq = 0; qq < QI; ++qq) {
+              const int q = qh * QI + qq;
+              const float* l = lrs + q * CG * SRC;
+              // every tap read unconditionally (the clamped taps lie in the
+              // region), all 4 x CG in flight at once, the halo's zero applied
+              // after as a product with 0 / 1 (finite values: the same as the
+              // select): with `in ? interp : 0` the compiler sank the reads
+              // into a branch per channel, an exposed LDS round trip each
+              float t0[CG], t1[CG], t2[CG], t3[CG];
 #pragma unroll
-            for (int e = 0; e < CG; ++e)
-              v[e] = keep * ((1.f - ly) * ((1.f - lx) * t0[e] + lx * t1[e]) + ly * ((1.f - lx) * t2[e] + lx * t3[e]));
-            xs[pix * QS + q] = pack_quad<PREC>(v);
+              for (int e = 0; e < CG; ++e) {
+                t0[e] = l[e * SRC + t00];
+                t1[e] = l[e * SRC + t01];
+                t2[e] = l[e * SRC + t10];
+                t3[e] = l[e * SRC + t11];
+              }
+              float v[CG];
+#pragma unroll
+              for (int e = 0; e < CG; ++e)
+                v[e] = keep * ((1.f - ly) * ((1.f - lx) * t0[e] + lx * t1[e]) + ly * ((1.f - lx) * t2[e] + lx * t3[e]));
+              xs[pix * QS + q] = pack_quad<PREC>(v);
+            }
           }
         }
       }
