@@ -558,7 +558,11 @@ static bool pw_kernel(const ConvParams& p, int* wm, int* dwk) {
     return pw_pair_fits(p.N, p.C, (long)p.pre.H * p.pre.W, P, p.M);
   }
   if ((long)p.C * P >= (1L << 31) || (long)p.M * P >= (1L << 31)) return false;  // 32-bit offsets within an image
-  return wgs >= 256 || p.C <= 192;
+  static const bool plain_on = [] {  // (VSO_PW=0: plain 1x1s on k_conv_small / k_conv_gemm, an A/B knob)
+    const char* e = std::getenv("VSO_PW");
+    return !(e && e[0] == '0');
+  }();
+  return plain_on && (wgs >= 256 || p.C <= 192);
 }
 
 // Index arithmetic in 32 bits whenever the tensor allows (I = int): a 64-bit
